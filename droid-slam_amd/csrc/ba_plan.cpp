@@ -1,0 +1,225 @@
+// Host-side structure analysis for one ba() call (the part of ba_cuda that
+// depends only on ii, jj, t0, t1): droid_kernels.cu:1336-1345 (ts, kx, kk),
+// :1241-1272 (Schur row graph) and the triplet lists of
+// SparseBlock::update_lhs/rhs (:1131-1173).  Unlike the reference, this runs
+// once per edge set (cached by the caller), never inside the GN loop.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <utility>
+
+#include "ba.hpp"
+#include "common.hpp"
+
+namespace droid {
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, int N, int H, int W,
+                      int t0, int t1, int eta_rows, int motion_only, int own_lo, int own_hi) {
+  if (E < 0 || N <= 0 || H <= 0 || W <= 0) return fail(kInvalidArgument, "ba: bad sizes");
+  if (t0 < 0 || t1 <= t0 || t1 > N)
+    return fail(kInvalidArgument, "ba: need 0 <= t0 < t1 <= num_frames");
+  p.E = E; p.N = N; p.H = H; p.W = W; p.HW = H * W;
+  p.t0 = t0; p.t1 = t1; p.P = t1 - t0; p.n = 6 * p.P;
+  p.motion_only = motion_only; p.eta_rows = eta_rows;
+  p.ii.resize(E); p.jj.resize(E);
+  for (int e = 0; e < E; ++e) {
+    if (ii[e] < 0 || ii[e] >= N || jj[e] < 0 || jj[e] >= N)
+      return fail(kInvalidArgument, "ba: edge index out of range");
+    p.ii[e] = (int)ii[e];
+    p.jj[e] = (int)jj[e];
+  }
+  const int HW = p.HW;
+
+  // kx = unique(cat(ts, ii)) with ts the optimised poses this rank owns
+  std::vector<char> present(N, 0);
+  const int lo = std::max(t0, own_lo), hi = std::min(t1, own_hi);
+  for (int t = lo; t < hi; ++t) present[t] = 1;
+  for (int e = 0; e < E; ++e) present[p.ii[e]] = 1;
+  std::vector<int> fidx(N, -1);
+  p.kx.clear();
+  for (int f = 0; f < N; ++f)
+    if (present[f]) { fidx[f] = (int)p.kx.size(); p.kx.push_back(f); }
+  p.K = (int)p.kx.size();
+  if (!motion_only && eta_rows != p.K && eta_rows != 1)
+    return fail(kInvalidArgument,
+                "ba: eta must have one row per frame of unique([t0,t1) U ii) (got " +
+                    std::to_string(eta_rows) + ", need " + std::to_string(p.K) + ")");
+
+  // edges grouped by source frame, ascending edge index (stable)
+  p.f_eptr.assign(p.K + 1, 0);
+  for (int e = 0; e < E; ++e) p.f_eptr[fidx[p.ii[e]] + 1]++;
+  for (int f = 0; f < p.K; ++f) p.f_eptr[f + 1] += p.f_eptr[f];
+  p.f_edges.assign(E, 0);
+  {
+    std::vector<int> fill(p.f_eptr.begin(), p.f_eptr.end() - 1);
+    for (int e = 0; e < E; ++e) p.f_edges[fill[fidx[p.ii[e]]]++] = e;
+  }
+
+  // launch geometry
+  p.nsplit = std::max(1, std::min(std::max(1, HW / 256), (2048 + std::max(E, 1) - 1) / std::max(E, 1)));
+  const int rounds = ceil_div(HW, 256);
+  p.group_per_wave = std::max(1, std::min(rounds, (int)((long)p.K * rounds / 1024)));
+  p.nchunk = ceil_div(rounds, p.group_per_wave);
+
+  // Schur rows per frame: [Ei row if the frame's pose is optimised] + one Eij row per edge
+  p.f_rptr.assign(p.K + 1, 0);
+  p.r_pose.clear(); p.r_edge.clear();
+  p.f_nb.assign(p.K, 0); p.f_goff.assign(p.K, 0);
+  p.nb_max = 1;
+  p.gram_floats = 0;
+  for (int f = 0; f < p.K; ++f) {
+    const int kf = p.kx[f];
+    if (kf >= t0 && kf < t1) { p.r_pose.push_back(kf - t0); p.r_edge.push_back(-1); }
+    for (int k = p.f_eptr[f]; k < p.f_eptr[f + 1]; ++k) {
+      const int e = p.f_edges[k];
+      const int j = p.jj[e];
+      p.r_pose.push_back((j >= t0 && j < t1) ? j - t0 : -1);
+      p.r_edge.push_back(e);
+    }
+    p.f_rptr[f + 1] = (int)p.r_pose.size();
+    const int nrows = p.f_rptr[f + 1] - p.f_rptr[f];
+    const int nb = ceil_div(6 * nrows + 1, 16);
+    if (!motion_only && nb > kNbMax)
+      return fail(kUnsupported, "ba: a depth frame has " + std::to_string(nrows - 1) +
+                                    " outgoing edges; the Schur kernel supports up to 20");
+    p.f_nb[f] = nb;
+    p.nb_max = std::max(p.nb_max, nb);
+    p.f_goff[f] = (int)p.gram_floats;
+    p.gram_floats += (long)p.nchunk * (nb * (nb + 1) / 2) * 256;
+  }
+  if (motion_only) p.gram_floats = 0;
+
+  // Block contribution lists for the lower triangle of the reduced system.
+  std::map<std::pair<int, int>, std::vector<Contrib>> blocks;
+  std::vector<std::vector<Contrib>> rhs(p.P);
+  const int P = p.P;
+  for (int e = 0; e < E; ++e) {
+    const int i = p.ii[e] - t0, j = p.jj[e] - t0;
+    const int idx[2] = {i, j};
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b) {
+        const int r = idx[a], c = idx[b];
+        if (r < 0 || c < 0 || r >= P || c >= P || r < c) continue;
+        blocks[{r, c}].push_back({kEdgeBlock, e, 6 * a, 6 * b});
+      }
+    if (i >= 0 && i < P) rhs[i].push_back({kEdgeRhs, e, 0, 0});
+    if (j >= 0 && j < P) rhs[j].push_back({kEdgeRhs, e, 6, 0});
+  }
+  if (!motion_only) {
+    for (int f = 0; f < p.K; ++f) {
+      const int r0 = p.f_rptr[f], r1 = p.f_rptr[f + 1];
+      for (int ra = r0; ra < r1; ++ra) {
+        const int pa = p.r_pose[ra];
+        if (pa < 0) continue;
+        rhs[pa].push_back({kSchurRhs, f, ra - r0, 0});
+        for (int rb = r0; rb < r1; ++rb) {
+          const int pb = p.r_pose[rb];
+          if (pb < 0 || pa < pb) continue;
+          blocks[{pa, pb}].push_back({kSchurBlock, f, ra - r0, rb - r0});
+        }
+      }
+    }
+  }
+  p.blk_a.clear(); p.blk_b.clear(); p.blk_cptr.assign(1, 0); p.contrib.clear();
+  for (auto& kv : blocks) {
+    p.blk_a.push_back(kv.first.first);
+    p.blk_b.push_back(kv.first.second);
+    for (auto& c : kv.second) p.contrib.push_back(c);
+    p.blk_cptr.push_back((int)p.contrib.size());
+  }
+  p.rhs_cptr.assign(1, 0); p.rhs_contrib.clear();
+  for (int a = 0; a < P; ++a) {
+    for (auto& c : rhs[a]) p.rhs_contrib.push_back(c);
+    p.rhs_cptr.push_back((int)p.rhs_contrib.size());
+  }
+
+  // pack the int section
+  p.ints.clear();
+  auto put = [&](const std::vector<int>& v) {
+    size_t o = p.ints.size();
+    p.ints.insert(p.ints.end(), v.begin(), v.end());
+    while (p.ints.size() % 4) p.ints.push_back(0);
+    return o;
+  };
+  auto putc = [&](const std::vector<Contrib>& v) {
+    size_t o = p.ints.size();
+    for (auto& c : v) { p.ints.push_back(c.kind); p.ints.push_back(c.src); p.ints.push_back(c.a0); p.ints.push_back(c.a1); }
+    return o;
+  };
+  p.o_ii = put(p.ii); p.o_jj = put(p.jj); p.o_kx = put(p.kx);
+  p.o_feptr = put(p.f_eptr); p.o_fedges = put(p.f_edges);
+  p.o_frptr = put(p.f_rptr); p.o_rpose = put(p.r_pose); p.o_redge = put(p.r_edge);
+  p.o_fnb = put(p.f_nb); p.o_fgoff = put(p.f_goff);
+  p.o_blka = put(p.blk_a); p.o_blkb = put(p.blk_b); p.o_blkcptr = put(p.blk_cptr);
+  p.o_rhscptr = put(p.rhs_cptr);
+  p.o_contrib = putc(p.contrib); p.o_rhscontrib = putc(p.rhs_contrib);
+  if (p.ints.empty()) p.ints.push_back(0);
+
+  // workspace layout
+  size_t off = 0;
+  p.off_ints = off; off = align_up(off + p.ints.size() * 4, 256);
+  p.off_hpart = off; off = align_up(off + (size_t)std::max(E, 1) * p.nsplit * kHessStride * 4, 256);
+  p.off_gram = off; off = align_up(off + (size_t)std::max(p.gram_floats, 1L) * 4, 256);
+  p.off_qw = off; off = align_up(off + (size_t)2 * p.K * HW * 4 + 4, 256);
+  p.off_M = off; off = align_up(off + (size_t)(p.n + 1) * (p.n + 1) * 8, 256);
+  p.off_x = off; off = align_up(off + (size_t)(p.n + 1) * 8, 256);
+  p.off_flag = off; off = align_up(off + 64, 256);
+  p.total = off;
+  return kOk;
+}
+
+}  // namespace droid
+
+using namespace droid;
+
+extern "C" {
+
+int droid_ba_plan_create(const int64_t* ii, const int64_t* jj, int num_edges, int num_frames,
+                         int ht, int wd, int t0, int t1, int eta_rows, int motion_only,
+                         int own_lo, int own_hi, void** plan_out) {
+  if (!plan_out) return fail(kInvalidArgument, "ba_plan_create: null output");
+  *plan_out = nullptr;
+  auto* p = new BaPlan();
+  int st = build_plan(*p, ii, jj, num_edges, num_frames, ht, wd, t0, t1, eta_rows, motion_only,
+                      own_lo, own_hi);
+  if (st != kOk) { delete p; return st; }
+  *plan_out = p;
+  return kOk;
+}
+
+void droid_ba_plan_destroy(void* plan) { delete static_cast<BaPlan*>(plan); }
+
+size_t droid_ba_plan_workspace_bytes(const void* plan) {
+  return plan ? static_cast<const BaPlan*>(plan)->total : 0;
+}
+
+int droid_ba_plan_info(const void* plan, int* K, int* P, int* nblocks, int* nb_max) {
+  auto* p = static_cast<const BaPlan*>(plan);
+  if (!p) return fail(kInvalidArgument, "ba_plan_info: null plan");
+  if (K) *K = p->K;
+  if (P) *P = p->P;
+  if (nblocks) *nblocks = (int)p->blk_a.size();
+  if (nb_max) *nb_max = p->nb_max;
+  return kOk;
+}
+
+int droid_ba_plan_kx(const void* plan, int64_t* out) {
+  auto* p = static_cast<const BaPlan*>(plan);
+  if (!p) return fail(kInvalidArgument, "ba_plan_kx: null plan");
+  for (int k = 0; k < p->K; ++k) out[k] = p->kx[k];
+  return kOk;
+}
+
+// Byte offset/size of the reduced system (augmented (n+1)x(n+1) fp64, rhs in
+// the last row) inside the workspace: the buffer a multi-GPU caller all-reduces.
+int droid_ba_plan_system_region(const void* plan, size_t* offset, size_t* bytes) {
+  auto* p = static_cast<const BaPlan*>(plan);
+  if (!p) return fail(kInvalidArgument, "ba_plan_system_region: null plan");
+  *offset = p->off_M;
+  *bytes = (size_t)(p->n + 1) * (p->n + 1) * 8;
+  return kOk;
+}
+
+}  // extern "C"

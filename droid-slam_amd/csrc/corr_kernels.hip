@@ -1,0 +1,451 @@
+// Correlation lookup kernels for gfx950.
+//
+//  corr_index_forward / backward  — drop-in for correlation_kernels.cu:19-185
+//  corr_pyramid_lookup            — CorrBlock.__call__ (modules/corr.py:40-50) for all
+//                                   levels in ONE launch, writing the concatenated
+//                                   (E, L*(2r+1)^2, H, W) tensor directly
+//  altcorr_forward / backward     — drop-in for altcorr_kernel.cu:27-356
+//
+// Lookup arithmetic (all dtypes) follows the reference loop order: taps are
+// visited i = x-offset outer, j = y-offset inner, and every output (a,b)
+// receives its four bilinear terms in the order
+//     (a,b)*(1-dx)(1-dy), (a,b+1)*(1-dx)dy, (a+1,b)*dx(1-dy), (a+1,b+1)*dx*dy.
+// fp16 reproduces at::Half semantics bit-exactly (weight rounded to half,
+// product rounded to half, every += rounded to half); fp32/fp64 use the fused
+// multiply-add nvcc emits for `corr += s * w`.
+#include "common.hpp"
+
+namespace droid {
+
+template <typename T> struct Acc;
+template <> struct Acc<__half> {
+  // weight -> half, product -> half, sum -> half (at::Half operator semantics)
+  __device__ static float weight(float w) { return round_half(w); }
+  __device__ static float madd(float acc, float s, float w) {
+    return round_half(acc + round_half(s * w));
+  }
+  __device__ static float load(const __half* p) { return __half2float(*p); }
+  __device__ static __half store(float v) { return __float2half(v); }
+};
+template <> struct Acc<float> {
+  __device__ static float weight(float w) { return w; }
+  __device__ static float madd(float acc, float s, float w) { return fmaf(s, w, acc); }
+  __device__ static float load(const float* p) { return *p; }
+  __device__ static float store(float v) { return v; }
+};
+template <> struct Acc<double> {
+  __device__ static double weight(float w) { return (double)w; }
+  __device__ static double madd(double acc, double s, double w) { return fma(s, w, acc); }
+  __device__ static double load(const double* p) { return *p; }
+  __device__ static double store(double v) { return v; }
+};
+
+template <typename T> struct Compute { using type = float; };
+template <> struct Compute<double> { using type = double; };
+
+// ---------------------------------------------------------------------------
+// Generic per-level lookup: one thread per (n, y, x).  `out_bstride` lets the
+// pyramid path write level i straight into its channel slice of the
+// concatenated output.  Taps outside the volume are skipped (adding an exact
+// zero is identical: the running sum can never be -0).
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256)
+corr_index_fwd_kernel(const T* __restrict__ volume, const float* __restrict__ coords,
+                      int coords_layout_hw2, float scale, T* __restrict__ corr,
+                      long out_bstride, int B, int H, int W, int H2, int W2, int r) {
+  using C = typename Compute<T>::type;
+  const int HW = H * W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = blockIdx.y;
+  if (p >= HW) return;
+  float x0, y0;
+  if (coords_layout_hw2) {  // (B, H, W, 2)
+    x0 = coords[((long)n * HW + p) * 2 + 0] * scale;
+    y0 = coords[((long)n * HW + p) * 2 + 1] * scale;
+  } else {  // (B, 2, H, W)
+    x0 = coords[((long)n * 2 + 0) * HW + p] * scale;
+    y0 = coords[((long)n * 2 + 1) * HW + p] * scale;
+  }
+  const float fx0 = floorf(x0), fy0 = floorf(y0);
+  const float dx = x0 - fx0, dy = y0 - fy0;
+  const int xi0 = (int)fx0, yi0 = (int)fy0;
+  const int rd = 2 * r + 1;
+  const C w11 = Acc<T>::weight(dx * dy);
+  const C w10 = Acc<T>::weight(dx * (1.0f - dy));
+  const C w01 = Acc<T>::weight((1.0f - dx) * dy);
+  const C w00 = Acc<T>::weight((1.0f - dx) * (1.0f - dy));
+  const T* vol = volume + ((long)n * HW + p) * (long)H2 * W2;
+  T* out = corr + (long)n * out_bstride + p;
+  // Gather the (rd+1)^2 taps one x-column at a time, producing column a = i-1
+  // once column i is known.  Columns of the window live in registers only
+  // for the fixed radius-3 instantiation; generic radii use a small local
+  // array (r <= 7 supported).
+  C prev[16], cur[16];
+  for (int i = 0; i <= rd; ++i) {
+    const int x1 = xi0 - r + i;
+    for (int j = 0; j <= rd; ++j) {
+      const int y1 = yi0 - r + j;
+      C s = 0;
+      if (x1 >= 0 && x1 < W2 && y1 >= 0 && y1 < H2) s = (C)Acc<T>::load(vol + (long)y1 * W2 + x1);
+      cur[j] = s;
+    }
+    if (i > 0) {
+      const int a = i - 1;
+      for (int b = 0; b < rd; ++b) {
+        C acc = 0;
+        acc = Acc<T>::madd(acc, prev[b], w00);
+        acc = Acc<T>::madd(acc, prev[b + 1], w01);
+        acc = Acc<T>::madd(acc, cur[b], w10);
+        acc = Acc<T>::madd(acc, cur[b + 1], w11);
+        out[(long)(a * rd + b) * HW] = Acc<T>::store(acc);
+      }
+    }
+    for (int j = 0; j <= rd; ++j) prev[j] = cur[j];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fast fp16 radius-3 pyramid lookup: one thread per (edge, pixel), all levels.
+// Each window row (8 taps = 16 B at an arbitrary 2-B offset) is fetched as the
+// two aligned 16-B chunks that cover it (requires W2 % 8 == 0) and funnel-
+// shifted into place; arithmetic identical to corr_index_fwd_kernel<__half>.
+// ---------------------------------------------------------------------------
+struct PyramidArgs {
+  const __half* vol[4];
+  int H2[4];
+  int W2[4];
+  int levels;
+};
+
+__device__ __forceinline__ void load_row8_f16(const __half* row, int xs, int W2, float* t) {
+  // taps x = xs .. xs+7 of one volume row; zero outside [0, W2)
+  const int c0 = (xs >= 0) ? (xs >> 3) : -((-xs + 7) >> 3);  // floor(xs/8)
+  const int off = xs - 8 * c0;                                // 0..7
+  const int nch = W2 >> 3;
+  uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
+  if (c0 >= 0 && c0 < nch) a = *reinterpret_cast<const uint4*>(row + 8 * c0);
+  if (c0 + 1 >= 0 && c0 + 1 < nch) b = *reinterpret_cast<const uint4*>(row + 8 * (c0 + 1));
+  unsigned u[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const int k = off >> 1;
+  unsigned v[6], w[5];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) v[i] = (k & 2) ? u[i + 2] : u[i];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) w[i] = (k & 1) ? v[i + 1] : v[i];
+  const unsigned sh = (off & 1) ? 16u : 0u;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const unsigned o = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
+    t[2 * m + 0] = __half2float(__ushort_as_half((unsigned short)(o & 0xffffu)));
+    t[2 * m + 1] = __half2float(__ushort_as_half((unsigned short)(o >> 16)));
+  }
+}
+
+__global__ void __launch_bounds__(256)
+corr_pyramid_f16_r3_kernel(PyramidArgs args, const float* __restrict__ coords,
+                           __half* __restrict__ out, int H, int W) {
+  constexpr int R = 3, RD = 7;
+  const int HW = H * W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = blockIdx.y;
+  if (p >= HW) return;
+  const float cx = coords[((long)e * HW + p) * 2 + 0];
+  const float cy = coords[((long)e * HW + p) * 2 + 1];
+  const int nch = args.levels * RD * RD;
+  __half* o = out + (long)e * nch * HW + p;
+  for (int lvl = 0; lvl < args.levels; ++lvl) {
+    const float s = 1.0f / (float)(1 << lvl);
+    const float x0 = cx * s, y0 = cy * s;
+    const float fx0 = floorf(x0), fy0 = floorf(y0);
+    const float dx = x0 - fx0, dy = y0 - fy0;
+    const int xi0 = (int)fx0, yi0 = (int)fy0;
+    const float w11 = round_half(dx * dy);
+    const float w10 = round_half(dx * (1.0f - dy));
+    const float w01 = round_half((1.0f - dx) * dy);
+    const float w00 = round_half((1.0f - dx) * (1.0f - dy));
+    const int H2 = args.H2[lvl], W2 = args.W2[lvl];
+    const __half* vol = args.vol[lvl] + ((long)e * HW + p) * (long)H2 * W2;
+    float prev[8], cur[8];
+    __half* ol = o + (long)lvl * RD * RD * HW;
+#pragma unroll
+    for (int j = 0; j <= RD; ++j) {
+      const int y1 = yi0 - R + j;
+      if (y1 >= 0 && y1 < H2) {
+        load_row8_f16(vol + (long)y1 * W2, xi0 - R, W2, cur);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cur[i] = 0.f;
+      }
+      if (j > 0) {
+        const int b = j - 1;
+#pragma unroll
+        for (int a = 0; a < RD; ++a) {
+          float acc = 0.f + round_half(prev[a] * w00);
+          acc = round_half(acc + round_half(cur[a] * w01));
+          acc = round_half(acc + round_half(prev[a + 1] * w10));
+          acc = round_half(acc + round_half(cur[a + 1] * w11));
+          ol[(long)(a * RD + b) * HW] = __float2half(acc);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) prev[i] = cur[i];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// corr_index_backward: scatter bilinear-weighted gradients into the volume
+// (correlation_kernels.cu:73-124).  Each (n,y,x) owns its volume slice, so no
+// atomics are needed.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256)
+corr_index_bwd_kernel(const float* __restrict__ coords, const T* __restrict__ grad,
+                      T* __restrict__ vgrad, int B, int H, int W, int H2, int W2, int r) {
+  using C = typename Compute<T>::type;
+  const int HW = H * W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = blockIdx.y;
+  if (p >= HW) return;
+  const float x0 = coords[((long)n * 2 + 0) * HW + p];
+  const float y0 = coords[((long)n * 2 + 1) * HW + p];
+  const float fx0 = floorf(x0), fy0 = floorf(y0);
+  const float dx = x0 - fx0, dy = y0 - fy0;
+  const int xi0 = (int)fx0, yi0 = (int)fy0;
+  const int rd = 2 * r + 1;
+  const T* g = grad + (long)n * rd * rd * HW + p;
+  T* vg = vgrad + ((long)n * HW + p) * (long)H2 * W2;
+  for (int i = 0; i <= rd; ++i) {
+    for (int j = 0; j <= rd; ++j) {
+      const int x1 = xi0 - r + i, y1 = yi0 - r + j;
+      if (!(x1 >= 0 && x1 < W2 && y1 >= 0 && y1 < H2)) continue;
+      C acc = 0;
+      if (i > 0 && j > 0) acc += (C)Acc<T>::load(g + (long)((i - 1) * rd + (j - 1)) * HW) * (C)(dx * dy);
+      if (i > 0 && j < rd) acc += (C)Acc<T>::load(g + (long)((i - 1) * rd + j) * HW) * (C)(dx * (1.0f - dy));
+      if (i < rd && j > 0) acc += (C)Acc<T>::load(g + (long)(i * rd + (j - 1)) * HW) * (C)((1.0f - dx) * dy);
+      if (i < rd && j < rd) acc += (C)Acc<T>::load(g + (long)(i * rd + j) * HW) * (C)((1.0f - dx) * (1.0f - dy));
+      T* dst = vg + (long)y1 * W2 + x1;
+      *dst = Acc<T>::store((C)Acc<T>::load(dst) + acc);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// altcorr_forward: corr[b,s,7*ix+iy,h,w] = bilinear sample of <f1(h,w), f2(.)>
+// over the radius window, computed on the fly from channels-last fmaps
+// (altcorr_kernel.cu:27-149, race-free).  One thread per (b, s, pixel); the
+// 64 per-tap dot products are accumulated over 32-channel chunks in fp32.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(64)
+altcorr_fwd_kernel(const T* __restrict__ fmap1, const T* __restrict__ fmap2,
+                   const float* __restrict__ coords, T* __restrict__ corr,
+                   int B, int S, int H, int W, int H2, int W2, int C) {
+  constexpr int R = 3, RD = 7, NT = 8;
+  const int HW = H * W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int s = blockIdx.y;
+  const int b = blockIdx.z;
+  if (p >= HW) return;
+  const float x = coords[(((long)b * S + s) * HW + p) * 2 + 0];
+  const float y = coords[(((long)b * S + s) * HW + p) * 2 + 1];
+  const float fx0 = floorf(x), fy0 = floorf(y);
+  const float dx = x - fx0, dy = y - fy0;
+  const int xi0 = (int)fx0, yi0 = (int)fy0;
+  float dots[NT * NT];
+#pragma unroll
+  for (int k = 0; k < NT * NT; ++k) dots[k] = 0.f;
+  const T* f1 = fmap1 + ((long)b * HW + p) * C;
+  const T* f2b = fmap2 + (long)b * H2 * W2 * C;
+  for (int c0 = 0; c0 < C; c0 += 8) {
+    float a[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) a[c] = (c0 + c < C) ? (float)f1[c0 + c] : 0.f;
+#pragma unroll
+    for (int iy = 0; iy < NT; ++iy) {
+      const int h2 = yi0 - R + iy;
+#pragma unroll
+      for (int ix = 0; ix < NT; ++ix) {
+        const int w2 = xi0 - R + ix;
+        if (h2 < 0 || h2 >= H2 || w2 < 0 || w2 >= W2) continue;
+        const T* f2 = f2b + ((long)h2 * W2 + w2) * C + c0;
+        float acc = dots[iy * NT + ix];
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (c0 + c < C) acc = fmaf(a[c], (float)f2[c], acc);
+        dots[iy * NT + ix] = acc;
+      }
+    }
+  }
+  T* out = corr + (((long)b * S + s) * RD * RD) * HW + p;
+#pragma unroll
+  for (int ix = 0; ix < RD; ++ix) {
+#pragma unroll
+    for (int iy = 0; iy < RD; ++iy) {
+      // output (iy, ix) collects taps (iy,ix) se, (iy+1,ix) ne, (iy,ix+1) sw, (iy+1,ix+1) nw
+      float v = dots[iy * NT + ix] * ((1.f - dy) * (1.f - dx));
+      v += dots[(iy + 1) * NT + ix] * (dy * (1.f - dx));
+      v += dots[iy * NT + ix + 1] * ((1.f - dy) * dx);
+      v += dots[(iy + 1) * NT + ix + 1] * (dy * dx);
+      out[(long)(iy + RD * ix) * HW] = (T)v;
+    }
+  }
+}
+
+// altcorr_backward (fp32): g1 owned per pixel, g2 scattered with atomics.
+__global__ void __launch_bounds__(64)
+altcorr_bwd_kernel(const float* __restrict__ fmap1, const float* __restrict__ fmap2,
+                   const float* __restrict__ coords, const float* __restrict__ grad,
+                   float* __restrict__ g1, float* __restrict__ g2,
+                   int B, int S, int H, int W, int H2, int W2, int C) {
+  constexpr int R = 3, RD = 7, NT = 8;
+  const int HW = H * W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.z;
+  if (p >= HW) return;
+  for (int s = 0; s < S; ++s) {
+    const float x = coords[(((long)b * S + s) * HW + p) * 2 + 0];
+    const float y = coords[(((long)b * S + s) * HW + p) * 2 + 1];
+    const float fx0 = floorf(x), fy0 = floorf(y);
+    const float dx = x - fx0, dy = y - fy0;
+    const int xi0 = (int)fx0, yi0 = (int)fy0;
+    const float* G = grad + (((long)b * S + s) * RD * RD) * HW + p;
+    for (int iy = 0; iy < NT; ++iy) {
+      for (int ix = 0; ix < NT; ++ix) {
+        const int h2 = yi0 - R + iy, w2 = xi0 - R + ix;
+        if (h2 < 0 || h2 >= H2 || w2 < 0 || w2 >= W2) continue;
+        float g = 0.f;
+        if (iy > 0 && ix > 0) g += G[(long)((iy - 1) + RD * (ix - 1)) * HW] * dy * dx;
+        if (iy > 0 && ix < RD) g += G[(long)((iy - 1) + RD * ix) * HW] * dy * (1 - dx);
+        if (iy < RD && ix > 0) g += G[(long)(iy + RD * (ix - 1)) * HW] * (1 - dy) * dx;
+        if (iy < RD && ix < RD) g += G[(long)(iy + RD * ix) * HW] * (1 - dy) * (1 - dx);
+        if (g == 0.f) continue;
+        const float* f2 = fmap2 + (((long)b * H2 + h2) * W2 + w2) * C;
+        const float* f1 = fmap1 + ((long)b * HW + p) * C;
+        float* d1 = g1 + ((long)b * HW + p) * C;
+        float* d2 = g2 + (((long)b * H2 + h2) * W2 + w2) * C;
+        for (int c = 0; c < C; ++c) {
+          d1[c] += g * f2[c];
+          atomicAdd(d2 + c, g * f1[c]);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace droid
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+using namespace droid;
+
+extern "C" {
+
+// dtype codes: 0 = fp16, 1 = fp32, 2 = fp64
+int droid_corr_index_forward(int dtype, const void* volume, const float* coords, void* corr,
+                             int B, int H, int W, int H2, int W2, int radius, hipStream_t stream) {
+  if (B < 0 || H <= 0 || W <= 0 || H2 <= 0 || W2 <= 0 || radius < 0 || radius > 7)
+    return fail(kInvalidArgument, "corr_index_forward: bad shape or radius (0..7)");
+  if (B == 0) return kOk;
+  const int rd = 2 * radius + 1;
+  const long bstride = (long)rd * rd * H * W;
+  dim3 grid(ceil_div(H * W, 256), B);
+  switch (dtype) {
+    case 0: corr_index_fwd_kernel<__half><<<grid, 256, 0, stream>>>((const __half*)volume, coords, 0, 1.0f, (__half*)corr, bstride, B, H, W, H2, W2, radius); break;
+    case 1: corr_index_fwd_kernel<float><<<grid, 256, 0, stream>>>((const float*)volume, coords, 0, 1.0f, (float*)corr, bstride, B, H, W, H2, W2, radius); break;
+    case 2: corr_index_fwd_kernel<double><<<grid, 256, 0, stream>>>((const double*)volume, coords, 0, 1.0f, (double*)corr, bstride, B, H, W, H2, W2, radius); break;
+    default: return fail(kUnsupported, "corr_index_forward: dtype must be fp16/fp32/fp64");
+  }
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+int droid_corr_index_backward(int dtype, const float* coords, const void* corr_grad, void* volume_grad,
+                              int B, int H, int W, int H2, int W2, int radius, hipStream_t stream) {
+  if (B < 0 || H <= 0 || W <= 0 || H2 <= 0 || W2 <= 0 || radius < 0)
+    return fail(kInvalidArgument, "corr_index_backward: bad shape");
+  if (B == 0) return kOk;
+  dim3 grid(ceil_div(H * W, 256), B);
+  switch (dtype) {
+    case 0: corr_index_bwd_kernel<__half><<<grid, 256, 0, stream>>>(coords, (const __half*)corr_grad, (__half*)volume_grad, B, H, W, H2, W2, radius); break;
+    case 1: corr_index_bwd_kernel<float><<<grid, 256, 0, stream>>>(coords, (const float*)corr_grad, (float*)volume_grad, B, H, W, H2, W2, radius); break;
+    case 2: corr_index_bwd_kernel<double><<<grid, 256, 0, stream>>>(coords, (const double*)corr_grad, (double*)volume_grad, B, H, W, H2, W2, radius); break;
+    default: return fail(kUnsupported, "corr_index_backward: dtype must be fp16/fp32/fp64");
+  }
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+int droid_corr_pyramid_lookup(int dtype, const void* const* levels, const int* H2s, const int* W2s,
+                              int num_levels, const float* coords, void* out,
+                              int E, int H, int W, int radius, hipStream_t stream) {
+  if (num_levels < 1 || num_levels > 4 || E < 0 || H <= 0 || W <= 0 || radius < 0 || radius > 7)
+    return fail(kInvalidArgument, "corr_pyramid_lookup: bad arguments");
+  if (E == 0) return kOk;
+  const int rd = 2 * radius + 1;
+  bool fast = (dtype == 0 && radius == 3);
+  for (int l = 0; l < num_levels; ++l) {
+    if (H2s[l] <= 0 || W2s[l] <= 0) return fail(kInvalidArgument, "corr_pyramid_lookup: empty level");
+    if (W2s[l] % 8 != 0 || (reinterpret_cast<uintptr_t>(levels[l]) & 15u)) fast = false;
+  }
+  dim3 grid(ceil_div(H * W, 256), E);
+  if (fast) {
+    PyramidArgs a;
+    for (int l = 0; l < 4; ++l) {
+      a.vol[l] = (const __half*)levels[l < num_levels ? l : 0];
+      a.H2[l] = H2s[l < num_levels ? l : 0];
+      a.W2[l] = W2s[l < num_levels ? l : 0];
+    }
+    a.levels = num_levels;
+    corr_pyramid_f16_r3_kernel<<<grid, 256, 0, stream>>>(a, coords, (__half*)out, H, W);
+    DROID_LAUNCH_CHECK();
+    return kOk;
+  }
+  const long bstride = (long)num_levels * rd * rd * H * W;
+  for (int l = 0; l < num_levels; ++l) {
+    const float scale = 1.0f / (float)(1 << l);
+    const long off = (long)l * rd * rd * H * W;
+    switch (dtype) {
+      case 0: corr_index_fwd_kernel<__half><<<grid, 256, 0, stream>>>((const __half*)levels[l], coords, 1, scale, (__half*)out + off, bstride, E, H, W, H2s[l], W2s[l], radius); break;
+      case 1: corr_index_fwd_kernel<float><<<grid, 256, 0, stream>>>((const float*)levels[l], coords, 1, scale, (float*)out + off, bstride, E, H, W, H2s[l], W2s[l], radius); break;
+      case 2: corr_index_fwd_kernel<double><<<grid, 256, 0, stream>>>((const double*)levels[l], coords, 1, scale, (double*)out + off, bstride, E, H, W, H2s[l], W2s[l], radius); break;
+      default: return fail(kUnsupported, "corr_pyramid_lookup: dtype must be fp16/fp32/fp64");
+    }
+    DROID_LAUNCH_CHECK();
+  }
+  return kOk;
+}
+
+int droid_altcorr_forward(int dtype, const void* fmap1, const void* fmap2, const float* coords,
+                          void* corr, int B, int S, int H, int W, int H2, int W2, int C,
+                          int radius, hipStream_t stream) {
+  if (radius != 3) return fail(kUnsupported, "altcorr_forward: only radius 3 is implemented");
+  if (B < 0 || S <= 0 || H <= 0 || W <= 0 || H2 <= 0 || W2 <= 0 || C <= 0)
+    return fail(kInvalidArgument, "altcorr_forward: bad shape");
+  if (B == 0) return kOk;
+  dim3 grid(ceil_div(H * W, 64), S, B);
+  switch (dtype) {
+    case 0: altcorr_fwd_kernel<__half><<<grid, 64, 0, stream>>>((const __half*)fmap1, (const __half*)fmap2, coords, (__half*)corr, B, S, H, W, H2, W2, C); break;
+    case 1: altcorr_fwd_kernel<float><<<grid, 64, 0, stream>>>((const float*)fmap1, (const float*)fmap2, coords, (float*)corr, B, S, H, W, H2, W2, C); break;
+    default: return fail(kUnsupported, "altcorr_forward: dtype must be fp16/fp32");
+  }
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+int droid_altcorr_backward(const float* fmap1, const float* fmap2, const float* coords,
+                           const float* corr_grad, float* fmap1_grad, float* fmap2_grad,
+                           int B, int S, int H, int W, int H2, int W2, int C, int radius,
+                           hipStream_t stream) {
+  if (radius != 3) return fail(kUnsupported, "altcorr_backward: only radius 3 is implemented");
+  if (B == 0) return kOk;
+  dim3 grid(ceil_div(H * W, 64), 1, B);
+  altcorr_bwd_kernel<<<grid, 64, 0, stream>>>(fmap1, fmap2, coords, corr_grad, fmap1_grad, fmap2_grad,
+                                             B, S, H, W, H2, W2, C);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+}  // extern "C"

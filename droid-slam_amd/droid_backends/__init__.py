@@ -1,0 +1,347 @@
+"""MI355X-native drop-in for the reference's `droid_backends` C extension.
+
+Same module name, the same 9 functions and argument conventions as
+/root/reference/src/droid.cpp:237-250, so `modules/corr.py`, `depth_video.py`
+and `factor_graph.py` can import it unchanged.  Every call validates
+contiguity like the reference (`RuntimeError: x must be contiguous`,
+droid.cpp:84-85), then calls the hand-written gfx950 kernels of
+libdroid_hip.so through its C ABI (include/droid_backends.h) on the caller's
+current HIP stream.  There is no CPU fallback: host tensors raise.
+
+Extensions beyond the reference surface (used by the MI355X-native host
+mirror in `droid_mi355x`): `corr_pyramid_lookup`, `projective_transform`,
+`BaPlan`, and optional host copies of ii/jj for `ba` (avoids the D2H sync).
+"""
+import ctypes
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from ._lib import EXPORTS, check, lib
+
+__all__ = ["ba", "frame_distance", "projmap", "depth_filter", "iproj", "altcorr_forward",
+           "altcorr_backward", "corr_index_forward", "corr_index_backward",
+           "corr_pyramid_lookup", "projective_transform", "BaPlan", "EXPORTS"]
+
+_DTYPES = {torch.float16: 0, torch.float32: 1, torch.float64: 2}
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _check_inputs(names, tensors):
+    dev = None
+    for name, t in zip(names, tensors):
+        if not isinstance(t, torch.Tensor):
+            raise TypeError("%s must be a torch.Tensor" % name)
+        if not t.is_contiguous():
+            raise RuntimeError("%s must be contiguous" % name)
+        if t.device.type != "cuda":
+            raise RuntimeError("droid_backends: %s must be a HIP device tensor (no CPU path)" % name)
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError("droid_backends: all tensors must be on one device")
+    return dev
+
+
+def _need(t, dtype, name):
+    if t.dtype != dtype:
+        raise RuntimeError("%s must be %s (got %s)" % (name, dtype, t.dtype))
+
+
+# ---------------------------------------------------------------------------
+# correlation
+# ---------------------------------------------------------------------------
+def corr_index_forward(volume, coords, radius):
+    """correlation_kernels.cu:126-155: volume (B,H,W,H2,W2), coords (B,2,H,W)
+    -> [corr (B,2r+1,2r+1,H,W)] in volume's dtype."""
+    _check_inputs(("volume", "coords"), (volume, coords))
+    _need(coords, torch.float32, "coords")
+    if volume.dtype not in _DTYPES:
+        raise RuntimeError("volume must be float16/float32/float64")
+    B, H, W, H2, W2 = volume.shape
+    rd = 2 * radius + 1
+    corr = torch.empty((B, rd, rd, H, W), dtype=volume.dtype, device=volume.device)
+    with torch.cuda.device(volume.device):
+        check(lib.droid_corr_index_forward(_DTYPES[volume.dtype], _ptr(volume), _ptr(coords), _ptr(corr),
+                                           B, H, W, H2, W2, int(radius), _stream(volume)),
+              "corr_index_forward")
+    return [corr]
+
+
+def corr_index_backward(volume, coords, corr_grad, radius):
+    """correlation_kernels.cu:157-185 -> [volume_grad]."""
+    _check_inputs(("volume", "coords", "corr_grad"), (volume, coords, corr_grad))
+    B, H, W, H2, W2 = volume.shape
+    if corr_grad.dtype != volume.dtype:
+        raise RuntimeError("corr_grad must have the volume's dtype")
+    grad = torch.zeros_like(volume)
+    with torch.cuda.device(volume.device):
+        check(lib.droid_corr_index_backward(_DTYPES[volume.dtype], _ptr(coords), _ptr(corr_grad),
+                                            _ptr(grad), B, H, W, H2, W2, int(radius), _stream(volume)),
+              "corr_index_backward")
+    return [grad]
+
+
+def corr_pyramid_lookup(levels, coords, radius, out=None):
+    """All levels of CorrBlock.__call__ (modules/corr.py:40-50) in one launch.
+
+    levels: list of (E,H,W,H2_l,W2_l) volumes; coords (E,H,W,2) f32 at level-0
+    scale -> (E, L*(2r+1)^2, H, W)."""
+    _check_inputs(["level%d" % i for i in range(len(levels))] + ["coords"], list(levels) + [coords])
+    _need(coords, torch.float32, "coords")
+    E, H, W = levels[0].shape[:3]
+    dt = levels[0].dtype
+    L = len(levels)
+    rd = 2 * radius + 1
+    if out is None:
+        out = torch.empty((E, L * rd * rd, H, W), dtype=dt, device=coords.device)
+    ptrs = (ctypes.c_void_p * L)(*[lv.data_ptr() for lv in levels])
+    h2s = (ctypes.c_int * L)(*[lv.shape[3] for lv in levels])
+    w2s = (ctypes.c_int * L)(*[lv.shape[4] for lv in levels])
+    with torch.cuda.device(coords.device):
+        check(lib.droid_corr_pyramid_lookup(_DTYPES[dt], ptrs, h2s, w2s, L, _ptr(coords), _ptr(out),
+                                            E, H, W, int(radius), _stream(coords)),
+              "corr_pyramid_lookup")
+    return out
+
+
+def altcorr_forward(fmap1, fmap2, coords, radius):
+    """altcorr_kernel.cu:290-319: fmap1 (B,H,W,C), fmap2 (B,H2,W2,C),
+    coords (B,S,H,W,2) -> [corr (B,S,(2r+1)^2,H,W)]."""
+    _check_inputs(("fmap1", "fmap2", "coords"), (fmap1, fmap2, coords))
+    _need(coords, torch.float32, "coords")
+    if fmap1.dtype not in (torch.float16, torch.float32) or fmap2.dtype != fmap1.dtype:
+        raise RuntimeError("fmaps must both be float16 or float32")
+    B, H, W, C = fmap1.shape
+    _, H2, W2, _ = fmap2.shape
+    S = coords.shape[1]
+    rd = 2 * radius + 1
+    corr = torch.empty((B, S, rd * rd, H, W), dtype=fmap1.dtype, device=fmap1.device)
+    with torch.cuda.device(fmap1.device):
+        check(lib.droid_altcorr_forward(_DTYPES[fmap1.dtype], _ptr(fmap1), _ptr(fmap2), _ptr(coords),
+                                        _ptr(corr), B, S, H, W, H2, W2, C, int(radius), _stream(fmap1)),
+              "altcorr_forward")
+    return [corr]
+
+
+def altcorr_backward(fmap1, fmap2, coords, corr_grad, radius):
+    """altcorr_kernel.cu:321-356 (fp32) -> [fmap1_grad, fmap2_grad, coords_grad(=0)]."""
+    _check_inputs(("fmap1", "fmap2", "coords", "corr_grad"), (fmap1, fmap2, coords, corr_grad))
+    for n, t in (("fmap1", fmap1), ("fmap2", fmap2), ("coords", coords), ("corr_grad", corr_grad)):
+        _need(t, torch.float32, n)
+    B, H, W, C = fmap1.shape
+    _, H2, W2, _ = fmap2.shape
+    S = coords.shape[1]
+    g1 = torch.zeros_like(fmap1)
+    g2 = torch.zeros_like(fmap2)
+    gc = torch.zeros((B, S, H, W, 2), dtype=fmap1.dtype, device=fmap1.device)
+    with torch.cuda.device(fmap1.device):
+        check(lib.droid_altcorr_backward(_ptr(fmap1), _ptr(fmap2), _ptr(coords), _ptr(corr_grad),
+                                         _ptr(g1), _ptr(g2), B, S, H, W, H2, W2, C, int(radius),
+                                         _stream(fmap1)), "altcorr_backward")
+    return [g1, g2, gc]
+
+
+# ---------------------------------------------------------------------------
+# geometry
+# ---------------------------------------------------------------------------
+def projective_transform(poses, disps, intrinsics, ii, jj, target=None, with_valid=True):
+    """pops.projective_transform semantics (projective_ops.py:96-125), lietorch-free.
+
+    poses (N,7), disps (N,H,W), intrinsics (N,4), ii/jj (E) int64 ->
+    coords (E,H,W,2), valid (E,H,W,1) or None, and - when `target` (E,H,W,2)
+    is given - the clamped update() motion features motn (E,4,H,W)."""
+    args = [poses, disps, intrinsics, ii, jj] + ([target] if target is not None else [])
+    _check_inputs(("poses", "disps", "intrinsics", "ii", "jj", "target")[:len(args)], args)
+    for n, t in (("poses", poses), ("disps", disps), ("intrinsics", intrinsics)):
+        _need(t, torch.float32, n)
+    _need(ii, torch.int64, "ii")
+    _need(jj, torch.int64, "jj")
+    E = ii.shape[0]
+    _, H, W = disps.shape
+    coords = torch.empty((E, H, W, 2), dtype=torch.float32, device=poses.device)
+    valid = torch.empty((E, H, W, 1), dtype=torch.float32, device=poses.device) if with_valid else None
+    motn = None
+    if target is not None:
+        _need(target, torch.float32, "target")
+        motn = torch.empty((E, 4, H, W), dtype=torch.float32, device=poses.device)
+    with torch.cuda.device(poses.device):
+        check(lib.droid_projective_transform(_ptr(poses), _ptr(disps), _ptr(intrinsics), _ptr(ii), _ptr(jj),
+                                             E, H, W, _ptr(coords), _ptr(valid), _ptr(target), _ptr(motn),
+                                             _stream(poses)), "projective_transform")
+    if target is not None:
+        return coords, valid, motn
+    return coords, valid
+
+
+def frame_distance(poses, disps, intrinsics, ii, jj, beta):
+    """droid_kernels.cu:1438-1460 -> dist (E)."""
+    _check_inputs(("poses", "disps", "intrinsics", "ii", "jj"), (poses, disps, intrinsics, ii, jj))
+    E = ii.shape[0]
+    _, H, W = disps.shape
+    dist = torch.zeros((E,), dtype=torch.float32, device=poses.device)
+    with torch.cuda.device(poses.device):
+        check(lib.droid_frame_distance(_ptr(poses), _ptr(disps), _ptr(intrinsics), _ptr(ii), _ptr(jj),
+                                       E, H, W, float(beta), _ptr(dist), _stream(poses)), "frame_distance")
+    return dist
+
+
+def projmap(poses, disps, intrinsics, ii, jj):
+    """droid_kernels.cu:1463-1488 -> [coords (E,H,W,3), valid (E,H,W,1)]."""
+    _check_inputs(("poses", "disps", "intrinsics", "ii", "jj"), (poses, disps, intrinsics, ii, jj))
+    E = ii.shape[0]
+    _, H, W = disps.shape
+    coords = torch.empty((E, H, W, 3), dtype=torch.float32, device=poses.device)
+    valid = torch.empty((E, H, W, 1), dtype=torch.float32, device=poses.device)
+    with torch.cuda.device(poses.device):
+        check(lib.droid_projmap(_ptr(poses), _ptr(disps), _ptr(intrinsics), _ptr(ii), _ptr(jj), E, H, W,
+                                _ptr(coords), _ptr(valid), _stream(poses)), "projmap")
+    return [coords, valid]
+
+
+def iproj(poses, disps, intrinsics):
+    """droid_kernels.cu:1518-1541 -> points (N,H,W,3)."""
+    _check_inputs(("poses", "disps", "intrinsics"), (poses, disps, intrinsics))
+    N, H, W = disps.shape
+    pts = torch.empty((N, H, W, 3), dtype=torch.float32, device=poses.device)
+    with torch.cuda.device(poses.device):
+        check(lib.droid_iproj(_ptr(poses), _ptr(disps), _ptr(intrinsics), N, H, W, _ptr(pts), _stream(poses)),
+              "iproj")
+    return pts
+
+
+def depth_filter(poses, disps, intrinsics, ix, thresh):
+    """droid_kernels.cu:1491-1515 -> counter (n,H,W)."""
+    _check_inputs(("poses", "disps", "intrinsics", "ix", "thresh"), (poses, disps, intrinsics, ix, thresh))
+    num, H, W = disps.shape
+    n = ix.shape[0]
+    counter = torch.empty((n, H, W), dtype=torch.float32, device=poses.device)
+    with torch.cuda.device(poses.device):
+        check(lib.droid_depth_filter(_ptr(poses), _ptr(disps), _ptr(intrinsics), _ptr(ix), _ptr(thresh),
+                                     n, num, H, W, _ptr(counter), _stream(poses)), "depth_filter")
+    return counter
+
+
+# ---------------------------------------------------------------------------
+# dense bundle adjustment
+# ---------------------------------------------------------------------------
+class BaPlan:
+    """Host-built structure of one ba() call plus its device workspace.
+
+    Built from host copies of ii/jj (no device sync), uploaded once; reused by
+    every ba() with the same edge set.  `own` = (lo, hi) restricts the depth
+    rows to poses owned by this rank (edge-sharded multi-GPU BA)."""
+
+    def __init__(self, ii, jj, num_frames, ht, wd, t0, t1, eta_rows, motion_only, device, own=None):
+        ii = np.ascontiguousarray(np.asarray(ii, dtype=np.int64))
+        jj = np.ascontiguousarray(np.asarray(jj, dtype=np.int64))
+        lo, hi = own if own is not None else (0, 2 ** 31 - 1)
+        h = ctypes.c_void_p()
+        check(lib.droid_ba_plan_create(ii.ctypes.data_as(ctypes.c_void_p), jj.ctypes.data_as(ctypes.c_void_p),
+                                       len(ii), int(num_frames), int(ht), int(wd), int(t0), int(t1),
+                                       int(eta_rows), int(bool(motion_only)), int(lo), int(hi),
+                                       ctypes.byref(h)), "ba plan")
+        self._h = h
+        self.device = torch.device(device)
+        self.t0, self.t1, self.motion_only = int(t0), int(t1), bool(motion_only)
+        K, P, nblk, nbm = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib.droid_ba_plan_info(h, ctypes.byref(K), ctypes.byref(P), ctypes.byref(nblk), ctypes.byref(nbm)),
+              "ba plan info")
+        self.K, self.P, self.nblocks, self.nb_max = K.value, P.value, nblk.value, nbm.value
+        kx = np.zeros(max(self.K, 1), dtype=np.int64)
+        check(lib.droid_ba_plan_kx(h, kx.ctypes.data_as(ctypes.c_void_p)), "ba plan kx")
+        self.kx = kx[:self.K]
+        nbytes = lib.droid_ba_plan_workspace_bytes(h)
+        self.workspace = torch.empty((nbytes,), dtype=torch.uint8, device=self.device)
+        off, sz = ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib.droid_ba_plan_system_region(h, ctypes.byref(off), ctypes.byref(sz)), "ba plan region")
+        self.n = 6 * self.P
+        self.system = self.workspace[off.value:off.value + sz.value].view(torch.float64).view(self.n + 1, self.n + 1)
+        with torch.cuda.device(self.device):
+            check(lib.droid_ba_plan_upload(h, _ptr(self.workspace), _stream(self.workspace)), "ba plan upload")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.droid_ba_plan_destroy(h)
+            self._h = None
+
+    def build_system(self, poses, disps, intrinsics, disps_sens, targets, weights, eta):
+        check(lib.droid_ba_build_system(self._h, _ptr(self.workspace), _ptr(poses), _ptr(disps), _ptr(intrinsics),
+                                        _ptr(disps_sens), _ptr(targets), _ptr(weights), _ptr(eta),
+                                        _stream(poses)), "ba build_system")
+
+    def solve_update(self, poses, disps, intrinsics, disps_sens, targets, weights, eta, lm, ep, dx, dz):
+        check(lib.droid_ba_solve_update(self._h, _ptr(self.workspace), _ptr(poses), _ptr(disps), _ptr(intrinsics),
+                                        _ptr(disps_sens), _ptr(targets), _ptr(weights), _ptr(eta),
+                                        float(lm), float(ep), _ptr(dx), _ptr(dz), _stream(poses)),
+              "ba solve_update")
+
+    def run(self, poses, disps, intrinsics, disps_sens, targets, weights, eta, iterations, lm, ep):
+        dx = torch.empty((self.P, 6), dtype=torch.float32, device=poses.device)
+        dz = None if self.motion_only else torch.empty((self.K, disps.shape[1] * disps.shape[2]),
+                                                      dtype=torch.float32, device=poses.device)
+        if iterations <= 0:
+            return dx.zero_(), dz
+        with torch.cuda.device(poses.device):
+            check(lib.droid_ba_run(self._h, _ptr(self.workspace), _ptr(poses), _ptr(disps), _ptr(intrinsics),
+                                   _ptr(disps_sens), _ptr(targets), _ptr(weights), _ptr(eta), int(iterations),
+                                   float(lm), float(ep), _ptr(dx), _ptr(dz), _stream(poses)), "ba")
+        return dx, dz
+
+
+_PLAN_CACHE = OrderedDict()
+_PLAN_CACHE_SIZE = 8
+
+
+def get_plan(ii_host, jj_host, num_frames, ht, wd, t0, t1, eta_rows, motion_only, device, own=None):
+    ii_host = np.ascontiguousarray(np.asarray(ii_host, dtype=np.int64))
+    jj_host = np.ascontiguousarray(np.asarray(jj_host, dtype=np.int64))
+    key = (ii_host.tobytes(), jj_host.tobytes(), int(num_frames), int(ht), int(wd), int(t0), int(t1),
+           int(eta_rows), bool(motion_only), str(device), own)
+    plan = _PLAN_CACHE.get(key)
+    if plan is None:
+        plan = BaPlan(ii_host, jj_host, num_frames, ht, wd, t0, t1, eta_rows, motion_only, device, own)
+        _PLAN_CACHE[key] = plan
+        while len(_PLAN_CACHE) > _PLAN_CACHE_SIZE:
+            _PLAN_CACHE.popitem(last=False)
+    else:
+        _PLAN_CACHE.move_to_end(key)
+    return plan
+
+
+def ba(poses, disps, intrinsics, disps_sens, targets, weights, eta, ii, jj, t0, t1, iterations, lm, ep,
+       motion_only, ii_host=None, jj_host=None):
+    """droid.cpp:88-117 / ba_cuda: dense BA over poses [t0,t1) and the disparity
+    maps of unique([t0,t1) U ii); mutates poses/disps in place and returns
+    [dx (P,6), dz (K,H*W) or None if motion_only].
+
+    ii_host/jj_host (numpy) are an optional extension: with them no device ->
+    host copy of the edge list is needed (the reference copies it every call)."""
+    _check_inputs(("targets", "weights", "poses", "disps", "intrinsics", "disps_sens", "ii", "jj", "eta"),
+                  (targets, weights, poses, disps, intrinsics, disps_sens, ii, jj, eta))
+    for n, t in (("poses", poses), ("disps", disps), ("intrinsics", intrinsics), ("disps_sens", disps_sens),
+                 ("targets", targets), ("weights", weights), ("eta", eta)):
+        _need(t, torch.float32, n)
+    _need(ii, torch.int64, "ii")
+    _need(jj, torch.int64, "jj")
+    N, H, W = disps.shape
+    E = ii.shape[0]
+    if targets.shape != (E, 2, H, W) or weights.shape != (E, 2, H, W):
+        raise RuntimeError("targets/weights must be (E,2,H,W)")
+    if ii_host is None:
+        ii_host = ii.cpu().numpy()
+    if jj_host is None:
+        jj_host = jj.cpu().numpy()
+    eta_rows = eta.numel() // (H * W) if eta.numel() else 0
+    plan = get_plan(ii_host, jj_host, N, H, W, int(t0), int(t1), eta_rows, motion_only, poses.device)
+    dx, dz = plan.run(poses, disps, intrinsics, disps_sens, targets, weights, eta, int(iterations), lm, ep)
+    return [dx, dz]

@@ -1,0 +1,60 @@
+"""ctypes binding of libdroid_hip.so (declarations mirror include/droid_backends.h)."""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads torch's HIP runtime first; the library shares it)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdroid_hip.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        "droid_backends: HIP library %s is missing - run `python -c \"import __graft_entry__ as g; "
+        "g.build()\"` (or `make -C droid-slam_amd/csrc`) first" % LIB_PATH)
+
+lib = ctypes.CDLL(LIB_PATH)
+
+_p = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+_sz = ctypes.c_size_t
+
+_SIGS = {
+    "droid_last_error": ([], ctypes.c_char_p),
+    "droid_abi_version": ([], _i),
+    "droid_device_count": ([], _i),
+    "droid_corr_index_forward": ([_i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p], _i),
+    "droid_corr_index_backward": ([_i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p], _i),
+    "droid_corr_pyramid_lookup": ([_i, _p, _p, _p, _i, _p, _p, _i, _i, _i, _i, _p], _i),
+    "droid_altcorr_forward": ([_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p], _i),
+    "droid_altcorr_backward": ([_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p], _i),
+    "droid_projective_transform": ([_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p], _i),
+    "droid_frame_distance": ([_p, _p, _p, _p, _p, _i, _i, _i, _f, _p, _p], _i),
+    "droid_projmap": ([_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p], _i),
+    "droid_iproj": ([_p, _p, _p, _i, _i, _i, _p, _p], _i),
+    "droid_depth_filter": ([_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p], _i),
+    "droid_ba_plan_create": ([_p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, ctypes.POINTER(_p)], _i),
+    "droid_ba_plan_destroy": ([_p], None),
+    "droid_ba_plan_workspace_bytes": ([_p], _sz),
+    "droid_ba_plan_info": ([_p, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),
+                            ctypes.POINTER(_i)], _i),
+    "droid_ba_plan_kx": ([_p, _p], _i),
+    "droid_ba_plan_system_region": ([_p, ctypes.POINTER(_sz), ctypes.POINTER(_sz)], _i),
+    "droid_ba_plan_upload": ([_p, _p, _p], _i),
+    "droid_ba_build_system": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _p], _i),
+    "droid_ba_solve_update": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p], _i),
+    "droid_ba_run": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _f, _f, _p, _p, _p], _i),
+}
+
+EXPORTS = tuple(_SIGS)
+
+for _name, (_args, _res) in _SIGS.items():
+    _fn = getattr(lib, _name)
+    _fn.argtypes = _args
+    _fn.restype = _res
+
+
+def check(status, what):
+    if status != 0:
+        msg = lib.droid_last_error().decode("utf-8", "replace")
+        raise RuntimeError("%s failed (status %d): %s" % (what, status, msg))

@@ -1,0 +1,128 @@
+"""Correlation blocks (mirror of modules/corr.py) on the HIP kernels.
+
+CorrBlock keeps the reference's volume pyramid layout (E, H, W, H/2^i, W/2^i)
+built by a batched GEMM (hipBLASLt) + avg-pool, exactly as corr.py:24-38,
+63-71; its lookup runs all 4 levels in ONE kernel launch and writes the
+concatenated (B, N, 196, H, W) tensor directly (corr.py:40-50 does 4 launches
++ cat).  Under autograd it falls back to the per-level CorrSampler so the
+backward kernel is used (training path).
+"""
+import torch
+import torch.nn.functional as F
+
+import droid_backends
+
+
+class CorrSampler(torch.autograd.Function):
+    """corr.py:6-20."""
+
+    @staticmethod
+    def forward(ctx, volume, coords, radius):
+        ctx.save_for_backward(volume, coords)
+        ctx.radius = radius
+        corr, = droid_backends.corr_index_forward(volume, coords, radius)
+        return corr
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        volume, coords = ctx.saved_tensors
+        grad_volume, = droid_backends.corr_index_backward(volume, coords, grad_output.contiguous(), ctx.radius)
+        return grad_volume, None, None
+
+
+class CorrBlock:
+    """corr.py:23-71 (volume correlation pyramid)."""
+
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=3):
+        self.num_levels = num_levels
+        self.radius = radius
+        self.corr_pyramid = []
+        vol = CorrBlock.corr(fmap1, fmap2)
+        batch, num, h1, w1, h2, w2 = vol.shape
+        vol = vol.reshape(batch * num * h1 * w1, 1, h2, w2)
+        for i in range(num_levels):
+            self.corr_pyramid.append(vol.view(batch * num, h1, w1, h2 // 2 ** i, w2 // 2 ** i))
+            if i + 1 < num_levels:
+                vol = F.avg_pool2d(vol, 2, stride=2)
+
+    def __call__(self, coords):
+        batch, num, ht, wd, _ = coords.shape
+        if torch.is_grad_enabled() and any(v.requires_grad for v in self.corr_pyramid):
+            c = coords.permute(0, 1, 4, 2, 3).contiguous().view(batch * num, 2, ht, wd)
+            out = [CorrSampler.apply(self.corr_pyramid[i], c / 2 ** i, self.radius).view(batch, num, -1, ht, wd)
+                   for i in range(self.num_levels)]
+            return torch.cat(out, dim=2)
+        c = coords.reshape(batch * num, ht, wd, 2).float().contiguous()
+        out = droid_backends.corr_pyramid_lookup(self.corr_pyramid, c, self.radius)
+        return out.view(batch, num, -1, ht, wd)
+
+    def cat(self, other):
+        for i in range(self.num_levels):
+            self.corr_pyramid[i] = torch.cat([self.corr_pyramid[i], other.corr_pyramid[i]], 0)
+        return self
+
+    def __getitem__(self, index):
+        for i in range(self.num_levels):
+            self.corr_pyramid[i] = self.corr_pyramid[i][index]
+        return self
+
+    @staticmethod
+    def corr(fmap1, fmap2):
+        """all-pairs correlation <f1/4, f2/4> (corr.py:63-71)."""
+        batch, num, dim, ht, wd = fmap1.shape
+        f1 = fmap1.reshape(batch * num, dim, ht * wd) / 4.0
+        f2 = fmap2.reshape(batch * num, dim, ht * wd) / 4.0
+        return torch.matmul(f1.transpose(1, 2), f2).view(batch, num, ht, wd, ht, wd)
+
+
+class CorrLayer(torch.autograd.Function):
+    """corr.py:74-88."""
+
+    @staticmethod
+    def forward(ctx, fmap1, fmap2, coords, r):
+        ctx.r = r
+        ctx.save_for_backward(fmap1, fmap2, coords)
+        corr, = droid_backends.altcorr_forward(fmap1, fmap2, coords, r)
+        return corr
+
+    @staticmethod
+    def backward(ctx, grad_corr):
+        fmap1, fmap2, coords = ctx.saved_tensors
+        g1, g2, gc = droid_backends.altcorr_backward(fmap1, fmap2, coords, grad_corr.contiguous(), ctx.r)
+        return g1, g2, gc, None
+
+
+class AltCorrBlock:
+    """corr.py:91-139 (on-the-fly correlation for update_lowmem)."""
+
+    def __init__(self, fmaps, num_levels=4, radius=3):
+        self.num_levels = num_levels
+        self.radius = radius
+        B, N, C, H, W = fmaps.shape
+        f = fmaps.view(B * N, C, H, W) / 4.0
+        self.pyramid = []
+        for i in range(num_levels):
+            self.pyramid.append(f.permute(0, 2, 3, 1).contiguous().view(B, N, H // 2 ** i, W // 2 ** i, C))
+            if i + 1 < num_levels:
+                f = F.avg_pool2d(f, 2, stride=2)
+
+    def corr_fn(self, coords, ii, jj):
+        B, N, H, W, S, _ = coords.shape
+        coords = coords.permute(0, 1, 4, 2, 3, 5)
+        out = []
+        for i in range(self.num_levels):
+            f1 = self.pyramid[0][:, ii].reshape((B * N,) + self.pyramid[0].shape[2:])
+            f2 = self.pyramid[i][:, jj].reshape((B * N,) + self.pyramid[i].shape[2:])
+            ci = (coords / 2 ** i).reshape(B * N, S, H, W, 2).contiguous()
+            corr = CorrLayer.apply(f1.float().contiguous(), f2.float().contiguous(), ci, self.radius)
+            out.append(corr.view(B, N, S, -1, H, W).permute(0, 1, 3, 4, 5, 2))
+        return torch.cat(out, dim=2)
+
+    def __call__(self, coords, ii, jj):
+        squeeze = coords.dim() == 5
+        if squeeze:
+            coords = coords.unsqueeze(dim=-2)
+        corr = self.corr_fn(coords, ii, jj)
+        if squeeze:
+            corr = corr.squeeze(dim=-1)
+        return corr.contiguous()

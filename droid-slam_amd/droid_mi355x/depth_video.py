@@ -1,0 +1,189 @@
+"""Keyframe state buffers (mirror of droid_slam/depth_video.py).
+
+Same buffers and methods as the reference DepthVideo (depth_video.py:12-193)
+for the parts the update path touches: poses/disps/disps_sens/intrinsics,
+fmaps/nets/inps, `reproject`, `distance`, `ba`, `normalize`, `upsample`.
+Geometry is lietorch-free: `reproject` calls the fused HIP projective-transform
+kernel.  Buffers live in HBM; torch.multiprocessing sharing (the reference's
+visualiser process) is out of scope.
+"""
+import threading
+
+import numpy as np
+import torch
+
+import droid_backends
+
+from .update import cvx_upsample
+
+
+class _Counter:
+    """Stand-in for multiprocessing.Value('i') with its lock."""
+
+    def __init__(self):
+        self.value = 0
+        self._lock = threading.RLock()
+
+    def get_lock(self):
+        return self._lock
+
+
+class DepthVideo:
+    def __init__(self, image_size=(480, 640), buffer=1024, stereo=False, device="cuda:0"):
+        self.counter = _Counter()
+        self.ready = _Counter()
+        self.ht = ht = image_size[0]
+        self.wd = wd = image_size[1]
+        self.device = torch.device(device)
+        dev = self.device
+        self.tstamp = torch.zeros(buffer, device=dev, dtype=torch.float)
+        self.images = torch.zeros(buffer, 3, ht, wd, device=dev, dtype=torch.uint8)
+        self.dirty = torch.zeros(buffer, device=dev, dtype=torch.bool)
+        self.red = torch.zeros(buffer, device=dev, dtype=torch.bool)
+        self.poses = torch.zeros(buffer, 7, device=dev, dtype=torch.float)
+        self.disps = torch.ones(buffer, ht // 8, wd // 8, device=dev, dtype=torch.float)
+        self.disps_sens = torch.zeros(buffer, ht // 8, wd // 8, device=dev, dtype=torch.float)
+        self.disps_up = torch.zeros(buffer, ht, wd, device=dev, dtype=torch.float)
+        self.intrinsics = torch.zeros(buffer, 4, device=dev, dtype=torch.float)
+        self.stereo = stereo
+        c = 2 if stereo else 1
+        self.fmaps = torch.zeros(buffer, c, 128, ht // 8, wd // 8, dtype=torch.half, device=dev)
+        self.nets = torch.zeros(buffer, 128, ht // 8, wd // 8, dtype=torch.half, device=dev)
+        self.inps = torch.zeros(buffer, 128, ht // 8, wd // 8, dtype=torch.half, device=dev)
+        self.poses[:] = torch.as_tensor([0, 0, 0, 0, 0, 0, 1], dtype=torch.float, device=dev)
+
+    def get_lock(self):
+        return self.counter.get_lock()
+
+    def __item_setter(self, index, item):
+        if isinstance(index, int) and index >= self.counter.value:
+            self.counter.value = index + 1
+        elif isinstance(index, torch.Tensor) and index.max().item() > self.counter.value:
+            self.counter.value = index.max().item() + 1
+        self.tstamp[index] = item[0]
+        self.images[index] = item[1]
+        if item[2] is not None:
+            self.poses[index] = item[2]
+        if item[3] is not None:
+            self.disps[index] = item[3]
+        if item[4] is not None:
+            depth = item[4][3::8, 3::8]
+            self.disps_sens[index] = torch.where(depth > 0, 1.0 / depth, depth)
+        if item[5] is not None:
+            self.intrinsics[index] = item[5]
+        if len(item) > 6:
+            self.fmaps[index] = item[6]
+        if len(item) > 7:
+            self.nets[index] = item[7]
+        if len(item) > 8:
+            self.inps[index] = item[8]
+
+    def __setitem__(self, index, item):
+        with self.get_lock():
+            self.__item_setter(index, item)
+
+    def __getitem__(self, index):
+        with self.get_lock():
+            if isinstance(index, int) and index < 0:
+                index = self.counter.value + index
+            return (self.poses[index], self.disps[index], self.intrinsics[index],
+                    self.fmaps[index], self.nets[index], self.inps[index])
+
+    def append(self, *item):
+        with self.get_lock():
+            self.__item_setter(self.counter.value, item)
+
+    @staticmethod
+    def format_indicies(ii, jj, device="cuda"):
+        if not isinstance(ii, torch.Tensor):
+            ii = torch.as_tensor(ii)
+        if not isinstance(jj, torch.Tensor):
+            jj = torch.as_tensor(jj)
+        return (ii.to(device=device, dtype=torch.long).reshape(-1),
+                jj.to(device=device, dtype=torch.long).reshape(-1))
+
+    def upsample(self, ix, mask):
+        disps_up = cvx_upsample(self.disps[ix].unsqueeze(-1), mask)
+        self.disps_up[ix] = disps_up.squeeze()
+
+    def normalize(self):
+        with self.get_lock():
+            n = self.counter.value
+            s = self.disps[:n].mean()
+            self.disps[:n] /= s
+            self.poses[:n, :3] *= s
+            self.dirty[:n] = True
+
+    def reproject(self, ii, jj, target=None):
+        """project pixels of ii into jj (depth_video.py:139-147) -> coords
+        (1,E,H,W,2), valid (1,E,H,W,1) [, motion features (1,E,4,H,W) if target]."""
+        ii, jj = DepthVideo.format_indicies(ii, jj, self.device)
+        out = droid_backends.projective_transform(self.poses, self.disps, self.intrinsics, ii, jj,
+                                                  target=None if target is None else target.reshape(
+                                                      -1, self.ht // 8, self.wd // 8, 2).contiguous())
+        return tuple(o.unsqueeze(0) for o in out)
+
+    def distance(self, ii=None, jj=None, beta=0.3, bidirectional=True):
+        """frame distance metric (depth_video.py:149-179)."""
+        return_matrix = False
+        N = self.counter.value
+        if ii is None:
+            return_matrix = True
+            ii, jj = torch.meshgrid(torch.arange(N), torch.arange(N), indexing="ij")
+        ii, jj = DepthVideo.format_indicies(ii, jj, self.device)
+        if bidirectional:
+            poses = self.poses[:N].clone()
+            d1 = droid_backends.frame_distance(poses, self.disps, self.intrinsics[0].contiguous(), ii, jj, beta)
+            d2 = droid_backends.frame_distance(poses, self.disps, self.intrinsics[0].contiguous(), jj, ii, beta)
+            d = 0.5 * (d1 + d2)
+        else:
+            d = droid_backends.frame_distance(self.poses, self.disps, self.intrinsics[0].contiguous(), ii, jj, beta)
+        if return_matrix:
+            return d.reshape(N, N)
+        return d
+
+    def ba(self, target, weight, eta, ii, jj, t0=1, t1=None, itrs=2, lm=1e-4, ep=0.1, motion_only=False,
+           ii_host=None, jj_host=None, comm=None):
+        """dense bundle adjustment (depth_video.py:181-193).
+
+        comm (edge-sharded multi-GPU): dict(group=process group, own=(lo, hi),
+        t1=global t1).  Each rank passes only the edges whose source frame it
+        owns; the reduced camera system is summed with one all-reduce per
+        Gauss-Newton iteration and solved identically on every rank."""
+        with self.get_lock():
+            if ii_host is None:
+                ii_host = ii.cpu().numpy()
+            if jj_host is None:
+                jj_host = jj.cpu().numpy()
+            if comm is not None and comm.get("t1") is not None and t1 is None:
+                t1 = comm["t1"]
+            if t1 is None:
+                t1 = int(max(np.max(ii_host), np.max(jj_host))) + 1
+            intr = self.intrinsics[0].contiguous()
+            if comm is None:
+                out = droid_backends.ba(self.poses, self.disps, intr, self.disps_sens, target, weight, eta, ii, jj,
+                                        t0, t1, itrs, lm, ep, motion_only, ii_host=ii_host, jj_host=jj_host)
+            else:
+                out = ba_sharded(self.poses, self.disps, intr, self.disps_sens, target, weight, eta, ii_host,
+                                 jj_host, t0, t1, itrs, lm, ep, motion_only, comm)
+            self.disps.clamp_(min=0.001)
+            return out
+
+
+def ba_sharded(poses, disps, intrinsics, disps_sens, target, weight, eta, ii_host, jj_host, t0, t1, itrs, lm, ep,
+               motion_only, comm):
+    """One rank of the edge-sharded BA: local linearisation + Schur terms,
+    all_reduce(SUM) of the augmented reduced system (RCCL over xGMI), then the
+    same damped fp64 Cholesky on every rank; dz only for owned frames."""
+    import torch.distributed as dist
+    N, H, W = disps.shape
+    eta_rows = eta.numel() // (H * W)
+    plan = droid_backends.get_plan(ii_host, jj_host, N, H, W, int(t0), int(t1), eta_rows, motion_only,
+                                   poses.device, own=tuple(comm["own"]))
+    dx = torch.empty((plan.P, 6), dtype=torch.float32, device=poses.device)
+    dz = None if motion_only else torch.empty((plan.K, H * W), dtype=torch.float32, device=poses.device)
+    for _ in range(itrs):
+        plan.build_system(poses, disps, intrinsics, disps_sens, target, weight, eta)
+        dist.all_reduce(plan.system, op=dist.ReduceOp.SUM, group=comm.get("group"))
+        plan.solve_update(poses, disps, intrinsics, disps_sens, target, weight, eta, lm, ep, dx, dz)
+    return [dx, dz]

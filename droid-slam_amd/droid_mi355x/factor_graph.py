@@ -1,0 +1,321 @@
+"""Frame graph + recurrent update (mirror of droid_slam/factor_graph.py).
+
+Interface and semantics follow the reference FactorGraph
+(factor_graph.py:11-369): edges (ii, jj) with per-edge state net/inp/corr/
+target/weight/age, an inactive edge store, `update()` (the hot path,
+:196-242) and `update_lowmem()` (:245-290).  Differences are in how, not
+what: the edge list is mirrored on the host (numpy) so t0, unique(ii),
+scatter indices and the BA plan never need a device->host sync; the motion
+features come out of the fused reprojection kernel; the correlation lookup
+is one kernel for all levels; BA runs fully on the GPU.
+"""
+import numpy as np
+import torch
+
+import droid_backends
+
+from .corr import AltCorrBlock, CorrBlock
+
+
+def _coords_grid(ht, wd, device):
+    y, x = torch.meshgrid(torch.arange(ht, device=device, dtype=torch.float),
+                          torch.arange(wd, device=device, dtype=torch.float), indexing="ij")
+    return torch.stack([x, y], dim=-1)
+
+
+class FactorGraph:
+    def __init__(self, video, update_op, device="cuda:0", corr_impl="volume", max_factors=-1):
+        self.video = video
+        self.update_op = update_op
+        self.device = torch.device(device)
+        self.max_factors = max_factors
+        self.corr_impl = corr_impl
+        self.ht = ht = video.ht // 8
+        self.wd = wd = video.wd // 8
+        self.coords0 = _coords_grid(ht, wd, self.device)
+        self._ii = np.zeros(0, np.int64)   # host mirrors of the edge list
+        self._jj = np.zeros(0, np.int64)
+        self._ii_inac = np.zeros(0, np.int64)
+        self._jj_inac = np.zeros(0, np.int64)
+        self._ii_bad = np.zeros(0, np.int64)
+        self._jj_bad = np.zeros(0, np.int64)
+        self.age = torch.zeros(0, dtype=torch.long, device=self.device)
+        self.corr, self.net, self.inp = None, None, None
+        self.damping = 1e-6 * torch.ones_like(self.video.disps)
+        self.target = torch.zeros([1, 0, ht, wd, 2], device=self.device, dtype=torch.float)
+        self.weight = torch.zeros([1, 0, ht, wd, 2], device=self.device, dtype=torch.float)
+        self.target_inac = torch.zeros([1, 0, ht, wd, 2], device=self.device, dtype=torch.float)
+        self.weight_inac = torch.zeros([1, 0, ht, wd, 2], device=self.device, dtype=torch.float)
+        self._dev_cache = {}
+        self.comm = None  # set for edge-sharded multi-GPU: dict(group, own=(lo,hi), t0, t1)
+
+    # -- edge-list views ------------------------------------------------------
+    def _dev(self, name, arr):
+        key = (name, arr.tobytes())
+        t = self._dev_cache.get(name)
+        if t is None or t[0] != key:
+            t = (key, torch.as_tensor(arr, dtype=torch.long).to(self.device, non_blocking=True))
+            self._dev_cache[name] = t
+        return t[1]
+
+    @property
+    def ii(self):
+        return self._dev("ii", self._ii)
+
+    @property
+    def jj(self):
+        return self._dev("jj", self._jj)
+
+    @property
+    def ii_inac(self):
+        return self._dev("ii_inac", self._ii_inac)
+
+    @property
+    def jj_inac(self):
+        return self._dev("jj_inac", self._jj_inac)
+
+    @staticmethod
+    def _host(x):
+        if isinstance(x, torch.Tensor):
+            return x.detach().to("cpu", torch.long).numpy().reshape(-1)
+        return np.asarray(x, dtype=np.int64).reshape(-1)
+
+    # -- graph edits (factor_graph.py:43-193) ---------------------------------
+    def _filter_repeated(self, ii, jj):
+        seen = set(zip(self._ii.tolist(), self._jj.tolist())) | set(zip(self._ii_inac.tolist(),
+                                                                      self._jj_inac.tolist()))
+        keep = np.array([(a, b) not in seen for a, b in zip(ii.tolist(), jj.tolist())], dtype=bool)
+        return ii[keep], jj[keep]
+
+    def print_edges(self):
+        order = np.argsort(self._ii, kind="stable")
+        w = torch.mean(self.weight, dim=[0, 2, 3, 4]).cpu().numpy()
+        for e in zip(self._ii[order], self._jj[order], w[order]):
+            print(e)
+        print()
+
+    def filter_edges(self):
+        conf = torch.mean(self.weight, dim=[0, 2, 3, 4]).cpu().numpy()
+        mask = (np.abs(self._ii - self._jj) > 2) & (conf < 0.001)
+        self._ii_bad = np.concatenate([self._ii_bad, self._ii[mask]])
+        self._jj_bad = np.concatenate([self._jj_bad, self._jj[mask]])
+        self.rm_factors(mask, store=False)
+
+    def clear_edges(self):
+        self.rm_factors(np.ones(len(self._ii), dtype=bool))
+        self.net = None
+        self.inp = None
+
+    def add_factors(self, ii, jj, remove=False):
+        ii, jj = self._filter_repeated(self._host(ii), self._host(jj))
+        if ii.shape[0] == 0:
+            return
+        if (self.max_factors > 0 and len(self._ii) + len(ii) > self.max_factors
+                and self.corr is not None and remove):
+            # factor_graph.py:105-106 masks POSITION k by argsort(age)[k] (kept literally)
+            order = np.argsort(self.age.cpu().numpy(), kind="stable")
+            self.rm_factors(order >= self.max_factors - len(ii), store=True)
+
+        dii = torch.as_tensor(ii, device=self.device)
+        djj = torch.as_tensor(jj, device=self.device)
+        net = self.video.nets[dii].to(self.device).unsqueeze(0)
+        if self.corr_impl == "volume":
+            c = torch.as_tensor((ii == jj).astype(np.int64), device=self.device)
+            fmap1 = self.video.fmaps[dii, 0].to(self.device).unsqueeze(0)
+            fmap2 = self.video.fmaps[djj, c].to(self.device).unsqueeze(0)
+            corr = CorrBlock(fmap1, fmap2)
+            self.corr = corr if self.corr is None else self.corr.cat(corr)
+            inp = self.video.inps[dii].to(self.device).unsqueeze(0)
+            self.inp = inp if self.inp is None else torch.cat([self.inp, inp], 1)
+
+        target, _ = self.video.reproject(dii, djj)
+        weight = torch.zeros_like(target)
+        self._ii = np.concatenate([self._ii, ii])
+        self._jj = np.concatenate([self._jj, jj])
+        self.age = torch.cat([self.age, torch.zeros_like(dii)], 0)
+        self.net = net if self.net is None else torch.cat([self.net, net], 1)
+        self.target = torch.cat([self.target, target], 1)
+        self.weight = torch.cat([self.weight, weight], 1)
+
+    def rm_factors(self, mask, store=False):
+        mask = np.asarray(mask, dtype=bool)
+        keep = ~mask
+        dmask = torch.as_tensor(mask, device=self.device)
+        dkeep = ~dmask
+        if store:
+            self._ii_inac = np.concatenate([self._ii_inac, self._ii[mask]])
+            self._jj_inac = np.concatenate([self._jj_inac, self._jj[mask]])
+            self.target_inac = torch.cat([self.target_inac, self.target[:, dmask]], 1)
+            self.weight_inac = torch.cat([self.weight_inac, self.weight[:, dmask]], 1)
+        self._ii = self._ii[keep]
+        self._jj = self._jj[keep]
+        self.age = self.age[dkeep]
+        if self.corr_impl == "volume" and self.corr is not None:
+            self.corr = self.corr[dkeep]
+        if self.net is not None:
+            self.net = self.net[:, dkeep]
+        if self.inp is not None:
+            self.inp = self.inp[:, dkeep]
+        self.target = self.target[:, dkeep]
+        self.weight = self.weight[:, dkeep]
+
+    def rm_keyframe(self, ix):
+        v = self.video
+        with v.get_lock():
+            for buf in (v.images, v.poses, v.disps, v.disps_sens, v.intrinsics, v.nets, v.inps, v.fmaps):
+                buf[ix] = buf[ix + 1]
+        m = (self._ii_inac == ix) | (self._jj_inac == ix)
+        self._ii_inac = np.where(self._ii_inac >= ix, self._ii_inac - 1, self._ii_inac)
+        self._jj_inac = np.where(self._jj_inac >= ix, self._jj_inac - 1, self._jj_inac)
+        if m.any():
+            dm = torch.as_tensor(~m, device=self.device)
+            self._ii_inac = self._ii_inac[~m]
+            self._jj_inac = self._jj_inac[~m]
+            self.target_inac = self.target_inac[:, dm]
+            self.weight_inac = self.weight_inac[:, dm]
+        m = (self._ii == ix) | (self._jj == ix)
+        self._ii = np.where(self._ii >= ix, self._ii - 1, self._ii)
+        self._jj = np.where(self._jj >= ix, self._jj - 1, self._jj)
+        self.rm_factors(m, store=False)
+
+    # -- the hot path (factor_graph.py:196-242) -------------------------------
+    def update(self, t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, motion_only=False):
+        ht, wd = self.ht, self.wd
+        E = len(self._ii)
+        ii, jj = self.ii, self.jj
+        with torch.autocast("cuda", enabled=False):
+            coords1, _, motn = droid_backends.projective_transform(
+                self.video.poses, self.video.disps, self.video.intrinsics, ii, jj,
+                target=self.target.view(E, ht, wd, 2), with_valid=False)
+            coords1 = coords1.view(1, E, ht, wd, 2)
+            motn = motn.view(1, E, 4, ht, wd)
+
+        corr = self.corr(coords1)
+        uniq, inverse = np.unique(self._ii, return_inverse=True)
+        dinv = self._dev("inverse", inverse.astype(np.int64))
+        with torch.autocast("cuda", enabled=True):
+            self.net, delta, weight, damping, upmask = self.update_op(
+                self.net, self.inp, corr, motn, ii, jj, inverse=dinv, num_unique=len(uniq))
+
+        if t0 is None:
+            t0 = self.comm["t0"] if self.comm is not None else max(1, int(self._ii.min()) + 1)
+
+        with torch.autocast("cuda", enabled=False):
+            self.target = coords1 + delta.to(dtype=torch.float)
+            self.weight = weight.to(dtype=torch.float)
+            self.damping[self._dev("uniq", uniq)] = damping[0].to(torch.float)
+
+            if use_inactive:
+                m = (self._ii_inac >= t0 - 3) & (self._jj_inac >= t0 - 3)
+                dm = torch.as_tensor(m, device=self.device)
+                ii_h = np.concatenate([self._ii_inac[m], self._ii])
+                jj_h = np.concatenate([self._jj_inac[m], self._jj])
+                target = torch.cat([self.target_inac[:, dm], self.target], 1)
+                weight = torch.cat([self.weight_inac[:, dm], self.weight], 1)
+            else:
+                ii_h, jj_h, target, weight = self._ii, self._jj, self.target, self.weight
+
+            uniq_ba = np.unique(ii_h)
+            damping = 0.2 * self.damping[self._dev("uniq_ba", uniq_ba)].contiguous() + EP
+            target = target.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
+            weight = weight.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
+            self.video.ba(target, weight, damping, self._dev("ii_ba", ii_h), self._dev("jj_ba", jj_h),
+                          t0, t1, itrs=itrs, lm=1e-4, ep=0.1, motion_only=motion_only,
+                          ii_host=ii_h, jj_host=jj_h, comm=self.comm)
+        self.age += 1
+
+    def update_lowmem(self, t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, steps=8):
+        """factor_graph.py:245-290: alternate (on-the-fly) correlation, chunks of 8 sources."""
+        t = self.video.counter.value
+        num, rig, ch, ht, wd = self.video.fmaps.shape
+        corr_op = AltCorrBlock(self.video.fmaps.view(1, num * rig, ch, ht, wd))
+        E = len(self._ii)
+        for _ in range(steps):
+            with torch.autocast("cuda", enabled=False):
+                coords1, _, motn = droid_backends.projective_transform(
+                    self.video.poses, self.video.disps, self.video.intrinsics, self.ii, self.jj,
+                    target=self.target.view(E, ht, wd, 2), with_valid=False)
+                coords1 = coords1.view(1, E, ht, wd, 2)
+                motn = motn.view(1, E, 4, ht, wd)
+            s = 8
+            for i in range(0, int(self._jj.max()) + 1, s):
+                vh = (self._ii >= i) & (self._ii < i + s)
+                if not vh.any():
+                    continue
+                v = torch.as_tensor(vh, device=self.device)
+                iis_h, jjs_h = self._ii[vh], self._jj[vh]
+                iis = torch.as_tensor(iis_h, device=self.device)
+                jjs = torch.as_tensor(jjs_h, device=self.device)
+                src = torch.as_tensor(rig * iis_h, device=self.device)
+                dst = torch.as_tensor(rig * jjs_h + (iis_h == jjs_h), device=self.device)
+                corr1 = corr_op(coords1[:, v], src, dst)
+                uq, inv = np.unique(iis_h, return_inverse=True)
+                with torch.autocast("cuda", enabled=True):
+                    net, delta, weight, damping, _ = self.update_op(
+                        self.net[:, v], self.video.inps[None, iis], corr1, motn[:, v], iis, jjs,
+                        inverse=torch.as_tensor(inv, device=self.device), num_unique=len(uq))
+                self.net[:, v] = net
+                self.target[:, v] = coords1[:, v] + delta.float()
+                self.weight[:, v] = weight.float()
+                self.damping[torch.as_tensor(uq, device=self.device)] = damping[0].float()
+            damping = 0.2 * self.damping[self._dev("uniq_all", np.unique(self._ii))].contiguous() + EP
+            target = self.target.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
+            weight = self.weight.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
+            self.video.ba(target, weight, damping, self.ii, self.jj, 1, t, itrs=itrs, lm=1e-5, ep=1e-2,
+                          motion_only=False, ii_host=self._ii, jj_host=self._jj)
+            self.video.dirty[:t] = True
+
+    # -- edge construction (factor_graph.py:292-369) --------------------------
+    def add_neighborhood_factors(self, t0, t1, r=3):
+        ii, jj = np.meshgrid(np.arange(t0, t1), np.arange(t0, t1), indexing="ij")
+        ii, jj = ii.reshape(-1), jj.reshape(-1)
+        c = 1 if self.video.stereo else 0
+        keep = (np.abs(ii - jj) > c) & (np.abs(ii - jj) <= r)
+        self.add_factors(ii[keep], jj[keep])
+
+    def add_proximity_factors(self, t0=0, t1=0, rad=2, nms=2, beta=0.25, thresh=16.0, remove=False):
+        t = self.video.counter.value
+        ix = np.arange(t0, t)
+        jx = np.arange(t1, t)
+        ii, jj = np.meshgrid(ix, jx, indexing="ij")
+        ii, jj = ii.reshape(-1), jj.reshape(-1)
+        d = self.video.distance(ii, jj, beta=beta).cpu().numpy().astype(np.float64)
+        d[ii - rad < jj] = np.inf
+        d[d > 100] = np.inf
+        ncol = t - t1
+
+        def suppress(i, j):
+            lim = max(min(abs(i - j) - 2, nms), 0)
+            for di in range(-nms, nms + 1):
+                for dj in range(-nms, nms + 1):
+                    if abs(di) + abs(dj) <= lim:
+                        i1, j1 = i + di, j + dj
+                        if t0 <= i1 < t and t1 <= j1 < t:
+                            d[(i1 - t0) * ncol + (j1 - t1)] = np.inf
+
+        for i, j in zip(np.concatenate([self._ii, self._ii_bad, self._ii_inac]).tolist(),
+                        np.concatenate([self._jj, self._jj_bad, self._jj_inac]).tolist()):
+            suppress(i, j)
+
+        es = []
+        for i in range(t0, t):
+            if self.video.stereo:
+                es.append((i, i))
+                d[(i - t0) * ncol + (i - t1)] = np.inf
+            for j in range(max(i - rad - 1, 0), i):
+                es.append((i, j))
+                es.append((j, i))
+                d[(i - t0) * ncol + (j - t1)] = np.inf
+
+        for k in np.argsort(d, kind="stable"):
+            if d[k] > thresh:
+                continue
+            if len(es) > self.max_factors:
+                break
+            i, j = int(ii[k]), int(jj[k])
+            es.append((i, j))
+            es.append((j, i))
+            suppress(i, j)
+
+        es = np.asarray(es, dtype=np.int64).reshape(-1, 2)
+        self.add_factors(es[:, 0], es[:, 1], remove)

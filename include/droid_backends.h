@@ -1,0 +1,152 @@
+/*
+ * droid_backends.h — C ABI of the MI355X-native replacement for the
+ * reference's `droid_backends` CUDA extension (src/droid.cpp:237-250).
+ *
+ * Library: droid-slam_amd/lib/libdroid_hip.so (hipcc --offload-arch=gfx950).
+ * All pointers are DEVICE pointers unless marked "host"; every tensor is
+ * dense row-major (C-contiguous) in the layout the reference uses.  Calls are
+ * asynchronous on `stream` (a hipStream_t; pass the caller's current stream).
+ * Every function returns 0 on success, non-zero on error; the message is in
+ * droid_last_error() (thread local).  No torch types cross this boundary.
+ */
+#ifndef DROID_BACKENDS_H
+#define DROID_BACKENDS_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define DROID_OK 0
+#define DROID_INVALID_ARGUMENT 1
+#define DROID_UNSUPPORTED 2
+#define DROID_HIP_ERROR 3
+
+/* dtype codes for the correlation entry points */
+#define DROID_F16 0
+#define DROID_F32 1
+#define DROID_F64 2
+
+const char* droid_last_error(void);
+int droid_abi_version(void);
+int droid_device_count(void);
+
+/* ---- correlation -------------------------------------------------------- */
+
+/* replaces corr_index_forward  (src/droid.cpp:170-178, correlation_kernels.cu:126-155)
+ * volume (B,H,W,H2,W2) dtype, coords (B,2,H,W) f32 -> corr (B,2r+1,2r+1,H,W) dtype.
+ * corr[:,i,j] = bilinear sample at (x0-r+i, y0-r+j), zero outside; fp16 is
+ * bit-exact with the reference's at::Half arithmetic. */
+int droid_corr_index_forward(int dtype, const void* volume, const float* coords, void* corr,
+                             int B, int H, int W, int H2, int W2, int radius, hipStream_t stream);
+
+/* replaces corr_index_backward (src/droid.cpp:180-191, correlation_kernels.cu:157-185)
+ * volume_grad must be zero-initialised (B,H,W,H2,W2). */
+int droid_corr_index_backward(int dtype, const float* coords, const void* corr_grad,
+                              void* volume_grad, int B, int H, int W, int H2, int W2, int radius,
+                              hipStream_t stream);
+
+/* CorrBlock.__call__ (modules/corr.py:40-50) for all pyramid levels in one launch:
+ * levels[l] (E,H,W,H2s[l],W2s[l]), coords (E,H,W,2) f32 at level-0 scale
+ * -> out (E, num_levels*(2r+1)^2, H, W), identical to cat of per-level lookups. */
+int droid_corr_pyramid_lookup(int dtype, const void* const* levels, const int* H2s, const int* W2s,
+                              int num_levels, const float* coords, void* out, int E, int H, int W,
+                              int radius, hipStream_t stream);
+
+/* replaces altcorr_forward (src/droid.cpp:193-203, altcorr_kernel.cu:290-319)
+ * fmap1 (B,H,W,C), fmap2 (B,H2,W2,C) dtype (f16|f32), coords (B,S,H,W,2) f32
+ * -> corr (B,S,(2r+1)^2,H,W) dtype.  radius must be 3. */
+int droid_altcorr_forward(int dtype, const void* fmap1, const void* fmap2, const float* coords,
+                          void* corr, int B, int S, int H, int W, int H2, int W2, int C, int radius,
+                          hipStream_t stream);
+
+/* replaces altcorr_backward (src/droid.cpp:205-217, altcorr_kernel.cu:321-356), f32 only.
+ * fmap1_grad/fmap2_grad must be zero-initialised; coords grad is identically 0. */
+int droid_altcorr_backward(const float* fmap1, const float* fmap2, const float* coords,
+                           const float* corr_grad, float* fmap1_grad, float* fmap2_grad, int B,
+                           int S, int H, int W, int H2, int W2, int C, int radius,
+                           hipStream_t stream);
+
+/* ---- geometry ----------------------------------------------------------- */
+
+/* DepthVideo.reproject -> pops.projective_transform (depth_video.py:139-147,
+ * projective_ops.py:96-125), optionally fused with the update() motion
+ * features (factor_graph.py:202-204):
+ * poses (N,7), disps (N,H,W), intrinsics (N,4), ii/jj (E) int64
+ * -> coords (E,H,W,2), valid (E,H,W) [nullable],
+ *    motn (E,4,H,W) = clamp([coords-grid, target-coords], +-64) [nullable; needs target (E,H,W,2)]. */
+int droid_projective_transform(const float* poses, const float* disps, const float* intrinsics,
+                               const int64_t* ii, const int64_t* jj, int E, int H, int W,
+                               float* coords, float* valid, const float* target, float* motn,
+                               hipStream_t stream);
+
+/* replaces frame_distance (src/droid.cpp:120-136, droid_kernels.cu:1438-1460) -> dist (E) */
+int droid_frame_distance(const float* poses, const float* disps, const float* intrinsics,
+                         const int64_t* ii, const int64_t* jj, int E, int H, int W, float beta,
+                         float* dist, hipStream_t stream);
+
+/* replaces projmap (src/droid.cpp:139-154, droid_kernels.cu:1463-1488)
+ * -> coords (E,H,W,3), valid (E,H,W,1) */
+int droid_projmap(const float* poses, const float* disps, const float* intrinsics,
+                  const int64_t* ii, const int64_t* jj, int E, int H, int W, float* coords,
+                  float* valid, hipStream_t stream);
+
+/* replaces iproj (src/droid.cpp:157-166, droid_kernels.cu:1518-1541) -> points (N,H,W,3) */
+int droid_iproj(const float* poses, const float* disps, const float* intrinsics, int N, int H,
+                int W, float* points, hipStream_t stream);
+
+/* replaces depth_filter (src/droid.cpp:220-234, droid_kernels.cu:1491-1515)
+ * ix (n) int64, thresh (n) f32, disps (num,H,W) -> counter (n,H,W) */
+int droid_depth_filter(const float* poses, const float* disps, const float* intrinsics,
+                       const int64_t* ix, const float* thresh, int n, int num, int H, int W,
+                       float* counter, hipStream_t stream);
+
+/* ---- dense bundle adjustment -------------------------------------------
+ * replaces ba (src/droid.cpp:88-117 -> ba_cuda droid_kernels.cu:1314-1434).
+ *
+ * A plan captures everything of one ba() call that depends only on the edge
+ * list (kx = unique([t0,t1) U ii), per-frame edge lists, Schur row graph and
+ * the assembly lists of the reduced camera system).  Build it on the host
+ * from host copies of ii/jj, upload it once into a caller-allocated device
+ * workspace, then run any number of solves with no host synchronisation.
+ * own_lo/own_hi restrict which optimised poses get a depth row on this rank
+ * (edge-sharded multi-GPU BA); pass 0 / INT32_MAX for a single device. */
+int droid_ba_plan_create(const int64_t* ii_host, const int64_t* jj_host, int num_edges,
+                         int num_frames, int ht, int wd, int t0, int t1, int eta_rows,
+                         int motion_only, int own_lo, int own_hi, void** plan_out);
+void droid_ba_plan_destroy(void* plan);
+size_t droid_ba_plan_workspace_bytes(const void* plan);
+int droid_ba_plan_info(const void* plan, int* K, int* P, int* nblocks, int* nb_max);
+int droid_ba_plan_kx(const void* plan, int64_t* kx_host);
+/* the augmented (6P+1)^2 fp64 reduced system (rhs = last row) inside the workspace */
+int droid_ba_plan_system_region(const void* plan, size_t* offset, size_t* bytes);
+int droid_ba_plan_upload(void* plan, void* workspace, hipStream_t stream);
+
+/* one GN linearisation -> reduced system in the workspace (all-reduce it here for multi-GPU) */
+int droid_ba_build_system(void* plan, void* workspace, float* poses, float* disps,
+                          const float* intrinsics, const float* disps_sens, const float* targets,
+                          const float* weights, const float* eta, hipStream_t stream);
+/* damping (diag += ep + lm*diag), fp64 Cholesky (dx = 0 on failure), back
+ * substitution of dz (skipping pose t0 as the reference does), retraction of
+ * poses [t0,t1) and of disps[kx] in place.  dz may be NULL when motion_only. */
+int droid_ba_solve_update(void* plan, void* workspace, float* poses, float* disps,
+                          const float* intrinsics, const float* disps_sens, const float* targets,
+                          const float* weights, const float* eta, float lm, float ep, float* dx,
+                          float* dz, hipStream_t stream);
+/* `iterations` x (build_system + solve_update): droid_backends.ba on one device.
+ * poses (N,7) f32, disps (N,H,W) f32 mutated in place; intrinsics (4); disps_sens (N,H,W);
+ * targets/weights (E,2,H,W); eta (K or 1,H,W); dx (P,6) and dz (K,H*W) outputs. */
+int droid_ba_run(void* plan, void* workspace, float* poses, float* disps, const float* intrinsics,
+                 const float* disps_sens, const float* targets, const float* weights,
+                 const float* eta, int iterations, float lm, float ep, float* dx, float* dz,
+                 hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DROID_BACKENDS_H */

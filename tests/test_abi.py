@@ -1,0 +1,81 @@
+"""The C-ABI library loads on a GPU-less host and exports every entry point
+include/droid_backends.h declares; host-only plan construction works (no
+device calls are made here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    text = open(os.path.join(ROOT, "include", "droid_backends.h")).read()
+    return sorted(set(re.findall(r"\b(droid_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_header():
+    import droid_backends
+    from droid_backends import _lib
+    syms = _header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(_lib.lib, s), s
+    assert set(syms) == set(_lib.EXPORTS)
+    assert _lib.lib.droid_abi_version() == 1
+    for name in ("ba", "frame_distance", "projmap", "depth_filter", "iproj", "altcorr_forward",
+                 "altcorr_backward", "corr_index_forward", "corr_index_backward"):
+        assert callable(getattr(droid_backends, name))
+
+
+def _plan(ii, jj, N=6, H=4, W=6, t0=1, t1=5, eta_rows=None, motion_only=0, own=(0, 2 ** 31 - 1)):
+    from droid_backends._lib import lib
+    ii = np.ascontiguousarray(ii, dtype=np.int64)
+    jj = np.ascontiguousarray(jj, dtype=np.int64)
+    if eta_rows is None:
+        eta_rows = len(np.unique(np.concatenate([np.arange(t0, t1), ii])))
+    h = ctypes.c_void_p()
+    st = lib.droid_ba_plan_create(ii.ctypes.data_as(ctypes.c_void_p), jj.ctypes.data_as(ctypes.c_void_p),
+                                  len(ii), N, H, W, t0, t1, eta_rows, motion_only, own[0], own[1], ctypes.byref(h))
+    return st, h
+
+
+def test_plan_structure_host_only():
+    from droid_backends._lib import lib
+    ii = np.array([1, 2, 2, 3, 0, 4], np.int64)
+    jj = np.array([2, 1, 3, 2, 1, 3], np.int64)
+    st, h = _plan(ii, jj)
+    assert st == 0, lib.droid_last_error()
+    K, P, nb, nbm = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    assert lib.droid_ba_plan_info(h, ctypes.byref(K), ctypes.byref(P), ctypes.byref(nb), ctypes.byref(nbm)) == 0
+    assert (K.value, P.value) == (5, 4)        # kx = {0,1,2,3,4}, poses [1,5)
+    kx = np.zeros(5, np.int64)
+    lib.droid_ba_plan_kx(h, kx.ctypes.data_as(ctypes.c_void_p))
+    np.testing.assert_array_equal(kx, [0, 1, 2, 3, 4])
+    assert lib.droid_ba_plan_workspace_bytes(h) > 0
+    lib.droid_ba_plan_destroy(h)
+
+
+def test_plan_errors_like_reference():
+    from droid_backends._lib import lib
+    ii = np.array([1, 2], np.int64)
+    jj = np.array([2, 1], np.int64)
+    st, _ = _plan(ii, jj, eta_rows=7)          # eta rows != len(kx): reference raises a size mismatch
+    assert st != 0 and b"eta" in lib.droid_last_error()
+    st, _ = _plan(ii, np.array([2, 9], np.int64))
+    assert st != 0 and b"out of range" in lib.droid_last_error()
+    st, _ = _plan(ii, jj, t0=3, t1=3)
+    assert st != 0
+
+
+def test_python_layer_rejects_host_tensors():
+    import torch
+    import droid_backends
+    vol = torch.zeros(1, 2, 2, 4, 4)
+    coords = torch.zeros(1, 2, 2, 2)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        droid_backends.corr_index_forward(vol, coords, 3)
+    with pytest.raises(RuntimeError, match="contiguous"):
+        droid_backends.corr_index_forward(vol.transpose(3, 4), coords, 3)

@@ -1,0 +1,103 @@
+"""droid_backends.ba on the GPU vs the fp64 oracle restatement of ba_cuda.
+
+Bar (BASELINE.json north_star): dx, dz and the in-place poses/disps within
+1e-4 absolute of the reference semantics on identical inputs."""
+import numpy as np
+import pytest
+import torch
+
+from droid_mi355x import synthetic
+from gpu_util import dev, host
+from oracle import ba as oba
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+KEYS = ("poses", "disps", "intrinsics", "disps_sens", "targets", "weights", "eta", "ii", "jj", "t0", "t1")
+
+
+def run_both(prob, iterations=2, lm=1e-4, ep=0.1, motion_only=False):
+    import droid_backends
+    poses = dev(prob["poses"])
+    disps = dev(prob["disps"])
+    args = [poses, disps, dev(prob["intrinsics"]), dev(prob["disps_sens"]), dev(prob["targets"]),
+            dev(prob["weights"]), dev(prob["eta"]), dev(prob["ii"]), dev(prob["jj"])]
+    dx, dz = droid_backends.ba(*args, prob["t0"], prob["t1"], iterations, lm, ep, motion_only)
+    torch.cuda.synchronize()
+    ref = oba.ba(**{k: prob[k] for k in KEYS}, iterations=iterations, lm=lm, ep=ep, motion_only=motion_only)
+    return dict(dx=host(dx), dz=None if dz is None else host(dz), poses=host(poses), disps=host(disps)), ref
+
+
+def check(got, ref, tol=TOL):
+    np.testing.assert_allclose(got["dx"], ref["dx"], atol=tol, rtol=0)
+    if ref["dz"] is not None:
+        np.testing.assert_allclose(got["dz"], ref["dz"], atol=tol, rtol=0)
+    np.testing.assert_allclose(got["poses"], ref["poses"], atol=tol, rtol=0)
+    np.testing.assert_allclose(got["disps"], ref["disps"], atol=tol, rtol=0)
+
+
+def test_ba_frontend_c2():
+    prob = synthetic.ba_problem("C2")
+    got, ref = run_both(prob)
+    check(got, ref)
+    assert np.abs(ref["dx"]).max() > 1e-4   # non-trivial update
+
+
+@pytest.mark.parametrize("iterations", [1, 3])
+def test_ba_iterations_and_depth_prior(iterations):
+    prob = synthetic.ba_problem("C2", seed=77, sens_fraction=0.3)
+    got, ref = run_both(prob, iterations=iterations)
+    check(got, ref)
+
+
+def test_ba_stereo_edges_and_lowmem_damping():
+    ii, jj = synthetic.c2_edges()
+    ii = np.concatenate([ii, np.arange(8, 16)])
+    jj = np.concatenate([jj, np.arange(8, 16)])
+    prob = synthetic.ba_problem("C2", seed=78, edges=(ii, jj))
+    got, ref = run_both(prob, lm=1e-5, ep=1e-2)
+    check(got, ref)
+
+
+def test_ba_motion_only():
+    prob = synthetic.ba_problem("C2", seed=79)
+    got, ref = run_both(prob, motion_only=True)
+    assert got["dz"] is None
+    check(got, ref)
+
+
+def test_ba_failed_factorisation_gives_zero_dx():
+    prob = synthetic.ba_problem("C2", seed=80)
+    got, ref = run_both(prob, iterations=1, lm=0.0, ep=-1e9)
+    assert not ref["ok"]
+    assert np.all(got["dx"] == 0)
+    check(got, ref)
+
+
+def test_ba_eta_precondition_raises():
+    import droid_backends
+    prob = synthetic.ba_problem("C2", seed=81)
+    with pytest.raises(RuntimeError, match="eta"):
+        droid_backends.ba(dev(prob["poses"]), dev(prob["disps"]), dev(prob["intrinsics"]), dev(prob["disps_sens"]),
+                          dev(prob["targets"]), dev(prob["weights"]), dev(prob["eta"][:-1]), dev(prob["ii"]),
+                          dev(prob["jj"]), prob["t0"], prob["t1"], 2, 1e-4, 0.1, False)
+
+
+def test_ba_global_c3():
+    """256 KF / 2048 edges, t0 = 1 (config C3)."""
+    prob = synthetic.ba_problem("C3")
+    got, ref = run_both(prob, iterations=2, lm=1e-5, ep=1e-2)
+    check(got, ref)
+
+
+def test_ba_plan_reuse_is_deterministic():
+    import droid_backends
+    prob = synthetic.ba_problem("C2", seed=82)
+    outs = []
+    for _ in range(2):
+        poses, disps = dev(prob["poses"]), dev(prob["disps"])
+        dx, dz = droid_backends.ba(poses, disps, dev(prob["intrinsics"]), dev(prob["disps_sens"]),
+                                   dev(prob["targets"]), dev(prob["weights"]), dev(prob["eta"]), dev(prob["ii"]),
+                                   dev(prob["jj"]), prob["t0"], prob["t1"], 2, 1e-4, 0.1, False)
+        outs.append((host(dx), host(dz), host(poses), host(disps)))
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)

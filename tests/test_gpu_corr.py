@@ -1,0 +1,119 @@
+"""HIP correlation kernels vs the CPU oracle (through the C ABI)."""
+import numpy as np
+import pytest
+import torch
+
+from gpu_util import dev, host
+from oracle import corr as oc
+
+pytestmark = pytest.mark.gpu
+
+
+def _coords(rng, B, H, W, H2, W2, spread=3.0):
+    base = np.stack(np.meshgrid(np.arange(W) * W2 / W, np.arange(H) * H2 / H), 0)[None]
+    c = base + rng.normal(0, spread, (B, 2, H, W))
+    c[:, :, 0, 0] = -50.0            # far out of bounds
+    c[:, 0, 0, 1] = W2 - 0.5         # right edge
+    c[:, 1, 1, 0] = -0.25            # top edge
+    return c.astype(np.float32)
+
+
+@pytest.mark.parametrize("dtype", [np.float16, np.float32, np.float64])
+@pytest.mark.parametrize("r", [3, 1])
+def test_corr_index_forward_vs_oracle(dtype, r):
+    import droid_backends
+    rng = np.random.default_rng(11)
+    B, H, W, H2, W2 = 3, 12, 16, 12, 16
+    vol = rng.normal(size=(B, H, W, H2, W2)).astype(dtype)
+    coords = _coords(rng, B, H, W, H2, W2)
+    out, = droid_backends.corr_index_forward(dev(vol), dev(coords), r)
+    ref = oc.corr_index_forward(vol, coords, r)
+    got = host(out)
+    assert got.dtype == ref.dtype and got.shape == ref.shape
+    if dtype == np.float16:
+        np.testing.assert_array_equal(got.view(np.uint16), ref.view(np.uint16))  # bit-exact at::Half semantics
+    else:
+        np.testing.assert_allclose(got, ref, rtol=1e-6 if dtype == np.float32 else 1e-12,
+                                   atol=1e-6 if dtype == np.float32 else 1e-12)
+
+
+def test_pyramid_lookup_bitexact_and_equals_per_level():
+    """the fused 4-level kernel == 4 x corr_index_forward + cat, bit for bit, and == oracle."""
+    import droid_backends
+    from droid_mi355x.corr import CorrBlock
+    rng = np.random.default_rng(12)
+    E, C, H, W = 3, 128, 16, 24
+    f1 = dev(rng.normal(size=(1, E, C, H, W)).astype(np.float16))
+    f2 = dev(rng.normal(size=(1, E, C, H, W)).astype(np.float16))
+    cb = CorrBlock(f1, f2)
+    coords = np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None, None].astype(np.float32)
+    coords = np.repeat(coords, E, axis=1) + rng.normal(0, 2.5, (1, E, H, W, 2)).astype(np.float32)
+    coords[0, 0, 0, 0] = [-40.0, 100.0]
+    with torch.no_grad():
+        fused = cb(dev(coords))
+    c2 = dev(coords).permute(0, 1, 4, 2, 3).reshape(E, 2, H, W).contiguous()
+    per = torch.cat([droid_backends.corr_index_forward(cb.corr_pyramid[i], (c2 / 2 ** i).contiguous(), 3)[0]
+                     .view(1, E, -1, H, W) for i in range(4)], dim=2)
+    np.testing.assert_array_equal(host(fused).view(np.uint16), host(per).view(np.uint16))
+    ref = oc.lookup_pyramid([host(v) for v in cb.corr_pyramid], coords, 3)
+    np.testing.assert_array_equal(host(fused).view(np.uint16), ref.view(np.uint16))
+
+
+def test_corr_index_backward_vs_oracle():
+    import droid_backends
+    rng = np.random.default_rng(13)
+    B, H, W, H2, W2 = 2, 8, 10, 8, 10
+    vol = rng.normal(size=(B, H, W, H2, W2)).astype(np.float32)
+    coords = _coords(rng, B, H, W, H2, W2, 2.0)
+    g = rng.normal(size=(B, 7, 7, H, W)).astype(np.float32)
+    out, = droid_backends.corr_index_backward(dev(vol), dev(coords), dev(g), 3)
+    ref = oc.corr_index_backward(vol, coords, g, 3)
+    np.testing.assert_allclose(host(out), ref, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float16])
+def test_altcorr_forward_vs_oracle(dtype):
+    import droid_backends
+    rng = np.random.default_rng(14)
+    B, S, H, W, H2, W2, C = 2, 1, 12, 16, 6, 8, 64
+    f1 = rng.normal(size=(B, H, W, C)).astype(dtype)
+    f2 = rng.normal(size=(B, H2, W2, C)).astype(dtype)
+    coords = np.stack(np.meshgrid(np.arange(W) / 2, np.arange(H) / 2), -1)[None, None]
+    coords = (np.repeat(np.repeat(coords, B, 0), S, 1) + rng.normal(0, 1.5, (B, S, H, W, 2))).astype(np.float32)
+    out, = droid_backends.altcorr_forward(dev(f1), dev(f2), dev(coords), 3)
+    ref = oc.altcorr_forward(f1, f2, coords, 3)
+    tol = 2e-4 if dtype == np.float32 else 2e-2
+    np.testing.assert_allclose(host(out).astype(np.float64), ref, atol=tol * np.abs(ref).max(), rtol=tol)
+
+
+def test_altcorr_matches_volume_lookup():
+    """alt path == volume path on the same features (level 0, fp32)."""
+    import droid_backends
+    from droid_mi355x.corr import AltCorrBlock, CorrBlock
+    rng = np.random.default_rng(15)
+    C, H, W = 32, 16, 16
+    fm = rng.normal(size=(1, 2, C, H, W)).astype(np.float32)
+    vol = CorrBlock(dev(fm[:, :1]), dev(fm[:, 1:]))
+    alt = AltCorrBlock(dev(fm))
+    coords = (np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None, None]
+              + rng.normal(0, 2, (1, 1, H, W, 2))).astype(np.float32)
+    with torch.no_grad():
+        a = vol(dev(coords))
+        b = alt(dev(coords), torch.tensor([0], device="cuda"), torch.tensor([1], device="cuda"))
+    np.testing.assert_allclose(host(a), host(b), atol=2e-4)
+
+
+def test_altcorr_backward_vs_oracle():
+    import droid_backends
+    rng = np.random.default_rng(16)
+    B, S, H, W, H2, W2, C = 1, 1, 6, 8, 6, 8, 16
+    f1 = rng.normal(size=(B, H, W, C)).astype(np.float32)
+    f2 = rng.normal(size=(B, H2, W2, C)).astype(np.float32)
+    coords = (np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None, None]
+              + rng.normal(0, 1.0, (B, S, H, W, 2))).astype(np.float32)
+    g = rng.normal(size=(B, S, 49, H, W)).astype(np.float32)
+    g1, g2, gc = droid_backends.altcorr_backward(dev(f1), dev(f2), dev(coords), dev(g), 3)
+    r1, r2, rc = oc.altcorr_backward(f1, f2, coords, g, 3)
+    np.testing.assert_allclose(host(g1), r1, atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(host(g2), r2, atol=1e-4, rtol=1e-4)
+    assert np.all(host(gc) == 0)

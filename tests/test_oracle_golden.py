@@ -1,0 +1,127 @@
+"""The CPU oracle against golden vectors produced by the reference's own Python
+(tests/golden/make_golden.py) - this is what pins the oracle."""
+import os
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from fill import det_state_dict
+from oracle import corr as oc
+from oracle import update_module as um
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def test_corr_pyramid_matches_reference(golden_dir):
+    g = _load(golden_dir, "corr_pyramid.npz")
+    pyr = oc.corr_pyramid(g["fmap1"].astype(np.float64), g["fmap2"].astype(np.float64))
+    for i in range(4):
+        ref = g["level%d" % i]
+        assert pyr[i].shape == ref.shape
+        np.testing.assert_allclose(pyr[i], ref, atol=5e-6, rtol=1e-5)
+
+
+def test_alt_pyramid_matches_reference(golden_dir):
+    g = _load(golden_dir, "alt_pyramid.npz")
+    pyr = oc.alt_pyramid(g["fmaps"].astype(np.float64))
+    for i in range(4):
+        np.testing.assert_allclose(pyr[i], g["level%d" % i], atol=1e-6)
+
+
+def test_volume_level_equals_feature_pyramid_dot(golden_dir):
+    """level i of the volume == <f1/4, avgpool^i(f2/4)> (volume and alt paths agree)."""
+    g = _load(golden_dir, "corr_pyramid.npz")
+    f1 = g["fmap1"].astype(np.float64)
+    f2 = g["fmap2"].astype(np.float64)
+    pyr = oc.corr_pyramid(f1, f2)
+    B, N, C, H, W = f1.shape
+    alt2 = oc.alt_pyramid(f2)
+    a1 = oc.alt_pyramid(f1)[0].reshape(B * N, H * W, C)
+    for i in range(4):
+        f2i = alt2[i].reshape(B * N, -1, C)
+        vol = np.einsum("npc,nqc->npq", a1, f2i).reshape(pyr[i].shape)
+        np.testing.assert_allclose(vol, pyr[i], atol=1e-9)
+
+
+def test_update_module_matches_reference(golden_dir):
+    u = _load(golden_dir, "update_module.npz")
+    p = {k: torch.from_numpy(v) for k, v in det_state_dict(um.PARAM_SHAPES).items()}
+    t = lambda k: torch.from_numpy(u[k])
+    out = um.update_module(p, t("net"), t("inp"), t("corr"), t("flow"), t("ii"), t("jj"))
+    for name, o in zip(["net_out", "delta", "weight", "eta", "upmask"], out):
+        np.testing.assert_allclose(o.numpy(), u[name], atol=1e-5, rtol=1e-5)
+
+
+def test_convgru_and_upsample_match_reference(golden_dir):
+    c = _load(golden_dir, "convgru.npz")
+    shapes = {}
+    for n in ("convz", "convr", "convq"):
+        shapes[n + ".weight"] = (16, 40, 3, 3)
+        shapes[n + ".bias"] = (16,)
+    for n in ("w", "convz_glo", "convr_glo", "convq_glo"):
+        shapes[n + ".weight"] = (16, 16, 1, 1)
+        shapes[n + ".bias"] = (16,)
+    p = {k: torch.from_numpy(v) for k, v in det_state_dict(shapes).items()}
+    o = um.conv_gru(p, "", torch.from_numpy(c["h"]), torch.from_numpy(c["x1"]), torch.from_numpy(c["x2"]))
+    np.testing.assert_allclose(o.numpy(), c["out"], atol=1e-6)
+    cu = _load(golden_dir, "cvx_upsample.npz")
+    up = um.cvx_upsample(torch.from_numpy(cu["data"]), torch.from_numpy(cu["mask"]))
+    np.testing.assert_allclose(up.numpy(), cu["up"], atol=1e-6)
+
+
+def _grid_sample_lookup(vol, coords, r):
+    B, H, W, H2, W2 = vol.shape
+    vt = torch.from_numpy(vol.astype(np.float64)).reshape(B * H * W, 1, H2, W2)
+    out = np.zeros((B, 2 * r + 1, 2 * r + 1, H, W))
+    for i in range(2 * r + 1):
+        for j in range(2 * r + 1):
+            gx = torch.from_numpy((coords[:, 0] - r + i).astype(np.float64)).reshape(-1, 1, 1)
+            gy = torch.from_numpy((coords[:, 1] - r + j).astype(np.float64)).reshape(-1, 1, 1)
+            grid = torch.stack([2 * gx / (W2 - 1) - 1, 2 * gy / (H2 - 1) - 1], -1)
+            s = F.grid_sample(vt, grid, align_corners=True, padding_mode="zeros")
+            out[:, i, j] = s.reshape(B, H, W).numpy()
+    return out
+
+
+def test_lookup_equals_grid_sample(golden_dir):
+    """corr_index_forward semantics == bilinear grid_sample(align_corners, zeros)
+    sampled at (x0 - r + i, y0 - r + j), i the x offset."""
+    g = _load(golden_dir, "corr_pyramid.npz")
+    vol = g["level0"].astype(np.float32)
+    B, H, W, H2, W2 = vol.shape
+    rng = np.random.default_rng(0)
+    base = np.stack(np.meshgrid(np.arange(W), np.arange(H)), 0)[None].astype(np.float32)
+    coords = (base + rng.normal(0, 4, (B, 2, H, W))).astype(np.float32)
+    out = oc.corr_index_forward(vol, coords, 3)
+    ref = _grid_sample_lookup(vol, coords, 3)
+    np.testing.assert_allclose(out, ref, atol=2e-5)
+
+
+def test_fp16_lookup_is_half_rounded_fp32_lookup(golden_dir):
+    g = _load(golden_dir, "corr_pyramid.npz")
+    vol = g["level1"].astype(np.float32)
+    B, H, W, H2, W2 = vol.shape
+    rng = np.random.default_rng(1)
+    coords = (rng.uniform(-3, max(H2, W2) + 3, (B, 2, H, W))).astype(np.float32)
+    o16 = oc.corr_index_forward(vol.astype(np.float16), coords, 3)
+    o32 = oc.corr_index_forward(vol.astype(np.float16).astype(np.float32), coords, 3)
+    assert o16.dtype == np.float16
+    np.testing.assert_allclose(o16.astype(np.float32), o32, atol=4e-3 * np.abs(o32).max())
+
+
+def test_lookup_edge_cases():
+    """far out-of-bounds coords give exact zeros; integer coords sample the taps."""
+    rng = np.random.default_rng(2)
+    vol = rng.normal(size=(1, 2, 3, 6, 7)).astype(np.float32)
+    coords = np.full((1, 2, 2, 3), -100.0, dtype=np.float32)
+    assert np.all(oc.corr_index_forward(vol, coords, 3) == 0)
+    coords = np.zeros((1, 2, 2, 3), dtype=np.float32)
+    coords[:, 0] = 3.0
+    coords[:, 1] = 2.0
+    out = oc.corr_index_forward(vol, coords, 1)
+    for i in range(3):
+        for j in range(3):
+            np.testing.assert_allclose(out[0, i, j], vol[0, :, :, 2 - 1 + j, 3 - 1 + i], atol=1e-6)
