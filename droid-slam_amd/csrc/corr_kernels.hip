@@ -15,14 +15,27 @@
 // multiply-add nvcc emits for `corr += s * w`.
 #include "common.hpp"
 
+// Bit-exact at::Half semantics need every product and sum rounded separately:
+// forbid fusing them into v_fma_mix / v_fma_f16 (hipcc contracts by default).
+#pragma clang fp contract(off)
+
 namespace droid {
+
+// fp32 value -> nearest fp16 -> fp32, with the fp32 operand materialised first.
+// Without the empty asm, hipcc folds round(a*b) / round(a+b) into one
+// v_fma_mixlo_f16 that rounds the EXACT result once - not the reference's
+// fp32-then-half double rounding, so 1-ulp differences appear on rare ties.
+__device__ __forceinline__ float rnd16(float x) {
+  asm volatile("" : "+v"(x));
+  return __half2float(__float2half(x));
+}
 
 template <typename T> struct Acc;
 template <> struct Acc<__half> {
   // weight -> half, product -> half, sum -> half (at::Half operator semantics)
-  __device__ static float weight(float w) { return round_half(w); }
+  __device__ static float weight(float w) { return rnd16(w); }
   __device__ static float madd(float acc, float s, float w) {
-    return round_half(acc + round_half(s * w));
+    return rnd16(acc + rnd16(s * w));
   }
   __device__ static float load(const __half* p) { return __half2float(*p); }
   __device__ static __half store(float v) { return __float2half(v); }
@@ -160,10 +173,10 @@ corr_pyramid_f16_r3_kernel(PyramidArgs args, const float* __restrict__ coords,
     const float fx0 = floorf(x0), fy0 = floorf(y0);
     const float dx = x0 - fx0, dy = y0 - fy0;
     const int xi0 = (int)fx0, yi0 = (int)fy0;
-    const float w11 = round_half(dx * dy);
-    const float w10 = round_half(dx * (1.0f - dy));
-    const float w01 = round_half((1.0f - dx) * dy);
-    const float w00 = round_half((1.0f - dx) * (1.0f - dy));
+    const float w11 = rnd16(dx * dy);
+    const float w10 = rnd16(dx * (1.0f - dy));
+    const float w01 = rnd16((1.0f - dx) * dy);
+    const float w00 = rnd16((1.0f - dx) * (1.0f - dy));
     const int H2 = args.H2[lvl], W2 = args.W2[lvl];
     const __half* vol = args.vol[lvl] + ((long)e * HW + p) * (long)H2 * W2;
     float prev[8], cur[8];
@@ -181,10 +194,10 @@ corr_pyramid_f16_r3_kernel(PyramidArgs args, const float* __restrict__ coords,
         const int b = j - 1;
 #pragma unroll
         for (int a = 0; a < RD; ++a) {
-          float acc = 0.f + round_half(prev[a] * w00);
-          acc = round_half(acc + round_half(cur[a] * w01));
-          acc = round_half(acc + round_half(prev[a + 1] * w10));
-          acc = round_half(acc + round_half(cur[a + 1] * w11));
+          float acc = 0.f + rnd16(prev[a] * w00);
+          acc = rnd16(acc + rnd16(cur[a] * w01));
+          acc = rnd16(acc + rnd16(prev[a + 1] * w10));
+          acc = rnd16(acc + rnd16(cur[a + 1] * w11));
           ol[(long)(a * RD + b) * HW] = __float2half(acc);
         }
       }

@@ -30,6 +30,19 @@ class CorrSampler(torch.autograd.Function):
         return grad_volume, None, None
 
 
+def _avg_pool2(x, max_elems=1 << 30):
+    """F.avg_pool2d(x, 2, stride=2) in batch chunks: the ROCm kernel indexes
+    with 32 bits and a 2048-edge level-0 volume has 1.9e10 elements."""
+    n = x.shape[0]
+    per = max(1, max_elems // max(1, x[0].numel()))
+    if n <= per:
+        return F.avg_pool2d(x, 2, stride=2)
+    out = torch.empty((n, x.shape[1], x.shape[2] // 2, x.shape[3] // 2), dtype=x.dtype, device=x.device)
+    for s in range(0, n, per):
+        out[s:s + per] = F.avg_pool2d(x[s:s + per], 2, stride=2)
+    return out
+
+
 class CorrBlock:
     """corr.py:23-71 (volume correlation pyramid)."""
 
@@ -43,7 +56,7 @@ class CorrBlock:
         for i in range(num_levels):
             self.corr_pyramid.append(vol.view(batch * num, h1, w1, h2 // 2 ** i, w2 // 2 ** i))
             if i + 1 < num_levels:
-                vol = F.avg_pool2d(vol, 2, stride=2)
+                vol = _avg_pool2(vol)
 
     def __call__(self, coords):
         batch, num, ht, wd, _ = coords.shape
