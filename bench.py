@@ -31,6 +31,9 @@ PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 LOOKUP_BYTES_PER_EDGE = 2801664  # volume-API lookup, 4 lvl x 64 taps x 2 B x HW + coords + out
 
 
+LOOKUP_FN = ["corr_pyramid_lookup_nhwc"]
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -62,6 +65,9 @@ def build_state(args, rank, world, device):
     video.counter.value = n
     torch.manual_seed(1003)
     net = UpdateModule().to(device).eval()
+    if not args.reference_op:
+        from droid_mi355x.fused import FusedUpdateModule
+        net = FusedUpdateModule(net)
     graph = FactorGraph(video, net, device=device)
     graph.comm = comm
     with torch.no_grad():
@@ -103,7 +109,7 @@ def stage_breakdown(graph, video, steps=3):
     """ms per stage of update() (separate, untimed pass)."""
     import droid_backends
     names = {"reproject+motn": (droid_backends, "projective_transform"),
-             "corr lookup": (droid_backends, "corr_pyramid_lookup")}
+             "corr lookup": (droid_backends, LOOKUP_FN[0])}
     timers = {k: KernelTimer(m, n) for k, (m, n) in names.items()}
     # update operator and BA: wrap bound callables
     op_t, ba_t = [], []
@@ -185,6 +191,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-edges", type=int, default=8)
     ap.add_argument("--breakdown", action="store_true")
+    ap.add_argument("--reference-op", action="store_true",
+                    help="run the reference-structured UpdateModule (torch/MIOpen convs, NCHW) instead of the fused MFMA operator")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -204,7 +212,8 @@ def main():
         log("setup %.1fs (local edges %d)" % (time.time() - t_setup, e_local))
 
     import droid_backends
-    lookup = KernelTimer(droid_backends, "corr_pyramid_lookup")
+    LOOKUP_FN[0] = "corr_pyramid_lookup" if args.reference_op else "corr_pyramid_lookup_nhwc"
+    lookup = KernelTimer(droid_backends, LOOKUP_FN[0])
 
     with torch.no_grad():
         t_w = time.time()
@@ -255,7 +264,8 @@ def main():
             "config": {"workload": "C3 global graph: update(itrs=2), volume corr", "keyframes": args.frames,
                        "edges": len(ii), "image": [args.ht, args.wd], "fmap": [args.ht // 8, args.wd // 8],
                        "parallelism": "edge-sharded x%d (RCCL all-reduce of reduced camera system)" % world},
-            "roofline": {"kernel": "corr_pyramid_f16_r3_kernel (4-level lookup)", "bound": "hbm",
+            "roofline": {"kernel": "corr_pyramid_f16_r3_kernel<%s> (4-level lookup)" % (
+                "NCHW" if args.reference_op else "NHWC"), "bound": "hbm",
                          "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
                          "traffic": traffic, "launch_ms": lookup_ms,

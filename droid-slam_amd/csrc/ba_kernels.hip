@@ -379,54 +379,68 @@ __global__ void ba_damp_kernel(double* M, int n, int ld, float lm, float ep, int
 // ---------------------------------------------------------------------------
 constexpr int CB = kCholBlock;
 
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)(u & 0xffffffffu), lane);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), lane);
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+// Diagonal block: one wave, lane i owns row i of the 64x64 block in
+// registers; column j is broadcast with v_readlane (no LDS, no barriers).
 __global__ void __launch_bounds__(64) chol_diag_kernel(double* M, int n, int ld, int k0, int* flag) {
-  __shared__ double A[CB][CB + 1];
   const int i = threadIdx.x;
   const int Br = min(CB, n + 1 - k0);
   const int Bp = min(CB, n - k0);
-  if (i < Br) {
-    const int cmax = min(i, Bp - 1);
-    for (int c = 0; c <= cmax; ++c) A[i][c] = M[(long)(k0 + i) * ld + k0 + c];
-  }
-  for (int j = 0; j < Bp; ++j) {
-    __syncthreads();
-    const double piv = A[j][j];
-    if (i == 0 && !(piv > 0.0 && piv < 1e300)) atomicOr(flag, 1);
-    const double s = sqrt(piv);
-    __syncthreads();
-    if (i == j) A[i][j] = s;
-    else if (i > j && i < Br) A[i][j] = A[i][j] / s;
-    __syncthreads();
-    if (i > j && i < Br) {
-      const double lij = A[i][j];
-      const int cmax = min(i, Bp - 1);
-      for (int c = j + 1; c <= cmax; ++c) A[i][c] -= lij * A[c][j];
+  double r[CB];
+  const double* src = M + (long)(k0 + i) * ld + k0;
+#pragma unroll
+  for (int c = 0; c < CB; ++c) r[c] = (i < Br && c <= i && c < Bp) ? src[c] : 0.0;
+#pragma unroll
+  for (int j = 0; j < CB; ++j) {
+    if (j < Bp) {
+      const double piv = readlane_f64(r[j], j);
+      if (i == 0 && !(piv > 0.0 && piv < 1e300)) atomicOr(flag, 1);
+      const double sd = sqrt(piv);
+      if (i == j) r[j] = sd;
+      else if (i > j) r[j] = r[j] / sd;
+      const double lij = r[j];
+#pragma unroll
+      for (int c = j + 1; c < CB; ++c) {
+        const double lcj = readlane_f64(lij, c);
+        r[c] = (c <= i) ? fma(-lij, lcj, r[c]) : r[c];
+      }
     }
   }
-  __syncthreads();
   if (i < Br) {
-    const int cmax = min(i, Bp - 1);
-    for (int c = 0; c <= cmax; ++c) M[(long)(k0 + i) * ld + k0 + c] = A[i][c];
+    double* dst = M + (long)(k0 + i) * ld + k0;
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+      if (c <= i && c < Bp) dst[c] = r[c];
   }
 }
 
-// rows below the diagonal block: X = A_ik L_kk^-T
+// rows below the diagonal block: X = A_ik L_kk^-T.  L_kk and the rows of X
+// live in LDS; column-oriented elimination keeps every inner-loop update of a
+// lane independent (pipelined LDS traffic, broadcast reads of L).
 __global__ void __launch_bounds__(64) chol_trsm_kernel(double* M, int n, int ld, int k0) {
   __shared__ double L[CB][CB + 1];
   __shared__ double X[CB][CB + 1];
   const int i = threadIdx.x;
   const int Bp = min(CB, n - k0);
   const int row = k0 + CB * (blockIdx.x + 1) + i;
-  for (int r = 0; r < Bp; ++r)
-    if (i <= r) L[r][i] = M[(long)(k0 + r) * ld + k0 + i];
-  __syncthreads();
-  if (row > n) return;
+  for (int r = 0; r < CB; ++r) L[r][i] = (r < Bp && i <= r) ? M[(long)(k0 + r) * ld + k0 + i] : (r == i ? 1.0 : 0.0);
+  const bool live = row <= n;
   const double* src = M + (long)row * ld + k0;
-  for (int c = 0; c < Bp; ++c) {
-    double s = src[c];
-    for (int t = 0; t < c; ++t) s -= X[i][t] * L[c][t];
-    X[i][c] = s / L[c][c];
+  for (int c = 0; c < CB; ++c) X[i][c] = (live && c < Bp) ? src[c] : 0.0;
+  __syncthreads();
+  for (int c = 0; c < CB; ++c) {
+    const double xc = X[i][c] / L[c][c];
+    X[i][c] = xc;
+#pragma unroll 8
+    for (int t = c + 1; t < CB; ++t) X[i][t] = fma(-xc, L[t][c], X[i][t]);
   }
+  if (!live) return;
   double* dst = M + (long)row * ld + k0;
   for (int c = 0; c < Bp; ++c) dst[c] = X[i][c];
 }
@@ -483,32 +497,39 @@ __global__ void __launch_bounds__(256) chol_update_kernel(double* M, int n, int 
 
 // back substitution L^T x = y (y = row n), one workgroup; writes dx (fp32),
 // zeroed when the factorisation failed (SparseBlock::solve :1207-1210).
+// Per 64-column block: stage L_bb in LDS, wave 0 solves it with register
+// broadcasts, then all 1024 threads update the rhs of the earlier blocks with
+// coalesced reads of the block's 64 rows.
 __global__ void __launch_bounds__(1024) chol_backsolve_kernel(const double* M, int n, int ld,
                                                               const int* flag, double* xout,
                                                               float* dx) {
   extern __shared__ __attribute__((aligned(16))) double y[];
+  __shared__ double Lb[CB][CB + 1];
   for (int k = threadIdx.x; k < n; k += blockDim.x) y[k] = M[(long)n * ld + k];
-  __syncthreads();
   const int ncolblk = ceil_div(n, CB);
   for (int cb = ncolblk - 1; cb >= 0; --cb) {
     const int c0 = CB * cb;
     const int Bc = min(CB, n - c0);
+    for (int idx = threadIdx.x; idx < CB * CB; idx += blockDim.x) {
+      const int r = idx / CB, c = idx % CB;
+      Lb[r][c] = (r < Bc && c <= r) ? M[(long)(c0 + r) * ld + c0 + c] : (r == c ? 1.0 : 0.0);
+    }
+    __syncthreads();
     if (threadIdx.x < 64) {
       const int i = threadIdx.x;
-      for (int c = Bc - 1; c >= 0; --c) {
-        if (i == c) y[c0 + c] = y[c0 + c] / M[(long)(c0 + c) * ld + c0 + c];
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        const double xc = y[c0 + c];
-        if (i < c) y[c0 + i] -= M[(long)(c0 + c) * ld + c0 + i] * xc;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      double yi = (i < Bc) ? y[c0 + i] : 0.0;
+#pragma unroll
+      for (int c = CB - 1; c >= 0; --c) {
+        const double xc = readlane_f64(yi, c) / Lb[c][c];
+        if (i == c) yi = xc;
+        else if (i < c) yi = fma(-Lb[c][i], xc, yi);
       }
+      if (i < Bc) y[c0 + i] = yi;
     }
     __syncthreads();
     for (int jx = threadIdx.x; jx < c0; jx += blockDim.x) {
       double s = 0.0;
-      for (int c = 0; c < Bc; ++c) s += M[(long)(c0 + c) * ld + jx] * y[c0 + c];
+      for (int c = 0; c < Bc; ++c) s = fma(M[(long)(c0 + c) * ld + jx], y[c0 + c], s);
       y[jx] -= s;
     }
     __syncthreads();

@@ -129,7 +129,16 @@ struct PyramidArgs {
   int H2[4];
   int W2[4];
   int levels;
+  int fast;  // bit l: level l rows are 16-B aligned (W2 % 8 == 0)
 };
+
+__device__ __forceinline__ void load_row8_f16_scalar(const __half* row, int xs, int W2, float* t) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int x = xs + i;
+    t[i] = (x >= 0 && x < W2) ? __half2float(row[x]) : 0.f;
+  }
+}
 
 __device__ __forceinline__ void load_row8_f16(const __half* row, int xs, int W2, float* t) {
   // taps x = xs .. xs+7 of one volume row; zero outside [0, W2)
@@ -155,10 +164,11 @@ __device__ __forceinline__ void load_row8_f16(const __half* row, int xs, int W2,
   }
 }
 
+template <bool NHWC>
 __global__ void __launch_bounds__(256)
 corr_pyramid_f16_r3_kernel(PyramidArgs args, const float* __restrict__ coords,
-                           __half* __restrict__ out, int H, int W) {
-  constexpr int R = 3, RD = 7;
+                           __half* __restrict__ out, int H, int W, int ocs) {
+  constexpr int R = 3, RD = 7, L = 4;
   const int HW = H * W;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = blockIdx.y;
@@ -167,7 +177,15 @@ corr_pyramid_f16_r3_kernel(PyramidArgs args, const float* __restrict__ coords,
   const float cy = coords[((long)e * HW + p) * 2 + 1];
   const int nch = args.levels * RD * RD;
   __half* o = out + (long)e * nch * HW + p;
-  for (int lvl = 0; lvl < args.levels; ++lvl) {
+  // NHWC: the pixel's channels are packed in registers and written as 16-B rows
+  unsigned pk[NHWC ? (L * RD * RD + 7) / 2 + 4 : 1];
+  if (NHWC) {
+#pragma unroll
+    for (int q = 0; q < (int)(sizeof(pk) / sizeof(unsigned)); ++q) pk[q] = 0u;
+  }
+#pragma unroll
+  for (int lvl = 0; lvl < L; ++lvl) {
+    if (lvl >= args.levels) break;
     const float s = 1.0f / (float)(1 << lvl);
     const float x0 = cx * s, y0 = cy * s;
     const float fx0 = floorf(x0), fy0 = floorf(y0);
@@ -185,7 +203,8 @@ corr_pyramid_f16_r3_kernel(PyramidArgs args, const float* __restrict__ coords,
     for (int j = 0; j <= RD; ++j) {
       const int y1 = yi0 - R + j;
       if (y1 >= 0 && y1 < H2) {
-        load_row8_f16(vol + (long)y1 * W2, xi0 - R, W2, cur);
+        if ((args.fast >> lvl) & 1) load_row8_f16(vol + (long)y1 * W2, xi0 - R, W2, cur);
+        else load_row8_f16_scalar(vol + (long)y1 * W2, xi0 - R, W2, cur);
       } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) cur[i] = 0.f;
@@ -198,12 +217,25 @@ corr_pyramid_f16_r3_kernel(PyramidArgs args, const float* __restrict__ coords,
           acc = rnd16(acc + rnd16(cur[a] * w01));
           acc = rnd16(acc + rnd16(prev[a + 1] * w10));
           acc = rnd16(acc + rnd16(cur[a + 1] * w11));
-          ol[(long)(a * RD + b) * HW] = __float2half(acc);
+          if (NHWC) {
+            const int ch = lvl * RD * RD + a * RD + b;
+            const unsigned hv = (unsigned)__half_as_ushort(__float2half(acc));
+            pk[ch >> 1] |= (ch & 1) ? (hv << 16) : hv;
+          } else {
+            ol[(long)(a * RD + b) * HW] = __float2half(acc);
+          }
         }
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) prev[i] = cur[i];
     }
+  }
+  if (NHWC) {
+    uint4* dst = reinterpret_cast<uint4*>(out + ((long)e * HW + p) * ocs);
+    const int n16 = ocs / 8;
+#pragma unroll
+    for (int q = 0; q < (L * RD * RD + 7) / 8; ++q)
+      if (q < n16) dst[q] = make_uint4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
   }
 }
 
@@ -412,7 +444,8 @@ int droid_corr_pyramid_lookup(int dtype, const void* const* levels, const int* H
       a.W2[l] = W2s[l < num_levels ? l : 0];
     }
     a.levels = num_levels;
-    corr_pyramid_f16_r3_kernel<<<grid, 256, 0, stream>>>(a, coords, (__half*)out, H, W);
+    a.fast = 0xf;
+    corr_pyramid_f16_r3_kernel<false><<<grid, 256, 0, stream>>>(a, coords, (__half*)out, H, W, 0);
     DROID_LAUNCH_CHECK();
     return kOk;
   }
@@ -428,6 +461,31 @@ int droid_corr_pyramid_lookup(int dtype, const void* const* levels, const int* H
     }
     DROID_LAUNCH_CHECK();
   }
+  return kOk;
+}
+
+// CorrBlock lookup writing channels-last (E, H, W, out_cstride) fp16 rows with
+// zero padding past L*(2r+1)^2 channels: the A operand layout of the fused
+// update operator.  fp16 volumes, radius 3, 4 levels, W2 % 8 == 0.
+int droid_corr_pyramid_lookup_nhwc(const void* const* levels, const int* H2s, const int* W2s,
+                                   int num_levels, const float* coords, void* out, int out_cstride,
+                                   int E, int H, int W, hipStream_t stream) {
+  if (num_levels != 4 || out_cstride % 8 || out_cstride < 196 || out_cstride > 200)
+    return fail(kUnsupported, "corr_pyramid_lookup_nhwc: needs 4 levels and channel stride 200");
+  PyramidArgs a;
+  a.fast = 0;
+  for (int l = 0; l < 4; ++l) {
+    if (H2s[l] <= 0 || W2s[l] <= 0) return fail(kInvalidArgument, "corr_pyramid_lookup_nhwc: empty level");
+    a.vol[l] = (const __half*)levels[l];
+    a.H2[l] = H2s[l];
+    a.W2[l] = W2s[l];
+    if (W2s[l] % 8 == 0 && (reinterpret_cast<uintptr_t>(levels[l]) & 15) == 0) a.fast |= 1 << l;
+  }
+  a.levels = 4;
+  if (E == 0) return kOk;
+  dim3 grid(ceil_div(H * W, 256), E);
+  corr_pyramid_f16_r3_kernel<true><<<grid, 256, 0, stream>>>(a, coords, (__half*)out, H, W, out_cstride);
+  DROID_LAUNCH_CHECK();
   return kOk;
 }
 

@@ -113,6 +113,54 @@ def corr_pyramid_lookup(levels, coords, radius, out=None):
     return out
 
 
+def corr_pyramid_lookup_nhwc(levels, coords, out_cstride=200, out=None):
+    """CorrBlock lookup (fp16, r=3, 4 levels) -> channels-last (E,H,W,out_cstride)
+    rows, zero past channel 196 (A operand of the fused update operator)."""
+    _check_inputs(["level%d" % i for i in range(len(levels))] + ["coords"], list(levels) + [coords])
+    _need(coords, torch.float32, "coords")
+    E, H, W = levels[0].shape[:3]
+    if out is None:
+        out = torch.empty((E, H, W, out_cstride), dtype=torch.float16, device=coords.device)
+    L = len(levels)
+    ptrs = (ctypes.c_void_p * L)(*[lv.data_ptr() for lv in levels])
+    h2s = (ctypes.c_int * L)(*[lv.shape[3] for lv in levels])
+    w2s = (ctypes.c_int * L)(*[lv.shape[4] for lv in levels])
+    with torch.cuda.device(coords.device):
+        check(lib.droid_corr_pyramid_lookup_nhwc(ptrs, h2s, w2s, L, _ptr(coords), _ptr(out), int(out_cstride),
+                                                 E, H, W, _stream(coords)), "corr_pyramid_lookup_nhwc")
+    return out
+
+
+EPI_ACT, EPI_GRU_ZR, EPI_GRU_Q, EPI_HEAD, EPI_GLO = 0, 1, 2, 3, 4
+
+
+def conv_nhwc_f16(sources, wp, cout, ks, bias=None, bbias=None, act=0, epi=EPI_ACT, out=None, out_coff=0,
+                  h=None, z=None, zout=None, rnet=None, out32=None, gru_ch=128):
+    """Implicit-GEMM MFMA conv (include/droid_backends.h: droid_conv_nhwc_f16).
+
+    sources: list of (tensor, channel_offset, channels); each tensor NHWC fp16
+    contiguous (B,H,W,cstride).  wp: packed weights (droid_mi355x.fused.pack_conv)."""
+    t0 = sources[0][0]
+    B, H, W = t0.shape[:3]
+    n = len(sources)
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() + 2 * off for t, off, _ in sources])
+    cs = (ctypes.c_int * n)(*[c for _, _, c in sources])
+    strides = (ctypes.c_int * n)(*[t.shape[-1] for t, _, _ in sources])
+    for t, _, _ in sources:
+        if t.dtype != torch.float16 or not t.is_contiguous() or t.shape[:3] != (B, H, W):
+            raise RuntimeError("conv_nhwc_f16: sources must be contiguous fp16 (B,H,W,C) tensors")
+    out_cs = out.shape[-1] if out is not None else 0
+    if epi == EPI_HEAD:
+        out_cs = out32.shape[-1]
+    with torch.cuda.device(t0.device):
+        check(lib.droid_conv_nhwc_f16(ptrs, cs, strides, n, _ptr(wp), _ptr(bias), _ptr(bbias), B, H, W, int(cout),
+                                      int(ks), int(act), int(epi), _ptr(out), int(out_cs), int(out_coff),
+                                      _ptr(h), h.shape[-1] if h is not None else 0, _ptr(z),
+                                      z.shape[-1] if z is not None else 0, _ptr(zout), _ptr(rnet), int(gru_ch),
+                                      _ptr(out32), _stream(t0)), "conv_nhwc_f16")
+    return out
+
+
 def altcorr_forward(fmap1, fmap2, coords, radius):
     """altcorr_kernel.cu:290-319: fmap1 (B,H,W,C), fmap2 (B,H2,W2,C),
     coords (B,S,H,W,2) -> [corr (B,S,(2r+1)^2,H,W)]."""

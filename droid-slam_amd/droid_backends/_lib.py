@@ -26,6 +26,9 @@ _SIGS = {
     "droid_corr_index_forward": ([_i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p], _i),
     "droid_corr_index_backward": ([_i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p], _i),
     "droid_corr_pyramid_lookup": ([_i, _p, _p, _p, _i, _p, _p, _i, _i, _i, _i, _p], _i),
+    "droid_corr_pyramid_lookup_nhwc": ([_p, _p, _p, _i, _p, _p, _i, _i, _i, _i, _p], _i),
+    "droid_conv_nhwc_f16": ([_p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _i, _i,
+                             _p, _i, _p, _i, _p, _p, _i, _p, _p], _i),
     "droid_altcorr_forward": ([_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p], _i),
     "droid_altcorr_backward": ([_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p], _i),
     "droid_projective_transform": ([_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p], _i),

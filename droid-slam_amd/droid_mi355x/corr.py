@@ -69,6 +69,12 @@ class CorrBlock:
         out = droid_backends.corr_pyramid_lookup(self.corr_pyramid, c, self.radius)
         return out.view(batch, num, -1, ht, wd)
 
+    def lookup_nhwc(self, coords):
+        """fused-operator layout: (E,H,W,200) fp16 rows (196 used), one launch."""
+        batch, num, ht, wd, _ = coords.shape
+        c = coords.reshape(batch * num, ht, wd, 2).float().contiguous()
+        return droid_backends.corr_pyramid_lookup_nhwc(self.corr_pyramid, c, 200)
+
     def cat(self, other):
         for i in range(self.num_levels):
             self.corr_pyramid[i] = torch.cat([self.corr_pyramid[i], other.corr_pyramid[i]], 0)

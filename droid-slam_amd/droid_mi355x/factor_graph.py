@@ -48,6 +48,20 @@ class FactorGraph:
         self.weight_inac = torch.zeros([1, 0, ht, wd, 2], device=self.device, dtype=torch.float)
         self._dev_cache = {}
         self.comm = None  # set for edge-sharded multi-GPU: dict(group, own=(lo,hi), t0, t1)
+        # fused (MI355X) operator: per-edge hidden state kept channels-last (E,H,W,128)
+        from .fused import FusedUpdateModule
+        self.fused = isinstance(update_op, FusedUpdateModule)
+
+    # -- per-edge state layout ------------------------------------------------
+    @property
+    def _edim(self):
+        return 0 if self.fused else 1
+
+    def _edge_state(self, x):
+        """(E,128,H,W) -> (1,E,128,H,W) (reference layout) or (E,H,W,128) (fused)."""
+        if self.fused:
+            return x.permute(0, 2, 3, 1).contiguous()
+        return x.unsqueeze(0)
 
     # -- edge-list views ------------------------------------------------------
     def _dev(self, name, arr):
@@ -118,22 +132,22 @@ class FactorGraph:
 
         dii = torch.as_tensor(ii, device=self.device)
         djj = torch.as_tensor(jj, device=self.device)
-        net = self.video.nets[dii].to(self.device).unsqueeze(0)
+        net = self._edge_state(self.video.nets[dii].to(self.device))
         if self.corr_impl == "volume":
             c = torch.as_tensor((ii == jj).astype(np.int64), device=self.device)
             fmap1 = self.video.fmaps[dii, 0].to(self.device).unsqueeze(0)
             fmap2 = self.video.fmaps[djj, c].to(self.device).unsqueeze(0)
             corr = CorrBlock(fmap1, fmap2)
             self.corr = corr if self.corr is None else self.corr.cat(corr)
-            inp = self.video.inps[dii].to(self.device).unsqueeze(0)
-            self.inp = inp if self.inp is None else torch.cat([self.inp, inp], 1)
+            inp = self._edge_state(self.video.inps[dii].to(self.device))
+            self.inp = inp if self.inp is None else torch.cat([self.inp, inp], self._edim)
 
         target, _ = self.video.reproject(dii, djj)
         weight = torch.zeros_like(target)
         self._ii = np.concatenate([self._ii, ii])
         self._jj = np.concatenate([self._jj, jj])
         self.age = torch.cat([self.age, torch.zeros_like(dii)], 0)
-        self.net = net if self.net is None else torch.cat([self.net, net], 1)
+        self.net = net if self.net is None else torch.cat([self.net, net], self._edim)
         self.target = torch.cat([self.target, target], 1)
         self.weight = torch.cat([self.weight, weight], 1)
 
@@ -153,9 +167,9 @@ class FactorGraph:
         if self.corr_impl == "volume" and self.corr is not None:
             self.corr = self.corr[dkeep]
         if self.net is not None:
-            self.net = self.net[:, dkeep]
+            self.net = self.net[dkeep] if self.fused else self.net[:, dkeep]
         if self.inp is not None:
-            self.inp = self.inp[:, dkeep]
+            self.inp = self.inp[dkeep] if self.fused else self.inp[:, dkeep]
         self.target = self.target[:, dkeep]
         self.weight = self.weight[:, dkeep]
 
@@ -190,12 +204,16 @@ class FactorGraph:
             coords1 = coords1.view(1, E, ht, wd, 2)
             motn = motn.view(1, E, 4, ht, wd)
 
-        corr = self.corr(coords1)
         uniq, inverse = np.unique(self._ii, return_inverse=True)
         dinv = self._dev("inverse", inverse.astype(np.int64))
-        with torch.autocast("cuda", enabled=True):
-            self.net, delta, weight, damping, upmask = self.update_op(
-                self.net, self.inp, corr, motn, ii, jj, inverse=dinv, num_unique=len(uniq))
+        if self.fused:
+            corr = self.corr.lookup_nhwc(coords1)
+            self.net, delta, weight, damping = self.update_op(self.net, self.inp, corr, motn[0], dinv, len(uniq))
+        else:
+            corr = self.corr(coords1)
+            with torch.autocast("cuda", enabled=True):
+                self.net, delta, weight, damping, upmask = self.update_op(
+                    self.net, self.inp, corr, motn, ii, jj, inverse=dinv, num_unique=len(uniq))
 
         if t0 is None:
             t0 = self.comm["t0"] if self.comm is not None else max(1, int(self._ii.min()) + 1)
@@ -250,11 +268,21 @@ class FactorGraph:
                 dst = torch.as_tensor(rig * jjs_h + (iis_h == jjs_h), device=self.device)
                 corr1 = corr_op(coords1[:, v], src, dst)
                 uq, inv = np.unique(iis_h, return_inverse=True)
-                with torch.autocast("cuda", enabled=True):
-                    net, delta, weight, damping, _ = self.update_op(
-                        self.net[:, v], self.video.inps[None, iis], corr1, motn[:, v], iis, jjs,
-                        inverse=torch.as_tensor(inv, device=self.device), num_unique=len(uq))
-                self.net[:, v] = net
+                dinv = torch.as_tensor(inv, device=self.device)
+                if self.fused:
+                    ev = len(iis_h)
+                    c200 = torch.zeros((ev, ht, wd, 200), dtype=torch.float16, device=self.device)
+                    c200[..., :196] = corr1[0].permute(0, 2, 3, 1)
+                    inp = self.video.inps[iis].permute(0, 2, 3, 1).contiguous()
+                    net, delta, weight, damping = self.update_op(self.net[v].contiguous(), inp, c200,
+                                                                 motn[0, v].contiguous(), dinv, len(uq))
+                    self.net[v] = net
+                else:
+                    with torch.autocast("cuda", enabled=True):
+                        net, delta, weight, damping, _ = self.update_op(
+                            self.net[:, v], self.video.inps[None, iis], corr1, motn[:, v], iis, jjs,
+                            inverse=dinv, num_unique=len(uq))
+                    self.net[:, v] = net
                 self.target[:, v] = coords1[:, v] + delta.float()
                 self.weight[:, v] = weight.float()
                 self.damping[torch.as_tensor(uq, device=self.device)] = damping[0].float()

@@ -1,0 +1,158 @@
+"""Fused update operator on the MFMA implicit-GEMM conv kernel.
+
+Same parameters (state-dict names) and forward semantics as UpdateModule
+(droid_net.py:78-143), restructured for MI355X:
+  * activations stay channels-last fp16 (E,H,W,C) end to end - no NCHW<->NHWC
+    transposes and no torch.cat of the GRU inputs (the conv gathers its K
+    dimension straight from up to 4 source tensors);
+  * convz and convr run as ONE conv with 256 outputs whose epilogue applies
+    both sigmoids and writes z and r*h; convq's epilogue applies tanh and the
+    GRU blend (1-z) h + z q in place of four elementwise kernels;
+  * the global-context branch (sigmoid(w(h)) * h averaged over pixels) is a
+    conv epilogue that reduces over the tile and atomically accumulates;
+  * delta.0 and weight.0 share one conv (256 outputs); delta.2 and weight.2
+    run as one block-diagonal conv whose epilogue applies the weight sigmoid;
+  * GraphAgg's upmask is not computed: update() discards it (factor_graph.py:209).
+All convs: fp16 operands, fp32 accumulation (the reference's autocast).
+"""
+import torch
+import torch.nn.functional as F
+
+import droid_backends
+from droid_backends import EPI_ACT, EPI_GLO, EPI_GRU_Q, EPI_GRU_ZR, EPI_HEAD
+
+from .update import UpdateModule, scatter_mean
+
+TK = 32
+
+
+def pack_conv(weight, splits):
+    """(Cout, Cin, k, k) conv weight -> [Cout][sum_s ceil(C_s/32)*k*k][32] fp16,
+    K walked as (source, 32-channel chunk, tap) like the kernel.  `splits`
+    lists the channel count of each input source (sum = Cin); channels past a
+    source's end within its last chunk are zero."""
+    cout, cin, k, _ = weight.shape
+    assert sum(splits) == cin, (splits, cin)
+    w = weight.detach().float()
+    blocks = []
+    off = 0
+    for c in splits:
+        nch = (c + TK - 1) // TK
+        ws = torch.zeros(cout, nch * TK, k, k, device=w.device)
+        ws[:, :c] = w[:, off:off + c]
+        # (cout, nch, 32, k, k) -> (cout, nch, k*k, 32)
+        ws = ws.view(cout, nch, TK, k * k).permute(0, 1, 3, 2).reshape(cout, nch * k * k, TK)
+        blocks.append(ws)
+        off += c
+    return torch.cat(blocks, dim=1).to(torch.float16).contiguous()
+
+
+class FusedUpdateModule(torch.nn.Module):
+    """Drop-in for UpdateModule on channels-last state (see module docstring)."""
+
+    def __init__(self, module=None):
+        super().__init__()
+        self.m = module if module is not None else UpdateModule()
+        self._packed = None
+
+    def load_state_dict(self, *a, **k):
+        self._packed = None
+        return self.m.load_state_dict(*a, **k)
+
+    def state_dict(self, *a, **k):
+        return self.m.state_dict(*a, **k)
+
+    @torch.no_grad()
+    def pack(self):
+        m = self.m
+        g = m.gru
+        P = {}
+        ce0 = torch.zeros(128, 200, 1, 1, device=m.corr_encoder[0].weight.device)
+        ce0[:, :196] = m.corr_encoder[0].weight   # lookup rows are padded to 200 channels
+        P["ce0"] = pack_conv(ce0, [200])
+        P["ce0_b"] = m.corr_encoder[0].bias.float().contiguous()
+        P["ce2"] = pack_conv(m.corr_encoder[2].weight, [128])
+        P["ce2_b"] = m.corr_encoder[2].bias.float().contiguous()
+        fe0 = torch.zeros(128, 8, 7, 7, device=m.flow_encoder[0].weight.device)
+        fe0[:, :4] = m.flow_encoder[0].weight
+        P["fe0"] = pack_conv(fe0, [8])
+        P["fe0_b"] = m.flow_encoder[0].bias.float().contiguous()
+        P["fe2"] = pack_conv(m.flow_encoder[2].weight, [128])
+        P["fe2_b"] = m.flow_encoder[2].bias.float().contiguous()
+        P["w"] = pack_conv(g.w.weight, [128])
+        P["w_b"] = g.w.bias.float().contiguous()
+        splits = [128, 128, 128, 64]
+        P["zr"] = pack_conv(torch.cat([g.convz.weight, g.convr.weight], 0), splits)
+        P["zr_b"] = torch.cat([g.convz.bias, g.convr.bias]).float().contiguous()
+        P["q"] = pack_conv(g.convq.weight, splits)
+        P["q_b"] = g.convq.bias.float().contiguous()
+        P["glo_w"] = torch.cat([g.convz_glo.weight, g.convr_glo.weight, g.convq_glo.weight], 0)[:, :, 0, 0].float()
+        P["glo_b"] = torch.cat([g.convz_glo.bias, g.convr_glo.bias, g.convq_glo.bias]).float()
+        P["dw0"] = pack_conv(torch.cat([m.delta[0].weight, m.weight[0].weight], 0), [128])
+        P["dw0_b"] = torch.cat([m.delta[0].bias, m.weight[0].bias]).float().contiguous()
+        head = torch.zeros(4, 256, 3, 3, device=m.delta[2].weight.device)
+        head[0:2, :128] = m.delta[2].weight
+        head[2:4, 128:] = m.weight[2].weight
+        P["head"] = pack_conv(head, [256])
+        P["head_b"] = torch.cat([m.delta[2].bias, m.weight[2].bias]).float().contiguous()
+        a = m.agg
+        P["a1"] = pack_conv(a.conv1.weight, [128])
+        P["a1_b"] = a.conv1.bias.float().contiguous()
+        P["a2"] = pack_conv(a.conv2.weight, [128])
+        P["a2_b"] = a.conv2.bias.float().contiguous()
+        P["eta"] = pack_conv(a.eta[0].weight, [128])
+        P["eta_b"] = a.eta[0].bias.float().contiguous()
+        self._packed = P
+
+    @torch.no_grad()
+    def forward(self, net, inp, corr, motn, inverse, num_unique):
+        """net, inp (E,H,W,128) fp16; corr (E,H,W,200) fp16 (196 used); motn
+        (E,4,H,W) fp32; inverse (E) frame slot of each edge's source, num_unique
+        frames -> net' (E,H,W,128) fp16, delta (1,E,H,W,2) f32, weight (1,E,H,W,2)
+        f32, eta (1,U,H,W) f32."""
+        if self._packed is None:
+            self.pack()
+        P = self._packed
+        E, H, W, _ = net.shape
+        dev = net.device
+        conv = droid_backends.conv_nhwc_f16
+        e16 = lambda c: torch.empty((E, H, W, c), dtype=torch.float16, device=dev)
+
+        c1 = e16(128)
+        conv([(corr, 0, 200)], P["ce0"], 128, 1, bias=P["ce0_b"], act=1, out=c1)
+        cf = e16(128)
+        conv([(c1, 0, 128)], P["ce2"], 128, 3, bias=P["ce2_b"], act=1, out=cf)
+        m8 = torch.zeros((E, H, W, 8), dtype=torch.float16, device=dev)
+        m8[..., :4] = motn.permute(0, 2, 3, 1)
+        f1 = e16(128)
+        conv([(m8, 0, 8)], P["fe0"], 128, 7, bias=P["fe0_b"], act=1, out=f1)
+        ff = e16(64)
+        conv([(f1, 0, 128)], P["fe2"], 64, 3, bias=P["fe2_b"], act=1, out=ff)
+
+        glo = torch.zeros((E, 128), dtype=torch.float32, device=dev)
+        conv([(net, 0, 128)], P["w"], 128, 1, bias=P["w_b"], epi=EPI_GLO, h=net, out32=glo)
+        gb = torch.addmm(P["glo_b"], glo, P["glo_w"].t())          # (E, 384): z | r | q
+        z = e16(128)
+        rn = e16(128)
+        conv([(net, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["zr"], 256, 3, bias=P["zr_b"],
+             bbias=gb[:, :256].contiguous(), epi=EPI_GRU_ZR, h=net, zout=z, rnet=rn)
+        net_new = e16(128)
+        conv([(rn, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["q"], 128, 3, bias=P["q_b"],
+             bbias=gb[:, 256:].contiguous(), epi=EPI_GRU_Q, h=net, z=z, out=net_new)
+
+        dw = e16(256)
+        conv([(net_new, 0, 128)], P["dw0"], 256, 3, bias=P["dw0_b"], act=1, out=dw)
+        head = torch.empty((E, H, W, 4), dtype=torch.float32, device=dev)
+        conv([(dw, 0, 256)], P["head"], 4, 3, bias=P["head_b"], epi=EPI_HEAD, out32=head)
+        delta = head[..., 0:2].unsqueeze(0)
+        weight = head[..., 2:4].unsqueeze(0)
+
+        a1 = e16(128)
+        conv([(net_new, 0, 128)], P["a1"], 128, 3, bias=P["a1_b"], act=1, out=a1)
+        agg = scatter_mean(a1.float().view(E, -1), inverse, 0, num_unique).view(num_unique, H, W, 128).half()
+        a2 = torch.empty((num_unique, H, W, 128), dtype=torch.float16, device=dev)
+        conv([(agg, 0, 128)], P["a2"], 128, 3, bias=P["a2_b"], act=1, out=a2)
+        er = torch.empty((num_unique, H, W, 1), dtype=torch.float16, device=dev)
+        conv([(a2, 0, 128)], P["eta"], 1, 3, bias=P["eta_b"], out=er)
+        eta = 0.01 * F.softplus(er.float()).view(1, num_unique, H, W)
+        return net_new, delta, weight, eta

@@ -57,6 +57,30 @@ int droid_corr_pyramid_lookup(int dtype, const void* const* levels, const int* H
                               int num_levels, const float* coords, void* out, int E, int H, int W,
                               int radius, hipStream_t stream);
 
+/* CorrBlock lookup (fp16, r=3, 4 levels) writing channels-last rows
+ * out (E,H,W,out_cstride) with zeros past channel 196: the A operand of the
+ * fused update operator's first (1x1) conv. */
+int droid_corr_pyramid_lookup_nhwc(const void* const* levels, const int* H2s, const int* W2s,
+                                   int num_levels, const float* coords, void* out, int out_cstride,
+                                   int E, int H, int W, hipStream_t stream);
+
+/* ---- update operator ----------------------------------------------------
+ * Implicit-GEMM convolution on MFMA (UpdateModule / ConvGRU convs,
+ * droid_net.py:78-143, modules/gru.py:19-32), NHWC fp16 in, fp32 accumulate.
+ * Input = channel concatenation of nsrc (<=4) NHWC sources (C[s] channels at
+ * pixel stride cstride[s], multiples of 8); wp = packed weights
+ * [Cout][sum_s ceil(C_s/32)*ks*ks][32] fp16; ks odd <= 7, "same" padding.
+ * epi: 0 = act(acc + bias + bbias[b]) (act 0 none / 1 relu) -> out fp16 slice;
+ *      1 = GRU z|r gates (sigmoid; z -> zout, r*h -> rnet);
+ *      2 = GRU update  h' = (1-z) h + z tanh(.) -> out;
+ *      3 = heads: out32 fp32, channels >= 2 through sigmoid;
+ *      4 = GRU global context: mean over pixels of sigmoid(.)*h added into out32[b][co]. */
+int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc,
+                        const void* wp, const float* bias, const float* bbias, int B, int H, int W,
+                        int Cout, int ks, int act, int epi, void* out, int out_cstride, int out_coff,
+                        const void* h, int h_cstride, const void* z, int z_cstride, void* zout,
+                        void* rnet, int gru_ch, void* out32, hipStream_t stream);
+
 /* replaces altcorr_forward (src/droid.cpp:193-203, altcorr_kernel.cu:290-319)
  * fmap1 (B,H,W,C), fmap2 (B,H2,W2,C) dtype (f16|f32), coords (B,S,H,W,2) f32
  * -> corr (B,S,(2r+1)^2,H,W) dtype.  radius must be 3. */

@@ -1,0 +1,121 @@
+"""MFMA implicit-GEMM conv and the fused update operator vs fp32 references."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fill import det_fill
+from gpu_util import host
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.mark.parametrize("ks,splits,cout,B,H,W", [(3, [128, 64], 128, 2, 16, 24), (1, [200], 128, 3, 8, 16),
+                                                   (7, [8], 128, 2, 12, 16), (3, [256], 4, 2, 8, 16),
+                                                   (3, [128, 128, 128, 64], 256, 1, 16, 16)])
+def test_conv_matches_torch(ks, splits, cout, B, H, W):
+    import droid_backends
+    from droid_mi355x.fused import pack_conv
+    g = torch.Generator(device=DEV).manual_seed(5)
+    xs = [torch.randn((B, H, W, c), generator=g, device=DEV).half() for c in splits]
+    w = (torch.randn((cout, sum(splits), ks, ks), generator=g, device=DEV) / (sum(splits) * ks * ks) ** 0.5)
+    bias = torch.randn(cout, generator=g, device=DEV)
+    bb = torch.randn((B, cout), generator=g, device=DEV)
+    out = torch.empty((B, H, W, cout), dtype=torch.float16, device=DEV)
+    droid_backends.conv_nhwc_f16([(x, 0, x.shape[-1]) for x in xs], pack_conv(w, splits), cout, ks, bias=bias,
+                                 bbias=bb, act=1, out=out)
+    xin = torch.cat([x.float() for x in xs], -1).permute(0, 3, 1, 2)
+    ref = F.conv2d(xin, w.half().float(), bias, padding=ks // 2) + bb[:, :, None, None]
+    ref = F.relu(ref).permute(0, 2, 3, 1)
+    np.testing.assert_allclose(host(out.float()), host(ref), atol=2e-2, rtol=1e-2)
+
+
+def test_fused_update_matches_reference_module():
+    from droid_mi355x.fused import FusedUpdateModule
+    from droid_mi355x.update import UpdateModule
+    E, H, W = 6, 16, 24
+    m = UpdateModule().to(DEV).eval()
+    det_fill(m)
+    f = FusedUpdateModule(m)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    net = torch.tanh(torch.randn((1, E, 128, H, W), generator=g, device=DEV)).half()
+    inp = torch.relu(torch.randn((1, E, 128, H, W), generator=g, device=DEV)).half()
+    corr = (2 * torch.randn((1, E, 196, H, W), generator=g, device=DEV)).half()
+    flow = (4 * torch.randn((1, E, 4, H, W), generator=g, device=DEV)).clamp(-64, 64)
+    ii = torch.tensor([0, 0, 1, 2, 2, 3], device=DEV)
+    jj = torch.tensor([1, 2, 0, 1, 3, 2], device=DEV)
+    with torch.no_grad():
+        rn, rd, rw, re, _ = m(net.float(), inp.float(), corr.float(), flow, ii, jj)
+        nhwc = lambda t: t[0].permute(0, 2, 3, 1).contiguous()
+        c200 = torch.zeros((E, H, W, 200), dtype=torch.float16, device=DEV)
+        c200[..., :196] = nhwc(corr)
+        uq, inv = torch.unique(ii, return_inverse=True)
+        fn, fd, fw, fe = f(nhwc(net), nhwc(inp), c200, flow[0], inv, len(uq))
+    np.testing.assert_allclose(host(fn.float()), host(nhwc(rn)), atol=1.5e-2)
+    np.testing.assert_allclose(host(fd), host(rd), atol=3e-2 * max(1.0, float(rd.abs().max())))
+    np.testing.assert_allclose(host(fw), host(rw), atol=1.5e-2)
+    np.testing.assert_allclose(host(fe), host(re), atol=1e-3 + 2e-2 * float(re.abs().max()))
+
+
+def test_corr_lookup_nhwc_equals_nchw():
+    import droid_backends
+    from droid_mi355x.corr import CorrBlock
+    rng = np.random.default_rng(4)
+    E, H, W = 3, 16, 24
+    f1 = torch.from_numpy(rng.normal(size=(1, E, 128, H, W)).astype(np.float16)).to(DEV)
+    f2 = torch.from_numpy(rng.normal(size=(1, E, 128, H, W)).astype(np.float16)).to(DEV)
+    cb = CorrBlock(f1, f2)
+    coords = (np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None, None]
+              + rng.normal(0, 3, (1, E, H, W, 2))).astype(np.float32)
+    c = torch.from_numpy(coords).to(DEV)
+    with torch.no_grad():
+        a = cb(c)[0].permute(0, 2, 3, 1)
+        b = cb.lookup_nhwc(c)
+    np.testing.assert_array_equal(host(b[..., :196]).view(np.uint16), host(a.contiguous()).view(np.uint16))
+    assert torch.all(b[..., 196:] == 0)
+
+
+def test_factor_graph_update_fused_path():
+    """FactorGraph.update() with the fused operator: finite, and BA parity on its inputs."""
+    import droid_backends
+    from droid_mi355x import DepthVideo, FactorGraph, UpdateModule, synthetic
+    from droid_mi355x.fused import FusedUpdateModule
+    from oracle import ba as oba
+    rng = np.random.default_rng(33)
+    n, H, W = 8, 16, 24
+    video = DepthVideo(image_size=(8 * H, 8 * W), buffer=n, device=DEV)
+    poses = synthetic.trajectory(n, rng)
+    poses, disps = synthetic.perturb(poses, synthetic.smooth_disps(n, H, W, rng), rng)
+    video.poses[:n] = torch.from_numpy(poses.astype(np.float32)).to(DEV)
+    video.disps[:n] = torch.from_numpy(disps.astype(np.float32)).to(DEV)
+    video.intrinsics[:n] = torch.tensor([[H / 1.5, H / 1.5, W / 2, H / 2]] * n, device=DEV)
+    video.fmaps[:n] = torch.from_numpy(rng.normal(size=(n, 1, 128, H, W)).astype(np.float16)).to(DEV)
+    video.nets[:n] = torch.from_numpy(np.tanh(rng.normal(size=(n, 128, H, W))).astype(np.float16)).to(DEV)
+    video.inps[:n] = torch.from_numpy(np.maximum(rng.normal(size=(n, 128, H, W)), 0).astype(np.float16)).to(DEV)
+    video.counter.value = n
+    m = UpdateModule().to(DEV).eval()
+    det_fill(m)
+    g = FactorGraph(video, FusedUpdateModule(m), device=DEV)
+    g.add_neighborhood_factors(0, n, r=2)
+    captured = {}
+    orig = droid_backends.ba
+
+    def spy(*a, **k):
+        captured["a"] = [x.detach().clone() if isinstance(x, torch.Tensor) else x for x in a]
+        return orig(*a, **k)
+
+    droid_backends.ba = spy
+    try:
+        with torch.no_grad():
+            g.update()
+            g.update()
+    finally:
+        droid_backends.ba = orig
+    a = captured["a"]
+    ref = oba.ba(poses=host(a[0]), disps=host(a[1]), intrinsics=host(a[2]), disps_sens=host(a[3]),
+                 targets=host(a[4]), weights=host(a[5]), eta=host(a[6]), ii=host(a[7]), jj=host(a[8]), t0=a[9],
+                 t1=a[10], iterations=a[11], lm=a[12], ep=a[13], motion_only=a[14])
+    np.testing.assert_allclose(host(video.poses[:n]), ref["poses"][:n], atol=1e-4)
+    np.testing.assert_allclose(host(video.disps[:n]), np.maximum(ref["disps"][:n], 1e-3), atol=1e-4)
+    assert g.net.shape == (len(g._ii), H, W, 128) and torch.isfinite(g.net.float()).all()
