@@ -3,15 +3,29 @@
 //
 //   out[b,y,x,co] = epilogue( sum_{tap,ci} in[b, y+ty, x+tx, ci] * W[co, tap, ci] )
 //
-// GEMM view: M = B*H*W pixels, N = Cout, K = taps * Cin.  A workgroup owns a
-// 128-pixel x 128-channel output tile; 4 waves (2x2) each hold 4x4 tiles of
-// v_mfma_f32_16x16x32_f16.  K is walked as (source, 32-channel chunk, tap):
-// the A tile is gathered straight from up to 4 NHWC source tensors (the
-// channel concatenations of the reference never materialise), shifted per tap
-// with zero padding; the B tile is the packed weight [Cout][kstep][32].
-// Both are double-buffered through LDS with one barrier per k-step.
+// GEMM view: M = B*H*W pixels, N = Cout, K = taps * Cin.  A workgroup (4
+// waves) owns a 128-pixel x TN-channel output tile (TN = 128, 64 or 16, so the
+// narrow heads do not pay for 128 columns of MFMA work); each wave holds FMxFN
+// tiles of v_mfma_f32_16x16x32_f16.  K is consumed in 64-wide stages (two MFMA
+// K-steps per barrier):
+//   CHUNKED : stage = (source, 64-channel chunk, tap) - the A tile is gathered
+//             straight from up to 4 NHWC sources (the reference's channel
+//             concatenations never materialise), shifted per tap, zero padded;
+//   IM2COL8 : one 8-channel source, stage = 8 consecutive taps x 8 channels
+//             (the 7x7 flow-encoder conv: 7 stages instead of 49 mostly-zero ones).
+// Stage t+1 sits in registers while stage t is multiplied; it is written into
+// the other LDS buffer right after the barrier and stage t+2 is issued at once
+// (one barrier per stage).  The stage decode is wave-uniform (scalar).
+// 3x3 convs (CHUNKED, Cout % 128 == 0) run the LDS-halo variant instead: a
+// 256-pixel x 128-channel tile on 8 waves that loads each 64-channel chunk of
+// its pixels plus a +-(W+1) halo once and serves all 9 taps from LDS (the A
+// operand crosses L2->CU once per chunk, not once per tap).
+// Tiles are mapped XCD-major so each XCD's L2 sees contiguous pixel rows (3x3
+// halos) and both N tiles of a pixel tile.
 //
-// Epilogues fuse what the reference runs as separate elementwise kernels:
+// Epilogues fuse what the reference runs as separate elementwise kernels;
+// inputs (h, z) and outputs go through LDS so every global access is a
+// coalesced 16-B row piece:
 //   EPI_ACT   : act(acc + bias[co] + bbias[b,co]), act in {none, relu}
 //   EPI_GRU_ZR: co <  Ch: z = sigmoid(.)            -> zout
 //               co >= Ch: r = sigmoid(.); r*h       -> rnet
@@ -37,15 +51,20 @@ struct ConvSrc {
 struct ConvArgs {
   ConvSrc src[4];
   int nsrc;
-  int chunk_end[4];  // cumulative 32-channel chunk counts per source
-  int nchunk;
-  const __half* wp;  // [Cout][nchunk*taps][32]
+  int chunk_end[4];  // cumulative 64-channel chunk counts per source (within one tap)
+  int cpt;           // chunks per tap
+  int nstage;        // K / 64
+  int im2col;        // IM2COL8 loader
+  const __half* wp;  // [Cout][nstage][64]
   const float* bias;   // [Cout] or null
   const float* bbias;  // [B][Cout] or null (per-image bias, e.g. the GRU global branch)
   int B, H, W, Cout, ks, act;
   int epi;
+  int n_tiles;  // Cout tiles
+  long m_tiles;
   __half* out;
   int out_cstride, out_coff;
+  int stage_out;  // fp16 output rows can be written as 16-B pieces
   // GRU
   const __half* h;  // hidden state, NHWC
   int h_cstride;
@@ -57,178 +76,757 @@ struct ConvArgs {
   float* out32;  // EPI_HEAD / EPI_GLO fp32 output
 };
 
-constexpr int TM = 128, TN = 128, TK = 32;
-constexpr int LROW = 40;  // LDS row stride in halves (80 B: 16-B aligned, spreads banks)
+constexpr int TM = 128, BK = 64;
+constexpr int LDA = BK;  // LDS row = 128 B; 16-B slot q of row r is stored at q ^ (r & 7)
+// (conflict-free for the gfx950 ds_read_b128 lane groups at any row offset)
+__device__ __forceinline__ int swz(int row, int slot) { return ((slot ^ (row & 7)) << 3); }
+
+template <int TN>
+struct Tile;
+template <>
+struct Tile<128> { static constexpr int WM = 2, WN = 2, FM = 4, FN = 4; };
+template <>
+struct Tile<64> { static constexpr int WM = 2, WN = 2, FM = 4, FN = 2; };
+template <>
+struct Tile<16> { static constexpr int WM = 4, WN = 1, FM = 2, FN = 1; };
+
+template <int TN>
+constexpr int conv_lds_bytes() {
+  constexpr int main_b = (2 * TM * LDA + 2 * TN * LDA) * 2;
+  constexpr int epi_b = 2 * TM * (TN + 8) * 2;
+  return main_b > epi_b ? main_b : epi_b;
+}
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
+// ---------------------------------------------------------------------------
+// Shared epilogue.  Lane holds rows row0 + i*16 + k (k < 4), column col0 + j*16
+// of the workgroup's TMx x TN tile.  `smem` must hold 2*TMx*(TN+8) halves.
+template <int TMx, int TN, int FM, int FN, int NT>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
+                                              int n0, int row0, int col0, int lane, int tid) {
+  const int HW = a.H * a.W;
+  const long Mtot = (long)a.B * HW;
+  const int epi = a.epi;
+  constexpr int ER = TN + 8;  // epilogue LDS row stride (halves)
+  _Float16* Hs = smem;            // [TMx][ER] h tile, then the output tile (in place)
+  _Float16* Zs = smem + TMx * ER; // [TMx][ER] z tile
+  const int b_tile = (int)(m0 / HW);
+
+  // bias (+ per-image bias) into the accumulators
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int co = n0 + col0 + j * 16;
+    const float bv = (a.bias && co < a.Cout) ? a.bias[co] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float v = acc[i][j][k] + bv;
+        if (a.bbias && co < a.Cout) {
+          const long m = m0 + row0 + i * 16 + k;
+          int b = b_tile;
+          if (HW >= TMx) b += (m >= (long)(b_tile + 1) * HW) ? 1 : 0;
+          else b = (int)(m / HW);
+          if (m >= Mtot) b = 0;
+          v += a.bbias[(long)b * a.Cout + co];
+        }
+        acc[i][j][k] = v;
+      }
+  }
+
+  if (epi == EPI_HEAD || (epi == EPI_ACT && !a.stage_out)) {
+    // narrow outputs: direct element stores
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const long m = m0 + row0 + i * 16 + k;
+        if (m >= Mtot) continue;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int co = n0 + col0 + j * 16;
+          if (co >= a.Cout) continue;
+          float v = acc[i][j][k];
+          if (epi == EPI_HEAD) {
+            a.out32[m * a.out_cstride + co] = (co >= 2) ? sigmoidf_(v) : v;
+          } else {
+            if (a.act == 1) v = fmaxf(v, 0.f);
+            a.out[m * a.out_cstride + a.out_coff + co] = __float2half(v);
+          }
+        }
+      }
+    return;
+  }
+
+  // stage the h (and z) tiles through LDS with coalesced 16-B loads
+  const bool zr_r = (epi == EPI_GRU_ZR) && n0 >= a.gru_ch;
+  const bool need_h = zr_r || epi == EPI_GRU_Q || epi == EPI_GLO;
+  const bool need_z = epi == EPI_GRU_Q;
+  constexpr int PPR = TN / 8;  // 16-B pieces per tile row
+  __syncthreads();             // main-loop LDS reads are done
+  if (need_h || need_z) {
+    const int hc0 = zr_r ? n0 - a.gru_ch : n0;
+    for (int idx = tid; idx < TMx * PPR; idx += NT) {
+      const int r = idx / PPR, p = idx - r * PPR;
+      const long m = m0 + r;
+      if (m >= Mtot) continue;
+      if (need_h)
+        *reinterpret_cast<uint4*>(&Hs[r * ER + p * 8]) =
+            *reinterpret_cast<const uint4*>(a.h + m * a.h_cstride + hc0 + p * 8);
+      if (need_z)
+        *reinterpret_cast<uint4*>(&Zs[r * ER + p * 8]) =
+            *reinterpret_cast<const uint4*>(a.z + m * a.z_cstride + n0 + p * 8);
+    }
+    __syncthreads();
+  }
+
+  if (epi == EPI_GLO) {
+    // all pixels of the tile belong to one image (HW % TMx == 0, checked by
+    // the host): sum each column over rows, then one atomic per column.
+    const int b = b_tile;
+    const float inv = 1.0f / (float)HW;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int r = row0 + i * 16 + k;
+          const float hv = (float)Hs[r * ER + col0 + j * 16];
+          sacc += (m0 + r < Mtot) ? sigmoidf_(acc[i][j][k]) * hv : 0.f;
+        }
+      sacc += __shfl_xor(sacc, 16);
+      sacc += __shfl_xor(sacc, 32);
+      const int co = n0 + col0 + j * 16;
+      if (lane < 16 && co < a.Cout) atomicAdd(a.out32 + (long)b * a.Cout + co, sacc * inv);
+    }
+    return;
+  }
+
+  // elementwise epilogue into the LDS output tile (in place over Hs)
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = row0 + i * 16 + k;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = col0 + j * 16;
+        const float v = acc[i][j][k];
+        float o;
+        if (epi == EPI_ACT) {
+          o = (a.act == 1) ? fmaxf(v, 0.f) : v;
+        } else if (epi == EPI_GRU_ZR) {
+          const float g = sigmoidf_(v);
+          o = zr_r ? g * (float)Hs[r * ER + c] : g;
+        } else {  // EPI_GRU_Q
+          const float q = tanhf(v);
+          const float zv = (float)Zs[r * ER + c];
+          const float hv = (float)Hs[r * ER + c];
+          o = (1.0f - zv) * hv + zv * q;
+        }
+        Hs[r * ER + c] = (_Float16)o;
+      }
+    }
+  __syncthreads();
+  __half* dst;
+  int dcs, dco;
+  if (epi == EPI_GRU_ZR) {
+    dst = zr_r ? a.rnet : a.zout;
+    dcs = a.gru_ch;
+    dco = zr_r ? n0 - a.gru_ch : n0;
+  } else {
+    dst = a.out;
+    dcs = a.out_cstride;
+    dco = a.out_coff + n0;
+  }
+  const int ncol = min(TN, a.Cout - n0);
+  for (int idx = tid; idx < TMx * PPR; idx += NT) {
+    const int r = idx / PPR, p = idx - r * PPR;
+    const long m = m0 + r;
+    if (m >= Mtot || p * 8 >= ncol) continue;
+    *reinterpret_cast<uint4*>(dst + m * dcs + dco + p * 8) = *reinterpret_cast<const uint4*>(&Hs[r * ER + p * 8]);
+  }
+}
+
+// XCD-major work id: consecutive ids share an XCD (bijective remap)
+__device__ __forceinline__ long xcd_work_id(long nwg) {
+  const long orig = blockIdx.x;
+  const long xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// ---------------------------------------------------------------------------
+// Generic kernel: 128 x TN tile, 4 waves, A and B staged per 64-wide K stage.
+template <int TN>
 __global__ void __launch_bounds__(256) conv_nhwc_f16_kernel(ConvArgs a) {
-  __shared__ __attribute__((aligned(16))) _Float16 As[2][TM * LROW];
-  __shared__ __attribute__((aligned(16))) _Float16 Bs[2][TN * LROW];
+  using T = Tile<TN>;
+  constexpr int FM = T::FM, FN = T::FN;
+  constexpr int BROWS = TN * 8 / 256 > 0 ? TN * 8 / 256 : 1;  // B pieces per thread
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+  _Float16* As = smem;                  // [2][TM][LDA]
+  _Float16* Bs = smem + 2 * TM * LDA;   // [2][TN][LDA]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / T::WN, wn = wave % T::WN;
+  const int HW = a.H * a.W;
+  const long Mtot = (long)a.B * HW;
+
+  const long wgid = xcd_work_id(a.m_tiles * a.n_tiles);
+  const long mt = wgid / a.n_tiles;
+  const int nt = (int)(wgid - mt * a.n_tiles);
+  const long m0 = mt * TM;
+  const int n0 = nt * TN;
+  const int pad = a.ks >> 1;
+
+  // this thread's 4 A rows and 8-channel piece
+  const int piece = tid & 7;
+  int am[4], ay[4], ax[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const long m = m0 + (tid >> 3) + 32 * r;
+    if (m < Mtot) {
+      am[r] = (int)m;
+      const int p = (int)(m % HW);
+      ay[r] = p / a.W;
+      ax[r] = p - ay[r] * a.W;
+    } else {
+      am[r] = 0;
+      ay[r] = -100000;  // never inside the image
+      ax[r] = 0;
+    }
+  }
+  const int brow = (tid >> 3);
+  const bool bthread = TN * 8 >= 256 || tid < TN * 8;
+
+  // wave-uniform stage cursor (CHUNKED, K order (chunk, tap)): tap (ty,tx), chunk
+  int cur_ty = -pad, cur_tx = -pad, cur_ci = 0;
+  // per-thread tap cursor (IM2COL8)
+  int i2_tap = piece, i2_ty = 0, i2_tx = piece;
+  if (a.im2col) {
+    i2_ty = piece / a.ks;
+    i2_tx = piece - i2_ty * a.ks;
+  }
+  const int taps = a.ks * a.ks;
+
+  uint4 ra[4], rb[BROWS];
+  auto load_stage = [&](int st) {
+    // A operand
+    int dy, dx, c, cs;
+    const __half* base;
+    bool ok_k;
+    if (a.im2col) {
+      dy = i2_ty - pad;
+      dx = i2_tx - pad;
+      c = 0;
+      cs = a.src[0].cstride;
+      base = a.src[0].ptr;
+      ok_k = i2_tap < taps;
+      // advance to the next stage's tap (8 further)
+      i2_tap += 8;
+      i2_tx += 8;
+      while (i2_tx >= a.ks) { i2_tx -= a.ks; ++i2_ty; }
+    } else {
+      int s = 0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (q + 1 < a.nsrc && cur_ci >= a.chunk_end[q]) s = q + 1;
+      const int cstart = s ? a.chunk_end[s - 1] : 0;
+      const ConvSrc src = a.src[s];
+      dy = cur_ty;
+      dx = cur_tx;
+      c = (cur_ci - cstart) * BK + piece * 8;
+      cs = src.cstride;
+      base = src.ptr;
+      ok_k = c < src.C;
+      if (++cur_tx > pad) {
+        cur_tx = -pad;
+        if (++cur_ty > pad) { cur_ty = -pad; ++cur_ci; }
+      }
+    }
+    const int doff = dy * a.W + dx;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int y = ay[r] + dy, x = ax[r] + dx;
+      const bool ok = ok_k && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W;
+      ra[r] = ok ? *reinterpret_cast<const uint4*>(base + (long)(am[r] + doff) * cs + c) : make_uint4(0, 0, 0, 0);
+    }
+    // B operand (packed weights)
+#pragma unroll
+    for (int r = 0; r < BROWS; ++r) {
+      const int co = n0 + brow + 32 * r;
+      rb[r] = (bthread && co < a.Cout)
+                  ? *reinterpret_cast<const uint4*>(a.wp + ((long)co * a.nstage + st) * BK + piece * 8)
+                  : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_stage = [&](int buf) {
+    _Float16* A = As + buf * TM * LDA;
+    _Float16* Bm = Bs + buf * TN * LDA;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      *reinterpret_cast<uint4*>(&A[((tid >> 3) + 32 * r) * LDA + swz(tid >> 3, piece)]) = ra[r];
+    if (bthread) {
+#pragma unroll
+      for (int r = 0; r < BROWS; ++r)
+        *reinterpret_cast<uint4*>(&Bm[(brow + 32 * r) * LDA + swz(brow, piece)]) = rb[r];
+    }
+  };
+
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nst = a.nstage;
+  load_stage(0);
+  store_stage(0);
+  if (nst > 1) load_stage(1);
+  const int fr = lane & 15;
+  for (int st = 0; st < nst; ++st) {
+    __syncthreads();
+    if (st + 1 < nst) {
+      store_stage((st + 1) & 1);
+      if (st + 2 < nst) load_stage(st + 2);
+    }
+    const _Float16* A = As + (st & 1) * TM * LDA + (wm * FM * 16 + fr) * LDA;
+    const _Float16* Bm = Bs + (st & 1) * TN * LDA + (wn * FN * 16 + fr) * LDA;
+#pragma unroll
+    for (int hk = 0; hk < 2; ++hk) {
+      const int ko = swz(fr, (lane >> 4) + hk * 4);
+      half8 af[FM], bf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const half8*>(A + i * 16 * LDA + ko);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const half8*>(Bm + j * 16 * LDA + ko);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  conv_epilogue<TM, TN, FM, FN, 256>(a, acc, smem, m0, n0, wm * FM * 16 + (lane >> 4) * 4, wn * FN * 16 + fr,
+                                     lane, tid);
+}
+
+// ---------------------------------------------------------------------------
+// Halo kernel (ks > 1, CHUNKED): HTM-pixel x 128-channel tile, NW waves
+// ((NW/2) x 2, 64x64 per wave).  For each 64-channel chunk the tile's pixels
+// plus a +-pad*(W+1) halo are loaded ONCE into LDS and all ks*ks taps read
+// their shifted A fragments from it (rows whose shifted pixel leaves the image
+// are masked to zero), so the A operand crosses L2->CU once per chunk instead
+// of once per tap.  B (weights) is double-buffered per (chunk, tap) stage.
+constexpr int kHaloMax = 192;  // max pad*(W+1) supported by the register-staged halo loader
+#ifndef DROID_HALO_ISSUE_TAP
+#define DROID_HALO_ISSUE_TAP 0
+#endif
+constexpr int kHaloIssueTap = DROID_HALO_ISSUE_TAP;
+constexpr int kRowsSlotsMax = 448;  // padded band pixels the row-band kernel's loader covers
+
+template <int NW>
+struct Halo {
+  static constexpr int NT = NW * 64;
+  static constexpr int HTM = (NW / 2) * 64;
+  static constexpr int NP = ((HTM + 2 * kHaloMax) * 8 + NT - 1) / NT;  // halo pieces per thread
+  static constexpr int NB = 128 * 8 / NT;                              // B pieces per thread
+};
+
+template <int NW>
+__host__ __device__ constexpr int halo_lds_bytes_max() {
+  return ((Halo<NW>::HTM + 2 * kHaloMax) * LDA + 2 * 128 * LDA) * 2 > 2 * Halo<NW>::HTM * 136 * 2
+             ? ((Halo<NW>::HTM + 2 * kHaloMax) * LDA + 2 * 128 * LDA) * 2
+             : 2 * Halo<NW>::HTM * 136 * 2;
+}
+
+template <int NW>
+__global__ void __launch_bounds__(NW * 64) conv_halo_kernel(ConvArgs a) {
+  using HP = Halo<NW>;
+  constexpr int TN = 128, FM = 4, FN = 4, NT = HP::NT, HTM = HP::HTM;
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int HW = a.H * a.W;
   const long Mtot = (long)a.B * HW;
-  const long m0 = (long)blockIdx.x * TM;
-  const int n0 = blockIdx.y * TN;
-  const int taps = a.ks * a.ks;
+  const long wgid = xcd_work_id(a.m_tiles * a.n_tiles);
+  const long mt = wgid / a.n_tiles;
+  const int nt = (int)(wgid - mt * a.n_tiles);
+  const long m0 = mt * HTM;
+  const int n0 = nt * TN;
   const int pad = a.ks >> 1;
-  const int nk = a.nchunk * taps;
+  const int hal = pad * (a.W + 1);
+  const int HR = HTM + 2 * hal;
+  _Float16* Ah = smem;              // [HR][LDA]
+  _Float16* Bs = smem + HR * LDA;   // [2][TN][LDA]
 
-  // this thread's two A rows / B rows and its 8-channel piece
-  const int piece = tid & 3;
-  int arow[2], ab[2], ay[2], ax[2];
-  bool avalid[2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    arow[r] = (tid >> 2) + 64 * r;
-    const long m = m0 + arow[r];
-    avalid[r] = m < Mtot;
-    const long mm = avalid[r] ? m : 0;
-    ab[r] = (int)(mm / HW);
-    const int p = (int)(mm % HW);
-    ay[r] = p / a.W;
-    ax[r] = p % a.W;
-  }
+  const int piece = tid & 7;
+  const int prow = tid >> 3;        // NT/8 rows per pass
+  uint4 rh[HP::NP], rb[HP::NB];
 
-  auto load_tiles = [&](int ks, uint4* ra, uint4* rb) {
-    const int chunk = ks / taps;
-    const int tap = ks - chunk * taps;
-    const int ty = tap / a.ks - pad, tx = tap % a.ks - pad;
+  auto load_halo = [&](int chunk) {
     int s = 0;
 #pragma unroll
     for (int q = 0; q < 3; ++q)
       if (q + 1 < a.nsrc && chunk >= a.chunk_end[q]) s = q + 1;
-    const int cc = chunk - (s ? a.chunk_end[s - 1] : 0);
+    const int cstart = s ? a.chunk_end[s - 1] : 0;
     const ConvSrc src = a.src[s];
-    const int c = cc * TK + piece * 8;
+    const int c = (chunk - cstart) * BK + piece * 8;
+    const bool okc = c < src.C;
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int y = ay[r] + ty, x = ax[r] + tx;
-      const bool ok = avalid[r] && c < src.C && y >= 0 && y < a.H && x >= 0 && x < a.W;
-      ra[r] = ok ? *reinterpret_cast<const uint4*>(src.ptr + ((long)ab[r] * HW + (long)y * a.W + x) * src.cstride + c)
-                 : make_uint4(0, 0, 0, 0);
-      const int co = n0 + arow[r];
-      rb[r] = (co < a.Cout) ? *reinterpret_cast<const uint4*>(a.wp + ((long)co * nk + ks) * TK + piece * 8)
-                            : make_uint4(0, 0, 0, 0);
+    for (int q = 0; q < HP::NP; ++q) {
+      const int r = prow + (NT / 8) * q;
+      const long m = m0 - hal + r;
+      const bool ok = okc && r < HR && m >= 0 && m < Mtot;
+      rh[q] = ok ? *reinterpret_cast<const uint4*>(src.ptr + m * src.cstride + c) : make_uint4(0, 0, 0, 0);
     }
   };
-  auto store_tiles = [&](int buf, const uint4* ra, const uint4* rb) {
+  auto store_halo = [&]() {
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      *reinterpret_cast<uint4*>(&As[buf][arow[r] * LROW + piece * 8]) = ra[r];
-      *reinterpret_cast<uint4*>(&Bs[buf][arow[r] * LROW + piece * 8]) = rb[r];
+    for (int q = 0; q < HP::NP; ++q) {
+      const int r = prow + (NT / 8) * q;
+      if (r < HR) *reinterpret_cast<uint4*>(&Ah[r * LDA + swz(r, piece)]) = rh[q];
     }
   };
+  auto load_b = [&](int st) {
+#pragma unroll
+    for (int q = 0; q < HP::NB; ++q) {
+      const int co = n0 + prow + (NT / 8) * q;
+      rb[q] = co < a.Cout ? *reinterpret_cast<const uint4*>(a.wp + ((long)co * a.nstage + st) * BK + piece * 8)
+                          : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < HP::NB; ++q)
+      *reinterpret_cast<uint4*>(&Bs[buf * TN * LDA + (prow + (NT / 8) * q) * LDA + swz(prow, piece)]) = rb[q];
+  };
 
-  floatx4 acc[4][4];
+  // the lane's fragment rows: pixel m0 + wm*64 + i*16 + fr
+  const int fr = lane & 15;
+  int fy[FM], fx[FM];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  uint4 ra[2], rb[2];
-  load_tiles(0, ra, rb);
-  store_tiles(0, ra, rb);
-  __syncthreads();
-  const int fr = lane & 15, fk = (lane >> 4) * 8;
-  int cur = 0;
-  for (int ks = 0; ks < nk; ++ks) {
-    const bool more = ks + 1 < nk;
-    if (more) load_tiles(ks + 1, ra, rb);
-    half8 af[4], bf[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      af[i] = *reinterpret_cast<const half8*>(&As[cur][(wm * 64 + i * 16 + fr) * LROW + fk]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      bf[j] = *reinterpret_cast<const half8*>(&Bs[cur][(wn * 64 + j * 16 + fr) * LROW + fk]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    if (more) store_tiles(cur ^ 1, ra, rb);
-    __syncthreads();
-    cur ^= 1;
+  for (int i = 0; i < FM; ++i) {
+    const long m = m0 + wm * 64 + i * 16 + fr;
+    if (m < Mtot) {
+      const int p = (int)(m % HW);
+      fy[i] = p / a.W;
+      fx[i] = p - fy[i] * a.W;
+    } else {
+      fy[i] = -100000;
+      fx[i] = 0;
+    }
   }
 
-  // epilogue: lane holds rows 4*(lane>>4)+k, column lane&15 of each 16x16 tile
+  floatx4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const long m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + k;
-      if (m >= Mtot) continue;
-      const int b = (int)(m / HW);
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int taps = a.ks * a.ks;
+  const int nch = a.cpt;
+  const int nst = a.nstage;  // nch * taps
+  load_halo(0);
+  load_b(0);
+  store_b(0);
+  if (nst > 1) load_b(1);
+  int st = 0;
+  for (int ch = 0; ch < nch; ++ch) {
+    __syncthreads();  // every wave is done reading the previous chunk's halo
+    store_halo();
+    int ty = -pad, tx = -pad;
+    for (int t = 0; t < taps; ++t, ++st) {
+      __syncthreads();
+      if (st + 1 < nst) {
+        store_b((st + 1) & 1);
+        if (st + 2 < nst) load_b(st + 2);
+      }
+      // the next chunk's halo is issued behind this stage's B loads: loads
+      // retire in order, so it is first waited for two stages later
+      if (t == min(kHaloIssueTap, taps - 1) && ch + 1 < nch) load_halo(ch + 1);
+      unsigned msk[FM];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int co = n0 + wn * 64 + j * 16 + fr;
-        if (co >= a.Cout) continue;
-        float v = acc[i][j][k];
-        if (a.bias) v += a.bias[co];
-        if (a.bbias) v += a.bbias[(long)b * a.Cout + co];
-        if (a.epi == EPI_ACT) {
-          if (a.act == 1) v = fmaxf(v, 0.f);
-          a.out[m * a.out_cstride + a.out_coff + co] = __float2half(v);
-        } else if (a.epi == EPI_GRU_ZR) {
-          const float g = sigmoidf_(v);
-          if (co < a.gru_ch) {
-            a.zout[m * a.gru_ch + co] = __float2half(g);
-          } else {
-            const int c = co - a.gru_ch;
-            const float hv = __half2float(a.h[m * a.h_cstride + c]);
-            a.rnet[m * a.gru_ch + c] = __float2half(g * hv);
-          }
-        } else if (a.epi == EPI_HEAD) {
-          a.out32[m * a.out_cstride + co] = (co >= 2) ? sigmoidf_(v) : v;
-        } else if (a.epi == EPI_GLO) {
-          acc[i][j][k] = sigmoidf_(v) * __half2float(a.h[m * a.h_cstride + co]);
-        } else {  // EPI_GRU_Q
-          const float q = tanhf(v);
-          const float zv = __half2float(a.z[m * a.z_cstride + co]);
-          const float hv = __half2float(a.h[m * a.h_cstride + co]);
-          a.out[m * a.out_cstride + a.out_coff + co] = __float2half((1.0f - zv) * hv + zv * q);
+      for (int i = 0; i < FM; ++i)
+        msk[i] = ((unsigned)(fy[i] + ty) < (unsigned)a.H && (unsigned)(fx[i] + tx) < (unsigned)a.W) ? ~0u : 0u;
+      const int arow = wm * 64 + fr + hal + ty * a.W + tx;
+      const _Float16* A = Ah + arow * LDA;
+      const _Float16* Bm = Bs + (st & 1) * TN * LDA + (wn * 64 + fr) * LDA;
+#pragma unroll
+      for (int hk = 0; hk < 2; ++hk) {
+        const int ka = swz(arow, (lane >> 4) + hk * 4), kb = swz(fr, (lane >> 4) + hk * 4);
+        half8 af[FM], bf[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          uint4 v = *reinterpret_cast<const uint4*>(A + i * 16 * LDA + ka);
+          v.x &= msk[i]; v.y &= msk[i]; v.z &= msk[i]; v.w &= msk[i];
+          af[i] = __builtin_bit_cast(half8, v);
         }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const half8*>(Bm + j * 16 * LDA + kb);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
       }
+      if (++tx > pad) { tx = -pad; ++ty; }
     }
   }
-  if (a.epi == EPI_GLO) {
-    // all 128 pixels of the tile belong to one image (HW % 128 == 0, checked
-    // by the host): sum each column over rows, then one atomic per column.
-    const long mrow = m0 + wm * 64;
-    if (mrow < Mtot) {
-      const int b = (int)(mrow / HW);
-      const float inv = 1.0f / (float)HW;
+  conv_epilogue<HTM, TN, FM, FN, NT>(a, acc, smem, m0, n0, wm * 64 + (lane >> 4) * 4, wn * 64 + fr, lane, tid);
+}
+
+// ---------------------------------------------------------------------------
+// Row-band kernel (ks > 1, CHUNKED, 256 % W == 0, 16 | W, H*W % 256 == 0):
+// the 256-pixel tile is R = 256/W whole image rows, so the halo is held in LDS
+// as a zero-padded (R+2*pad) x (W+2*pad) pixel image and every tap is a pure
+// row shift of it - no wrap-around, no masks.  All global loads are buffer
+// loads with per-thread offsets fixed for the whole kernel (zero VALU address
+// math in the loop); padding / out-of-image pixels use an out-of-range offset,
+// which the buffer unit returns as zeros.
+constexpr unsigned kOob = 0x80000000u;
+constexpr int kBufFlags = 0x00020000;
+
+__device__ __forceinline__ uint4 buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 0));
+}
+
+template <int NW>
+__global__ void __launch_bounds__(NW * 64) conv_rows_kernel(ConvArgs a) {
+  constexpr int TN = 128, FM = 4, FN = 4, NT = NW * 64, HTM = (NW / 2) * 64;
+  constexpr int NP = (kRowsSlotsMax * 8 + NT - 1) / NT;  // halo pieces per thread
+  constexpr int NB = TN * 8 / NT;                        // B pieces per thread
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int W = a.W, H = a.H, HW = H * W;
+  const long wgid = xcd_work_id(a.m_tiles * a.n_tiles);
+  const long mt = wgid / a.n_tiles;
+  const int nt = (int)(wgid - mt * a.n_tiles);
+  const long m0 = mt * HTM;
+  const int n0 = nt * TN;
+  const int pad = a.ks >> 1;
+  const int R = HTM / W;            // image rows in the tile
+  const int PW = W + 2 * pad;       // padded row length (pixels)
+  const int nslot = (R + 2 * pad) * PW;
+  const int y0 = (int)((m0 % HW) / W);
+  _Float16* Ah = smem;                  // [nslot][64]
+  _Float16* Bs = smem + nslot * LDA;    // [2][TN][64]
+
+  const int piece = tid & 7;
+  const int prow = tid >> 3;
+  // halo slot -> pixel offset relative to the band's first row (y0 - pad), or -1
+  int hpix[NP];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float sacc = 0.f;
+  for (int q = 0; q < NP; ++q) {
+    const int slot = prow + (NT / 8) * q;
+    const int ry = slot / PW, rx = slot - (slot / PW) * PW;
+    const int y = y0 + ry - pad, x = rx - pad;
+    hpix[q] = (slot < nslot && y >= 0 && y < H && x >= 0 && x < W) ? ry * W + x : -1;
+  }
+  const long band0 = m0 - (long)pad * W;  // pixel index of the band's first row
+  const int band_rows = R + 2 * pad;
+
+  // lane fragment slots (tap (0,0)) for i < FM
+  const int fr = lane & 15;
+  int fslot[FM];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i) {
+    const int p = wm * 64 + i * 16 + fr;
+    fslot[i] = (p / W + pad) * PW + (p % W) + pad;
+  }
+
+  // B: weights of this tile's 128 output channels
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.wp + (long)n0 * a.nstage * BK), (short)0, TN * a.nstage * BK * 2, kBufFlags);
+  unsigned boff[NB];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const long m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + k;
-            sacc += (m < Mtot) ? acc[i][j][k] : 0.f;
-          }
-        sacc += __shfl_xor(sacc, 16);
-        sacc += __shfl_xor(sacc, 32);
-        const int co = n0 + wn * 64 + j * 16 + fr;
-        if (lane < 16 && co < a.Cout) atomicAdd(a.out32 + (long)b * a.Cout + co, sacc * inv);
+  for (int q = 0; q < NB; ++q) boff[q] = (unsigned)(((prow + (NT / 8) * q) * a.nstage * BK + piece * 8) * 2);
+
+  uint4 rh[NP], rb[NB];
+  auto load_halo = [&](int chunk) {
+    int s = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (q + 1 < a.nsrc && chunk >= a.chunk_end[q]) s = q + 1;
+    const int cstart = s ? a.chunk_end[s - 1] : 0;
+    const ConvSrc src = a.src[s];
+    const int c0 = (chunk - cstart) * BK;
+    const bool okc = c0 + piece * 8 < src.C;
+    // the band may start before the tensor (first image rows): only valid
+    // slots ever read, and those lie inside it
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(src.ptr + band0 * src.cstride + c0), (short)0, band_rows * W * src.cstride * 2, kBufFlags);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const unsigned off = (okc && hpix[q] >= 0) ? (unsigned)((hpix[q] * src.cstride + piece * 8) * 2) : kOob;
+      rh[q] = buf_load16(rs, off, 0);
+    }
+  };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int slot = prow + (NT / 8) * q;
+      if (slot < nslot) *reinterpret_cast<uint4*>(&Ah[slot * LDA + swz(slot, piece)]) = rh[q];
+    }
+  };
+  auto load_b = [&](int st) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) rb[q] = buf_load16(rsb, boff[q], st * BK * 2);
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q)
+      *reinterpret_cast<uint4*>(&Bs[buf * TN * LDA + (prow + (NT / 8) * q) * LDA + swz(prow, piece)]) = rb[q];
+  };
+
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int taps = a.ks * a.ks;
+  const int nch = a.cpt;
+  const int nst = a.nstage;
+  load_halo(0);
+  load_b(0);
+  store_b(0);
+  if (nst > 1) load_b(1);
+  int st = 0;
+  for (int ch = 0; ch < nch; ++ch) {
+    __syncthreads();  // every wave is done reading the previous chunk's halo
+    store_halo();
+    int ty = -pad, tx = -pad;
+    for (int t = 0; t < taps; ++t, ++st) {
+      __syncthreads();
+      if (st + 1 < nst) {
+        store_b((st + 1) & 1);
+        if (st + 2 < nst) load_b(st + 2);
       }
+      if (t == min(kHaloIssueTap, taps - 1) && ch + 1 < nch) load_halo(ch + 1);
+      const int sh = ty * PW + tx;
+      const _Float16* Bm = Bs + (st & 1) * TN * LDA + (wn * 64 + fr) * LDA;
+#pragma unroll
+      for (int hk = 0; hk < 2; ++hk) {
+        const int kq = (lane >> 4) + hk * 4;
+        const int kb = swz(fr, kq);
+        half8 af[FM], bf[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int sl = fslot[i] + sh;
+          af[i] = *reinterpret_cast<const half8*>(Ah + sl * LDA + swz(sl, kq));
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const half8*>(Bm + j * 16 * LDA + kb);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+      if (++tx > pad) { tx = -pad; ++ty; }
     }
   }
+  conv_epilogue<HTM, TN, FM, FN, NT>(a, acc, smem, m0, n0, wm * 64 + (lane >> 4) * 4, wn * 64 + fr, lane, tid);
+}
+
+template <int NW>
+static int launch_rows(const ConvArgs& a0, hipStream_t stream) {
+  constexpr int HTM = (NW / 2) * 64;
+  ConvArgs a = a0;
+  a.n_tiles = a.Cout / 128;
+  const long M = (long)a.B * a.H * a.W;
+  a.m_tiles = M / HTM;
+  const int pad = a.ks >> 1;
+  const int nslot = (HTM / a.W + 2 * pad) * (a.W + 2 * pad);
+  const int main_b = (nslot * LDA + 2 * 128 * LDA) * 2;
+  const int epi_b = 2 * HTM * 136 * 2;
+  const int lds = main_b > epi_b ? main_b : epi_b;
+  constexpr int lds_max = (kRowsSlotsMax * LDA + 2 * 128 * LDA) * 2 > 2 * HTM * 136 * 2
+                              ? (kRowsSlotsMax * LDA + 2 * 128 * LDA) * 2
+                              : 2 * HTM * 136 * 2;
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_rows_kernel<NW>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+    attr = true;
+  }
+  if (a.m_tiles * a.n_tiles > 0x7fffffffL) return fail(kUnsupported, "conv_nhwc_f16: problem too large");
+  conv_rows_kernel<NW><<<dim3((unsigned)(a.m_tiles * a.n_tiles)), NW * 64, lds, stream>>>(a);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+template <int TN>
+static int launch_conv(const ConvArgs& a0, hipStream_t stream) {
+  ConvArgs a = a0;
+  a.n_tiles = ceil_div(a.Cout, TN);
+  const long M = (long)a.B * a.H * a.W;
+  a.m_tiles = (M + TM - 1) / TM;
+  constexpr int lds = conv_lds_bytes<TN>();
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_nhwc_f16_kernel<TN>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr = true;
+  }
+  const long nwg = a.m_tiles * a.n_tiles;
+  if (nwg > 0x7fffffffL) return fail(kUnsupported, "conv_nhwc_f16: problem too large");
+  conv_nhwc_f16_kernel<TN><<<dim3((unsigned)nwg), 256, lds, stream>>>(a);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+template <int NW>
+static int launch_halo(const ConvArgs& a0, hipStream_t stream) {
+  using HP = Halo<NW>;
+  ConvArgs a = a0;
+  a.n_tiles = ceil_div(a.Cout, 128);
+  const long M = (long)a.B * a.H * a.W;
+  a.m_tiles = (M + HP::HTM - 1) / HP::HTM;
+  const int hal = (a.ks >> 1) * (a.W + 1);
+  const int main_b = ((HP::HTM + 2 * hal) * LDA + 2 * 128 * LDA) * 2;
+  const int epi_b = 2 * HP::HTM * 136 * 2;
+  const int lds = main_b > epi_b ? main_b : epi_b;
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_halo_kernel<NW>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, halo_lds_bytes_max<NW>()));
+    attr = true;
+  }
+  const long nwg = a.m_tiles * a.n_tiles;
+  if (nwg > 0x7fffffffL) return fail(kUnsupported, "conv_nhwc_f16: problem too large");
+  conv_halo_kernel<NW><<<dim3((unsigned)nwg), HP::NT, lds, stream>>>(a);
+  DROID_LAUNCH_CHECK();
+  return kOk;
 }
 
 }  // namespace droid
 
 using namespace droid;
 
+static bool rows_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("DROID_CONV_ROWS");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 extern "C" {
 
 // srcs/C/cstride: nsrc NHWC fp16 inputs concatenated along channels.
-// wp: packed weights [Cout][sum_s ceil(C_s/32) * ks*ks][32] fp16 (see droid_mi355x.fused).
+// wp: packed weights [Cout][nstage][64] fp16 (see droid_mi355x.fused.pack_conv):
+//   nsrc == 1 && C == 8 && ks > 1: IM2COL8, nstage = ceil(ks*ks/8), stage = 8 taps x 8 channels;
+//   otherwise CHUNKED, nstage = ks*ks * sum_s ceil(C_s/64), stage = (source, 64-ch chunk, tap).
 // epi: 0 act (act 0 none / 1 relu) -> out fp16 NHWC slice; 1 GRU z|r; 2 GRU q;
 // 3 head (fp32 out32, sigmoid on co >= 2); 4 GRU global mean (atomic fp32 out32, zeroed by caller).
 int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc,
@@ -236,8 +834,11 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
                         int Cout, int ks, int act, int epi, void* out, int out_cstride, int out_coff,
                         const void* h, int h_cstride, const void* z, int z_cstride, void* zout,
                         void* rnet, int gru_ch, void* out32, hipStream_t stream) {
-  if (nsrc < 1 || nsrc > 4 || B < 0 || H <= 0 || W <= 0 || Cout <= 0 || ks < 1 || ks > 7 || !(ks & 1))
+  if (nsrc < 1 || nsrc > 4 || B < 0 || H <= 0 || W <= 0 || Cout <= 0 || ks < 1 || ks > 7 || !(ks & 1) ||
+      epi < EPI_ACT || epi > EPI_GLO)
     return fail(kInvalidArgument, "conv_nhwc_f16: bad arguments");
+  if ((long)B * H * W * 8 > 0x7fffffffL)
+    return fail(kUnsupported, "conv_nhwc_f16: pixel count too large for 32-bit row indices");
   if (epi == EPI_GLO && (H * W) % TM != 0)
     return fail(kUnsupported, "conv_nhwc_f16: global-context epilogue needs H*W % 128 == 0");
   ConvArgs a{};
@@ -248,11 +849,13 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
     a.src[s].ptr = (const __half*)srcs[s];
     a.src[s].C = C[s];
     a.src[s].cstride = cstride[s];
-    chunks += ceil_div(C[s], TK);
+    chunks += ceil_div(C[s], BK);
     a.chunk_end[s] = chunks;
   }
   a.nsrc = nsrc;
-  a.nchunk = chunks;
+  a.cpt = chunks;
+  a.im2col = (nsrc == 1 && C[0] == 8 && ks > 1) ? 1 : 0;
+  a.nstage = a.im2col ? ceil_div(ks * ks, 8) : ks * ks * chunks;
   a.wp = (const __half*)wp;
   a.bias = bias;
   a.bbias = bbias;
@@ -262,12 +865,82 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
   a.z = (const __half*)z; a.z_cstride = z_cstride;
   a.zout = (__half*)zout; a.rnet = (__half*)rnet; a.gru_ch = gru_ch;
   a.out32 = (float*)out32;
+  const int TN = Cout >= 128 ? 128 : (Cout > 16 ? 64 : 16);
+  a.stage_out = (Cout % 8 == 0 && out_cstride % 8 == 0 && out_coff % 8 == 0) ? 1 : 0;
+  if (epi == EPI_ACT && !out) return fail(kInvalidArgument, "conv_nhwc_f16: out is null");
+  if ((epi == EPI_GRU_ZR || epi == EPI_GRU_Q || epi == EPI_GLO) &&
+      (!h || h_cstride % 8 || Cout % 8 || (reinterpret_cast<uintptr_t>(h) & 15)))
+    return fail(kInvalidArgument, "conv_nhwc_f16: GRU epilogues need h with 16-B aligned rows");
+  if (epi == EPI_GRU_ZR && (gru_ch % TN || Cout != 2 * gru_ch || !zout || !rnet))
+    return fail(kInvalidArgument, "conv_nhwc_f16: z|r epilogue needs Cout == 2*gru_ch, gru_ch % tile == 0");
+  if (epi == EPI_GRU_Q && (!z || z_cstride % 8 || !out || !a.stage_out || (reinterpret_cast<uintptr_t>(z) & 15)))
+    return fail(kInvalidArgument, "conv_nhwc_f16: q epilogue needs z and a 16-B aligned out");
+  if ((epi == EPI_HEAD || epi == EPI_GLO) && !out32)
+    return fail(kInvalidArgument, "conv_nhwc_f16: out32 is null");
+  if (a.stage_out && out && (reinterpret_cast<uintptr_t>(out) & 15)) a.stage_out = 0;
   if (B == 0) return kOk;
-  const long M = (long)B * H * W;
-  dim3 grid((unsigned)ceil_div((int)((M + TM - 1) / TM), 1), ceil_div(Cout, TN));
-  conv_nhwc_f16_kernel<<<grid, 256, 0, stream>>>(a);
-  DROID_LAUNCH_CHECK();
-  return kOk;
+  // 3x3 (and larger) convs over wide-enough outputs take the LDS-halo kernel;
+  // DROID_CONV_HALO=0 / 4 / 8 (default) selects none / 4-wave / 8-wave tiles;
+  // DROID_CONV_ROWS=0 disables the row-band variant.
+  static const int halo_nw = [] {
+    const char* e = getenv("DROID_CONV_HALO");
+    return e ? atoi(e) : 8;
+  }();
+  const bool halo_ok = !a.im2col && ks > 1 && Cout % 128 == 0 && (ks >> 1) * (W + 1) <= kHaloMax &&
+                       epi != EPI_GLO && epi != EPI_HEAD;
+  // row-band variant: tile = whole image rows, zero-padded halo, no masks
+  const int pad = ks >> 1;
+  const bool rows_ok = halo_ok && halo_nw == 8 && 256 % W == 0 && W % 16 == 0 && (H * W) % 256 == 0 &&
+                       (256 / W + 2 * pad) * (W + 2 * pad) <= kRowsSlotsMax &&
+                       (long)(256 / W + 2 * pad) * W * 256 * 2 < 0x7fffffffL && rows_enabled();
+  if (rows_ok) return launch_rows<8>(a, stream);
+  if (halo_ok && halo_nw == 8) return launch_halo<8>(a, stream);
+  if (halo_ok && halo_nw == 4) return launch_halo<4>(a, stream);
+  if (TN == 128) return launch_conv<128>(a, stream);
+  if (TN == 64) return launch_conv<64>(a, stream);
+  return launch_conv<16>(a, stream);
 }
 
 }  // extern "C"
+
+namespace droid {
+
+// GraphAgg's scatter_mean over edges sharing a source frame (droid_net.py:
+// 27-45): out[u] = mean_{e in segment u} src[e], rows of `row` fp16 values
+// (H*W*C), fp32 accumulation.  One thread per 16-B piece of a row.
+__global__ void __launch_bounds__(256) segment_mean_f16_kernel(const __half* __restrict__ src,
+                                                               const int64_t* __restrict__ seg_ptr,
+                                                               const int64_t* __restrict__ seg_idx,
+                                                               __half* __restrict__ out, long row) {
+  const long q = (long)blockIdx.x * 256 + threadIdx.x;
+  const int u = blockIdx.y;
+  if (q * 8 >= row) return;
+  const long e0 = seg_ptr[u], e1 = seg_ptr[u + 1];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (long e = e0; e < e1; ++e) {
+    const half8 v = *reinterpret_cast<const half8*>(src + seg_idx[e] * row + q * 8);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += (float)v[k];
+  }
+  const float inv = 1.0f / (float)max(e1 - e0, 1L);
+  half8 o;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = (_Float16)(acc[k] * inv);
+  *reinterpret_cast<half8*>(out + (long)u * row + q * 8) = o;
+}
+
+}  // namespace droid
+
+extern "C" int droid_segment_mean_f16(const void* src, const int64_t* seg_ptr, const int64_t* seg_idx,
+                                      void* out, int num_segments, long row, hipStream_t stream) {
+  if (num_segments < 0 || row <= 0 || row % 8 || (reinterpret_cast<uintptr_t>(src) & 15) ||
+      (reinterpret_cast<uintptr_t>(out) & 15))
+    return fail(kInvalidArgument, "segment_mean_f16: rows must be multiples of 8 halves, 16-B aligned");
+  if (num_segments == 0) return kOk;
+  const long pieces = row / 8;
+  if ((pieces + 255) / 256 > 0x7fffffffL) return fail(kUnsupported, "segment_mean_f16: row too long");
+  segment_mean_f16_kernel<<<dim3((unsigned)((pieces + 255) / 256), num_segments), 256, 0, stream>>>(
+      (const __half*)src, seg_ptr, seg_idx, (__half*)out, row);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}

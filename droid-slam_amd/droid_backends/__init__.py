@@ -161,6 +161,27 @@ def conv_nhwc_f16(sources, wp, cout, ks, bias=None, bbias=None, act=0, epi=EPI_A
     return out
 
 
+def segment_mean_f16(src, seg_ptr, seg_idx, num_segments, out=None):
+    """GraphAgg scatter_mean (include/droid_backends.h: droid_segment_mean_f16):
+    src (E, ...) fp16 contiguous; seg_ptr (U+1) / seg_idx (E) int64 CSR of the
+    edges per segment -> out (U, ...) fp16 = per-segment mean of src rows."""
+    _check_inputs(("src", "seg_ptr", "seg_idx"), (src, seg_ptr, seg_idx))
+    _need(src, torch.float16, "src")
+    _need(seg_ptr, torch.int64, "seg_ptr")
+    _need(seg_idx, torch.int64, "seg_idx")
+    if seg_ptr.numel() != num_segments + 1:
+        raise RuntimeError("seg_ptr must have num_segments + 1 entries")
+    row = src[0].numel() if src.shape[0] else 0
+    if out is None:
+        out = torch.empty((num_segments,) + tuple(src.shape[1:]), dtype=torch.float16, device=src.device)
+    if num_segments == 0 or row == 0:
+        return out
+    with torch.cuda.device(src.device):
+        check(lib.droid_segment_mean_f16(_ptr(src), _ptr(seg_ptr), _ptr(seg_idx), _ptr(out), int(num_segments),
+                                         int(row), _stream(src)), "segment_mean_f16")
+    return out
+
+
 def altcorr_forward(fmap1, fmap2, coords, radius):
     """altcorr_kernel.cu:290-319: fmap1 (B,H,W,C), fmap2 (B,H2,W2,C),
     coords (B,S,H,W,2) -> [corr (B,S,(2r+1)^2,H,W)]."""

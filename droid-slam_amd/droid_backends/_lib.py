@@ -5,7 +5,8 @@ import os
 import torch  # noqa: F401  (loads torch's HIP runtime first; the library shares it)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdroid_hip.so")
+# DROID_HIP_LIB points at an alternative build (kernel A/B experiments)
+LIB_PATH = os.environ.get("DROID_HIP_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libdroid_hip.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -29,6 +30,7 @@ _SIGS = {
     "droid_corr_pyramid_lookup_nhwc": ([_p, _p, _p, _i, _p, _p, _i, _i, _i, _i, _p], _i),
     "droid_conv_nhwc_f16": ([_p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _i, _i,
                              _p, _i, _p, _i, _p, _p, _i, _p, _p], _i),
+    "droid_segment_mean_f16": ([_p, _p, _p, _p, _i, ctypes.c_long, _p], _i),
     "droid_altcorr_forward": ([_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p], _i),
     "droid_altcorr_backward": ([_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p], _i),
     "droid_projective_transform": ([_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p], _i),

@@ -15,6 +15,7 @@ import torch
 import droid_backends
 
 from .corr import AltCorrBlock, CorrBlock
+from .fused import edge_segments
 
 
 def _coords_grid(ht, wd, device):
@@ -208,7 +209,10 @@ class FactorGraph:
         dinv = self._dev("inverse", inverse.astype(np.int64))
         if self.fused:
             corr = self.corr.lookup_nhwc(coords1)
-            self.net, delta, weight, damping = self.update_op(self.net, self.inp, corr, motn[0], dinv, len(uniq))
+            ptr, idx = edge_segments(inverse, len(uniq))
+            segs = (self._dev("seg_ptr", ptr), self._dev("seg_idx", idx))
+            self.net, delta, weight, damping = self.update_op(self.net, self.inp, corr, motn[0], dinv, len(uniq),
+                                                              segments=segs)
         else:
             corr = self.corr(coords1)
             with torch.autocast("cuda", enabled=True):

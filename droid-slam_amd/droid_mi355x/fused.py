@@ -15,36 +15,59 @@ Same parameters (state-dict names) and forward semantics as UpdateModule
   * GraphAgg's upmask is not computed: update() discards it (factor_graph.py:209).
 All convs: fp16 operands, fp32 accumulation (the reference's autocast).
 """
+import numpy as np
 import torch
 import torch.nn.functional as F
 
 import droid_backends
 from droid_backends import EPI_ACT, EPI_GLO, EPI_GRU_Q, EPI_GRU_ZR, EPI_HEAD
 
-from .update import UpdateModule, scatter_mean
+from .update import UpdateModule
 
-TK = 32
+BK = 64
 
 
 def pack_conv(weight, splits):
-    """(Cout, Cin, k, k) conv weight -> [Cout][sum_s ceil(C_s/32)*k*k][32] fp16,
-    K walked as (source, 32-channel chunk, tap) like the kernel.  `splits`
-    lists the channel count of each input source (sum = Cin); channels past a
-    source's end within its last chunk are zero."""
+    """(Cout, Cin, k, k) conv weight -> [Cout][nstage][64] fp16 in the kernel's
+    K order (csrc/conv_kernels.hip).  `splits` lists the channel count of each
+    input source (sum = Cin).
+      * one 8-channel source with k > 1 (IM2COL8): stage s holds taps 8s..8s+7,
+        8 channels each (taps past k*k are zero);
+      * otherwise (CHUNKED): stage = (source, 64-channel chunk, tap), channels
+        past a source's end within its last chunk are zero."""
     cout, cin, k, _ = weight.shape
     assert sum(splits) == cin, (splits, cin)
-    w = weight.detach().float()
+    w = weight.detach().float().reshape(cout, cin, k * k)      # (cout, cin, tap)
+    taps = k * k
+    if len(splits) == 1 and splits[0] == 8 and k > 1:
+        nst = (taps + 7) // 8
+        wp = torch.zeros(cout, nst * 8, 8, device=w.device)
+        wp[:, :taps] = w.permute(0, 2, 1)                      # (cout, tap, 8)
+        return wp.reshape(cout, nst, BK).to(torch.float16).contiguous()
     blocks = []
     off = 0
     for c in splits:
-        nch = (c + TK - 1) // TK
-        ws = torch.zeros(cout, nch * TK, k, k, device=w.device)
+        nch = (c + BK - 1) // BK
+        ws = torch.zeros(cout, nch * BK, taps, device=w.device)
         ws[:, :c] = w[:, off:off + c]
-        # (cout, nch, 32, k, k) -> (cout, nch, k*k, 32)
-        ws = ws.view(cout, nch, TK, k * k).permute(0, 1, 3, 2).reshape(cout, nch * k * k, TK)
-        blocks.append(ws)
+        blocks.append(ws.view(cout, nch, BK, taps))
         off += c
-    return torch.cat(blocks, dim=1).to(torch.float16).contiguous()
+    wp = torch.cat(blocks, dim=1)                              # (cout, chunks, 64, tap)
+    return wp.permute(0, 1, 3, 2).reshape(cout, -1, BK).to(torch.float16).contiguous()
+
+
+def edge_segments(inverse, num_unique):
+    """CSR (seg_ptr (U+1), seg_idx (E)) int64 of the edges per source-frame slot.
+    `inverse` may be a numpy array (built on the host) or a device tensor."""
+    if isinstance(inverse, np.ndarray):
+        idx = np.argsort(inverse, kind="stable").astype(np.int64)
+        ptr = np.zeros(num_unique + 1, np.int64)
+        ptr[1:] = np.cumsum(np.bincount(inverse, minlength=num_unique))
+        return ptr, idx
+    idx = torch.argsort(inverse, stable=True)
+    ptr = torch.zeros(num_unique + 1, dtype=torch.int64, device=inverse.device)
+    ptr[1:] = torch.cumsum(torch.bincount(inverse, minlength=num_unique), 0)
+    return ptr, idx
 
 
 class FusedUpdateModule(torch.nn.Module):
@@ -105,11 +128,12 @@ class FusedUpdateModule(torch.nn.Module):
         self._packed = P
 
     @torch.no_grad()
-    def forward(self, net, inp, corr, motn, inverse, num_unique):
+    def forward(self, net, inp, corr, motn, inverse, num_unique, segments=None):
         """net, inp (E,H,W,128) fp16; corr (E,H,W,200) fp16 (196 used); motn
         (E,4,H,W) fp32; inverse (E) frame slot of each edge's source, num_unique
-        frames -> net' (E,H,W,128) fp16, delta (1,E,H,W,2) f32, weight (1,E,H,W,2)
-        f32, eta (1,U,H,W) f32."""
+        frames; segments = optional (seg_ptr (U+1), seg_idx (E)) int64 CSR of
+        `inverse` (edge_segments) -> net' (E,H,W,128) fp16, delta (1,E,H,W,2)
+        f32, weight (1,E,H,W,2) f32, eta (1,U,H,W) f32."""
         if self._packed is None:
             self.pack()
         P = self._packed
@@ -149,7 +173,9 @@ class FusedUpdateModule(torch.nn.Module):
 
         a1 = e16(128)
         conv([(net_new, 0, 128)], P["a1"], 128, 3, bias=P["a1_b"], act=1, out=a1)
-        agg = scatter_mean(a1.float().view(E, -1), inverse, 0, num_unique).view(num_unique, H, W, 128).half()
+        if segments is None:
+            segments = edge_segments(inverse, num_unique)
+        agg = droid_backends.segment_mean_f16(a1, segments[0], segments[1], num_unique)
         a2 = torch.empty((num_unique, H, W, 128), dtype=torch.float16, device=dev)
         conv([(agg, 0, 128)], P["a2"], 128, 3, bias=P["a2_b"], act=1, out=a2)
         er = torch.empty((num_unique, H, W, 1), dtype=torch.float16, device=dev)

@@ -81,6 +81,13 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
                         const void* h, int h_cstride, const void* z, int z_cstride, void* zout,
                         void* rnet, int gru_ch, void* out32, hipStream_t stream);
 
+/* GraphAgg scatter_mean (droid_net.py:27-45, torch_scatter.scatter_mean over
+ * dim 1): out[u] = mean of src rows seg_idx[seg_ptr[u] .. seg_ptr[u+1]), rows of
+ * `row` fp16 values (row % 8 == 0), fp32 accumulation.  seg_ptr (U+1), seg_idx
+ * (E) int64: the edges grouped by source frame (CSR of `inverse`). */
+int droid_segment_mean_f16(const void* src, const int64_t* seg_ptr, const int64_t* seg_idx, void* out,
+                           int num_segments, long row, hipStream_t stream);
+
 /* replaces altcorr_forward (src/droid.cpp:193-203, altcorr_kernel.cu:290-319)
  * fmap1 (B,H,W,C), fmap2 (B,H2,W2,C) dtype (f16|f32), coords (B,S,H,W,2) f32
  * -> corr (B,S,(2r+1)^2,H,W) dtype.  radius must be 3. */

@@ -9,6 +9,7 @@ import droid_backends
 from droid_mi355x.fused import pack_conv
 
 E = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+ONLY = sys.argv[2] if len(sys.argv) > 2 else None
 H, W = 48, 64
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
@@ -27,6 +28,8 @@ cases = {
 }
 flops_total = 0
 for name, (srcs, cout, ks, kw) in cases.items():
+    if ONLY and not name.startswith(ONLY):
+        continue
     cin = sum(c for _, _, c in srcs)
     w = torch.randn((cout, cin, ks, ks), generator=g, device=dev) * 0.02
     wp = pack_conv(w, [c for _, _, c in srcs])

@@ -13,7 +13,10 @@ DEV = "cuda:0"
 
 @pytest.mark.parametrize("ks,splits,cout,B,H,W", [(3, [128, 64], 128, 2, 16, 24), (1, [200], 128, 3, 8, 16),
                                                    (7, [8], 128, 2, 12, 16), (3, [256], 4, 2, 8, 16),
-                                                   (3, [128, 128, 128, 64], 256, 1, 16, 16)])
+                                                   (3, [128, 128, 128, 64], 256, 1, 16, 16),
+                                                   (3, [128], 64, 2, 16, 24), (3, [128], 1, 3, 8, 12),
+                                                   (5, [8], 128, 3, 8, 12), (3, [64, 128], 16, 3, 8, 12),
+                                                   (3, [64], 128, 3, 8, 12), (5, [128], 128, 2, 12, 20)])
 def test_conv_matches_torch(ks, splits, cout, B, H, W):
     import droid_backends
     from droid_mi355x.fused import pack_conv
@@ -119,3 +122,20 @@ def test_factor_graph_update_fused_path():
     np.testing.assert_allclose(host(video.poses[:n]), ref["poses"][:n], atol=1e-4)
     np.testing.assert_allclose(host(video.disps[:n]), np.maximum(ref["disps"][:n], 1e-3), atol=1e-4)
     assert g.net.shape == (len(g._ii), H, W, 128) and torch.isfinite(g.net.float()).all()
+
+
+def test_segment_mean_matches_scatter_mean():
+    import droid_backends
+    from droid_mi355x.fused import edge_segments
+    from droid_mi355x.update import scatter_mean
+    g = torch.Generator(device=DEV).manual_seed(3)
+    E, H, W, C = 9, 8, 12, 128
+    src = torch.randn((E, H, W, C), generator=g, device=DEV).half()
+    inverse = np.array([2, 0, 2, 1, 0, 2, 3, 3, 0])
+    U = 5   # slot 4 has no edges -> zeros (torch_scatter semantics)
+    ptr, idx = edge_segments(inverse, U)
+    out = droid_backends.segment_mean_f16(src, torch.as_tensor(ptr, device=DEV), torch.as_tensor(idx, device=DEV), U)
+    ref = scatter_mean(src.float().view(E, -1), torch.as_tensor(inverse, device=DEV), 0, U).view(U, H, W, C)
+    np.testing.assert_allclose(host(out.float()), host(ref), atol=2e-3, rtol=2e-3)
+    dptr, didx = edge_segments(torch.as_tensor(inverse, device=DEV), U)
+    assert np.array_equal(host(dptr), ptr) and np.array_equal(host(didx), idx)
