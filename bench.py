@@ -10,8 +10,10 @@ source frame (strong scaling); each rank runs its edges and its depth frames,
 and the reduced camera system is all-reduced once per GN iteration.
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant hand-written
-kernel (the pyramid lookup) measured live with HIP events, and the CPU
-baseline (oracle restatement, bounded sample) on rank 0 at N=1.
+kernel (the ConvGRU z|r gate conv, MFMA-bound) measured live with
+HIP events on its launch stream, a secondary HBM roofline for the correlation
+lookup, and the CPU baseline (oracle restatement, bounded sample) on rank 0 at
+N=1.
 """
 import argparse
 import json
@@ -28,7 +30,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+PEAK_F16_TFLOPS = 2500.0        # MI355X_MICROARCH.md: dense fp16/bf16 MFMA peak (no sparsity)
 LOOKUP_BYTES_PER_EDGE = 2801664  # volume-API lookup, 4 lvl x 64 taps x 2 B x HW + coords + out
+# ConvGRU z|r conv (modules/gru.py:19-32, convz+convr fused): 3x3, 448 -> 256 channels
+ZR_FLOPS_PER_PIXEL = 2 * 256 * 448 * 9
 
 
 LOOKUP_FN = ["corr_pyramid_lookup_nhwc"]
@@ -80,14 +85,14 @@ class KernelTimer:
     """HIP events around every call of a droid_backends entry point, on the
     stream it launches on (torch's current stream)."""
 
-    def __init__(self, module, name):
+    def __init__(self, module, name, when=None):
         self.module, self.name = module, name
         self.orig = getattr(module, name)
         self.events = []
         self.active = False
 
         def wrapped(*a, **k):
-            if not self.active:
+            if not self.active or (when is not None and not when(*a, **k)):
                 return self.orig(*a, **k)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
@@ -168,12 +173,17 @@ def cpu_baseline(graph, video, args):
                           r["t_ba_iter"]))}
 
 
-def load_traffic():
-    p = os.path.join(ROOT, "profiles", "pmc_corr_lookup.json")
+def load_traffic(name, e_local):
+    """HBM bytes per launch from a committed PMC pass (profiles/pmc_<name>.json,
+    FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), scaled to
+    this launch's edge count; None when no measurement for this config exists."""
+    p = os.path.join(ROOT, "profiles", "pmc_%s.json" % name)
     if os.path.exists(p):
         try:
             with open(p) as f:
-                return json.load(f).get("traffic_bytes_per_launch")
+                d = json.load(f)
+            if d.get("edges") == e_local:
+                return d.get("traffic_bytes_per_launch")
         except Exception:
             return None
     return None
@@ -214,6 +224,9 @@ def main():
     import droid_backends
     LOOKUP_FN[0] = "corr_pyramid_lookup" if args.reference_op else "corr_pyramid_lookup_nhwc"
     lookup = KernelTimer(droid_backends, LOOKUP_FN[0])
+    zr = None
+    if not args.reference_op:
+        zr = KernelTimer(droid_backends, "conv_nhwc_f16", when=lambda *a, **k: k.get("epi") == droid_backends.EPI_GRU_ZR)
 
     with torch.no_grad():
         t_w = time.time()
@@ -226,6 +239,8 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(device)
         lookup.active = True
+        if zr:
+            zr.active = True
         t0 = time.perf_counter()
         for _ in range(args.steps):
             graph.update()
@@ -234,6 +249,8 @@ def main():
             dist.barrier()
         elapsed = time.perf_counter() - t0
         lookup.active = False
+        if zr:
+            zr.active = False
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -241,13 +258,28 @@ def main():
 
     finite = bool(torch.isfinite(video.poses).all() and torch.isfinite(video.disps).all())
     lookup_ms = lookup.mean_ms()
+    zr_ms = zr.mean_ms() if zr else None
     breakdown = stage_breakdown(graph, video) if args.breakdown else None
 
     if rank == 0:
         ms = 1000.0 * elapsed / args.steps
         bytes_per_launch = LOOKUP_BYTES_PER_EDGE * e_local
         achieved = bytes_per_launch / (lookup_ms * 1e-3) / 1e9 if lookup_ms else None
-        traffic = load_traffic()
+        lookup_roof = {"kernel": "corr_pyramid_f16_r3_kernel<%s> (4-level lookup)" % (
+            "NCHW" if args.reference_op else "NHWC"), "bound": "hbm",
+                       "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                       "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
+                       "traffic": load_traffic("corr_lookup", e_local), "launch_ms": lookup_ms,
+                       "algorithmic_bytes_per_launch": bytes_per_launch}
+        if zr_ms:
+            flops = ZR_FLOPS_PER_PIXEL * e_local * (args.ht // 8) * (args.wd // 8)
+            tf = flops / (zr_ms * 1e-3) / 1e12
+            roofline = {"kernel": "conv_rows_kernel<8> (ConvGRU z|r gates, 3x3 448->256, fp16 MFMA)",
+                        "bound": "mfma", "achieved": tf, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                        "frac": tf / PEAK_F16_TFLOPS, "traffic": load_traffic("conv_zr", e_local),
+                        "launch_ms": zr_ms, "algorithmic_flops_per_launch": flops}
+        else:
+            roofline, lookup_roof = lookup_roof, None
         result = {
             "metric": "factor_graph.update() iters/sec at 256 KF x 2k edges, 384x512",
             "value": 1000.0 / ms,
@@ -264,14 +296,11 @@ def main():
             "config": {"workload": "C3 global graph: update(itrs=2), volume corr", "keyframes": args.frames,
                        "edges": len(ii), "image": [args.ht, args.wd], "fmap": [args.ht // 8, args.wd // 8],
                        "parallelism": "edge-sharded x%d (RCCL all-reduce of reduced camera system)" % world},
-            "roofline": {"kernel": "corr_pyramid_f16_r3_kernel<%s> (4-level lookup)" % (
-                "NCHW" if args.reference_op else "NHWC"), "bound": "hbm",
-                         "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
-                         "traffic": traffic, "launch_ms": lookup_ms,
-                         "algorithmic_bytes_per_launch": bytes_per_launch},
+            "roofline": roofline,
             "state_finite": finite,
         }
+        if lookup_roof:
+            result["roofline_lookup"] = lookup_roof
         if breakdown:
             result["breakdown_ms"] = breakdown
         if world == 1 and not args.no_cpu_baseline:

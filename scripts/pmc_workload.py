@@ -1,0 +1,52 @@
+"""Workload for the PMC traffic passes (run under rocprofv3 --pmc; see
+scripts/pmc_traffic.sh): a 1 GiB device copy (calibration of the FETCH/WRITE
+counters on a known byte count), then the C3 ZR gate conv and the C3 4-level
+correlation lookup, each launched 3 times on synthetic data."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "droid-slam_amd"))
+import numpy as np
+import torch
+
+import droid_backends
+from droid_mi355x.corr import CorrBlock
+from droid_mi355x.fused import pack_conv
+
+E, H, W = 2048, 48, 64
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev).manual_seed(0)
+
+x = torch.empty(1 << 29, dtype=torch.float16, device=dev).fill_(1.0)   # 1 GiB
+y = torch.empty_like(x)
+for _ in range(3):
+    y.copy_(x)
+torch.cuda.synchronize()
+del x, y
+
+t = lambda c: (torch.randn((E, H, W, c), generator=g, device=dev) * 0.5).half()
+net, inp, cf, ff = t(128), t(128), t(128), t(64)
+w = torch.randn((256, 448, 3, 3), generator=g, device=dev) * 0.02
+wp = pack_conv(w, [128, 128, 128, 64])
+bias = torch.zeros(256, device=dev)
+bb = torch.zeros((E, 256), device=dev)
+z, rn = torch.empty_like(net), torch.empty_like(net)
+for _ in range(3):
+    droid_backends.conv_nhwc_f16([(net, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)], wp, 256, 3, bias=bias,
+                                 bbias=bb, epi=droid_backends.EPI_GRU_ZR, h=net, zout=z, rnet=rn)
+torch.cuda.synchronize()
+del net, inp, cf, ff, z, rn
+
+nf = 256
+f = torch.randn((1, nf, 128, H, W), generator=g, device=dev).half()
+rng = np.random.default_rng(0)
+ii = torch.as_tensor(rng.integers(0, nf, E), device=dev)
+jj = torch.as_tensor(rng.integers(0, nf, E), device=dev)
+cb = CorrBlock(f[:, ii], f[:, jj])
+coords = torch.stack(torch.meshgrid(torch.arange(W, device=dev), torch.arange(H, device=dev), indexing="xy"), -1)
+coords = (coords[None, None].float() + torch.randn((1, E, H, W, 2), generator=g, device=dev) * 3).contiguous()
+with torch.no_grad():
+    for _ in range(3):
+        cb.lookup_nhwc(coords)
+torch.cuda.synchronize()
+print("ok")
