@@ -11,8 +11,11 @@
 //                        [E w]^T diag(Q) [E w] on f32 MFMA (S and S-rhs at once)
 //   ba_assemble          deterministic gather of A - S into a dense fp64 matrix
 //                        with the rhs appended as its last row
-//   chol_*               blocked right-looking fp64 Cholesky (forward solve rides
-//                        along in the appended row), single-WG back solve
+//   chol_dataflow        ONE persistent launch: 64x64-tile right-looking fp64
+//                        Cholesky (forward solve rides along in the appended
+//                        row) and the back solve, as ~3k tile tasks handed out
+//                        by ticket in critical-path order and synchronised by
+//                        per-tile version counters (no grid barriers)
 //   ba_backsub           dz = Q (w - sum E^T dx) with the reference's t0 skip
 //   ba_retract           poses <- Exp(dx) poses
 #pragma once
@@ -34,6 +37,9 @@ enum ContribKind : int {
   kEdgeRhs = 2,     // +v12(ro+r) of edge src
   kSchurRhs = 3,    // -S_f(6*ra+r, wcol)
 };
+
+// tile tasks of the dataflow Cholesky (int4: type, i, j, k)
+enum CholTaskType : int { kPotrf = 0, kTrsm = 1, kUpdate = 2, kBsolve = 3, kBupd = 4 };
 
 struct Contrib {
   int kind, src, a0, a1;
@@ -58,15 +64,25 @@ struct BaPlan {
   std::vector<int> rhs_cptr;            // P+1
   std::vector<Contrib> contrib, rhs_contrib;
   long gram_floats = 0;
+  // reduced system: (n+1) rows of ld doubles (ld = n+1 rounded up to 8: 64-B rows)
+  int ld = 0;
+  // dataflow Cholesky
+  int nbc = 0, nbr = 0;                 // pivot column blocks, row blocks (incl. the rhs row)
+  std::vector<int> tasks;               // 4 ints per task, in ticket order
+  int ntasks = 0;
+  size_t sync_bytes = 0;                // ticket, abort, tile versions, y versions, x flags
   // device layout (byte offsets into the workspace)
   size_t off_ints = 0, off_hpart = 0, off_gram = 0, off_qw = 0, off_M = 0, off_x = 0,
-         off_flag = 0, total = 0;
+         off_flag = 0, off_sync = 0, off_linv = 0, off_ybuf = 0, total = 0;
   // offsets (in ints) of each int array inside the int section
   size_t o_ii, o_jj, o_kx, o_feptr, o_fedges, o_frptr, o_rpose, o_redge, o_fnb, o_fgoff,
-      o_blka, o_blkb, o_blkcptr, o_rhscptr, o_contrib, o_rhscontrib;
+      o_blka, o_blkb, o_blkcptr, o_rhscptr, o_contrib, o_rhscontrib, o_tasks;
   std::vector<int> ints;  // packed int section, uploaded once
   bool uploaded = false;
   void* uploaded_to = nullptr;
 };
+
+// dataflow Cholesky task list for an n-pivot augmented system (ba_plan.cpp)
+void build_chol_tasks(int n, int& nbc, int& nbr, std::vector<int>& tasks);
 
 }  // namespace droid

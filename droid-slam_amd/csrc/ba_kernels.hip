@@ -542,6 +542,421 @@ __global__ void __launch_bounds__(1024) chol_backsolve_kernel(const double* M, i
 }
 
 // ---------------------------------------------------------------------------
+// Dataflow Cholesky + solve: ONE persistent launch.
+//
+// The augmented system (n pivots, rhs as row n, rows of ld doubles) is cut
+// into 64x64 tiles.  Workgroups (one per CU) take tasks by ticket in the
+// host's critical-path order (ba_plan.cpp build_chol_tasks) and wait for
+// their inputs on per-tile version counters: ver(i,j) = number of updates
+// applied, +1 when the tile is final.  A task that is handed out only after
+// all its predecessors were handed out never waits on a workgroup that has
+// not started, so progress does not depend on residency.
+//
+// Cross-workgroup hand-off follows cdna_hip_programming.md Guideline 16 R1:
+// every handed-off byte (tiles, Linv, y, x) is stored AND loaded with sc1
+// buffer operations (write-through / L1 bypass), every storing wave drains
+// vmcnt before the workgroup barrier, then one lane stores the counter with
+// an agent-scope atomic; consumers poll relaxed.  Spins are bounded (an
+// abort word stops every workgroup).  Tiles are products of f64 MFMA
+// (v_mfma_f64_16x16x4f64); the diagonal factor is panel-blocked (16 wide)
+// with register rows and LDS column broadcasts, and also returns L_kk^-1 so
+// the off-diagonal solves are GEMMs.
+// ---------------------------------------------------------------------------
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+constexpr int LT = 66;          // LDS tile row stride (doubles): conflict-free f64 MFMA operand reads
+constexpr int kSc1 = 16;        // buffer-op aux bit: sc1
+constexpr unsigned kOobOff = 0x80000000u;
+constexpr unsigned kSpinLimit = 1u << 24;
+constexpr unsigned long long kSpinTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+constexpr int kCholLds = (3 * 64 * LT + 256 + 4 * 272) * 8 + 16;
+#ifdef DROID_CHOL_TRACE
+#define CHOL_TRACE(...) do { if (threadIdx.x == 0) printf(__VA_ARGS__); } while (0)
+#else
+#define CHOL_TRACE(...) do { } while (0)
+#endif
+// debug-only progress marks (DROID_CHOL_MARKS=<device address of an int[grid*4]>):
+// per workgroup {ticket, phase, wave-0 phase, heartbeat}, system-scope stores a
+// host copy engine can read while the kernel runs
+#define CHOL_MARK(slot, v)                                                                          \
+  do {                                                                                              \
+    if (d.marks && (threadIdx.x & 63) == 0)                                                         \
+      __hip_atomic_store(d.marks + 16 * blockIdx.x + 4 * (threadIdx.x >> 6) + (slot), (v),          \
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);                              \
+  } while (0)
+
+struct CholDev {
+  double* M;
+  int n, ld, nbc, nbr;
+  const int4* tasks;
+  int ntasks;
+  int* sync;    // [0] ticket [1] abort [4..] ver[nbr*nbc] | yver[nbc] | xdone[nbc]
+  int* flag;    // bit 0: factorisation failed (dx = 0), bit 1: spin timeout
+  double* linv; // [nbc][64][64]
+  double* ybuf; // [nbc*64]
+  double* x;    // [n]
+  float* dx;    // [n]
+  int debug;    // unused (tracing is compile-time: DROID_CHOL_TRACE)
+  int* marks;   // debug progress marks or null
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mkrs(const void* p, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ dbl2 ld2(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(dbl2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kSc1));
+}
+__device__ __forceinline__ void st2(__amdgpu_buffer_rsrc_t r, unsigned off, dbl2 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, kSc1);
+}
+__device__ __forceinline__ double ld1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, kSc1));
+}
+__device__ __forceinline__ void st1(__amdgpu_buffer_rsrc_t r, unsigned off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)off, 0, kSc1);
+}
+
+// rows [R0,R0+nr) x cols [C0,C0+nc) of a row-major matrix with `ld` doubles per
+// row -> LDS T[64][LT]; zeros elsewhere (out-of-range offsets read 0).  nc even.
+__device__ __forceinline__ void tile_load(__amdgpu_buffer_rsrc_t r, int ld, int R0, int C0, int nr, int nc,
+                                          double* T) {
+  dbl2 v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
+    const unsigned off = (rr < nr && cc < nc) ? (unsigned)(((size_t)(R0 + rr) * ld + C0 + cc) * 8) : kOobOff;
+    v[q] = ld2(r, off);
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
+    *reinterpret_cast<dbl2*>(&T[rr * LT + cc]) = v[q];
+  }
+}
+__device__ __forceinline__ void tile_store(__amdgpu_buffer_rsrc_t r, int ld, int R0, int C0, int nr, int nc,
+                                           const double* T) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
+    if (rr < nr && cc < nc)
+      st2(r, (unsigned)(((size_t)(R0 + rr) * ld + C0 + cc) * 8), *reinterpret_cast<const dbl2*>(&T[rr * LT + cc]));
+  }
+}
+
+// MFMA f64 16x16x4: A operand lane l = A[l&15][l>>4], B operand lane l =
+// B[l>>4][l&15], D: acc[q] = D[4*q + (l>>4)][l&15]  (NOT the f32/f16 16x16
+// layout; measured on gfx950 by scripts/probe/mfma_f64_layout.hip).
+__device__ __forceinline__ dbl4 mfma64(double a, double b, dbl4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// the wave's 32x32 quadrant (wr, wc) of a 64x64 tile: acc += sgn * A B^T, K = 64
+__device__ __forceinline__ void gemm_nt64(const double* A, const double* B, dbl4 (&acc)[2][2], int wr, int wc,
+                                          int lane, double sgn) {
+  const int fr = lane & 15, fk = lane >> 4;
+#pragma unroll 4
+  for (int k0 = 0; k0 < 64; k0 += 4) {
+    const double a0 = sgn * A[(wr + fr) * LT + k0 + fk], a1 = sgn * A[(wr + 16 + fr) * LT + k0 + fk];
+    const double b0 = B[(wc + fr) * LT + k0 + fk], b1 = B[(wc + 16 + fr) * LT + k0 + fk];
+    acc[0][0] = mfma64(a0, b0, acc[0][0]);
+    acc[0][1] = mfma64(a0, b1, acc[0][1]);
+    acc[1][0] = mfma64(a1, b0, acc[1][0]);
+    acc[1][1] = mfma64(a1, b1, acc[1][1]);
+  }
+}
+__device__ __forceinline__ void acc_load(const double* T, dbl4 (&acc)[2][2], int wr, int wc, int lane) {
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc[a][b][q] = T[(wr + 16 * a + 4 * q + (lane >> 4)) * LT + wc + 16 * b + (lane & 15)];
+}
+__device__ __forceinline__ void acc_store(double* T, const dbl4 (&acc)[2][2], int wr, int wc, int lane) {
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        T[(wr + 16 * a + 4 * q + (lane >> 4)) * LT + wc + 16 * b + (lane & 15)] = acc[a][b][q];
+}
+
+// every storing wave drains, then one lane publishes (Guideline 16 R1)
+__device__ __forceinline__ void publish(int* w, int v, int* w2 = nullptr, int v2 = 0) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w2) __hip_atomic_store(w2, v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ bool poll_ge(int* w, int target, int* abort_w, int* flag) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  for (unsigned s = 0;; ++s) {
+    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+    if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    if (s > kSpinLimit || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+      __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicOr(flag, 2);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// 16-wide panel of the diagonal factor: wave 0, lane r owns row r's panel
+// values in registers; the scaled pivot column is broadcast through LDS.
+__device__ __forceinline__ void panel_factor(double* T, double* col, int c0, int pw, int lane, int* flag) {
+  double v[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = T[lane * LT + c0 + q];
+#pragma unroll
+  for (int jj = 0; jj < 16; ++jj) {
+    if (jj < pw) {
+      const int jr = c0 + jj;
+      if (lane == jr) col[64] = v[jj];          // pivot broadcast through LDS
+      asm volatile("" ::: "memory");
+      const double piv = col[64];
+      if (lane == 0 && !(piv > 0.0 && piv < 1e300)) atomicOr(flag, 1);
+      const double sd = sqrt(piv), inv = 1.0 / sd;
+      v[jj] = (lane == jr) ? sd : ((lane > jr) ? v[jj] * inv : v[jj]);
+      col[lane] = v[jj];
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int q = jj + 1; q < 16; ++q) {
+        const double lc = col[c0 + q];
+        v[q] = (c0 + q <= lane) ? fma(-v[jj], lc, v[q]) : v[q];
+      }
+      asm volatile("" ::: "memory");
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) T[lane * LT + c0 + q] = v[q];
+}
+
+__global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* T0 = sm;
+  double* T1 = sm + 64 * LT;
+  double* T2 = sm + 2 * 64 * LT;
+  double* vec = sm + 3 * 64 * LT;        // 256
+  double* scr = vec + 256;               // [4][16][17]
+  int* shi = reinterpret_cast<int*>(scr + 4 * 272);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: wave-conditional code branches, never masks
+  const int fr = lane & 15, fk = lane >> 4;
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+  const int n = d.n, ld = d.ld, nbc = d.nbc, nbr = d.nbr;
+  const __amdgpu_buffer_rsrc_t rM = mkrs(d.M, (size_t)(n + 1) * ld * 8);
+  const __amdgpu_buffer_rsrc_t rL = mkrs(d.linv, (size_t)nbc * 4096 * 8);
+  const __amdgpu_buffer_rsrc_t rY = mkrs(d.ybuf, (size_t)nbc * 64 * 8);
+  const __amdgpu_buffer_rsrc_t rX = mkrs(d.x, (size_t)n * 8);
+  int* ticket = d.sync;
+  int* abort_w = d.sync + 1;
+  int* ver = d.sync + 4;
+  int* yver = ver + nbr * nbc;
+  int* xdone = yver + nbc;
+
+  int nbar = 0;
+#define BAR() do { ++nbar; CHOL_MARK(3, nbar); __syncthreads(); } while (0)
+  for (;;) {
+    if (tid == 0) shi[0] = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    BAR();
+    const int tk = __builtin_amdgcn_readfirstlane(shi[0]);
+    CHOL_MARK(0, tk);
+    CHOL_MARK(1, 1);
+    CHOL_TRACE("[chol] wg %d got ticket %d\n", (int)blockIdx.x, tk);
+    if (tk >= d.ntasks) break;
+    const int4 tsk = d.tasks[tk];
+    const int type = __builtin_amdgcn_readfirstlane(tsk.x), i = __builtin_amdgcn_readfirstlane(tsk.y);
+    const int j = __builtin_amdgcn_readfirstlane(tsk.z), k = __builtin_amdgcn_readfirstlane(tsk.w);
+    CHOL_TRACE("[chol] wg %d ticket %d task %d (%d,%d,%d)\n", (int)blockIdx.x, tk, type, i, j, k);
+    if (tid == 0) {
+      bool ok = true;
+      switch (type) {
+        case kPotrf: ok = poll_ge(&ver[k * nbc + k], k, abort_w, d.flag); break;
+        case kTrsm:
+          ok = poll_ge(&ver[i * nbc + k], k, abort_w, d.flag) && poll_ge(&ver[k * nbc + k], k + 1, abort_w, d.flag);
+          break;
+        case kUpdate:
+          ok = poll_ge(&ver[i * nbc + j], k, abort_w, d.flag) && poll_ge(&ver[i * nbc + k], k + 1, abort_w, d.flag) &&
+               poll_ge(&ver[j * nbc + k], k + 1, abort_w, d.flag);
+          break;
+        case kBsolve:
+          ok = poll_ge(&ver[i * nbc + i], i + 1, abort_w, d.flag) &&
+               poll_ge(&yver[i], 1 + (nbc - 1 - i), abort_w, d.flag);
+          break;
+        default:  // kBupd (r = i, c = j)
+          ok = poll_ge(&xdone[i], 1, abort_w, d.flag) && poll_ge(&ver[i * nbc + j], j + 1, abort_w, d.flag) &&
+               poll_ge(&yver[j], 1 + (nbc - 1 - i), abort_w, d.flag);
+          break;
+      }
+      shi[1] = ok ? 1 : 0;
+    }
+    BAR();
+    CHOL_TRACE("[chol] wg %d ticket %d deps %s\n", (int)blockIdx.x, tk, shi[1] ? "ok" : "ABORT");
+    if (!__builtin_amdgcn_readfirstlane(shi[1])) break;
+    CHOL_MARK(1, 2);
+
+    if (type == kPotrf) {
+      const int R0 = 64 * k, Bp = min(64, n - R0), Br = min(64, n + 1 - R0);
+      tile_load(rM, ld, R0, R0, Br, Bp, T0);
+      BAR();
+      CHOL_TRACE("[chol] potrf %d loaded Bp %d Br %d\n", k, Bp, Br);
+      for (int c0 = 0; c0 < Bp; c0 += 16) {
+        CHOL_MARK(1, 100 + c0);
+        if (wave == 0) panel_factor(T0, vec, c0, min(16, Bp - c0), lane, d.flag);
+        if (wave == 0) CHOL_MARK(2, 100 + c0);
+        BAR();
+        CHOL_MARK(1, 200 + c0);
+        CHOL_TRACE("[chol] potrf %d panel %d done\n", k, c0);
+        const int s0 = c0 + 16;
+        const int nt = (64 - s0) / 16;
+        for (int ti = wave; ti < nt * nt; ti += 4) {
+          const int R = s0 + 16 * (ti / nt), C = s0 + 16 * (ti % nt);
+          if (C > R) continue;
+          dbl4 acc;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q] = T0[(R + 4 * q + fk) * LT + C + fr];
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+            acc = mfma64(-T0[(R + fr) * LT + c0 + 4 * kk + fk], T0[(C + fr) * LT + c0 + 4 * kk + fk], acc);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) T0[(R + 4 * q + fk) * LT + C + fr] = acc[q];
+        }
+        BAR();
+      }
+      CHOL_TRACE("[chol] potrf %d factored\n", k);
+      CHOL_MARK(1, 300);
+      // Linv of the Bp x Bp pivot block (unit-diagonal padding past Bp)
+      for (int idx = tid; idx < 64 * 64; idx += 256) {
+        const int r = idx >> 6, c = idx & 63;
+        T2[r * LT + c] = (r < Bp) ? (c <= r ? T0[r * LT + c] : 0.0) : (r == c ? 1.0 : 0.0);
+        T1[r * LT + c] = 0.0;
+      }
+      BAR();
+      if (wave == 0) {  // the four 16x16 diagonal blocks; lane = 16 * block + column
+        const int base = 16 * (lane >> 4), cc = lane & 15;
+        double xv[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          double sacc = (t == cc) ? 1.0 : 0.0;
+#pragma unroll
+          for (int u = 0; u < t; ++u) sacc = fma(-T2[(base + t) * LT + base + u], xv[u], sacc);
+          xv[t] = sacc / T2[(base + t) * LT + base + t];
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t) T1[(base + t) * LT + base + cc] = xv[t];
+      }
+      BAR();
+      for (int I = 1; I < 4; ++I) {  // Linv[I][J] = -Dinv_I sum_{K=J}^{I-1} L[I][K] Linv[K][J]
+        if (wave < I) {
+          const int J = wave;
+          dbl4 S = {0.0, 0.0, 0.0, 0.0};
+          for (int K = J; K < I; ++K)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+              S = mfma64(T2[(16 * I + fr) * LT + 16 * K + 4 * kk + fk], T1[(16 * K + 4 * kk + fk) * LT + 16 * J + fr], S);
+          double* sw = scr + wave * 272;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sw[(4 * q + fk) * 17 + fr] = S[q];
+          asm volatile("" ::: "memory");
+          dbl4 R = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+            R = mfma64(-T1[(16 * I + fr) * LT + 16 * I + 4 * kk + fk], sw[(4 * kk + fk) * 17 + fr], R);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) T1[(16 * I + 4 * q + fk) * LT + 16 * J + fr] = R[q];
+        }
+        BAR();
+        CHOL_TRACE("[chol] potrf %d linv row %d\n", k, I);
+      }
+      CHOL_MARK(1, 400);
+      tile_store(rM, ld, R0, R0, Br, Bp, T0);
+      tile_store(rL, 64, R0, 0, 64, 64, T1);
+      const bool rhs = Br > Bp;
+      if (rhs && tid < 32) st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[Bp * LT + 2 * tid]));
+      CHOL_TRACE("[chol] potrf %d stored\n", k);
+      publish(&ver[k * nbc + k], k + 1, rhs ? &yver[k] : nullptr, 1);
+      CHOL_TRACE("[chol] potrf %d published\n", k);
+    } else if (type == kTrsm) {
+      const int R0 = 64 * i, C0 = 64 * k, nr = min(64, n + 1 - R0), nc = min(64, n - C0);
+      tile_load(rM, ld, R0, C0, nr, nc, T0);
+      tile_load(rL, 64, C0, 0, 64, 64, T1);
+      BAR();
+      CHOL_TRACE("[chol] trsm %d,%d loaded\n", i, k);
+      dbl4 acc[2][2] = {};
+      gemm_nt64(T0, T1, acc, wr, wc, lane, 1.0);
+      BAR();
+      CHOL_TRACE("[chol] trsm %d,%d gemm\n", i, k);
+      acc_store(T0, acc, wr, wc, lane);
+      BAR();
+      tile_store(rM, ld, R0, C0, nr, nc, T0);
+      const bool rhs = (i == nbr - 1);
+      if (rhs && tid < 32) st2(rY, (unsigned)((C0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[(n - R0) * LT + 2 * tid]));
+      CHOL_TRACE("[chol] trsm %d,%d stored\n", i, k);
+      publish(&ver[i * nbc + k], k + 1, rhs ? &yver[k] : nullptr, 1);
+      CHOL_TRACE("[chol] trsm %d,%d published\n", i, k);
+    } else if (type == kUpdate) {
+      const int Ri = 64 * i, Rj = 64 * j, Ck = 64 * k;
+      const int nri = min(64, n + 1 - Ri), ncj = min(64, n - Rj), nck = min(64, n - Ck);
+      tile_load(rM, ld, Ri, Ck, nri, nck, T0);
+      tile_load(rM, ld, Rj, Ck, ncj, nck, T1);
+      tile_load(rM, ld, Ri, Rj, nri, ncj, T2);
+      BAR();
+      dbl4 acc[2][2];
+      acc_load(T2, acc, wr, wc, lane);
+      gemm_nt64(T0, T1, acc, wr, wc, lane, -1.0);
+      acc_store(T2, acc, wr, wc, lane);
+      BAR();
+      tile_store(rM, ld, Ri, Rj, nri, ncj, T2);
+      publish(&ver[i * nbc + j], k + 1);
+    } else if (type == kBsolve) {
+      const int C0 = 64 * i, Bp = min(64, n - C0);
+      tile_load(rL, 64, C0, 0, 64, 64, T1);
+      CHOL_TRACE("[chol] bsolve %d tile issued\n", i);
+      if (tid < 32) {
+        const dbl2 yv = ld2(rY, 2 * tid < Bp ? (unsigned)((C0 + 2 * tid) * 8) : kOobOff);
+        vec[2 * tid] = yv[0];
+        vec[2 * tid + 1] = yv[1];
+      }
+      BAR();
+      if (wave == 0) {
+        double sacc = 0.0;
+#pragma unroll 8
+        for (int t = 0; t < 64; ++t) sacc = fma(T1[t * LT + lane], vec[t], sacc);
+        const bool failed = (__hip_atomic_load(d.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1) != 0;
+        if (lane < Bp) {
+          st1(rX, (unsigned)((C0 + lane) * 8), sacc);
+          d.dx[C0 + lane] = failed ? 0.0f : (float)sacc;
+        }
+      }
+      CHOL_TRACE("[chol] bsolve %d computed\n", i);
+      publish(&xdone[i], 1);
+      CHOL_TRACE("[chol] bsolve %d published\n", i);
+    } else {  // kBupd: y_c -= L_rc^T x_r
+      const int R0 = 64 * i, C0 = 64 * j, nr = min(64, n - R0), nc = min(64, n - C0);
+      tile_load(rM, ld, R0, C0, nr, nc, T0);
+      if (tid < 64) vec[tid] = ld1(rX, tid < nr ? (unsigned)((R0 + tid) * 8) : kOobOff);
+      else if (tid < 128) vec[tid] = ld1(rY, tid - 64 < nc ? (unsigned)((C0 + tid - 64) * 8) : kOobOff);
+      BAR();
+      if (wave == 0) {
+        double sacc = vec[64 + lane];
+#pragma unroll 8
+        for (int t = 0; t < 64; ++t) sacc = fma(-T0[t * LT + lane], vec[t], sacc);
+        if (lane < nc) st1(rY, (unsigned)((C0 + lane) * 8), sacc);
+      }
+      publish(&yver[j], 1 + (nbc - i));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Kernel D: back substitution dz = Q (w - sum_rows E_row . dx[pose]) with the
 // EvT6x1 skip of rows whose pose index is <= 0 (:1105), then disps += dz.
 // grid = (ceil(HW/256), K).
@@ -673,10 +1088,83 @@ static BaDev make_dev(BaPlan& p, char* ws) {
   d.x = reinterpret_cast<double*>(ws + p.off_x);
   d.flag = reinterpret_cast<int*>(ws + p.off_flag);
   d.E = p.E; d.N = p.N; d.H = p.H; d.W = p.W; d.HW = p.HW;
-  d.t0 = p.t0; d.t1 = p.t1; d.P = p.P; d.K = p.K; d.n = p.n; d.ld = p.n + 1;
+  d.t0 = p.t0; d.t1 = p.t1; d.P = p.P; d.K = p.K; d.n = p.n; d.ld = p.ld;
   d.eta_rows = p.eta_rows; d.nsplit = p.nsplit; d.nchunk = p.nchunk; d.gpw = p.group_per_wave;
   d.nblk = (int)p.blk_a.size();
   return d;
+}
+
+// the previous launch-per-step blocked factorisation (A/B reference: DROID_CHOL=blocked)
+static int chol_blocked(const BaDev& d, int n, int ld, float* dx, hipStream_t stream) {
+  const int ncolblk = ceil_div(n, CB), nrowblk = ceil_div(n + 1, CB);
+  for (int kb = 0; kb < ncolblk; ++kb) {
+    const int k0 = CB * kb;
+    chol_diag_kernel<<<1, 64, 0, stream>>>(d.M, n, ld, k0, d.flag);
+    const int below = nrowblk - kb - 1;
+    if (below > 0) {
+      chol_trsm_kernel<<<below, 64, 0, stream>>>(d.M, n, ld, k0);
+      chol_update_kernel<<<dim3(below, below), 256, 0, stream>>>(d.M, n, ld, k0);
+    }
+  }
+  DROID_LAUNCH_CHECK();
+  static int backsolve_lds = 0;
+  const int need = n * (int)sizeof(double);
+  if (need > backsolve_lds) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&chol_backsolve_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, need));
+    backsolve_lds = need;
+  }
+  if (need > 160 * 1024) return fail(kUnsupported, "ba: reduced system too large for the single-WG back solve");
+  chol_backsolve_kernel<<<1, 1024, (size_t)n * sizeof(double), stream>>>(d.M, n, ld, d.flag, d.x, dx);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+static bool use_dataflow_chol() {
+  static const bool on = [] {
+    const char* e = getenv("DROID_CHOL");
+    return !(e && std::string(e) == "blocked");
+  }();
+  return on;
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+static int launch_chol_dataflow(const BaPlan& p, char* ws, const BaDev& bd, float* dx, hipStream_t stream) {
+  if ((size_t)(p.n + 1) * p.ld * 8 >= 0x80000000ull)
+    return fail(kUnsupported, "ba: reduced system exceeds the 2 GB dense-solver limit");
+  CholDev c{};
+  c.M = bd.M; c.n = p.n; c.ld = p.ld; c.nbc = p.nbc; c.nbr = p.nbr;
+  c.tasks = reinterpret_cast<const int4*>(reinterpret_cast<const int*>(ws + p.off_ints) + p.o_tasks);
+  c.ntasks = p.ntasks;
+  c.sync = reinterpret_cast<int*>(ws + p.off_sync);
+  c.flag = bd.flag;
+  c.linv = reinterpret_cast<double*>(ws + p.off_linv);
+  c.ybuf = reinterpret_cast<double*>(ws + p.off_ybuf);
+  c.x = bd.x;
+  c.dx = dx;
+  static int* const marks = getenv("DROID_CHOL_MARKS") ? reinterpret_cast<int*>(strtoull(getenv("DROID_CHOL_MARKS"), nullptr, 0)) : nullptr;
+  c.marks = marks;
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&chol_dataflow_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kCholLds));
+    attr = true;
+  }
+  DROID_HIP_CHECK(hipMemsetAsync(c.sync, 0, p.sync_bytes, stream));
+  const int grid = std::min(p.ntasks, num_cus());
+  chol_dataflow_kernel<<<grid, 256, kCholLds, stream>>>(c);
+  DROID_LAUNCH_CHECK();
+  return kOk;
 }
 
 }  // namespace droid
@@ -722,7 +1210,7 @@ int droid_ba_build_system(void* plan, void* workspace, float* poses, float* disp
     if (st) return st;
     DROID_LAUNCH_CHECK();
   }
-  DROID_HIP_CHECK(hipMemsetAsync(d.M, 0, (size_t)(p->n + 1) * (p->n + 1) * sizeof(double), stream));
+  DROID_HIP_CHECK(hipMemsetAsync(d.M, 0, (size_t)(p->n + 1) * p->ld * sizeof(double), stream));
   ba_assemble_kernel<<<d.nblk + p->P, 64, 0, stream>>>(d);
   DROID_LAUNCH_CHECK();
   return kOk;
@@ -741,38 +1229,44 @@ int droid_ba_solve_update(void* plan, void* workspace, float* poses, float* disp
   d.poses = poses; d.disps = disps; d.intr = intrinsics; d.disps_sens = disps_sens;
   d.targets = targets; d.weights = weights; d.eta = eta; d.dx = dx; d.dz = dz;
   d.lm = lm; d.ep = ep;
-  const int n = p->n, ld = p->n + 1;
-  ba_damp_kernel<<<ceil_div(n, 256), 256, 0, stream>>>(d.M, n, ld, lm, ep, d.flag);
+  const int n = p->n, ld = p->ld;
+  ba_damp_kernel<<<ceil_div(std::max(n, 1), 256), 256, 0, stream>>>(d.M, n, ld, lm, ep, d.flag);
   DROID_LAUNCH_CHECK();
-  const int ncolblk = ceil_div(n, CB), nrowblk = ceil_div(n + 1, CB);
-  for (int kb = 0; kb < ncolblk; ++kb) {
-    const int k0 = CB * kb;
-    chol_diag_kernel<<<1, 64, 0, stream>>>(d.M, n, ld, k0, d.flag);
-    const int below = nrowblk - kb - 1;
-    if (below > 0) {
-      chol_trsm_kernel<<<below, 64, 0, stream>>>(d.M, n, ld, k0);
-      chol_update_kernel<<<dim3(below, below), 256, 0, stream>>>(d.M, n, ld, k0);
-    }
+  if (n > 0 && use_dataflow_chol()) {
+    st = launch_chol_dataflow(*p, static_cast<char*>(workspace), d, dx, stream);
+    if (st) return st;
+  } else if (n > 0) {
+    st = chol_blocked(d, n, ld, dx, stream);
+    if (st) return st;
   }
-  DROID_LAUNCH_CHECK();
-  static int backsolve_lds = 0;
-  const int need = n * (int)sizeof(double);
-  if (need > backsolve_lds) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&chol_backsolve_kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, need));
-    backsolve_lds = need;
-  }
-  if (need > 160 * 1024) return fail(kUnsupported, "ba: reduced system too large for the single-WG back solve");
-  chol_backsolve_kernel<<<1, 1024, (size_t)n * sizeof(double), stream>>>(d.M, n, ld, d.flag, d.x, dx);
-  DROID_LAUNCH_CHECK();
   if (!p->motion_only && p->K > 0) {
     if (!dz) return fail(kInvalidArgument, "ba: dz output required unless motion_only");
     ba_backsub_kernel<<<dim3(ceil_div(p->HW, 256), p->K), 256, 0, stream>>>(d);
     DROID_LAUNCH_CHECK();
   }
-  ba_retract_kernel<<<ceil_div(p->P, 64), 64, 0, stream>>>(poses, dx, p->t0, p->P);
+  ba_retract_kernel<<<ceil_div(std::max(p->P, 1), 64), 64, 0, stream>>>(poses, dx, p->t0, p->P);
   DROID_LAUNCH_CHECK();
   return kOk;
+}
+
+
+// Dense damped SPD solve on a chol plan (droid_chol_plan_create): diag += ep +
+// lm*diag, factor, dx = solution (0 and flag bit 0 set if not SPD).
+int droid_chol_solve(void* plan, void* workspace, float lm, float ep, float* dx, hipStream_t stream) {
+  auto* p = static_cast<BaPlan*>(plan);
+  int st = check_ready(p, workspace);
+  if (st) return st;
+  char* ws = static_cast<char*>(workspace);
+  BaDev d{};
+  d.M = reinterpret_cast<double*>(ws + p->off_M);
+  d.x = reinterpret_cast<double*>(ws + p->off_x);
+  d.flag = reinterpret_cast<int*>(ws + p->off_flag);
+  d.n = p->n;
+  d.ld = p->ld;
+  ba_damp_kernel<<<ceil_div(std::max(p->n, 1), 256), 256, 0, stream>>>(d.M, p->n, p->ld, lm, ep, d.flag);
+  DROID_LAUNCH_CHECK();
+  if (p->n == 0) return kOk;
+  return use_dataflow_chol() ? launch_chol_dataflow(*p, ws, d, dx, stream) : chol_blocked(d, p->n, p->ld, dx, stream);
 }
 
 // Full ba(): `iterations` GN steps on one device (droid_backends.ba).

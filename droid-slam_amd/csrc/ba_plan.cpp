@@ -5,7 +5,10 @@
 // once per edge set (cached by the caller), never inside the GN loop.
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <map>
+#include <queue>
+#include <tuple>
 #include <utility>
 
 #include "ba.hpp"
@@ -14,6 +17,101 @@
 namespace droid {
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Task DAG of the dataflow Cholesky (ba_kernels.hip: chol_dataflow_kernel) for
+// the augmented system with n pivots and the rhs as row n:
+//   POTRF(k)     factor tile (k,k) (+ the rhs row when it lies in that tile), Linv_k
+//   TRSM(i,k)    tile (i,k) <- A_ik Linv_k^T
+//   UPD(i,j,k)   tile (i,j) -= L_ik L_jk^T               (k < j <= i)
+//   BSOLVE(c)    x_c = Linv_c^T y_c
+//   BUPD(r,c)    y_c -= L_rc^T x_r                       (c < r, applied in order r = nbc-1 .. c+1)
+// Tickets are handed out in a list-scheduling order: among ready tasks, the
+// longest remaining path (estimated microseconds incl. one hop per edge) first.
+void build_chol_tasks(int n, int& nbc, int& nbr, std::vector<int>& out) {
+  nbc = (n + 63) / 64;
+  nbr = (n + 1 + 63) / 64;
+  out.clear();
+  if (n <= 0) return;
+  struct Node { int type, i, j, k; double cost; std::vector<int> succ; int npred; double bl; };
+  std::vector<Node> t;
+  std::map<std::tuple<int, int, int, int>, int> id;
+  auto add = [&](int type, int i, int j, int k, double cost) {
+    id[std::make_tuple(type, i, j, k)] = (int)t.size();
+    t.push_back({type, i, j, k, cost, {}, 0, 0.0});
+  };
+  for (int k = 0; k < nbc; ++k) {
+    add(kPotrf, k, k, k, 6.0);
+    for (int i = k + 1; i < nbr; ++i) add(kTrsm, i, k, k, 2.0);
+    for (int j = k + 1; j < nbc; ++j)
+      for (int i = j; i < nbr; ++i) add(kUpdate, i, j, k, 2.0);
+  }
+  for (int c = 0; c < nbc; ++c) {
+    add(kBsolve, c, c, c, 1.0);
+    for (int r = c + 1; r < nbc; ++r) add(kBupd, r, c, c, 1.0);
+  }
+  auto get = [&](int type, int i, int j, int k) { return id.at(std::make_tuple(type, i, j, k)); };
+  auto fin = [&](int i, int k) { return i == k ? get(kPotrf, k, k, k) : get(kTrsm, i, k, k); };
+  auto edge = [&](int a, int b) {
+    for (int x : t[a].succ)
+      if (x == b) return;
+    t[a].succ.push_back(b);
+    t[b].npred++;
+  };
+  for (int v = 0; v < (int)t.size(); ++v) {
+    const Node nd = t[v];
+    switch (nd.type) {
+      case kPotrf:
+        if (nd.k > 0) edge(get(kUpdate, nd.k, nd.k, nd.k - 1), v);
+        break;
+      case kTrsm:
+        edge(get(kPotrf, nd.k, nd.k, nd.k), v);
+        if (nd.k > 0) edge(get(kUpdate, nd.i, nd.k, nd.k - 1), v);
+        break;
+      case kUpdate:
+        edge(fin(nd.i, nd.k), v);
+        edge(fin(nd.j, nd.k), v);
+        if (nd.k > 0) edge(get(kUpdate, nd.i, nd.j, nd.k - 1), v);
+        break;
+      case kBsolve:
+        edge(get(kPotrf, nd.i, nd.i, nd.i), v);
+        edge(nd.i == nbc - 1 ? fin(nbr - 1, nd.i) : get(kBupd, nd.i + 1, nd.i, nd.i), v);
+        break;
+      case kBupd:
+        edge(get(kBsolve, nd.i, nd.i, nd.i), v);
+        edge(fin(nd.i, nd.j), v);
+        edge(nd.i == nbc - 1 ? fin(nbr - 1, nd.j) : get(kBupd, nd.i + 1, nd.j, nd.j), v);
+        break;
+    }
+  }
+  // bottom levels (reverse topological order)
+  std::vector<int> order, indeg(t.size());
+  for (size_t v = 0; v < t.size(); ++v) indeg[v] = t[v].npred;
+  for (size_t v = 0; v < t.size(); ++v)
+    if (!indeg[v]) order.push_back((int)v);
+  for (size_t q = 0; q < order.size(); ++q)
+    for (int s2 : t[order[q]].succ)
+      if (--indeg[s2] == 0) order.push_back(s2);
+  for (int q = (int)order.size() - 1; q >= 0; --q) {
+    Node& nd = t[order[q]];
+    double m = 0.0;
+    for (int s2 : nd.succ) m = std::max(m, 1.0 + t[s2].bl);
+    nd.bl = nd.cost + m;
+  }
+  // list scheduling by bottom level
+  auto cmp = [&](int a, int b) { return t[a].bl != t[b].bl ? t[a].bl < t[b].bl : a > b; };
+  std::priority_queue<int, std::vector<int>, decltype(cmp)> ready(cmp);
+  for (size_t v = 0; v < t.size(); ++v) {
+    indeg[v] = t[v].npred;
+    if (!indeg[v]) ready.push((int)v);
+  }
+  while (!ready.empty()) {
+    const int v = ready.top();
+    ready.pop();
+    out.push_back(t[v].type); out.push_back(t[v].i); out.push_back(t[v].j); out.push_back(t[v].k);
+    for (int s2 : t[v].succ)
+      if (--indeg[s2] == 0) ready.push(s2);
+  }
+}
 
 static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, int N, int H, int W,
                       int t0, int t1, int eta_rows, int motion_only, int own_lo, int own_hi) {
@@ -155,7 +253,12 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, in
   p.o_blka = put(p.blk_a); p.o_blkb = put(p.blk_b); p.o_blkcptr = put(p.blk_cptr);
   p.o_rhscptr = put(p.rhs_cptr);
   p.o_contrib = putc(p.contrib); p.o_rhscontrib = putc(p.rhs_contrib);
+  build_chol_tasks(p.n, p.nbc, p.nbr, p.tasks);
+  p.ntasks = (int)p.tasks.size() / 4;
+  p.o_tasks = put(p.tasks);
   if (p.ints.empty()) p.ints.push_back(0);
+  p.ld = (p.n + 1 + 7) / 8 * 8;
+  p.sync_bytes = align_up((size_t)(4 + p.nbr * p.nbc + 2 * p.nbc) * 4, 16);
 
   // workspace layout
   size_t off = 0;
@@ -163,9 +266,12 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, in
   p.off_hpart = off; off = align_up(off + (size_t)std::max(E, 1) * p.nsplit * kHessStride * 4, 256);
   p.off_gram = off; off = align_up(off + (size_t)std::max(p.gram_floats, 1L) * 4, 256);
   p.off_qw = off; off = align_up(off + (size_t)2 * p.K * HW * 4 + 4, 256);
-  p.off_M = off; off = align_up(off + (size_t)(p.n + 1) * (p.n + 1) * 8, 256);
+  p.off_M = off; off = align_up(off + (size_t)(p.n + 1) * p.ld * 8, 256);
   p.off_x = off; off = align_up(off + (size_t)(p.n + 1) * 8, 256);
   p.off_flag = off; off = align_up(off + 64, 256);
+  p.off_sync = off; off = align_up(off + p.sync_bytes, 256);
+  p.off_linv = off; off = align_up(off + (size_t)std::max(p.nbc, 1) * 64 * 64 * 8, 256);
+  p.off_ybuf = off; off = align_up(off + (size_t)std::max(p.nbc, 1) * 64 * 8, 256);
   p.total = off;
   return kOk;
 }
@@ -186,6 +292,52 @@ int droid_ba_plan_create(const int64_t* ii, const int64_t* jj, int num_edges, in
                       own_lo, own_hi);
   if (st != kOk) { delete p; return st; }
   *plan_out = p;
+  return kOk;
+}
+
+// Dense SPD solve of an augmented system on the dataflow Cholesky alone (no
+// BA): n pivots, ld = n+1 rounded up to 8; rows 0..n-1 hold the lower
+// triangle of A, row n the rhs b (droid_ba_plan_system_region locates it).
+int droid_chol_plan_create(int n, void** plan_out) {
+  if (!plan_out || n < 0) return fail(kInvalidArgument, "chol_plan_create: bad arguments");
+  auto* p = new BaPlan();
+  p->n = n;
+  p->P = 0;
+  p->motion_only = 1;
+  build_chol_tasks(n, p->nbc, p->nbr, p->tasks);
+  p->ntasks = (int)p->tasks.size() / 4;
+  p->ints = p->tasks;
+  p->o_tasks = 0;
+  if (p->ints.empty()) p->ints.push_back(0);
+  p->ld = (n + 1 + 7) / 8 * 8;
+  p->sync_bytes = align_up((size_t)(4 + p->nbr * p->nbc + 2 * p->nbc) * 4, 16);
+  size_t off = 0;
+  p->off_ints = off; off = align_up(off + p->ints.size() * 4, 256);
+  p->off_M = off; off = align_up(off + (size_t)(n + 1) * p->ld * 8, 256);
+  p->off_x = off; off = align_up(off + (size_t)(n + 1) * 8, 256);
+  p->off_flag = off; off = align_up(off + 64, 256);
+  p->off_sync = off; off = align_up(off + p->sync_bytes, 256);
+  p->off_linv = off; off = align_up(off + (size_t)std::max(p->nbc, 1) * 64 * 64 * 8, 256);
+  p->off_ybuf = off; off = align_up(off + (size_t)std::max(p->nbc, 1) * 64 * 8, 256);
+  p->total = off;
+  *plan_out = p;
+  return kOk;
+}
+
+int droid_chol_plan_info(const void* plan, int* ld, int* ntasks, int* flag_offset) {
+  auto* p = static_cast<const BaPlan*>(plan);
+  if (!p) return fail(kInvalidArgument, "chol_plan_info: null plan");
+  if (ld) *ld = p->ld;
+  if (ntasks) *ntasks = p->ntasks;
+  if (flag_offset) *flag_offset = (int)p->off_flag;
+  return kOk;
+}
+
+// the plan's Cholesky task list in ticket order (4 ints per task: type, i, j, k)
+int droid_chol_plan_tasks(const void* plan, int* out) {
+  auto* p = static_cast<const BaPlan*>(plan);
+  if (!p || !out) return fail(kInvalidArgument, "chol_plan_tasks: null argument");
+  std::copy(p->tasks.begin(), p->tasks.end(), out);
   return kOk;
 }
 
@@ -212,13 +364,14 @@ int droid_ba_plan_kx(const void* plan, int64_t* out) {
   return kOk;
 }
 
-// Byte offset/size of the reduced system (augmented (n+1)x(n+1) fp64, rhs in
-// the last row) inside the workspace: the buffer a multi-GPU caller all-reduces.
+// Byte offset/size of the reduced system (augmented, n+1 rows of ld fp64 with
+// ld = n+1 rounded up to 8, rhs in the last row) inside the workspace: the
+// buffer a multi-GPU caller all-reduces.
 int droid_ba_plan_system_region(const void* plan, size_t* offset, size_t* bytes) {
   auto* p = static_cast<const BaPlan*>(plan);
   if (!p) return fail(kInvalidArgument, "ba_plan_system_region: null plan");
   *offset = p->off_M;
-  *bytes = (size_t)(p->n + 1) * (p->n + 1) * 8;
+  *bytes = (size_t)(p->n + 1) * p->ld * 8;
   return kOk;
 }
 

@@ -333,7 +333,9 @@ class BaPlan:
         off, sz = ctypes.c_size_t(), ctypes.c_size_t()
         check(lib.droid_ba_plan_system_region(h, ctypes.byref(off), ctypes.byref(sz)), "ba plan region")
         self.n = 6 * self.P
-        self.system = self.workspace[off.value:off.value + sz.value].view(torch.float64).view(self.n + 1, self.n + 1)
+        self.ld = sz.value // (8 * (self.n + 1))     # row stride (doubles): n+1 rounded up to 8
+        # augmented reduced system (rows 0..n-1 = A - S lower triangle, row n = rhs); all-reduce THIS
+        self.system = self.workspace[off.value:off.value + sz.value].view(torch.float64).view(self.n + 1, self.ld)
         with torch.cuda.device(self.device):
             check(lib.droid_ba_plan_upload(h, _ptr(self.workspace), _stream(self.workspace)), "ba plan upload")
 
@@ -369,6 +371,35 @@ class BaPlan:
 
 _PLAN_CACHE = OrderedDict()
 _PLAN_CACHE_SIZE = 8
+
+
+def dense_spd_solve(A, b, lm=0.0, ep=0.0):
+    """Damped dense SPD solve on the dataflow Cholesky (include/droid_backends.h:
+    droid_chol_*): A (n,n) fp64 HIP tensor (lower triangle read), b (n) fp64 ->
+    (dx (n) fp32, failed bool).  diag += ep + lm*diag first, as SparseBlock::solve."""
+    _check_inputs(("A", "b"), (A, b))
+    _need(A, torch.float64, "A")
+    _need(b, torch.float64, "b")
+    n = int(b.numel())
+    h = ctypes.c_void_p()
+    check(lib.droid_chol_plan_create(n, ctypes.byref(h)), "chol plan")
+    try:
+        ld, nt, foff = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib.droid_chol_plan_info(h, ctypes.byref(ld), ctypes.byref(nt), ctypes.byref(foff)), "chol plan info")
+        ws = torch.zeros((lib.droid_ba_plan_workspace_bytes(h),), dtype=torch.uint8, device=A.device)
+        off, sz = ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib.droid_ba_plan_system_region(h, ctypes.byref(off), ctypes.byref(sz)), "chol region")
+        sysm = ws[off.value:off.value + sz.value].view(torch.float64).view(n + 1, ld.value)
+        sysm[:n, :n] = torch.tril(A)
+        sysm[n, :n] = b
+        dx = torch.empty(n, dtype=torch.float32, device=A.device)
+        with torch.cuda.device(A.device):
+            check(lib.droid_ba_plan_upload(h, _ptr(ws), _stream(A)), "chol upload")
+            check(lib.droid_chol_solve(h, _ptr(ws), float(lm), float(ep), _ptr(dx), _stream(A)), "chol solve")
+        flag = int(ws[foff.value:foff.value + 4].view(torch.int32).item())
+        return dx, bool(flag & 1)
+    finally:
+        lib.droid_ba_plan_destroy(h)
 
 
 def get_plan(ii_host, jj_host, num_frames, ht, wd, t0, t1, eta_rows, motion_only, device, own=None):

@@ -48,6 +48,10 @@ _SIGS = {
     "droid_ba_plan_upload": ([_p, _p, _p], _i),
     "droid_ba_build_system": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _p], _i),
     "droid_ba_solve_update": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p], _i),
+    "droid_chol_plan_create": ([_i, ctypes.POINTER(_p)], _i),
+    "droid_chol_plan_info": ([_p, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)], _i),
+    "droid_chol_solve": ([_p, _p, _f, _f, _p, _p], _i),
+    "droid_chol_plan_tasks": ([_p, _p], _i),
     "droid_ba_run": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _f, _f, _p, _p, _p], _i),
 }
 

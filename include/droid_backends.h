@@ -176,6 +176,19 @@ int droid_ba_run(void* plan, void* workspace, float* poses, float* disps, const 
                  const float* eta, int iterations, float lm, float ep, float* dx, float* dz,
                  hipStream_t stream);
 
+/* Dense damped SPD solve on the same dataflow Cholesky (used by the BA; exposed
+ * for direct testing and for callers with their own reduced systems).  The
+ * plan's workspace holds the augmented system at droid_ba_plan_system_region:
+ * n+1 rows of ld doubles (ld from droid_chol_plan_info), lower triangle of A in
+ * rows 0..n-1, rhs b in row n.  droid_chol_solve adds ep + lm*diag, factors in
+ * place and writes dx (n, fp32; zero and flag bit 0 set when A is not SPD).
+ * Upload with droid_ba_plan_upload; free with droid_ba_plan_destroy. */
+int droid_chol_plan_create(int n, void** plan_out);
+int droid_chol_plan_info(const void* plan, int* ld, int* ntasks, int* flag_offset);
+int droid_chol_solve(void* plan, void* workspace, float lm, float ep, float* dx, hipStream_t stream);
+/* host copy of the task list (4 ints per task: type 0 POTRF 1 TRSM 2 UPDATE 3 BSOLVE 4 BUPD, i, j, k) */
+int droid_chol_plan_tasks(const void* plan, int* out);
+
 #ifdef __cplusplus
 }
 #endif
