@@ -74,6 +74,9 @@ struct ConvArgs {
   __half* rnet;
   int gru_ch;  // hidden channels (128)
   float* out32;  // EPI_HEAD / EPI_GLO fp32 output
+  // band kernel
+  int nslot;  // band pixels ((TMX/W + 2) * W)
+  int nhi;    // halo DMA instructions per wave per chunk
 };
 
 constexpr int TM = 128, BK = 64;
@@ -809,6 +812,314 @@ static int launch_halo(const ConvArgs& a0, hipStream_t stream) {
   return kOk;
 }
 
+// ---------------------------------------------------------------------------
+// Band kernel (3x3, CHUNKED; W in {16, 32, 64}, TMX | H*W, TN | Cout): a
+// TMX-pixel x TN-channel tile on 8 waves (4 along pixels x 2 along channels),
+// each wave 64x128 (TN = 256) or 96x64 (TN = 128) - the whole Cout = 256 of
+// the ConvGRU z|r gates in one workgroup, so the A operand crosses L2->CU once
+// per chunk for all outputs.  A wave's 16-pixel fragments are interleaved with
+// the other pixel waves' (fragment i of wave wm = tile pixels 16 (wm + 4i) ..),
+// so with W | 64 every fragment of a wave starts at the same image column.
+// Both operands reach LDS by LDS-DMA (buffer_load ... lds, no VGPR staging,
+// no ds_write):
+//   * the tile's R = TMX/W image rows plus one halo row above and below, an
+//     (R+2) x W pixel band of one 64-channel chunk, double buffered: the next
+//     chunk's band is in flight during the 9 taps of the current one;
+//   * the weights of one (chunk, tap) stage, double buffered, one stage ahead.
+// A tap is a row shift of the band (compile-time ds_read offsets; taps are
+// unrolled).  The x = -1 / x = W neighbours of the image's edge columns would
+// land on the adjacent row's edge pixel: those lanes (only lane 0 / 15 of the
+// waves whose fragments start at column 0 / W-16) read through a base address
+// past the LDS allocation instead, which the LDS returns as zeros - no masks.  Rows outside
+// the image and channels past a source's end are out-of-range buffer offsets,
+// which the DMA fills with zeros.  One raw s_barrier per stage with counted
+// vmcnt waits: a wave waits only for its own DMA of the stage about to be
+// read, the barrier then publishes every wave's.
+template <int TMX, int TN>
+struct Band {
+  static constexpr int WM = 4, WN = 2, FM = TMX / (WM * 16), FN = TN / (WN * 16);
+  static constexpr int NT = 512;
+  static constexpr int NBI = TN / 64;                    // weight DMA instructions per wave per stage
+  static constexpr int MAX_NHI = 8;
+  static_assert(WM * WN == 8 && FM * 16 * WM == TMX, "band tile");
+};
+constexpr int kLdsMax = 163840;
+
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  // n is wave-uniform; s_waitcnt takes an immediate
+  switch (n) {
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// LDS-DMA of 16 B per lane (buffer_load_dwordx4 ... lds): lane l's bytes land at
+// LDS byte address `lds` + 16 l.  Issued as inline asm so that hipcc does not
+// treat every later ds_read as dependent on the DMA (it inserts vmcnt(0) before
+// them otherwise); the kernel orders the DMA with explicit counted vmcnt waits +
+// s_barrier.  `rs` is a raw buffer descriptor in SGPRs; out-of-range offsets
+// (kOob) land as zeros.
+typedef int rsrc_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) char* lds_cptr_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  const unsigned long long pa = (unsigned long long)base;
+  return rsrc_t{(int)(unsigned)pa, (int)((unsigned)(pa >> 32) & 0xffffu), (int)bytes, kBufFlags};
+}
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(lds_cptr_t)(p);
+}
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma16(rsrc_t rs, unsigned lds, unsigned voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(lds), "v"(voff), "s"(rs)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// Band epilogue in two passes through one fp16 LDS tile [TMX][TN + 8]:
+// (1) each wave writes act(acc + bias + bbias) of its fragments (act = relu /
+//     none, sigmoid for z|r, tanh for q - rounded to fp16 as the reference's
+//     autocast rounds the gate before using it);
+// (2) coalesced 16-B row pieces: r * h for the r half, the GRU blend
+//     (1 - z) h + z q for q (h, z read as 16-B pieces), then the store.
+template <int TMX, int TN, int FM, int FN>
+__device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
+                                              int n0, int wm, int wn, int lane, int tid) {
+  constexpr int ER = TN + 8, NT = 512, PPR = TN / 8;
+  const int HW = a.H * a.W;
+  const int b = (int)(m0 / HW);  // a tile never straddles two images
+  const int fr = lane & 15, fq = lane >> 4;
+  const int epi = a.epi;
+  __syncthreads();  // main-loop LDS reads are done
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int c = wn * (TN / 2) + j * 16 + fr;
+    const int co = n0 + c;
+    float bv = a.bias ? a.bias[co] : 0.f;
+    if (a.bbias) bv += a.bbias[(long)b * a.Cout + co];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = 16 * (wm + 4 * i) + fq * 4 + k;
+        const float v = acc[i][j][k] + bv;
+        float o;
+        if (epi == EPI_GRU_ZR) o = sigmoidf_(v);
+        else if (epi == EPI_GRU_Q) o = tanhf(v);
+        else o = (a.act == 1) ? fmaxf(v, 0.f) : v;
+        smem[r * ER + c] = (_Float16)o;
+      }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < TMX * PPR; idx += NT) {
+    const int r = idx / PPR, p = idx - r * PPR;
+    const long m = m0 + r;
+    const int c = n0 + p * 8;
+    half8 v = *reinterpret_cast<const half8*>(&smem[r * ER + p * 8]);
+    if (epi == EPI_GRU_ZR) {
+      if (c >= a.gru_ch) {
+        const half8 h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c - a.gru_ch);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (_Float16)((float)v[e] * (float)h[e]);
+        *reinterpret_cast<half8*>(a.rnet + m * a.gru_ch + c - a.gru_ch) = v;
+      } else {
+        *reinterpret_cast<half8*>(a.zout + m * a.gru_ch + c) = v;
+      }
+    } else if (epi == EPI_GRU_Q) {
+      const half8 h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c);
+      const half8 z = *reinterpret_cast<const half8*>(a.z + m * a.z_cstride + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float zv = (float)z[e];
+        v[e] = (_Float16)((1.0f - zv) * (float)h[e] + zv * (float)v[e]);
+      }
+      *reinterpret_cast<half8*>(a.out + m * a.out_cstride + a.out_coff + c) = v;
+    } else {
+      *reinterpret_cast<half8*>(a.out + m * a.out_cstride + a.out_coff + c) = v;
+    }
+  }
+}
+
+template <int TMX, int TN>
+__global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
+  using BP = Band<TMX, TN>;
+  constexpr int FM = BP::FM, FN = BP::FN, WN = BP::WN, NBI = BP::NBI;
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int W = a.W, H = a.H, HW = H * W;
+  const long wgid = xcd_work_id(a.m_tiles * a.n_tiles);
+  const long mt = wgid / a.n_tiles;
+  const int nt = (int)(wgid - mt * a.n_tiles);
+  const long m0 = mt * TMX;
+  const int n0 = nt * TN;
+  const int y0 = (int)((m0 % HW) / W);
+  const long band0 = m0 - W;  // pixel index of the band's first (halo) row
+  const int nslot = a.nslot, nhi = a.nhi;
+  const int hbytes = nhi * 8 * 1024;  // one band buffer
+  char* Bl = lds;                     // [2][TN][128 B]
+  char* Hl = lds + 2 * TN * 128;      // [2][nhi * 64 slots][128 B]
+
+  // ---- DMA lane geometry: instruction q of this wave covers 8 LDS rows of
+  // 128 B; lane l writes row 8*(wave + 8q) + (l >> 3), 16-B slot l & 7, which
+  // holds logical piece (l & 7) ^ (row & 7) (the XOR swizzle)
+  const int lrow = lane >> 3;
+  const int lpiece = (lane & 7) ^ lrow;
+  // halo slot -> pixel offset within the band, or -1 (outside the image / padding)
+  int hpix[BP::MAX_NHI];
+#pragma unroll
+  for (int q = 0; q < BP::MAX_NHI; ++q) {
+    const int slot = (wave + 8 * q) * 8 + lrow;
+    const int ry = slot / W;
+    const int y = y0 - 1 + ry;
+    hpix[q] = (q < nhi && slot < nslot && y >= 0 && y < H) ? slot : -1;
+  }
+  const rsrc_t rsb = make_rsrc(a.wp + (long)n0 * a.nstage * BK, TN * a.nstage * BK * 2);
+  const unsigned Bl_a = lds_addr(Bl), Hl_a = lds_addr(Hl);
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  unsigned boff[NBI];
+#pragma unroll
+  for (int q = 0; q < NBI; ++q) boff[q] = (unsigned)((((wave + 8 * q) * 8 + lrow) * a.nstage * BK + lpiece * 8) * 2);
+
+  auto issue_b = [&](int st) {
+    const unsigned dst = Bl_a + (st & 1) * TN * 128;
+#pragma unroll
+    for (int q = 0; q < NBI; ++q) dma16(rsb, dst + (wave_u + 8 * q) * 1024, boff[q] + st * BK * 2);
+  };
+  auto issue_halo = [&](int chunk) {
+    int s = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (q + 1 < a.nsrc && chunk >= a.chunk_end[q]) s = q + 1;
+    const int cstart = s ? a.chunk_end[s - 1] : 0;
+    const ConvSrc src = a.src[s];
+    const int c = (chunk - cstart) * BK + lpiece * 8;
+    const bool okc = c < src.C;
+    const rsrc_t rs = make_rsrc(src.ptr + band0 * src.cstride, nslot * src.cstride * 2);
+    const unsigned dst = Hl_a + (chunk & 1) * hbytes;
+#pragma unroll
+    for (int q = 0; q < BP::MAX_NHI; ++q) {
+      if (q < nhi) {
+        const unsigned off = (okc && hpix[q] >= 0) ? (unsigned)((hpix[q] * src.cstride + c) * 2) : kOob;
+        dma16(rs, dst + (wave_u + 8 * q) * 1024, off);
+      }
+    }
+  };
+
+  // ---- fragment addresses.  Lane (fr, kq): A row = tile pixel p = 16 (wm + 4i) + fr,
+  // band slot W + p + ty*W + tx; B row wn*TN/2 + 16j + fr.  Since W % 16 == 0 the
+  // slot's low 3 bits are (fr + tx) & 7, so the swizzled byte offset splits into a
+  // per-lane base (by tx, K half) plus compile-time i*8192 and a uniform ty*W*128.
+  // Column of the lane's pixels: (16 wm + fr) % W for every i (W | 64).
+  const int fr = lane & 15;
+  const int xcol = (16 * wm + fr) % W;
+  constexpr int kLdsZero = 0x100000;  // base past the LDS allocation: reads return 0
+  int abase[3][2], bbase[2];
+#pragma unroll
+  for (int hk = 0; hk < 2; ++hk) {
+    const int kq = (lane >> 4) + hk * 4;
+#pragma unroll
+    for (int tx = -1; tx <= 1; ++tx) {
+      const int sl = W + 16 * wm + fr + tx;
+      const bool off_image = (tx < 0 && xcol == 0) || (tx > 0 && xcol == W - 1);
+      abase[tx + 1][hk] = off_image ? kLdsZero : sl * 128 + ((kq ^ ((fr + tx) & 7)) << 4);
+    }
+    bbase[hk] = (wn * (TN / 2) + fr) * 128 + ((kq ^ (fr & 7)) << 4);
+  }
+
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = a.cpt;
+  const int nst = a.nstage;  // nch * 9
+  const int rowb = W * 128;
+
+  issue_halo(0);
+  issue_b(0);
+  int st = 0;
+  for (int ch = 0; ch < nch; ++ch) {
+    const char* Hb = Hl + (ch & 1) * hbytes;
+#pragma unroll
+    for (int t = 0; t < 9; ++t, ++st) {
+      const int ty = t / 3 - 1, tx = t % 3 - 1;
+      // this stage's weights (and at t == 0 this chunk's band) must have landed;
+      // at t == 1 the next chunk's band (issued after them) may stay in flight
+      wait_vmcnt((t == 1 && ch + 1 < nch) ? nhi : 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (st + 1 < nst) issue_b(st + 1);
+      if (t == 0 && ch + 1 < nch) issue_halo(ch + 1);
+      const char* Bb = Bl + (st & 1) * TN * 128;
+#pragma unroll
+      for (int hk = 0; hk < 2; ++hk) {
+        const char* ap = Hb + abase[tx + 1][hk] + ty * rowb;
+        half8 af[FM], bf[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const half8*>(ap + i * 8192);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const half8*>(Bb + bbase[hk] + j * 2048);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  band_epilogue<TMX, TN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid);
+}
+
+template <int TMX, int TN>
+static bool band_fits(int W, int* nslot, int* nhi) {
+  const int ns = (TMX / W + 2) * W;
+  const int nh = ceil_div(ns, 64);
+  if (nh > Band<TMX, TN>::MAX_NHI) return false;
+  const int lds = 2 * TN * 128 + 2 * nh * 8 * 1024;
+  const int epi = TMX * (TN + 8) * 2;
+  if (lds > kLdsMax || epi > kLdsMax) return false;
+  *nslot = ns;
+  *nhi = nh;
+  return true;
+}
+
+template <int TMX, int TN>
+static int launch_band(const ConvArgs& a0, hipStream_t stream) {
+  ConvArgs a = a0;
+  if (!band_fits<TMX, TN>(a.W, &a.nslot, &a.nhi)) return fail(kUnsupported, "conv band: shape");
+  a.n_tiles = a.Cout / TN;
+  a.m_tiles = (long)a.B * a.H * a.W / TMX;
+  const int main_b = 2 * TN * 128 + 2 * a.nhi * 8 * 1024;
+  const int epi_b = TMX * (TN + 8) * 2;
+  const int lds = main_b > epi_b ? main_b : epi_b;
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    attr = true;
+  }
+  const long nwg = a.m_tiles * a.n_tiles;
+  if (nwg > 0x7fffffffL) return fail(kUnsupported, "conv_nhwc_f16: problem too large");
+  conv_band_kernel<TMX, TN><<<dim3((unsigned)nwg), 512, lds, stream>>>(a);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
 }  // namespace droid
 
 using namespace droid;
@@ -888,6 +1199,19 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
   }();
   const bool halo_ok = !a.im2col && ks > 1 && Cout % 128 == 0 && (ks >> 1) * (W + 1) <= kHaloMax &&
                        epi != EPI_GLO && epi != EPI_HEAD;
+  // LDS-DMA band kernel (DROID_CONV_BAND=0 disables): 3x3, whole-row tiles
+  static const bool band_on = [] {
+    const char* e = getenv("DROID_CONV_BAND");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool band_ok = band_on && !a.im2col && ks == 3 && W % 16 == 0 && 64 % W == 0 &&
+                       (epi == EPI_GRU_ZR || epi == EPI_GRU_Q || (epi == EPI_ACT && a.stage_out)) &&
+                       (epi != EPI_GRU_ZR || gru_ch % 128 == 0);
+  int ns_, nh_;
+  if (band_ok && Cout % 256 == 0 && 256 % W == 0 && (H * W) % 256 == 0 && band_fits<256, 256>(W, &ns_, &nh_))
+    return launch_band<256, 256>(a, stream);
+  if (band_ok && Cout % 128 == 0 && 384 % W == 0 && (H * W) % 384 == 0 && band_fits<384, 128>(W, &ns_, &nh_))
+    return launch_band<384, 128>(a, stream);
   // row-band variant: tile = whole image rows, zero-padded halo, no masks
   const int pad = ks >> 1;
   const bool rows_ok = halo_ok && halo_nw == 8 && 256 % W == 0 && W % 16 == 0 && (H * W) % 256 == 0 &&

@@ -139,3 +139,66 @@ def test_segment_mean_matches_scatter_mean():
     np.testing.assert_allclose(host(out.float()), host(ref), atol=2e-3, rtol=2e-3)
     dptr, didx = edge_segments(torch.as_tensor(inverse, device=DEV), U)
     assert np.array_equal(host(dptr), ptr) and np.array_equal(host(didx), idx)
+
+
+# shapes that take the LDS-DMA band kernel (3x3, W % 16 == 0, whole-row tiles):
+# <256,256> for Cout % 256 == 0 (W | 256, HW % 256 == 0), <384,128> for Cout % 128 == 0
+BAND_CASES = [([128, 128, 128, 64], 256, 2, 8, 64),    # z|r-shaped, 256-tile, image rows 0 and H-1 in the tile
+              ([128], 256, 3, 16, 32),                 # 256-tile with W = 32 (8 rows per tile)
+              ([128, 128, 128, 64], 128, 2, 12, 64),   # q-shaped, 384-tile (6 rows)
+              ([128], 128, 1, 48, 64),                 # the update operator's 48x64 maps
+              ([96, 64], 128, 2, 24, 32),              # source narrower than its 64-channel chunk
+              ([64], 256, 2, 16, 16)]                  # 256-tile of 16 rows
+
+
+def _conv_ref(xs, w, bias, bb):
+    xin = torch.cat([x.float() for x in xs], -1).permute(0, 3, 1, 2)
+    return (F.conv2d(xin, w.half().float(), bias, padding=1) + bb[:, :, None, None]).permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("splits,cout,B,H,W", BAND_CASES)
+def test_conv_band_act(splits, cout, B, H, W):
+    import droid_backends
+    from droid_mi355x.fused import pack_conv
+    g = torch.Generator(device=DEV).manual_seed(11)
+    xs = [torch.randn((B, H, W, c), generator=g, device=DEV).half() for c in splits]
+    w = torch.randn((cout, sum(splits), 3, 3), generator=g, device=DEV) / (sum(splits) * 9) ** 0.5
+    bias = torch.randn(cout, generator=g, device=DEV)
+    bb = torch.randn((B, cout), generator=g, device=DEV)
+    out = torch.empty((B, H, W, cout), dtype=torch.float16, device=DEV)
+    droid_backends.conv_nhwc_f16([(x, 0, x.shape[-1]) for x in xs], pack_conv(w, splits), cout, 3, bias=bias,
+                                 bbias=bb, act=1, out=out)
+    ref = F.relu(_conv_ref(xs, w, bias, bb))
+    # fp16 output: |err| <= fp16 rounding of the value + fp32 accumulation-order noise
+    np.testing.assert_allclose(host(out.float()), host(ref), atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 8, 64), (2, 12, 64), (1, 16, 32)])
+def test_conv_gru_epilogues(B, H, W):
+    """z|r (sigmoid, r*h) and q (tanh, (1-z)h + zq) epilogues vs torch fp32 (modules/gru.py:19-32)."""
+    import droid_backends
+    from droid_backends import EPI_GRU_Q, EPI_GRU_ZR
+    from droid_mi355x.fused import pack_conv
+    g = torch.Generator(device=DEV).manual_seed(12)
+    splits = [128, 128, 128, 64]
+    mk = lambda c: torch.randn((B, H, W, c), generator=g, device=DEV).half()
+    h = torch.tanh(mk(128).float()).half()
+    xs = [h, mk(128), mk(128), mk(64)]
+    wzr = torch.randn((256, 448, 3, 3), generator=g, device=DEV) / (448 * 9) ** 0.5
+    wq = torch.randn((128, 448, 3, 3), generator=g, device=DEV) / (448 * 9) ** 0.5
+    bzr, bq = torch.randn(256, generator=g, device=DEV), torch.randn(128, generator=g, device=DEV)
+    bbzr, bbq = torch.randn((B, 256), generator=g, device=DEV), torch.randn((B, 128), generator=g, device=DEV)
+    z = torch.empty((B, H, W, 128), dtype=torch.float16, device=DEV)
+    rn = torch.empty_like(z)
+    droid_backends.conv_nhwc_f16([(x, 0, x.shape[-1]) for x in xs], pack_conv(wzr, splits), 256, 3, bias=bzr,
+                                 bbias=bbzr, epi=EPI_GRU_ZR, h=h, zout=z, rnet=rn)
+    gates = torch.sigmoid(_conv_ref(xs, wzr, bzr, bbzr))
+    np.testing.assert_allclose(host(z.float()), host(gates[..., :128]), atol=2e-3)
+    np.testing.assert_allclose(host(rn.float()), host(gates[..., 128:] * h.float()), atol=2e-3)
+    hn = torch.empty_like(z)
+    xq = [rn] + xs[1:]
+    droid_backends.conv_nhwc_f16([(x, 0, x.shape[-1]) for x in xq], pack_conv(wq, splits), 128, 3, bias=bq,
+                                 bbias=bbq, epi=EPI_GRU_Q, h=h, z=z, out=hn)
+    q = torch.tanh(_conv_ref(xq, wq, bq, bbq))
+    ref = (1 - z.float()) * h.float() + z.float() * q
+    np.testing.assert_allclose(host(hn.float()), host(ref), atol=3e-3)
