@@ -34,6 +34,8 @@ PEAK_F16_TFLOPS = 2500.0        # MI355X_MICROARCH.md: dense fp16/bf16 MFMA peak
 LOOKUP_BYTES_PER_EDGE = 2801664  # volume-API lookup, 4 lvl x 64 taps x 2 B x HW + coords + out
 # ConvGRU z|r conv (modules/gru.py:19-32, convz+convr fused): 3x3, 448 -> 256 channels
 ZR_FLOPS_PER_PIXEL = 2 * 256 * 448 * 9
+ZR_KERNEL = "conv_band_kernel<256, 256>"   # csrc/conv_kernels.hip, chosen for 48x64 maps
+LOOKUP_KERNEL = "corr_pyramid_f16_r3_kernel"
 
 
 LOOKUP_FN = ["corr_pyramid_lookup_nhwc"]
@@ -173,16 +175,17 @@ def cpu_baseline(graph, video, args):
                           r["t_ba_iter"]))}
 
 
-def load_traffic(name, e_local):
+def load_traffic(name, e_local, kernel):
     """HBM bytes per launch from a committed PMC pass (profiles/pmc_<name>.json,
-    FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), scaled to
-    this launch's edge count; None when no measurement for this config exists."""
+    FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) of this
+    launch's edge count and of the kernel named; None when no such measurement
+    exists (e.g. the pass predates the current kernel)."""
     p = os.path.join(ROOT, "profiles", "pmc_%s.json" % name)
     if os.path.exists(p):
         try:
             with open(p) as f:
                 d = json.load(f)
-            if d.get("edges") == e_local:
+            if d.get("edges") == e_local and kernel in (d.get("kernel") or ""):
                 return d.get("traffic_bytes_per_launch")
         except Exception:
             return None
@@ -269,14 +272,14 @@ def main():
             "NCHW" if args.reference_op else "NHWC"), "bound": "hbm",
                        "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                        "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
-                       "traffic": load_traffic("corr_lookup", e_local), "launch_ms": lookup_ms,
+                       "traffic": load_traffic("corr_lookup", e_local, LOOKUP_KERNEL), "launch_ms": lookup_ms,
                        "algorithmic_bytes_per_launch": bytes_per_launch}
         if zr_ms:
             flops = ZR_FLOPS_PER_PIXEL * e_local * (args.ht // 8) * (args.wd // 8)
             tf = flops / (zr_ms * 1e-3) / 1e12
-            roofline = {"kernel": "conv_rows_kernel<8> (ConvGRU z|r gates, 3x3 448->256, fp16 MFMA)",
+            roofline = {"kernel": "%s (ConvGRU z|r gates, 3x3 448->256, fp16 MFMA)" % ZR_KERNEL,
                         "bound": "mfma", "achieved": tf, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-                        "frac": tf / PEAK_F16_TFLOPS, "traffic": load_traffic("conv_zr", e_local),
+                        "frac": tf / PEAK_F16_TFLOPS, "traffic": load_traffic("conv_zr", e_local, ZR_KERNEL),
                         "launch_ms": zr_ms, "algorithmic_flops_per_launch": flops}
         else:
             roofline, lookup_roof = lookup_roof, None

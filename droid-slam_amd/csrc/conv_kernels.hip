@@ -40,7 +40,7 @@ namespace droid {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-enum ConvEpi : int { EPI_ACT = 0, EPI_GRU_ZR = 1, EPI_GRU_Q = 2, EPI_HEAD = 3, EPI_GLO = 4 };
+enum ConvEpi : int { EPI_ACT = 0, EPI_GRU_ZR = 1, EPI_GRU_Q = 2, EPI_HEAD = 3, EPI_GLO = 4, EPI_DWHEAD = 5 };
 
 struct ConvSrc {
   const __half* ptr;
@@ -77,6 +77,7 @@ struct ConvArgs {
   // band kernel
   int nslot;  // band pixels ((TMX/W + 2) * W)
   int nhi;    // halo DMA instructions per wave per chunk
+  const __half* hw;  // EPI_DWHEAD: head weights [48][256] (row = tap*4 + out channel)
 };
 
 constexpr int TM = 128, BK = 64;
@@ -950,7 +951,101 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
   }
 }
 
-template <int TMX, int TN>
+// EPI_DWHEAD (band <256,256> only): the delta/weight heads (droid_net.py:
+// 95-103: conv3x3 128->256 + ReLU, then conv3x3 256->2 per head) in one launch.
+// The 256-channel hidden map dw of the tile's R image rows never leaves the CU:
+//   (1) T = relu(acc + bias) -> LDS fp16 [256 px][264];
+//   (2) Y[p][tap*4 + c] = sum_ch T[p][ch] Wh[c][ch][tap] for all 9 taps at once
+//       (one 256 x 48 x 256 MFMA GEMM: the taps ride on the N dimension, so the
+//       tile needs no halo);
+//   (3) out[o][c] = sum over taps of Y[o + shift(tap)][tap*4 + c] for the output
+//       rows y0-1 .. y0+R that this tile's rows feed, atomically added into the
+//       zero-initialised fp32 out32 (E,H,W,4).  Each output pixel receives at most
+//       two contributions (this tile and one neighbour), so the result does not
+//       depend on their order.  Head bias and the weight sigmoid are applied by
+//       the caller.
+template <int FM, int FN>
+__device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
+                                                int wm, int wn, int lane, int tid) {
+  constexpr int TMX = 256, TS = 264, YS = 37, NT = 512;
+  const int W = a.W, H = a.H, HW = H * W;
+  const int R = TMX / W;
+  const int b = (int)(m0 / HW);
+  const int y0 = (int)((m0 % HW) / W);
+  const int fr = lane & 15, fq = lane >> 4;
+  _Float16* T = smem;             // [256][TS]
+  _Float16* Bh = smem + TMX * TS; // [48][TS]
+  __syncthreads();  // main-loop LDS reads are done
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int c = wn * 128 + j * 16 + fr;
+    const float bv = a.bias ? a.bias[c] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        T[(16 * (wm + 4 * i) + fq * 4 + k) * TS + c] = (_Float16)fmaxf(acc[i][j][k] + bv, 0.f);
+  }
+  for (int idx = tid; idx < 48 * 32; idx += NT) {
+    const int r = idx >> 5, p = idx & 31;
+    *reinterpret_cast<uint4*>(&Bh[r * TS + p * 8]) = *reinterpret_cast<const uint4*>(a.hw + r * 256 + p * 8);
+  }
+  __syncthreads();
+  // (2) wave w: pixel fragments 2w, 2w+1; all 3 tap-channel fragments; K = 256
+  const int wave = tid >> 6;
+  floatx4 y[2][3];
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int n = 0; n < 3; ++n) y[f][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    half8 af[2], bf[3];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+      af[f] = *reinterpret_cast<const half8*>(&T[((2 * wave + f) * 16 + fr) * TS + s * 32 + fq * 8]);
+#pragma unroll
+    for (int n = 0; n < 3; ++n) bf[n] = *reinterpret_cast<const half8*>(&Bh[(n * 16 + fr) * TS + s * 32 + fq * 8]);
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int n = 0; n < 3; ++n) y[f][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[f], bf[n], y[f][n], 0, 0, 0);
+  }
+  __syncthreads();  // T and Bh reads done: Y overwrites them
+  float* Y = reinterpret_cast<float*>(smem);  // [256][YS]
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int n = 0; n < 3; ++n)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int col = n * 16 + fr;
+        if (col < 36) Y[((2 * wave + f) * 16 + fq * 4 + k) * YS + col] = y[f][n][k];
+      }
+  __syncthreads();
+  // (3) output rows y0-1 .. y0+R
+  for (int idx = tid; idx < (R + 2) * W * 4; idx += NT) {
+    const int c = idx & 3, px = idx >> 2;
+    const int orow = px / W - 1, x = px - (px / W) * W;
+    const int oy = y0 + orow;
+    if (oy < 0 || oy >= H) continue;
+    float sum = 0.f;
+#pragma unroll
+    for (int ty = -1; ty <= 1; ++ty) {
+      const int sr = orow + ty;
+      if (sr < 0 || sr >= R) continue;
+#pragma unroll
+      for (int tx = -1; tx <= 1; ++tx) {
+        const int sx = x + tx;
+        if (sx < 0 || sx >= W) continue;
+        sum += Y[(sr * W + sx) * YS + ((ty + 1) * 3 + tx + 1) * 4 + c];
+      }
+    }
+    atomicAdd(a.out32 + ((long)b * HW + (long)oy * W + x) * 4 + c, sum);
+  }
+}
+
+template <int TMX, int TN, bool DWHEAD>
 __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   using BP = Band<TMX, TN>;
   constexpr int FM = BP::FM, FN = BP::FN, WN = BP::WN, NBI = BP::NBI;
@@ -1082,7 +1177,12 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
       }
     }
   }
-  band_epilogue<TMX, TN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid);
+  if constexpr (DWHEAD) {
+    static_assert(TMX == 256 && TN == 256, "dw/head fusion runs on the 256x256 tile");
+    dwhead_epilogue<FM, FN>(a, acc, smem, m0, wm, wn, lane, tid);
+  } else {
+    band_epilogue<TMX, TN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid);
+  }
 }
 
 template <int TMX, int TN>
@@ -1098,24 +1198,26 @@ static bool band_fits(int W, int* nslot, int* nhi) {
   return true;
 }
 
-template <int TMX, int TN>
+template <int TMX, int TN, bool DWHEAD = false>
 static int launch_band(const ConvArgs& a0, hipStream_t stream) {
   ConvArgs a = a0;
   if (!band_fits<TMX, TN>(a.W, &a.nslot, &a.nhi)) return fail(kUnsupported, "conv band: shape");
   a.n_tiles = a.Cout / TN;
   a.m_tiles = (long)a.B * a.H * a.W / TMX;
   const int main_b = 2 * TN * 128 + 2 * a.nhi * 8 * 1024;
-  const int epi_b = TMX * (TN + 8) * 2;
+  // EPI_DWHEAD keeps the head weights [48][264] beside the hidden-map tile
+  const int epi_b = TMX * (TN + 8) * 2 + (DWHEAD ? 48 * 264 * 2 : 0);
   const int lds = main_b > epi_b ? main_b : epi_b;
+  if (lds > kLdsMax) return fail(kUnsupported, "conv band: LDS");
   static bool attr = false;
   if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN>),
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN, DWHEAD>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     attr = true;
   }
   const long nwg = a.m_tiles * a.n_tiles;
   if (nwg > 0x7fffffffL) return fail(kUnsupported, "conv_nhwc_f16: problem too large");
-  conv_band_kernel<TMX, TN><<<dim3((unsigned)nwg), 512, lds, stream>>>(a);
+  conv_band_kernel<TMX, TN, DWHEAD><<<dim3((unsigned)nwg), 512, lds, stream>>>(a);
   DROID_LAUNCH_CHECK();
   return kOk;
 }
@@ -1225,6 +1327,43 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
   return launch_conv<16>(a, stream);
 }
 
+
+// Fused delta/weight heads (EPI_DWHEAD): conv3x3 (srcs -> 256, bias, ReLU) feeding
+// conv3x3 256 -> 4 (hw: [48][256] fp16, row tap*4 + c, rows 36..47 zero); raw head
+// sums are atomically added into out32 (B,H,W,4) fp32, which the caller zeroes.
+// Needs the band tile: Cout == 256, ks == 3, W in {16,32,64}, H*W % 256 == 0;
+// returns kUnsupported otherwise (the caller then runs the two convs).
+int droid_conv_dw_head_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc, const void* wp,
+                           const float* bias, int B, int H, int W, const void* hw, void* out32,
+                           hipStream_t stream) {
+  if (nsrc < 1 || nsrc > 4 || B < 0 || H <= 0 || W <= 0 || !wp || !hw || !out32)
+    return fail(kInvalidArgument, "conv_dw_head_f16: bad arguments");
+  int ns_, nh_;
+  if (W % 16 || 64 % W || (H * W) % 256 || !band_fits<256, 256>(W, &ns_, &nh_))
+    return fail(kUnsupported, "conv_dw_head_f16: shape needs the band tile (W in {16,32,64}, H*W % 256 == 0)");
+  if ((long)B * H * W * 8 > 0x7fffffffL) return fail(kUnsupported, "conv_dw_head_f16: too many pixels");
+  ConvArgs a{};
+  int chunks = 0;
+  for (int s = 0; s < nsrc; ++s) {
+    if (C[s] % 8 || cstride[s] % 8 || cstride[s] < C[s] || (reinterpret_cast<uintptr_t>(srcs[s]) & 15))
+      return fail(kInvalidArgument, "conv_dw_head_f16: channels/strides must be multiples of 8, 16-B aligned");
+    a.src[s].ptr = (const __half*)srcs[s];
+    a.src[s].C = C[s];
+    a.src[s].cstride = cstride[s];
+    chunks += ceil_div(C[s], BK);
+    a.chunk_end[s] = chunks;
+  }
+  a.nsrc = nsrc;
+  a.cpt = chunks;
+  a.nstage = 9 * chunks;
+  a.wp = (const __half*)wp;
+  a.bias = bias;
+  a.B = B; a.H = H; a.W = W; a.Cout = 256; a.ks = 3; a.act = 1; a.epi = EPI_DWHEAD;
+  a.hw = (const __half*)hw;
+  a.out32 = (float*)out32;
+  if (B == 0) return kOk;
+  return launch_band<256, 256, true>(a, stream);
+}
 }  // extern "C"
 
 namespace droid {

@@ -161,6 +161,32 @@ def conv_nhwc_f16(sources, wp, cout, ks, bias=None, bbias=None, act=0, epi=EPI_A
     return out
 
 
+def dw_head_supported(H, W):
+    """Shapes droid_conv_dw_head_f16 accepts (the band tile: W in {16,32,64}, H*W % 256 == 0)."""
+    return W in (16, 32, 64) and (H * W) % 256 == 0
+
+
+def conv_dw_head_f16(sources, wp, bias, head_w, out32):
+    """Fused delta/weight heads (include/droid_backends.h: droid_conv_dw_head_f16):
+    relu(conv3x3(sources) + bias) -> 256 channels, kept on chip, then the 3x3
+    256->4 head conv accumulated into out32 (B,H,W,4) fp32 (zeroed by the caller)."""
+    t0 = sources[0][0]
+    B, H, W = t0.shape[:3]
+    n = len(sources)
+    for t, _, _ in sources:
+        if t.dtype != torch.float16 or not t.is_contiguous() or t.shape[:3] != (B, H, W):
+            raise RuntimeError("conv_dw_head_f16: sources must be contiguous fp16 (B,H,W,C) tensors")
+    if out32.dtype != torch.float32 or not out32.is_contiguous() or tuple(out32.shape) != (B, H, W, 4):
+        raise RuntimeError("conv_dw_head_f16: out32 must be a contiguous (B,H,W,4) float32 tensor")
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() + 2 * off for t, off, _ in sources])
+    cs = (ctypes.c_int * n)(*[c for _, _, c in sources])
+    strides = (ctypes.c_int * n)(*[t.shape[-1] for t, _, _ in sources])
+    with torch.cuda.device(t0.device):
+        check(lib.droid_conv_dw_head_f16(ptrs, cs, strides, n, _ptr(wp), _ptr(bias), B, H, W, _ptr(head_w),
+                                         _ptr(out32), _stream(t0)), "conv_dw_head_f16")
+    return out32
+
+
 def segment_mean_f16(src, seg_ptr, seg_idx, num_segments, out=None):
     """GraphAgg scatter_mean (include/droid_backends.h: droid_segment_mean_f16):
     src (E, ...) fp16 contiguous; seg_ptr (U+1) / seg_idx (E) int64 CSR of the

@@ -12,6 +12,9 @@ Same parameters (state-dict names) and forward semantics as UpdateModule
     conv epilogue that reduces over the tile and atomically accumulates;
   * delta.0 and weight.0 share one conv (256 outputs); delta.2 and weight.2
     run as one block-diagonal conv whose epilogue applies the weight sigmoid;
+  * on the 48x64 maps the delta/weight heads run as ONE launch (conv_dw_head_f16):
+    the 256-channel hidden map stays in LDS and the two 3x3 256->2 heads are
+    accumulated from it; head bias and sigmoid are applied afterwards;
   * GraphAgg's upmask is not computed: update() discards it (factor_graph.py:209).
 All convs: fp16 operands, fp32 accumulation (the reference's autocast).
 """
@@ -54,6 +57,14 @@ def pack_conv(weight, splits):
         off += c
     wp = torch.cat(blocks, dim=1)                              # (cout, chunks, 64, tap)
     return wp.permute(0, 1, 3, 2).reshape(cout, -1, BK).to(torch.float16).contiguous()
+
+
+def pack_head_taps(head):
+    """(4, 256, 3, 3) head weight -> [48][256] fp16 for droid_conv_dw_head_f16:
+    row tap*4 + c (tap = ky*3 + kx) holds head[c, :, ky, kx]; rows 36..47 zero."""
+    w = torch.zeros(48, 256, device=head.device)
+    w[:36] = head.detach().float().permute(2, 3, 0, 1).reshape(36, 256)
+    return w.to(torch.float16).contiguous()
 
 
 def edge_segments(inverse, num_unique):
@@ -118,6 +129,7 @@ class FusedUpdateModule(torch.nn.Module):
         head[2:4, 128:] = m.weight[2].weight
         P["head"] = pack_conv(head, [256])
         P["head_b"] = torch.cat([m.delta[2].bias, m.weight[2].bias]).float().contiguous()
+        P["head_taps"] = pack_head_taps(head)
         a = m.agg
         P["a1"] = pack_conv(a.conv1.weight, [128])
         P["a1_b"] = a.conv1.bias.float().contiguous()
@@ -164,12 +176,19 @@ class FusedUpdateModule(torch.nn.Module):
         conv([(rn, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["q"], 128, 3, bias=P["q_b"],
              bbias=gb[:, 256:].contiguous(), epi=EPI_GRU_Q, h=net, z=z, out=net_new)
 
-        dw = e16(256)
-        conv([(net_new, 0, 128)], P["dw0"], 256, 3, bias=P["dw0_b"], act=1, out=dw)
-        head = torch.empty((E, H, W, 4), dtype=torch.float32, device=dev)
-        conv([(dw, 0, 256)], P["head"], 4, 3, bias=P["head_b"], epi=EPI_HEAD, out32=head)
-        delta = head[..., 0:2].unsqueeze(0)
-        weight = head[..., 2:4].unsqueeze(0)
+        if droid_backends.dw_head_supported(H, W):
+            head = torch.zeros((E, H, W, 4), dtype=torch.float32, device=dev)
+            droid_backends.conv_dw_head_f16([(net_new, 0, 128)], P["dw0"], P["dw0_b"], P["head_taps"], head)
+            head += P["head_b"]
+            delta = head[..., 0:2].unsqueeze(0)
+            weight = torch.sigmoid(head[..., 2:4]).unsqueeze(0)
+        else:
+            dw = e16(256)
+            conv([(net_new, 0, 128)], P["dw0"], 256, 3, bias=P["dw0_b"], act=1, out=dw)
+            head = torch.empty((E, H, W, 4), dtype=torch.float32, device=dev)
+            conv([(dw, 0, 256)], P["head"], 4, 3, bias=P["head_b"], epi=EPI_HEAD, out32=head)
+            delta = head[..., 0:2].unsqueeze(0)
+            weight = head[..., 2:4].unsqueeze(0)
 
         a1 = e16(128)
         conv([(net_new, 0, 128)], P["a1"], 128, 3, bias=P["a1_b"], act=1, out=a1)

@@ -69,7 +69,8 @@ int droid_corr_pyramid_lookup_nhwc(const void* const* levels, const int* H2s, co
  * droid_net.py:78-143, modules/gru.py:19-32), NHWC fp16 in, fp32 accumulate.
  * Input = channel concatenation of nsrc (<=4) NHWC sources (C[s] channels at
  * pixel stride cstride[s], multiples of 8); wp = packed weights
- * [Cout][sum_s ceil(C_s/32)*ks*ks][32] fp16; ks odd <= 7, "same" padding.
+ * [Cout][nstage][64] fp16 (droid_mi355x.fused.pack_conv: nstage = ks*ks*sum_s ceil(C_s/64),
+ * or ceil(ks*ks/8) for one 8-channel source); ks odd <= 7, "same" padding.
  * epi: 0 = act(acc + bias + bbias[b]) (act 0 none / 1 relu) -> out fp16 slice;
  *      1 = GRU z|r gates (sigmoid; z -> zout, r*h -> rnet);
  *      2 = GRU update  h' = (1-z) h + z tanh(.) -> out;
@@ -80,6 +81,17 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
                         int Cout, int ks, int act, int epi, void* out, int out_cstride, int out_coff,
                         const void* h, int h_cstride, const void* z, int z_cstride, void* zout,
                         void* rnet, int gru_ch, void* out32, hipStream_t stream);
+
+/* UpdateModule delta/weight heads fused (droid_net.py:95-103, 132-133): conv3x3
+ * srcs -> 256 (wp, bias, ReLU; the delta.0 || weight.0 hidden map) feeding the
+ * block-diagonal conv3x3 256 -> 4 (hw [48][256] fp16, row = tap*4 + c, tap =
+ * ky*3 + kx, rows 36..47 zero) without writing the hidden map; raw head sums
+ * (no head bias, no sigmoid) are atomically added into out32 (B,H,W,4) fp32,
+ * which the caller zeroes.  Needs W in {16,32,64} and H*W % 256 == 0, else
+ * returns DROID_UNSUPPORTED. */
+int droid_conv_dw_head_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc, const void* wp,
+                           const float* bias, int B, int H, int W, const void* hw, void* out32,
+                           hipStream_t stream);
 
 /* GraphAgg scatter_mean (droid_net.py:27-45, torch_scatter.scatter_mean over
  * dim 1): out[u] = mean of src rows seg_idx[seg_ptr[u] .. seg_ptr[u+1]), rows of

@@ -49,3 +49,23 @@ for name, (srcs, cout, ks, kw) in cases.items():
     ms = min(ts)
     real = 2.0 * E * H * W * cout * cin * ks * ks
     print("%-20s %8.3f ms  %7.0f TFLOP/s (useful)" % (name, ms, real / ms / 1e9), flush=True)
+
+if not ONLY or ONLY == "dwhead":
+    from droid_mi355x.fused import pack_head_taps
+    w0 = torch.randn((256, 128, 3, 3), generator=g, device=dev) * 0.02
+    hw = pack_head_taps(torch.randn((4, 256, 3, 3), generator=g, device=dev) * 0.02)
+    wp, b0 = pack_conv(w0, [128]), torch.zeros(256, device=dev)
+    head = torch.zeros((E, H, W, 4), device=dev)
+    ts = []
+    for it in range(7):
+        head.zero_()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        droid_backends.conv_dw_head_f16([(net, 0, 128)], wp, b0, hw, head)
+        e.record()
+        torch.cuda.synchronize()
+        if it >= 2:
+            ts.append(s.elapsed_time(e))
+    ms = min(ts)
+    real = 2.0 * E * H * W * (256 * 128 * 9 + 4 * 256 * 9)
+    print("%-20s %8.3f ms  %7.0f TFLOP/s (useful)" % ("dw0+head fused", ms, real / ms / 1e9), flush=True)

@@ -17,6 +17,9 @@ src, dst = sys.argv[1], sys.argv[2]
 E = 2048
 
 
+KNAME = {}
+
+
 def per_kernel(counter):
     f = glob.glob(os.path.join(src, counter, "**", "*counter_collection.csv"), recursive=True)[0]
     out = {}
@@ -25,10 +28,11 @@ def per_kernel(counter):
             continue
         name = r["Kernel_Name"]
         key = ("copy" if name.startswith("__amd_rocclr_copyBuffer") and len(out.get("copy", [])) < 3 else
-               "zr" if "conv_rows_kernel" in name else
+               "zr" if ("conv_band_kernel<256, 256>" in name or "conv_rows_kernel" in name) else
                "lookup" if "corr_pyramid_f16_r3_kernel" in name else None)
         if key:
             out.setdefault(key, []).append(float(r["Counter_Value"]))
+            KNAME[key] = name
     return out
 
 
@@ -42,7 +46,7 @@ res = {"calibration": {"fetch_bytes_per_unit": kf, "write_bytes_per_unit": kw,
 for key, name, algo in (("zr", "conv_zr", None), ("lookup", "corr_lookup", 2801664 * E)):
     fb = kf * min(fetch[key])
     wb = kw * min(write[key])
-    d = {"edges": E, "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+    d = {"edges": E, "kernel": KNAME.get(key), "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
          "traffic_bytes_per_launch": fb + wb, "raw_fetch": fetch[key], "raw_write": write[key],
          "calibration": res["calibration"],
          "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; units calibrated on a "

@@ -34,10 +34,11 @@ def test_conv_matches_torch(ks, splits, cout, B, H, W):
     np.testing.assert_allclose(host(out.float()), host(ref), atol=2e-2, rtol=1e-2)
 
 
-def test_fused_update_matches_reference_module():
+@pytest.mark.parametrize("H,W", [(16, 24), (24, 32)])   # generic kernels / band tiles + fused heads
+def test_fused_update_matches_reference_module(H, W):
     from droid_mi355x.fused import FusedUpdateModule
     from droid_mi355x.update import UpdateModule
-    E, H, W = 6, 16, 24
+    E = 6
     m = UpdateModule().to(DEV).eval()
     det_fill(m)
     f = FusedUpdateModule(m)
@@ -202,3 +203,26 @@ def test_conv_gru_epilogues(B, H, W):
     q = torch.tanh(_conv_ref(xq, wq, bq, bbq))
     ref = (1 - z.float()) * h.float() + z.float() * q
     np.testing.assert_allclose(host(hn.float()), host(ref), atol=3e-3)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 8, 64), (3, 16, 32), (1, 48, 64)])
+def test_conv_dw_head_fused(B, H, W):
+    """relu(conv3x3 128->256) -> block-diagonal conv3x3 256->4 in one launch vs torch fp32."""
+    import droid_backends
+    from droid_mi355x.fused import pack_conv, pack_head_taps
+    g = torch.Generator(device=DEV).manual_seed(13)
+    x = torch.randn((B, H, W, 128), generator=g, device=DEV).half()
+    w0 = torch.randn((256, 128, 3, 3), generator=g, device=DEV) / (128 * 9) ** 0.5
+    b0 = torch.randn(256, generator=g, device=DEV) * 0.1
+    head = torch.zeros(4, 256, 3, 3, device=DEV)
+    head[0:2, :128] = torch.randn((2, 128, 3, 3), generator=g, device=DEV) / (128 * 9) ** 0.5
+    head[2:4, 128:] = torch.randn((2, 128, 3, 3), generator=g, device=DEV) / (128 * 9) ** 0.5
+    out = torch.zeros((B, H, W, 4), dtype=torch.float32, device=DEV)
+    droid_backends.conv_dw_head_f16([(x, 0, 128)], pack_conv(w0, [128]), b0, pack_head_taps(head), out)
+    dw = F.relu(F.conv2d(x.float().permute(0, 3, 1, 2), w0.half().float(), b0, padding=1))
+    dw = dw.half().float()   # the hidden map is fp16 (autocast), as in the reference
+    ref = F.conv2d(dw, head.half().float(), None, padding=1).permute(0, 2, 3, 1)
+    np.testing.assert_allclose(host(out), host(ref), atol=2e-3 * max(1.0, float(ref.abs().max())), rtol=1e-3)
+    out2 = torch.zeros_like(out)
+    droid_backends.conv_dw_head_f16([(x, 0, 128)], pack_conv(w0, [128]), b0, pack_head_taps(head), out2)
+    assert torch.equal(out, out2), "dw/head fusion must be deterministic"
