@@ -869,8 +869,11 @@ typedef int rsrc_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) char* lds_cptr_t;
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  // wave-uniform by construction; readfirstlane keeps the descriptor in SGPRs
   const unsigned long long pa = (unsigned long long)base;
-  return rsrc_t{(int)(unsigned)pa, (int)((unsigned)(pa >> 32) & 0xffffu), (int)bytes, kBufFlags};
+  return rsrc_t{__builtin_amdgcn_readfirstlane((int)(unsigned)pa),
+                __builtin_amdgcn_readfirstlane((int)((unsigned)(pa >> 32) & 0xffffu)),
+                __builtin_amdgcn_readfirstlane((int)bytes), kBufFlags};
 }
 
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
@@ -880,9 +883,11 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void dma16(rsrc_t rs, unsigned lds, unsigned voff) {
+  const rsrc_t r = {__builtin_amdgcn_readfirstlane(rs.x), __builtin_amdgcn_readfirstlane(rs.y),
+                    __builtin_amdgcn_readfirstlane(rs.z), __builtin_amdgcn_readfirstlane(rs.w)};
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
                :
-               : "s"(lds), "v"(voff), "s"(rs)
+               : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(r)
                : "memory", "m0");
 }
 #pragma clang diagnostic pop
@@ -893,7 +898,15 @@ __device__ __forceinline__ void dma16(rsrc_t rs, unsigned lds, unsigned voff) {
 //     autocast rounds the gate before using it);
 // (2) coalesced 16-B row pieces: r * h for the r half, the GRU blend
 //     (1 - z) h + z q for q (h, z read as 16-B pieces), then the store.
-template <int TMX, int TN, int FM, int FN>
+// tile row of accumulator row (i, fq, k): pixel fragments are interleaved across
+// the WM pixel waves (fragment i of wave wm = pixels 16 (wm + WM i) ..) or
+// contiguous (wave wm owns pixels wm*FM*16 .. + FM*16)
+template <int FM, int WM, bool CONTIG>
+__device__ __forceinline__ int frag_row(int wm, int i) {
+  return CONTIG ? wm * FM * 16 + 16 * i : 16 * (wm + WM * i);
+}
+
+template <int TMX, int TN, int FM, int FN, int WM = 4, bool CONTIG = false>
 __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
                                               int n0, int wm, int wn, int lane, int tid) {
   constexpr int ER = TN + 8, NT = 512, PPR = TN / 8;
@@ -904,7 +917,7 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
   __syncthreads();  // main-loop LDS reads are done
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
-    const int c = wn * (TN / 2) + j * 16 + fr;
+    const int c = wn * FN * 16 + j * 16 + fr;
     const int co = n0 + c;
     float bv = a.bias ? a.bias[co] : 0.f;
     if (a.bbias) bv += a.bbias[(long)b * a.Cout + co];
@@ -912,7 +925,7 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int r = 16 * (wm + 4 * i) + fq * 4 + k;
+        const int r = frag_row<FM, WM, CONTIG>(wm, i) + fq * 4 + k;
         const float v = acc[i][j][k] + bv;
         float o;
         if (epi == EPI_GRU_ZR) o = sigmoidf_(v);
@@ -964,7 +977,7 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
 //       two contributions (this tile and one neighbour), so the result does not
 //       depend on their order.  Head bias and the weight sigmoid are applied by
 //       the caller.
-template <int FM, int FN>
+template <int FM, int FN, int WM = 4, bool CONTIG = false>
 __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
                                                 int wm, int wn, int lane, int tid) {
   constexpr int TMX = 256, TS = 264, YS = 37, NT = 512;
@@ -978,13 +991,13 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
   __syncthreads();  // main-loop LDS reads are done
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
-    const int c = wn * 128 + j * 16 + fr;
+    const int c = wn * FN * 16 + j * 16 + fr;
     const float bv = a.bias ? a.bias[c] : 0.f;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        T[(16 * (wm + 4 * i) + fq * 4 + k) * TS + c] = (_Float16)fmaxf(acc[i][j][k] + bv, 0.f);
+        T[(frag_row<FM, WM, CONTIG>(wm, i) + fq * 4 + k) * TS + c] = (_Float16)fmaxf(acc[i][j][k] + bv, 0.f);
   }
   for (int idx = tid; idx < 48 * 32; idx += NT) {
     const int r = idx >> 5, p = idx & 31;
@@ -1226,6 +1239,14 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
 
 using namespace droid;
 
+static int band_version() {
+  static const int v = [] {
+    const char* e = getenv("DROID_CONV_BAND");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 static bool rows_enabled() {
   static const bool on = [] {
     const char* e = getenv("DROID_CONV_ROWS");
@@ -1301,11 +1322,8 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
   }();
   const bool halo_ok = !a.im2col && ks > 1 && Cout % 128 == 0 && (ks >> 1) * (W + 1) <= kHaloMax &&
                        epi != EPI_GLO && epi != EPI_HEAD;
-  // LDS-DMA band kernel (DROID_CONV_BAND=0 disables): 3x3, whole-row tiles
-  static const bool band_on = [] {
-    const char* e = getenv("DROID_CONV_BAND");
-    return !(e && atoi(e) == 0);
-  }();
+  // LDS-DMA band kernel (3x3, whole-row tiles); DROID_CONV_BAND=0 disables it
+  const bool band_on = band_version() > 0;
   const bool band_ok = band_on && !a.im2col && ks == 3 && W % 16 == 0 && 64 % W == 0 &&
                        (epi == EPI_GRU_ZR || epi == EPI_GRU_Q || (epi == EPI_ACT && a.stage_out)) &&
                        (epi != EPI_GRU_ZR || gru_ch % 128 == 0);
