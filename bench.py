@@ -32,13 +32,15 @@ import torch  # noqa: E402
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 PEAK_F16_TFLOPS = 2500.0        # MI355X_MICROARCH.md: dense fp16/bf16 MFMA peak (no sparsity)
 LOOKUP_BYTES_PER_EDGE = 2801664  # volume-API lookup, 4 lvl x 64 taps x 2 B x HW + coords + out
+# fused lookup + corr_encoder[0] (corr_ce0_kernel): the same window reads + coords, 128-ch fp16 output
+LOOKUP_CE0_BYTES_PER_EDGE = 4 * 64 * 2 * 3072 + 2 * 4 * 3072 + 128 * 2 * 3072
 # ConvGRU z|r conv (modules/gru.py:19-32, convz+convr fused): 3x3, 448 -> 256 channels
 ZR_FLOPS_PER_PIXEL = 2 * 256 * 448 * 9
 ZR_KERNEL = "conv_band_kernel<256, 256>"   # csrc/conv_kernels.hip, chosen for 48x64 maps
 LOOKUP_KERNEL = "corr_pyramid_f16_r3_kernel"
 
 
-LOOKUP_FN = ["corr_pyramid_lookup_nhwc"]
+LOOKUP_FN = ["corr_lookup_ce0"]
 
 
 def log(*a):
@@ -225,7 +227,7 @@ def main():
         log("setup %.1fs (local edges %d)" % (time.time() - t_setup, e_local))
 
     import droid_backends
-    LOOKUP_FN[0] = "corr_pyramid_lookup" if args.reference_op else "corr_pyramid_lookup_nhwc"
+    LOOKUP_FN[0] = "corr_pyramid_lookup" if args.reference_op else "corr_lookup_ce0"
     lookup = KernelTimer(droid_backends, LOOKUP_FN[0])
     zr = None
     if not args.reference_op:
@@ -266,13 +268,15 @@ def main():
 
     if rank == 0:
         ms = 1000.0 * elapsed / args.steps
-        bytes_per_launch = LOOKUP_BYTES_PER_EDGE * e_local
+        bytes_per_launch = (LOOKUP_BYTES_PER_EDGE if args.reference_op else LOOKUP_CE0_BYTES_PER_EDGE) * e_local
         achieved = bytes_per_launch / (lookup_ms * 1e-3) / 1e9 if lookup_ms else None
-        lookup_roof = {"kernel": "corr_pyramid_f16_r3_kernel<%s> (4-level lookup)" % (
-            "NCHW" if args.reference_op else "NHWC"), "bound": "hbm",
+        lookup_roof = {"kernel": ("corr_pyramid_f16_r3_kernel<NCHW> (4-level lookup)" if args.reference_op else
+                                  "corr_ce0_kernel (4-level lookup fused with corr_encoder[0] 1x1 196->128)"),
+                       "bound": "hbm",
                        "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                        "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
-                       "traffic": load_traffic("corr_lookup", e_local, LOOKUP_KERNEL), "launch_ms": lookup_ms,
+                       "traffic": load_traffic("corr_lookup", e_local, "corr_pyramid_f16_r3_kernel" if args.reference_op
+                                               else "corr_ce0_kernel"), "launch_ms": lookup_ms,
                        "algorithmic_bytes_per_launch": bytes_per_launch}
         if zr_ms:
             flops = ZR_FLOPS_PER_PIXEL * e_local * (args.ht // 8) * (args.wd // 8)

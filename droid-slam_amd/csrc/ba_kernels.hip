@@ -1128,16 +1128,7 @@ static bool use_dataflow_chol() {
   return on;
 }
 
-static int num_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
+static int num_cus() { return device_cu_count(); }
 
 static int launch_chol_dataflow(const BaPlan& p, char* ws, const BaDev& bd, float* dx, hipStream_t stream) {
   if ((size_t)(p.n + 1) * p.ld * 8 >= 0x80000000ull)

@@ -44,6 +44,18 @@ constexpr float kMinDepth = 0.25f;  // droid_kernels.cu:26
 
 __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
+// compute units of the current device (grid size of persistent kernels)
+inline int device_cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 // ---------------------------------------------------------------------------
 // SE3 device helpers.  Pose layout [tx,ty,tz,qx,qy,qz,qw], twist [tau,phi].
 // Formulas restate droid_kernels.cu:58-175 (actSO3, actSE3, adjSE3, relSE3,

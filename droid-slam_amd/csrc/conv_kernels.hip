@@ -1235,6 +1235,108 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
   return kOk;
 }
 
+// ---------------------------------------------------------------------------
+// ConvGRU global context (modules/gru.py:19-32, the glo branch):
+//   glo[e][co] = mean over the edge's pixels of sigmoid(w . h + b)[co] * h[co]
+// for a 1x1 128 -> 128 conv w on the hidden state h itself.  One workgroup per
+// edge streams its pixels in 64-pixel tiles (LDS-DMA, double buffered) against
+// the resident weights; wave w owns output columns 32w .. 32w+31 for every
+// pixel, so the per-column sums stay in registers and the mean is a plain
+// store - no atomics, deterministic.
+constexpr int kGloTP = 64;
+constexpr int kGloLds = 2 * 128 * 128 + 2 * 2 * kGloTP * 128;  // weights + 2 A tiles (bytes)
+
+__global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__ h, const __half* __restrict__ w,
+                                                      const float* __restrict__ bias, float* __restrict__ glo,
+                                                      int HW) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem_glo[];
+  char* lds = reinterpret_cast<char*>(smem_glo);
+  char* Wl = lds;                     // [2 k-chunks][128 co][128 B]
+  char* Al = lds + 2 * 128 * 128;     // [2 buf][2 k-chunks][64 px][128 B]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int e = blockIdx.x;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ntile = HW / kGloTP;
+  // weights -> LDS (swizzled 16-B slots)
+  for (int idx = tid; idx < 128 * 16; idx += 256) {
+    const int co = idx >> 4, q = idx & 15, c = q >> 3, piece = q & 7;
+    *reinterpret_cast<uint4*>(Wl + c * 16384 + co * 128 + ((piece ^ (co & 7)) << 4)) =
+        *reinterpret_cast<const uint4*>(w + co * 128 + c * 64 + piece * 8);
+  }
+  const __half* he = h + (long)e * HW * 128;
+  const rsrc_t rs = make_rsrc(he, (unsigned)HW * 256);
+  const unsigned Al_a = lds_addr(Al);
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  // DMA: 16 instructions of 8 pixel rows (one k-chunk) per tile, 4 per wave:
+  // instruction q = wave + 4*i: chunk q & 1, pixels 8 (q >> 1) .. +8
+  const int lrow = lane >> 3, lpiece = (lane & 7) ^ lrow;
+  auto issue = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = wave_u + 4 * i, c = q & 1, pr = (q >> 1) * 8;
+      const unsigned off = (unsigned)(((t * kGloTP + pr + lrow) * 128 + c * 64 + lpiece * 8) * 2);
+      dma16(rs, Al_a + (t & 1) * 16384 + c * 8192 + pr * 128, off);
+    }
+  };
+  float bj[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bj[j] = bias[wave * 32 + j * 16 + fr];
+  float colsum[2] = {0.f, 0.f};
+  issue(0);
+  for (int t = 0; t < ntile; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // tile t landed (all waves); tile t-1's reads done
+    if (t + 1 < ntile) issue(t + 1);
+    const char* At = Al + (t & 1) * 16384;
+    floatx4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int c = ks >> 1, kq = (ks & 1) * 4 + fq;
+      half8 af[4], bf[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = i * 16 + fr;
+        af[i] = *reinterpret_cast<const half8*>(At + c * 8192 + r * 128 + ((kq ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int co = wave * 32 + j * 16 + fr;
+        bf[j] = *reinterpret_cast<const half8*>(Wl + c * 16384 + co * 128 + ((kq ^ (co & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    // sigmoid(. + b) * h summed over the tile's pixels (h = the tile itself: k == co)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int co = wave * 32 + j * 16 + fr, c = co >> 6, kk = co & 63;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int r = i * 16 + fq * 4 + k;
+          const float hv = (float)*reinterpret_cast<const _Float16*>(
+              At + c * 8192 + r * 128 + ((((kk >> 3) ^ (r & 7)) << 4) | ((kk & 7) << 1)));
+          colsum[j] += sigmoidf_(acc[i][j][k] + bj[j]) * hv;
+        }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    float v = colsum[j];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (fq == 0) glo[(long)e * 128 + wave * 32 + j * 16 + fr] = v / (float)HW;
+  }
+}
+
 }  // namespace droid
 
 using namespace droid;
@@ -1332,6 +1434,8 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
     return launch_band<256, 256>(a, stream);
   if (band_ok && Cout % 128 == 0 && 384 % W == 0 && (H * W) % 384 == 0 && band_fits<384, 128>(W, &ns_, &nh_))
     return launch_band<384, 128>(a, stream);
+  if (band_ok && Cout == 64 && 384 % W == 0 && (H * W) % 384 == 0 && band_fits<384, 64>(W, &ns_, &nh_))
+    return launch_band<384, 64>(a, stream);
   // row-band variant: tile = whole image rows, zero-padded halo, no masks
   const int pad = ks >> 1;
   const bool rows_ok = halo_ok && halo_nw == 8 && 256 % W == 0 && W % 16 == 0 && (H * W) % 256 == 0 &&
@@ -1381,6 +1485,26 @@ int droid_conv_dw_head_f16(const void* const* srcs, const int* C, const int* cst
   a.out32 = (float*)out32;
   if (B == 0) return kOk;
   return launch_band<256, 256, true>(a, stream);
+}
+
+// ConvGRU global context (gru_glo_kernel): h (E, HW, 128) fp16, w [128][128]
+// fp16 (the 1x1 conv weight, [co][ci]), bias [128] f32 -> glo (E, 128) f32.
+int droid_gru_global_f16(const void* h, const void* w, const float* bias, float* glo, int E, int HW,
+                         hipStream_t stream) {
+  if (E < 0 || HW <= 0 || !h || !w || !bias || !glo) return fail(kInvalidArgument, "gru_global_f16: bad arguments");
+  if (HW % kGloTP || (long)HW * 256 > 0x7fffffffL || (reinterpret_cast<uintptr_t>(h) & 15) ||
+      (reinterpret_cast<uintptr_t>(w) & 15))
+    return fail(kUnsupported, "gru_global_f16: needs H*W % 64 == 0 and 16-B aligned operands");
+  if (E == 0) return kOk;
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gru_glo_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kGloLds));
+    attr = true;
+  }
+  gru_glo_kernel<<<E, 256, kGloLds, stream>>>((const __half*)h, (const __half*)w, bias, glo, HW);
+  DROID_LAUNCH_CHECK();
+  return kOk;
 }
 }  // extern "C"
 

@@ -489,6 +489,257 @@ int droid_corr_pyramid_lookup_nhwc(const void* const* levels, const int* H2s, co
   return kOk;
 }
 
+namespace droid {
+
+// ---------------------------------------------------------------------------
+// Fused CorrBlock lookup + corr_encoder[0] (modules/corr.py:40-50 feeding
+// droid_net.py:84-86: conv1x1 196 -> 128, bias, ReLU): the 196-channel
+// lookup of a 128-pixel tile is built in LDS (bit-identical to
+// corr_pyramid_f16_r3_kernel) and multiplied on MFMA by the resident 1x1
+// weights, so the 2.5 GB lookup tensor of a 2048-edge graph is never written
+// or re-read.  Persistent: one 8-wave workgroup per CU keeps the 128x224
+// weight tile in LDS and walks the pixel tiles; while tile t is multiplied and
+// stored, the window rows of tile t+1 (issued right after t's gather) and the
+// coordinates of tile t+2 are in flight.
+// Gather: wave w handles level w & 3 for pixels 64 (w >> 2) + lane; each
+// lane loads its 8 window rows as 2 aligned 16-B chunks (W2 % 8 == 0).
+// ---------------------------------------------------------------------------
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float floatx4_t __attribute__((ext_vector_type(4)));
+
+struct CorrCe0Args {
+  const __half* vol[4];
+  int H2[4], W2[4];
+  const float* coords;  // (E, H, W, 2)
+  int fast;             // bit l: level l rows are 16-B aligned (W2 % 8 == 0)
+  const __half* w;      // [128][224], columns >= 196 zero
+  const float* bias;    // [128]
+  __half* out;          // (E, H, W, 128)
+  int HW;
+  long ntiles;
+};
+
+constexpr int kCeTP = 128, kCeKS = 232, kCeOS = 136;
+constexpr int kCeLds = (2 * 128 * kCeKS + kCeTP * kCeOS) * 2;
+
+__global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem_ce[];
+  _Float16* Ws = smem_ce;                 // [128 co][kCeKS]
+  _Float16* As = Ws + 128 * kCeKS;        // [128 px][kCeKS] lookup tile (cols 196.. zero)
+  _Float16* Os = As + kCeTP * kCeKS;      // [128 px][kCeOS] output staging
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lvl = wave & 3, px = (wave >> 2) * 64 + lane;
+  const int HW = a.HW, tpe = HW / kCeTP;  // tiles per edge
+
+  for (int idx = tid; idx < 128 * 29; idx += 512) {
+    const int r = idx / 29, q = idx - r * 29;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (q < 28) v = *reinterpret_cast<const uint4*>(a.w + r * 224 + q * 8);
+    *reinterpret_cast<uint4*>(&Ws[r * kCeKS + q * 8]) = v;
+  }
+  for (int idx = tid; idx < kCeTP * 36; idx += 512) {
+    const int r = idx / 36, c = idx - r * 36;
+    As[r * kCeKS + 196 + c] = (_Float16)0.f;
+  }
+
+  const int H2 = a.H2[lvl], W2 = a.W2[lvl], nch = W2 >> 3;
+  const bool fast = (a.fast >> lvl) & 1;  // rows 16-B aligned
+  const __half* vol = a.vol[lvl];
+  const long slice = (long)H2 * W2;
+  const float scl = 1.0f / (float)(1 << lvl);
+
+  // per-lane gather state of one tile
+  uint4 raw[8][2];
+  float cx = 0.f, cy = 0.f;      // coordinates of the tile being loaded
+  float ncx = 0.f, ncy = 0.f;    // coordinates of the tile after it
+  float wdx = 0.f, wdy = 0.f;    // bilinear fractions of the loaded tile
+  int woff = 0;                  // window x offset within the first chunk
+  auto tile_pixel = [&](long t) { return (t / tpe) * (long)HW + (t % tpe) * kCeTP + px; };
+  auto load_coords = [&](long t, float& x, float& y) {
+    if (t < a.ntiles) {
+      const float2 c = *reinterpret_cast<const float2*>(a.coords + tile_pixel(t) * 2);
+      x = c.x; y = c.y;
+    }
+  };
+  auto issue = [&](long t) {
+    if (t >= a.ntiles) return;
+    const float x0 = cx * scl, y0 = cy * scl;
+    const float fx0 = floorf(x0), fy0 = floorf(y0);
+    wdx = x0 - fx0; wdy = y0 - fy0;
+    const int xi0 = (int)fx0, yi0 = (int)fy0;
+    const int xs = xi0 - 3;
+    const int c0 = (xs >= 0) ? (xs >> 3) : -((-xs + 7) >> 3);
+    woff = xs - 8 * c0;
+    const __half* base = vol + tile_pixel(t) * slice;
+    if (fast) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int y1 = yi0 - 3 + j;
+        const bool yok = y1 >= 0 && y1 < H2;
+        const __half* row = base + (long)y1 * W2;
+        raw[j][0] = (yok && c0 >= 0 && c0 < nch) ? *reinterpret_cast<const uint4*>(row + 8 * c0)
+                                                 : make_uint4(0, 0, 0, 0);
+        raw[j][1] = (yok && c0 + 1 >= 0 && c0 + 1 < nch) ? *reinterpret_cast<const uint4*>(row + 8 * (c0 + 1))
+                                                          : make_uint4(0, 0, 0, 0);
+      }
+    } else {
+      // rows not 16-B aligned (W2 % 8 != 0): the 8 taps one by one, packed as an
+      // aligned chunk (window offset 0)
+      woff = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int y1 = yi0 - 3 + j;
+        const bool yok = y1 >= 0 && y1 < H2;
+        const unsigned short* row = reinterpret_cast<const unsigned short*>(base + (long)y1 * W2);
+        unsigned u[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int xa = xs + 2 * m, xb = xa + 1;
+          const unsigned lo = (yok && xa >= 0 && xa < W2) ? row[xa] : 0u;
+          const unsigned hi = (yok && xb >= 0 && xb < W2) ? row[xb] : 0u;
+          u[m] = lo | (hi << 16);
+        }
+        raw[j][0] = make_uint4(u[0], u[1], u[2], u[3]);
+        raw[j][1] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  // row j of the loaded window as 8 floats (the taps x = xs .. xs+7)
+  auto row_taps = [&](int j, float* t) {
+    const unsigned u[8] = {raw[j][0].x, raw[j][0].y, raw[j][0].z, raw[j][0].w,
+                           raw[j][1].x, raw[j][1].y, raw[j][1].z, raw[j][1].w};
+    const int k = woff >> 1;
+    unsigned v[6], w[5];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v[i] = (k & 2) ? u[i + 2] : u[i];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) w[i] = (k & 1) ? v[i + 1] : v[i];
+    const unsigned sh = (woff & 1) ? 16u : 0u;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const unsigned o = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
+      t[2 * m + 0] = __half2float(__ushort_as_half((unsigned short)(o & 0xffffu)));
+      t[2 * m + 1] = __half2float(__ushort_as_half((unsigned short)(o >> 16)));
+    }
+  };
+
+  // GEMM geometry: waves 4 (32 px) x 2 (64 co)
+  const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fq = lane >> 4;
+  float bias[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bias[j] = a.bias[wn * 64 + j * 16 + fr];
+
+  long t = blockIdx.x;
+  load_coords(t, cx, cy);
+  load_coords(t + gridDim.x, ncx, ncy);
+  issue(t);
+  __syncthreads();  // weights and pad columns are in LDS
+  for (; t < a.ntiles; t += gridDim.x) {
+    // (1) bilinear windows of tile t -> As (corr_pyramid_f16_r3_kernel arithmetic)
+    {
+      const float w11 = rnd16(wdx * wdy);
+      const float w10 = rnd16(wdx * (1.0f - wdy));
+      const float w01 = rnd16((1.0f - wdx) * wdy);
+      const float w00 = rnd16((1.0f - wdx) * (1.0f - wdy));
+      _Float16* arow = As + px * kCeKS + lvl * 49;
+      float prev[8], cur[8];
+#pragma unroll
+      for (int j = 0; j <= 7; ++j) {
+        row_taps(j, cur);
+        if (j > 0) {
+          const int b = j - 1;
+#pragma unroll
+          for (int q = 0; q < 7; ++q) {
+            float acc = 0.f + rnd16(prev[q] * w00);
+            acc = rnd16(acc + rnd16(cur[q] * w01));
+            acc = rnd16(acc + rnd16(prev[q + 1] * w10));
+            acc = rnd16(acc + rnd16(cur[q + 1] * w11));
+            arow[q * 7 + b] = (_Float16)__half2float(__float2half(acc));
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) prev[i] = cur[i];
+      }
+    }
+    // (2) next tiles in flight while this one is multiplied and stored
+    cx = ncx; cy = ncy;
+    issue(t + gridDim.x);
+    load_coords(t + 2L * gridDim.x, ncx, ncy);
+    __syncthreads();
+    // (3) 128 px x 128 co x 224 on MFMA
+    floatx4_t acc[2][4];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[f][j] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 7; ++ks) {
+      half8_t af[2], bf[4];
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+        af[f] = *reinterpret_cast<const half8_t*>(&As[(wm * 32 + f * 16 + fr) * kCeKS + ks * 32 + fq * 8]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bf[j] = *reinterpret_cast<const half8_t*>(&Ws[(wn * 64 + j * 16 + fr) * kCeKS + ks * 32 + fq * 8]);
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[f], bf[j], acc[f][j], 0, 0, 0);
+    }
+    // (4) bias + ReLU -> Os -> coalesced 16-B stores
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          Os[(wm * 32 + f * 16 + fq * 4 + k) * kCeOS + wn * 64 + j * 16 + fr] =
+              (_Float16)fmaxf(acc[f][j][k] + bias[j], 0.f);
+    __syncthreads();
+    const long pix0 = (t / tpe) * (long)HW + (t % tpe) * kCeTP;
+    for (int idx = tid; idx < kCeTP * 16; idx += 512) {
+      const int r = idx >> 4, q = idx & 15;
+      *reinterpret_cast<uint4*>(a.out + (pix0 + r) * 128 + q * 8) = *reinterpret_cast<const uint4*>(&Os[r * kCeOS + q * 8]);
+    }
+  }
+}
+
+}  // namespace droid
+
+// Fused CorrBlock lookup + corr_encoder[0] (see corr_ce0_kernel).
+int droid_corr_lookup_ce0(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
+                          const void* w, const float* bias, void* out, int E, int H, int W, hipStream_t stream) {
+  using namespace droid;
+  if ((H * W) % kCeTP)
+    return fail(kUnsupported, "corr_lookup_ce0: H*W must be a multiple of 128");
+  CorrCe0Args a{};
+  for (int l = 0; l < 4; ++l) {
+    if (H2s[l] <= 0 || W2s[l] <= 0) return fail(kInvalidArgument, "corr_lookup_ce0: empty level");
+    if (W2s[l] % 8 == 0 && (reinterpret_cast<uintptr_t>(levels[l]) & 15) == 0) a.fast |= 1 << l;
+    a.vol[l] = (const __half*)levels[l];
+    a.H2[l] = H2s[l];
+    a.W2[l] = W2s[l];
+  }
+  if (!w || !bias || !out || !coords) return fail(kInvalidArgument, "corr_lookup_ce0: null pointer");
+  a.coords = coords;
+  a.w = (const __half*)w;
+  a.bias = bias;
+  a.out = (__half*)out;
+  a.HW = H * W;
+  a.ntiles = (long)E * (H * W / kCeTP);
+  if (a.ntiles == 0) return kOk;
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_ce0_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kCeLds));
+    attr = true;
+  }
+  const long grid = std::min<long>(a.ntiles, device_cu_count());
+  corr_ce0_kernel<<<dim3((unsigned)grid), 512, kCeLds, stream>>>(a);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
 int droid_altcorr_forward(int dtype, const void* fmap1, const void* fmap2, const float* coords,
                           void* corr, int B, int S, int H, int W, int H2, int W2, int C,
                           int radius, hipStream_t stream) {

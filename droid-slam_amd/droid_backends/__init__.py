@@ -131,6 +131,33 @@ def corr_pyramid_lookup_nhwc(levels, coords, out_cstride=200, out=None):
     return out
 
 
+def corr_lookup_ce0_supported(levels, H, W):
+    """Shapes droid_corr_lookup_ce0 accepts: 4 levels, H*W % 128 == 0."""
+    return len(levels) == 4 and (H * W) % 128 == 0
+
+
+def corr_lookup_ce0(levels, coords, w, bias, out=None):
+    """Fused CorrBlock lookup + corr_encoder[0] (include/droid_backends.h:
+    droid_corr_lookup_ce0): levels 4 x (E,H,W,H2,W2) fp16, coords (E,H,W,2) f32,
+    w [128][224] fp16, bias [128] f32 -> (E,H,W,128) fp16 = relu(w . lookup + b)."""
+    _check_inputs(["level%d" % i for i in range(len(levels))] + ["coords", "w", "bias"],
+                  list(levels) + [coords, w, bias])
+    _need(coords, torch.float32, "coords")
+    _need(w, torch.float16, "w")
+    _need(bias, torch.float32, "bias")
+    E, H, W = levels[0].shape[:3]
+    if out is None:
+        out = torch.empty((E, H, W, 128), dtype=torch.float16, device=coords.device)
+    L = len(levels)
+    ptrs = (ctypes.c_void_p * L)(*[lv.data_ptr() for lv in levels])
+    h2s = (ctypes.c_int * L)(*[lv.shape[3] for lv in levels])
+    w2s = (ctypes.c_int * L)(*[lv.shape[4] for lv in levels])
+    with torch.cuda.device(coords.device):
+        check(lib.droid_corr_lookup_ce0(ptrs, h2s, w2s, _ptr(coords), _ptr(w), _ptr(bias), _ptr(out), E, H, W,
+                                        _stream(coords)), "corr_lookup_ce0")
+    return out
+
+
 EPI_ACT, EPI_GRU_ZR, EPI_GRU_Q, EPI_HEAD, EPI_GLO = 0, 1, 2, 3, 4
 
 
@@ -185,6 +212,24 @@ def conv_dw_head_f16(sources, wp, bias, head_w, out32):
         check(lib.droid_conv_dw_head_f16(ptrs, cs, strides, n, _ptr(wp), _ptr(bias), B, H, W, _ptr(head_w),
                                          _ptr(out32), _stream(t0)), "conv_dw_head_f16")
     return out32
+
+
+def gru_global_f16(h, w, bias, out=None):
+    """ConvGRU global context (include/droid_backends.h: droid_gru_global_f16):
+    h (E,H,W,128) fp16, w [128][128] fp16, bias [128] f32 -> (E,128) f32."""
+    _check_inputs(("h", "w", "bias"), (h, w, bias))
+    _need(h, torch.float16, "h")
+    _need(w, torch.float16, "w")
+    _need(bias, torch.float32, "bias")
+    E, H, W, C = h.shape
+    if C != 128 or tuple(w.shape) != (128, 128):
+        raise RuntimeError("gru_global_f16: h must have 128 channels and w be 128x128")
+    if out is None:
+        out = torch.empty((E, 128), dtype=torch.float32, device=h.device)
+    with torch.cuda.device(h.device):
+        check(lib.droid_gru_global_f16(_ptr(h), _ptr(w), _ptr(bias), _ptr(out), E, H * W, _stream(h)),
+              "gru_global_f16")
+    return out
 
 
 def segment_mean_f16(src, seg_ptr, seg_idx, num_segments, out=None):

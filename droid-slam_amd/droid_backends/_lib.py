@@ -28,9 +28,11 @@ _SIGS = {
     "droid_corr_index_backward": ([_i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p], _i),
     "droid_corr_pyramid_lookup": ([_i, _p, _p, _p, _i, _p, _p, _i, _i, _i, _i, _p], _i),
     "droid_corr_pyramid_lookup_nhwc": ([_p, _p, _p, _i, _p, _p, _i, _i, _i, _i, _p], _i),
+    "droid_corr_lookup_ce0": ([_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_conv_nhwc_f16": ([_p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _i, _i,
                              _p, _i, _p, _i, _p, _p, _i, _p, _p], _i),
     "droid_conv_dw_head_f16": ([_p, _p, _p, _i, _p, _p, _i, _i, _i, _p, _p, _p], _i),
+    "droid_gru_global_f16": ([_p, _p, _p, _p, _i, _i, _p], _i),
     "droid_segment_mean_f16": ([_p, _p, _p, _p, _i, ctypes.c_long, _p], _i),
     "droid_altcorr_forward": ([_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p], _i),
     "droid_altcorr_backward": ([_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p], _i),

@@ -15,7 +15,7 @@ import torch
 import droid_backends
 
 from .corr import AltCorrBlock, CorrBlock
-from .fused import edge_segments
+from .fused import PendingLookup, edge_segments
 
 
 def _coords_grid(ht, wd, device):
@@ -208,7 +208,7 @@ class FactorGraph:
         uniq, inverse = np.unique(self._ii, return_inverse=True)
         dinv = self._dev("inverse", inverse.astype(np.int64))
         if self.fused:
-            corr = self.corr.lookup_nhwc(coords1)
+            corr = PendingLookup(self.corr, coords1)   # lookup runs fused with corr_encoder[0]
             ptr, idx = edge_segments(inverse, len(uniq))
             segs = (self._dev("seg_ptr", ptr), self._dev("seg_idx", idx))
             self.net, delta, weight, damping = self.update_op(self.net, self.inp, corr, motn[0], dinv, len(uniq),

@@ -8,13 +8,17 @@ Same parameters (state-dict names) and forward semantics as UpdateModule
   * convz and convr run as ONE conv with 256 outputs whose epilogue applies
     both sigmoids and writes z and r*h; convq's epilogue applies tanh and the
     GRU blend (1-z) h + z q in place of four elementwise kernels;
-  * the global-context branch (sigmoid(w(h)) * h averaged over pixels) is a
-    conv epilogue that reduces over the tile and atomically accumulates;
+  * the global-context branch (sigmoid(w(h)) * h averaged over pixels) is one
+    streaming kernel per edge (gru_global_f16): weights resident in LDS, column
+    sums in registers, no atomics;
   * delta.0 and weight.0 share one conv (256 outputs); delta.2 and weight.2
     run as one block-diagonal conv whose epilogue applies the weight sigmoid;
   * on the 48x64 maps the delta/weight heads run as ONE launch (conv_dw_head_f16):
     the 256-channel hidden map stays in LDS and the two 3x3 256->2 heads are
     accumulated from it; head bias and sigmoid are applied afterwards;
+  * the correlation lookup can be handed over unevaluated (PendingLookup): the
+    lookup and corr_encoder[0] then run as ONE kernel (corr_lookup_ce0) and the
+    196-channel lookup tensor is never materialised;
   * GraphAgg's upmask is not computed: update() discards it (factor_graph.py:209).
 All convs: fp16 operands, fp32 accumulation (the reference's autocast).
 """
@@ -67,6 +71,19 @@ def pack_head_taps(head):
     return w.to(torch.float16).contiguous()
 
 
+class PendingLookup:
+    """A CorrBlock lookup (modules/corr.py:40-50) at `coords` (1,E,H,W,2), not yet
+    evaluated: FusedUpdateModule runs it fused with corr_encoder[0] when the
+    shapes allow, else materialises it with CorrBlock.lookup_nhwc."""
+
+    def __init__(self, block, coords):
+        self.block = block
+        self.coords = coords
+
+    def materialise(self):
+        return self.block.lookup_nhwc(self.coords)
+
+
 def edge_segments(inverse, num_unique):
     """CSR (seg_ptr (U+1), seg_idx (E)) int64 of the edges per source-frame slot.
     `inverse` may be a numpy array (built on the host) or a device tensor."""
@@ -104,6 +121,9 @@ class FusedUpdateModule(torch.nn.Module):
         ce0 = torch.zeros(128, 200, 1, 1, device=m.corr_encoder[0].weight.device)
         ce0[:, :196] = m.corr_encoder[0].weight   # lookup rows are padded to 200 channels
         P["ce0"] = pack_conv(ce0, [200])
+        w224 = torch.zeros(128, 224, device=ce0.device)
+        w224[:, :196] = m.corr_encoder[0].weight[:, :, 0, 0]
+        P["ce0_224"] = w224.to(torch.float16).contiguous()
         P["ce0_b"] = m.corr_encoder[0].bias.float().contiguous()
         P["ce2"] = pack_conv(m.corr_encoder[2].weight, [128])
         P["ce2_b"] = m.corr_encoder[2].bias.float().contiguous()
@@ -115,6 +135,7 @@ class FusedUpdateModule(torch.nn.Module):
         P["fe2_b"] = m.flow_encoder[2].bias.float().contiguous()
         P["w"] = pack_conv(g.w.weight, [128])
         P["w_b"] = g.w.bias.float().contiguous()
+        P["w_128"] = g.w.weight[:, :, 0, 0].to(torch.float16).contiguous()
         splits = [128, 128, 128, 64]
         P["zr"] = pack_conv(torch.cat([g.convz.weight, g.convr.weight], 0), splits)
         P["zr_b"] = torch.cat([g.convz.bias, g.convr.bias]).float().contiguous()
@@ -141,7 +162,8 @@ class FusedUpdateModule(torch.nn.Module):
 
     @torch.no_grad()
     def forward(self, net, inp, corr, motn, inverse, num_unique, segments=None):
-        """net, inp (E,H,W,128) fp16; corr (E,H,W,200) fp16 (196 used); motn
+        """net, inp (E,H,W,128) fp16; corr (E,H,W,200) fp16 (196 used) or a
+        PendingLookup; motn
         (E,4,H,W) fp32; inverse (E) frame slot of each edge's source, num_unique
         frames; segments = optional (seg_ptr (U+1), seg_idx (E)) int64 CSR of
         `inverse` (edge_segments) -> net' (E,H,W,128) fp16, delta (1,E,H,W,2)
@@ -154,8 +176,15 @@ class FusedUpdateModule(torch.nn.Module):
         conv = droid_backends.conv_nhwc_f16
         e16 = lambda c: torch.empty((E, H, W, c), dtype=torch.float16, device=dev)
 
-        c1 = e16(128)
-        conv([(corr, 0, 200)], P["ce0"], 128, 1, bias=P["ce0_b"], act=1, out=c1)
+        levels = corr.block.corr_pyramid if isinstance(corr, PendingLookup) else None
+        if levels is not None and droid_backends.corr_lookup_ce0_supported(levels, H, W):
+            coords = corr.coords.reshape(E, H, W, 2).float().contiguous()
+            c1 = droid_backends.corr_lookup_ce0(levels, coords, P["ce0_224"], P["ce0_b"])
+        else:
+            if isinstance(corr, PendingLookup):
+                corr = corr.materialise()
+            c1 = e16(128)
+            conv([(corr, 0, 200)], P["ce0"], 128, 1, bias=P["ce0_b"], act=1, out=c1)
         cf = e16(128)
         conv([(c1, 0, 128)], P["ce2"], 128, 3, bias=P["ce2_b"], act=1, out=cf)
         m8 = torch.zeros((E, H, W, 8), dtype=torch.float16, device=dev)
@@ -165,8 +194,11 @@ class FusedUpdateModule(torch.nn.Module):
         ff = e16(64)
         conv([(f1, 0, 128)], P["fe2"], 64, 3, bias=P["fe2_b"], act=1, out=ff)
 
-        glo = torch.zeros((E, 128), dtype=torch.float32, device=dev)
-        conv([(net, 0, 128)], P["w"], 128, 1, bias=P["w_b"], epi=EPI_GLO, h=net, out32=glo)
+        if (H * W) % 64 == 0:
+            glo = droid_backends.gru_global_f16(net, P["w_128"], P["w_b"])
+        else:
+            glo = torch.zeros((E, 128), dtype=torch.float32, device=dev)
+            conv([(net, 0, 128)], P["w"], 128, 1, bias=P["w_b"], epi=EPI_GLO, h=net, out32=glo)
         gb = torch.addmm(P["glo_b"], glo, P["glo_w"].t())          # (E, 384): z | r | q
         z = e16(128)
         rn = e16(128)

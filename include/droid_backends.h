@@ -64,6 +64,16 @@ int droid_corr_pyramid_lookup_nhwc(const void* const* levels, const int* H2s, co
                                    int num_levels, const float* coords, void* out, int out_cstride,
                                    int E, int H, int W, hipStream_t stream);
 
+/* CorrBlock lookup fused with the update operator's corr_encoder[0]
+ * (modules/corr.py:40-50 + droid_net.py:84-86): out (E,H,W,128) fp16 =
+ * relu(conv1x1(lookup(coords), w) + bias), the 196-channel lookup never
+ * leaving the CU (bit-identical to droid_corr_pyramid_lookup_nhwc's values).
+ * levels: the 4 fp16 volumes (E,H,W,H2,W2); coords
+ * (E,H,W,2) f32; w [128][224] fp16 (channel-major rows, columns >= 196 zero);
+ * bias [128] f32.  Needs H*W % 128 == 0, else DROID_UNSUPPORTED. */
+int droid_corr_lookup_ce0(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
+                          const void* w, const float* bias, void* out, int E, int H, int W, hipStream_t stream);
+
 /* ---- update operator ----------------------------------------------------
  * Implicit-GEMM convolution on MFMA (UpdateModule / ConvGRU convs,
  * droid_net.py:78-143, modules/gru.py:19-32), NHWC fp16 in, fp32 accumulate.
@@ -92,6 +102,13 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
 int droid_conv_dw_head_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc, const void* wp,
                            const float* bias, int B, int H, int W, const void* hw, void* out32,
                            hipStream_t stream);
+
+/* ConvGRU global context (modules/gru.py:19-32): glo[e][co] = mean over the
+ * H*W pixels of edge e of sigmoid(w . h + bias)[co] * h[co], for h (E,H,W,128)
+ * fp16 and the 1x1 conv w [128][128] fp16 ([co][ci]), bias [128] f32 -> glo
+ * (E,128) f32 (plain stores, deterministic).  Needs H*W % 64 == 0. */
+int droid_gru_global_f16(const void* h, const void* w, const float* bias, float* glo, int E, int HW,
+                         hipStream_t stream);
 
 /* GraphAgg scatter_mean (droid_net.py:27-45, torch_scatter.scatter_mean over
  * dim 1): out[u] = mean of src rows seg_idx[seg_ptr[u] .. seg_ptr[u+1]), rows of

@@ -149,7 +149,8 @@ BAND_CASES = [([128, 128, 128, 64], 256, 2, 8, 64),    # z|r-shaped, 256-tile, i
               ([128, 128, 128, 64], 128, 2, 12, 64),   # q-shaped, 384-tile (6 rows)
               ([128], 128, 1, 48, 64),                 # the update operator's 48x64 maps
               ([96, 64], 128, 2, 24, 32),              # source narrower than its 64-channel chunk
-              ([64], 256, 2, 16, 16)]                  # 256-tile of 16 rows
+              ([64], 256, 2, 16, 16),                  # 256-tile of 16 rows
+              ([128], 64, 2, 12, 64)]                  # flow_encoder[2]-shaped, 384x64 tile
 
 
 def _conv_ref(xs, w, bias, bb):
@@ -226,3 +227,46 @@ def test_conv_dw_head_fused(B, H, W):
     out2 = torch.zeros_like(out)
     droid_backends.conv_dw_head_f16([(x, 0, 128)], pack_conv(w0, [128]), b0, pack_head_taps(head), out2)
     assert torch.equal(out, out2), "dw/head fusion must be deterministic"
+
+
+@pytest.mark.parametrize("E,H,W", [(3, 16, 24), (2, 8, 64)])
+def test_corr_lookup_ce0_fused(E, H, W):
+    """Lookup + corr_encoder[0] in one kernel == bit-exact lookup followed by the
+    1x1 conv in fp32 (modules/corr.py:40-50, droid_net.py:84-86)."""
+    import droid_backends
+    from droid_mi355x.corr import CorrBlock
+    rng = np.random.default_rng(21)
+    f1 = torch.from_numpy(rng.normal(size=(1, E, 128, H, W)).astype(np.float16)).to(DEV)
+    f2 = torch.from_numpy(rng.normal(size=(1, E, 128, H, W)).astype(np.float16)).to(DEV)
+    cb = CorrBlock(f1, f2)
+    coords = (np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None, None]
+              + rng.normal(0, 4, (1, E, H, W, 2))).astype(np.float32)   # windows leave the volume at borders
+    c = torch.from_numpy(coords).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(22)
+    w = torch.randn((128, 196), generator=g, device=DEV) / 14.0
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    w224 = torch.zeros((128, 224), device=DEV)
+    w224[:, :196] = w
+    w224 = w224.half().contiguous()
+    with torch.no_grad():
+        out = droid_backends.corr_lookup_ce0(cb.corr_pyramid, c.view(E, H, W, 2).contiguous(), w224, b)
+        look = cb.lookup_nhwc(c)[..., :196].float()
+    ref = F.relu(look @ w224[:, :196].float().t() + b)
+    np.testing.assert_allclose(host(out.float()), host(ref), atol=2e-3 * max(1.0, float(ref.abs().max())), rtol=2e-3)
+    out2 = droid_backends.corr_lookup_ce0(cb.corr_pyramid, c.view(E, H, W, 2).contiguous(), w224, b)
+    assert torch.equal(out, out2)
+
+
+@pytest.mark.parametrize("E,H,W", [(3, 8, 24), (2, 48, 64)])
+def test_gru_global_context(E, H, W):
+    """glo = mean_px sigmoid(conv1x1(h) + b) * h (modules/gru.py:24-26) vs torch fp32."""
+    import droid_backends
+    g = torch.Generator(device=DEV).manual_seed(23)
+    h = torch.tanh(torch.randn((E, H, W, 128), generator=g, device=DEV)).half()
+    w = (torch.randn((128, 128), generator=g, device=DEV) / 11.3).half()
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    out = droid_backends.gru_global_f16(h, w, b)
+    hf = h.float().view(E, H * W, 128)
+    ref = (torch.sigmoid(hf @ w.float().t() + b) * hf).mean(1)
+    np.testing.assert_allclose(host(out), host(ref), atol=1e-4, rtol=1e-3)
+    assert torch.equal(out, droid_backends.gru_global_f16(h, w, b))
