@@ -34,6 +34,7 @@
 //   EPI_GLO   : sigmoid(.) * h summed over the tile's pixels, atomically added
 //               (scaled by 1/HW) into glo[b][co]: the GRU global-context mean
 #include "common.hpp"
+#include <algorithm>
 
 namespace droid {
 
@@ -1337,6 +1338,119 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------
+// flow_encoder[0] (droid_net.py:88-90: conv7x7 4 -> 128, ReLU) straight from the
+// motion features motn (E,4,H,W) fp32 (the conv input cast to fp16 as under
+// autocast).  Persistent: one 8-wave workgroup per CU keeps the packed weights
+// (K = 52 taps x 8 channels, 4 real) in LDS and walks 128-pixel tiles; a tile's
+// input band (its rows +-3, fp16, 8 channels per pixel with zero padding) is a
+// few KB of LDS, built from registers loaded during the previous tile.  A K-step
+// of 32 = 4 taps x 8 channels, so each A fragment is one 16-B LDS read.
+constexpr int kFeTP = 128, kFeK = 416, kFeKS = kFeK + 8, kFeOS = 136;
+
+__host__ __device__ constexpr int fe_lds_bytes(int W) {
+  return 128 * kFeKS * 2 + (kFeTP / W + 6) * (W + 6) * 16 + kFeTP * kFeOS * 2;
+}
+
+__global__ void __launch_bounds__(512) flow_enc0_kernel(const float* __restrict__ motn, const __half* __restrict__ w,
+                                                        const float* __restrict__ bias, __half* __restrict__ out,
+                                                        int H, int W, long ntiles) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem_fe[];
+  const int RB = kFeTP / W + 6, PW = W + 6;  // band rows, padded row length (pixels)
+  _Float16* Ws = smem_fe;                    // [128][kFeKS]
+  _Float16* In = Ws + 128 * kFeKS;           // [RB][PW][8]
+  _Float16* Os = In + RB * PW * 8;           // [128][kFeOS]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int HW = H * W, tpe = HW / kFeTP;
+  for (int idx = tid; idx < 128 * (kFeK / 8); idx += 512) {
+    const int r = idx / (kFeK / 8), q = idx - r * (kFeK / 8);
+    *reinterpret_cast<uint4*>(&Ws[r * kFeKS + q * 8]) = *reinterpret_cast<const uint4*>(w + r * kFeK + q * 8);
+  }
+  for (int idx = tid; idx < RB * PW; idx += 512)
+    *reinterpret_cast<uint4*>(&In[idx * 8]) = make_uint4(0, 0, 0, 0);  // padding columns stay zero
+  // input staging: thread -> band pixel (row idx / W, column idx % W), several per thread
+  const int nin = (RB * W + 511) / 512;  // <= 2 for W <= 128
+  float v[2][4];
+  auto load_in = [&](long t) {
+    const long e = t / tpe;
+    const int y0 = (int)(t - e * tpe) * (kFeTP / W);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + 512 * u;
+      const int ry = idx / W, x = idx - ry * W, y = y0 - 3 + ry;
+      const bool ok = u < nin && ry < RB && t < ntiles && y >= 0 && y < H;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[u][c] = ok ? motn[(e * 4 + c) * HW + (long)y * W + x] : 0.f;
+    }
+  };
+  auto store_in = [&]() {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + 512 * u;
+      const int ry = idx / W, x = idx - ry * W;
+      if (u < nin && ry < RB) {
+        half8 h;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) { h[c] = (_Float16)v[u][c]; h[c + 4] = (_Float16)0.f; }
+        *reinterpret_cast<half8*>(&In[(ry * PW + x + 3) * 8]) = h;
+      }
+    }
+  };
+  const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fq = lane >> 4;
+  float bj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bj[j] = bias[wn * 64 + j * 16 + fr];
+  int pyx[2];  // band slot of the lane's pixel in fragment f, at tap (-3,-3)
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int p = wm * 32 + f * 16 + fr;
+    pyx[f] = (p / W) * PW + (p % W);
+  }
+  long t = blockIdx.x;
+  load_in(t);
+  __syncthreads();
+  for (; t < ntiles; t += gridDim.x) {
+    store_in();
+    __syncthreads();
+    load_in(t + gridDim.x);
+    floatx4 acc[2][4];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[f][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < kFeK / 32; ++ks) {
+      int tap = ks * 4 + fq;
+      if (tap > 48) tap = 48;  // taps 49..51 have zero weights; read any valid slot
+      const int ty = tap / 7, tx = tap - ty * 7;
+      half8 af[2], bf[4];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) af[f] = *reinterpret_cast<const half8*>(&In[(pyx[f] + ty * PW + tx) * 8]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bf[j] = *reinterpret_cast<const half8*>(&Ws[(wn * 64 + j * 16 + fr) * kFeKS + ks * 32 + fq * 8]);
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[f], bf[j], acc[f][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          Os[(wm * 32 + f * 16 + fq * 4 + k) * kFeOS + wn * 64 + j * 16 + fr] = (_Float16)fmaxf(acc[f][j][k] + bj[j], 0.f);
+    __syncthreads();
+    const long e = t / tpe;
+    const long pix0 = e * HW + (t - e * tpe) * kFeTP;
+    for (int idx = tid; idx < kFeTP * 16; idx += 512) {
+      const int r = idx >> 4, q = idx & 15;
+      *reinterpret_cast<uint4*>(out + (pix0 + r) * 128 + q * 8) = *reinterpret_cast<const uint4*>(&Os[r * kFeOS + q * 8]);
+    }
+  }
+}
+
 }  // namespace droid
 
 using namespace droid;
@@ -1503,6 +1617,30 @@ int droid_gru_global_f16(const void* h, const void* w, const float* bias, float*
     attr = true;
   }
   gru_glo_kernel<<<E, 256, kGloLds, stream>>>((const __half*)h, (const __half*)w, bias, glo, HW);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+// flow_encoder[0] (flow_enc0_kernel): motn (E,4,H,W) f32, w [128][416] fp16
+// (column t*8 + c = weight[co][c][t/7][t%7] for t < 49, c < 4; else zero), bias
+// [128] f32 -> out (E,H,W,128) fp16 = relu(conv7x7(motn) + bias).
+int droid_flow_enc0_f16(const float* motn, const void* w, const float* bias, void* out, int E, int H, int W,
+                        hipStream_t stream) {
+  if (E < 0 || H <= 0 || W <= 0 || !motn || !w || !bias || !out)
+    return fail(kInvalidArgument, "flow_enc0_f16: bad arguments");
+  if (W % 16 || kFeTP % W || (H * W) % kFeTP || (long)E * H * W * 4 > 0x7fffffffL)
+    return fail(kUnsupported, "flow_enc0_f16: needs W in {16,32,64,128} and H*W % 128 == 0");
+  if (E == 0) return kOk;
+  const int lds = fe_lds_bytes(W);
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&flow_enc0_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    attr = true;
+  }
+  const long ntiles = (long)E * H * W / kFeTP;
+  const long grid = std::min<long>(ntiles, device_cu_count());
+  flow_enc0_kernel<<<dim3((unsigned)grid), 512, lds, stream>>>(motn, (const __half*)w, bias, (__half*)out, H, W, ntiles);
   DROID_LAUNCH_CHECK();
   return kOk;
 }

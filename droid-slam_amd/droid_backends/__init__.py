@@ -214,6 +214,30 @@ def conv_dw_head_f16(sources, wp, bias, head_w, out32):
     return out32
 
 
+def flow_enc0_supported(H, W):
+    """Shapes droid_flow_enc0_f16 accepts."""
+    return W in (16, 32, 64, 128) and (H * W) % 128 == 0
+
+
+def flow_enc0_f16(motn, w, bias, out=None):
+    """flow_encoder[0] (include/droid_backends.h: droid_flow_enc0_f16): motn (E,4,H,W)
+    f32, w [128][416] fp16 (droid_mi355x.fused.pack_flow_enc0), bias [128] f32 ->
+    (E,H,W,128) fp16 = relu(conv7x7(motn) + bias)."""
+    _check_inputs(("motn", "w", "bias"), (motn, w, bias))
+    _need(motn, torch.float32, "motn")
+    _need(w, torch.float16, "w")
+    _need(bias, torch.float32, "bias")
+    E, C, H, W = motn.shape
+    if C != 4 or tuple(w.shape) != (128, 416):
+        raise RuntimeError("flow_enc0_f16: motn must have 4 channels and w be 128x416")
+    if out is None:
+        out = torch.empty((E, H, W, 128), dtype=torch.float16, device=motn.device)
+    with torch.cuda.device(motn.device):
+        check(lib.droid_flow_enc0_f16(_ptr(motn), _ptr(w), _ptr(bias), _ptr(out), E, H, W, _stream(motn)),
+              "flow_enc0_f16")
+    return out
+
+
 def gru_global_f16(h, w, bias, out=None):
     """ConvGRU global context (include/droid_backends.h: droid_gru_global_f16):
     h (E,H,W,128) fp16, w [128][128] fp16, bias [128] f32 -> (E,128) f32."""

@@ -63,6 +63,14 @@ def pack_conv(weight, splits):
     return wp.permute(0, 1, 3, 2).reshape(cout, -1, BK).to(torch.float16).contiguous()
 
 
+def pack_flow_enc0(weight):
+    """(128, 4, 7, 7) flow_encoder[0] weight -> [128][416] fp16 for
+    droid_flow_enc0_f16: column t*8 + c = weight[co, c, t // 7, t % 7]."""
+    w = torch.zeros(128, 52, 8, device=weight.device)
+    w[:, :49, :4] = weight.detach().float().reshape(128, 4, 49).permute(0, 2, 1)
+    return w.reshape(128, 416).to(torch.float16).contiguous()
+
+
 def pack_head_taps(head):
     """(4, 256, 3, 3) head weight -> [48][256] fp16 for droid_conv_dw_head_f16:
     row tap*4 + c (tap = ky*3 + kx) holds head[c, :, ky, kx]; rows 36..47 zero."""
@@ -131,6 +139,7 @@ class FusedUpdateModule(torch.nn.Module):
         fe0[:, :4] = m.flow_encoder[0].weight
         P["fe0"] = pack_conv(fe0, [8])
         P["fe0_b"] = m.flow_encoder[0].bias.float().contiguous()
+        P["fe0_416"] = pack_flow_enc0(m.flow_encoder[0].weight)
         P["fe2"] = pack_conv(m.flow_encoder[2].weight, [128])
         P["fe2_b"] = m.flow_encoder[2].bias.float().contiguous()
         P["w"] = pack_conv(g.w.weight, [128])
@@ -187,10 +196,13 @@ class FusedUpdateModule(torch.nn.Module):
             conv([(corr, 0, 200)], P["ce0"], 128, 1, bias=P["ce0_b"], act=1, out=c1)
         cf = e16(128)
         conv([(c1, 0, 128)], P["ce2"], 128, 3, bias=P["ce2_b"], act=1, out=cf)
-        m8 = torch.zeros((E, H, W, 8), dtype=torch.float16, device=dev)
-        m8[..., :4] = motn.permute(0, 2, 3, 1)
-        f1 = e16(128)
-        conv([(m8, 0, 8)], P["fe0"], 128, 7, bias=P["fe0_b"], act=1, out=f1)
+        if droid_backends.flow_enc0_supported(H, W):
+            f1 = droid_backends.flow_enc0_f16(motn.contiguous(), P["fe0_416"], P["fe0_b"])
+        else:
+            m8 = torch.zeros((E, H, W, 8), dtype=torch.float16, device=dev)
+            m8[..., :4] = motn.permute(0, 2, 3, 1)
+            f1 = e16(128)
+            conv([(m8, 0, 8)], P["fe0"], 128, 7, bias=P["fe0_b"], act=1, out=f1)
         ff = e16(64)
         conv([(f1, 0, 128)], P["fe2"], 64, 3, bias=P["fe2_b"], act=1, out=ff)
 

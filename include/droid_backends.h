@@ -103,6 +103,14 @@ int droid_conv_dw_head_f16(const void* const* srcs, const int* C, const int* cst
                            const float* bias, int B, int H, int W, const void* hw, void* out32,
                            hipStream_t stream);
 
+/* flow_encoder[0] (droid_net.py:88-90): out (E,H,W,128) fp16 = relu(conv7x7(motn)
+ * + bias) from the motion features motn (E,4,H,W) f32 (cast to fp16 as under
+ * autocast); w [128][416] fp16 with column t*8 + c = weight[co][c][t/7][t%7]
+ * for taps t < 49 and channels c < 4, zero elsewhere.  Needs W in
+ * {16,32,64,128} and H*W % 128 == 0. */
+int droid_flow_enc0_f16(const float* motn, const void* w, const float* bias, void* out, int E, int H, int W,
+                        hipStream_t stream);
+
 /* ConvGRU global context (modules/gru.py:19-32): glo[e][co] = mean over the
  * H*W pixels of edge e of sigmoid(w . h + bias)[co] * h[co], for h (E,H,W,128)
  * fp16 and the 1x1 conv w [128][128] fp16 ([co][ci]), bias [128] f32 -> glo

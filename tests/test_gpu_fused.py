@@ -270,3 +270,17 @@ def test_gru_global_context(E, H, W):
     ref = (torch.sigmoid(hf @ w.float().t() + b) * hf).mean(1)
     np.testing.assert_allclose(host(out), host(ref), atol=1e-4, rtol=1e-3)
     assert torch.equal(out, droid_backends.gru_global_f16(h, w, b))
+
+
+@pytest.mark.parametrize("E,H,W", [(3, 8, 32), (2, 48, 64), (2, 4, 128)])
+def test_flow_encoder0(E, H, W):
+    """relu(conv7x7(motn.half()) + b) (droid_net.py:88-90 under autocast) vs torch fp32."""
+    import droid_backends
+    from droid_mi355x.fused import pack_flow_enc0
+    g = torch.Generator(device=DEV).manual_seed(24)
+    motn = (8 * torch.randn((E, 4, H, W), generator=g, device=DEV)).clamp(-64, 64)
+    w = torch.randn((128, 4, 7, 7), generator=g, device=DEV) / 14.0
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    out = droid_backends.flow_enc0_f16(motn, pack_flow_enc0(w), b)
+    ref = F.relu(F.conv2d(motn.half().float(), w.half().float(), b, padding=3)).permute(0, 2, 3, 1)
+    np.testing.assert_allclose(host(out.float()), host(ref), atol=2e-3 * max(1.0, float(ref.abs().max())), rtol=2e-3)
