@@ -907,10 +907,10 @@ __device__ __forceinline__ int frag_row(int wm, int i) {
   return CONTIG ? wm * FM * 16 + 16 * i : 16 * (wm + WM * i);
 }
 
-template <int TMX, int TN, int FM, int FN, int WM = 4, bool CONTIG = false>
+template <int TMX, int TN, int FM, int FN, int WM = 4, bool CONTIG = false, int NT = 512>
 __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
                                               int n0, int wm, int wn, int lane, int tid) {
-  constexpr int ER = TN + 8, NT = 512, PPR = TN / 8;
+  constexpr int ER = TN + 8, PPR = TN / 8;
   const int HW = a.H * a.W;
   const int b = (int)(m0 / HW);  // a tile never straddles two images
   const int fr = lane & 15, fq = lane >> 4;
