@@ -36,7 +36,7 @@ LOOKUP_BYTES_PER_EDGE = 2801664  # volume-API lookup, 4 lvl x 64
 LOOKUP_CE0_BYTES_PER_EDGE = 4 * 64 * 2 * 3072 + 2 * 4 * 3072 + 128 * 2 * 3072
 # ConvGRU z|r conv (modules/gru.py:19-32, convz+convr fused): 3x3, 448 -> 256 channels
 ZR_FLOPS_PER_PIXEL = 2 * 256 * 448 * 9
-ZR_KERNEL = "conv_band_kernel<256, 256>"   # csrc/conv_kernels.hip, chosen for 48x64 maps
+ZR_KERNEL = "conv_band_kernel<256, 256"   # csrc/conv_kernels.hip, chosen for 48x64 maps
 LOOKUP_KERNEL = "corr_pyramid_f16_r3_kernel"
 
 
@@ -215,11 +215,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
-    device = torch.device("cuda", local_rank)
+    # DROID_BENCH_ONE_DEVICE=1 / DROID_BENCH_BACKEND=gloo: rehearse the N-rank path
+    # with every rank on cuda:0 (a one-GPU box); the driver's runs use RCCL, one GPU per rank
+    one_dev = os.environ.get("DROID_BENCH_ONE_DEVICE") == "1"
+    device = torch.device("cuda", 0 if one_dev else local_rank)
     torch.cuda.set_device(device)
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        backend = os.environ.get("DROID_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     t_setup = time.time()
     video, graph, (ii, jj), e_local = build_state(args, rank, world, device)

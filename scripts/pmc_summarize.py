@@ -28,8 +28,8 @@ def per_kernel(counter):
             continue
         name = r["Kernel_Name"]
         key = ("copy" if name.startswith("__amd_rocclr_copyBuffer") and len(out.get("copy", [])) < 3 else
-               "zr" if ("conv_band_kernel<256, 256>" in name or "conv_rows_kernel" in name) else
-               "lookup" if "corr_pyramid_f16_r3_kernel" in name else None)
+               "zr" if ("conv_band_kernel<256, 256," in name or "conv_rows_kernel" in name) else
+               "lookup" if ("corr_ce0_kernel" in name or "corr_pyramid_f16_r3_kernel" in name) else None)
         if key:
             out.setdefault(key, []).append(float(r["Counter_Value"]))
             KNAME[key] = name
@@ -43,7 +43,9 @@ kf = GiB / fetch["copy"][-1]
 kw = GiB / write["copy"][-1]
 res = {"calibration": {"fetch_bytes_per_unit": kf, "write_bytes_per_unit": kw,
                        "raw_fetch": fetch["copy"], "raw_write": write["copy"]}}
-for key, name, algo in (("zr", "conv_zr", None), ("lookup", "corr_lookup", 2801664 * E)):
+# fused lookup + corr_encoder[0]: window reads + coords + 128-channel fp16 output per edge
+LOOKUP_CE0 = 4 * 64 * 2 * 3072 + 2 * 4 * 3072 + 128 * 2 * 3072
+for key, name, algo in (("zr", "conv_zr", 2 * 256 * 448 * 9 * 3072 * E), ("lookup", "corr_lookup", LOOKUP_CE0 * E)):
     fb = kf * min(fetch[key])
     wb = kw * min(write[key])
     d = {"edges": E, "kernel": KNAME.get(key), "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
@@ -52,7 +54,7 @@ for key, name, algo in (("zr", "conv_zr", None), ("lookup", "corr_lookup", 28016
          "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; units calibrated on a "
                    "1 GiB device copy in the same process (min over 3 launches)"}
     if algo:
-        d["algorithmic_bytes_per_launch"] = algo
+        d["algorithmic_flops_per_launch" if key == "zr" else "algorithmic_bytes_per_launch"] = algo
     with open(os.path.join(dst, "pmc_%s.json" % name), "w") as f:
         json.dump(d, f, indent=1)
     print(name, "fetch %.3g B, write %.3g B" % (fb, wb))
