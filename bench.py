@@ -36,7 +36,8 @@ LOOKUP_BYTES_PER_EDGE = 2801664  # volume-API lookup, 4 lvl x 64
 LOOKUP_CE0_BYTES_PER_EDGE = 4 * 64 * 2 * 3072 + 2 * 4 * 3072 + 128 * 2 * 3072
 # ConvGRU z|r conv (modules/gru.py:19-32, convz+convr fused): 3x3, 448 -> 256 channels
 ZR_FLOPS_PER_PIXEL = 2 * 256 * 448 * 9
-ZR_KERNEL = "conv_band_kernel<256, 256"   # csrc/conv_kernels.hip, chosen for 48x64 maps
+ZR_KERNEL = "conv_band_kernel<256,256>"   # csrc/conv_kernels.hip, chosen for 48x64 maps
+ZR_KERNEL_MATCH = "conv_band_kernel<256, 256"   # its symbol in rocprof / PMC summaries
 LOOKUP_KERNEL = "corr_pyramid_f16_r3_kernel"
 
 
@@ -290,7 +291,7 @@ def main():
             tf = flops / (zr_ms * 1e-3) / 1e12
             roofline = {"kernel": "%s (ConvGRU z|r gates, 3x3 448->256, fp16 MFMA)" % ZR_KERNEL,
                         "bound": "mfma", "achieved": tf, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-                        "frac": tf / PEAK_F16_TFLOPS, "traffic": load_traffic("conv_zr", e_local, ZR_KERNEL),
+                        "frac": tf / PEAK_F16_TFLOPS, "traffic": load_traffic("conv_zr", e_local, ZR_KERNEL_MATCH),
                         "launch_ms": zr_ms, "algorithmic_flops_per_launch": flops}
         else:
             roofline, lookup_roof = lookup_roof, None
