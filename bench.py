@@ -78,7 +78,7 @@ def build_state(args, rank, world, device):
     if not args.reference_op:
         from droid_mi355x.fused import FusedUpdateModule
         net = FusedUpdateModule(net)
-    graph = FactorGraph(video, net, device=device)
+    graph = FactorGraph(video, net, device=device, corr_impl=args.corr if not args.reference_op else "volume")
     graph.comm = comm
     with torch.no_grad():
         graph.add_factors(ii_l, jj_l)
@@ -204,6 +204,9 @@ def main():
     ap.add_argument("--edges", type=int, default=2048)
     ap.add_argument("--ht", type=int, default=384)
     ap.add_argument("--wd", type=int, default=512)
+    ap.add_argument("--corr", choices=["pyramid", "volume"], default="volume",
+                    help="correlation: 'volume' = CorrBlock's all-pairs volume (built in add_factors), "
+                         "'pyramid' = windows computed on demand on MFMA from the feature pyramid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-edges", type=int, default=8)
     ap.add_argument("--breakdown", action="store_true")
@@ -235,7 +238,8 @@ def main():
         log("setup %.1fs (local edges %d)" % (time.time() - t_setup, e_local))
 
     import droid_backends
-    LOOKUP_FN[0] = "corr_pyramid_lookup" if args.reference_op else "corr_lookup_ce0"
+    LOOKUP_FN[0] = ("corr_pyramid_lookup" if args.reference_op else
+                    "corr_alt_ce0" if args.corr == "pyramid" else "corr_lookup_ce0")
     lookup = KernelTimer(droid_backends, LOOKUP_FN[0])
     zr = None
     if not args.reference_op:

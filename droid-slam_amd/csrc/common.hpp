@@ -44,6 +44,16 @@ constexpr float kMinDepth = 0.25f;  // droid_kernels.cu:26
 
 __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
+// fp32 value -> nearest fp16 -> fp32, with the fp32 operand materialised first.
+// Without the empty asm, hipcc folds round(a*b) / round(a+b) into one
+// v_fma_mixlo_f16 that rounds the EXACT result once - not the reference's
+// fp32-then-half double rounding (at::Half arithmetic), so 1-ulp differences
+// appear on rare ties.  Used by the bit-exact correlation lookups.
+__device__ __forceinline__ float rnd16(float x) {
+  asm volatile("" : "+v"(x));
+  return __half2float(__float2half(x));
+}
+
 // compute units of the current device (grid size of persistent kernels)
 inline int device_cu_count() {
   static int n = 0;

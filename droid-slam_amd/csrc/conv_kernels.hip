@@ -34,12 +34,11 @@
 //   EPI_GLO   : sigmoid(.) * h summed over the tile's pixels, atomically added
 //               (scaled by 1/HW) into glo[b][co]: the GRU global-context mean
 #include "common.hpp"
+#include "lds_dma.hpp"
 #include <algorithm>
 
 namespace droid {
 
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 enum ConvEpi : int { EPI_ACT = 0, EPI_GRU_ZR = 1, EPI_GRU_Q = 2, EPI_HEAD = 3, EPI_GLO = 4, EPI_DWHEAD = 5 };
 
@@ -594,8 +593,6 @@ __global__ void __launch_bounds__(NW * 64) conv_halo_kernel(ConvArgs a) {
 // loads with per-thread offsets fixed for the whole kernel (zero VALU address
 // math in the loop); padding / out-of-image pixels use an out-of-range offset,
 // which the buffer unit returns as zeros.
-constexpr unsigned kOob = 0x80000000u;
-constexpr int kBufFlags = 0x00020000;
 
 __device__ __forceinline__ uint4 buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 0));
@@ -860,38 +857,6 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
   }
 }
 
-// LDS-DMA of 16 B per lane (buffer_load_dwordx4 ... lds): lane l's bytes land at
-// LDS byte address `lds` + 16 l.  Issued as inline asm so that hipcc does not
-// treat every later ds_read as dependent on the DMA (it inserts vmcnt(0) before
-// them otherwise); the kernel orders the DMA with explicit counted vmcnt waits +
-// s_barrier.  `rs` is a raw buffer descriptor in SGPRs; out-of-range offsets
-// (kOob) land as zeros.
-typedef int rsrc_t __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) char* lds_cptr_t;
-
-__device__ __forceinline__ rsrc_t make_rsrc(const void* base, unsigned bytes) {
-  // wave-uniform by construction; readfirstlane keeps the descriptor in SGPRs
-  const unsigned long long pa = (unsigned long long)base;
-  return rsrc_t{__builtin_amdgcn_readfirstlane((int)(unsigned)pa),
-                __builtin_amdgcn_readfirstlane((int)((unsigned)(pa >> 32) & 0xffffu)),
-                __builtin_amdgcn_readfirstlane((int)bytes), kBufFlags};
-}
-
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-  return (unsigned)(uintptr_t)(lds_cptr_t)(p);
-}
-
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void dma16(rsrc_t rs, unsigned lds, unsigned voff) {
-  const rsrc_t r = {__builtin_amdgcn_readfirstlane(rs.x), __builtin_amdgcn_readfirstlane(rs.y),
-                    __builtin_amdgcn_readfirstlane(rs.z), __builtin_amdgcn_readfirstlane(rs.w)};
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-               :
-               : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(r)
-               : "memory", "m0");
-}
-#pragma clang diagnostic pop
 
 // Band epilogue in two passes through one fp16 LDS tile [TMX][TN + 8]:
 // (1) each wave writes act(acc + bias + bbias) of its fragments (act = relu /

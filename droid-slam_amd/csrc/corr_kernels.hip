@@ -21,15 +21,6 @@
 
 namespace droid {
 
-// fp32 value -> nearest fp16 -> fp32, with the fp32 operand materialised first.
-// Without the empty asm, hipcc folds round(a*b) / round(a+b) into one
-// v_fma_mixlo_f16 that rounds the EXACT result once - not the reference's
-// fp32-then-half double rounding, so 1-ulp differences appear on rare ties.
-__device__ __forceinline__ float rnd16(float x) {
-  asm volatile("" : "+v"(x));
-  return __half2float(__float2half(x));
-}
-
 template <typename T> struct Acc;
 template <> struct Acc<__half> {
   // weight -> half, product -> half, sum -> half (at::Half operator semantics)

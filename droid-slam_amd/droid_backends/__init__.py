@@ -158,6 +158,32 @@ def corr_lookup_ce0(levels, coords, w, bias, out=None):
     return out
 
 
+def corr_alt_ce0(pyramid, f1, f2, coords, w, bias, out=None):
+    """On-the-fly correlation lookup + corr_encoder[0] (include/droid_backends.h:
+    droid_corr_alt_ce0): pyramid 4 x (NF,H_l,W_l,128) fp16 (AltCorrBlock layout),
+    f1/f2 (E) int32 pyramid rows, coords (E,H,W,2) f32, w [128][224] fp16,
+    bias [128] f32 -> (E,H,W,128) fp16."""
+    _check_inputs(["level%d" % i for i in range(len(pyramid))] + ["f1", "f2", "coords", "w", "bias"],
+                  list(pyramid) + [f1, f2, coords, w, bias])
+    _need(coords, torch.float32, "coords")
+    _need(f1, torch.int32, "f1")
+    _need(f2, torch.int32, "f2")
+    _need(w, torch.float16, "w")
+    _need(bias, torch.float32, "bias")
+    if len(pyramid) != 4:
+        raise RuntimeError("corr_alt_ce0: needs 4 pyramid levels")
+    E, H, W, _ = coords.shape
+    if out is None:
+        out = torch.empty((E, H, W, 128), dtype=torch.float16, device=coords.device)
+    ptrs = (ctypes.c_void_p * 4)(*[lv.data_ptr() for lv in pyramid])
+    hs = (ctypes.c_int * 4)(*[lv.shape[-3] for lv in pyramid])
+    ws = (ctypes.c_int * 4)(*[lv.shape[-2] for lv in pyramid])
+    with torch.cuda.device(coords.device):
+        check(lib.droid_corr_alt_ce0(ptrs, hs, ws, _ptr(f1), _ptr(f2), _ptr(coords), _ptr(w), _ptr(bias), _ptr(out),
+                                     E, H, W, _stream(coords)), "corr_alt_ce0")
+    return out
+
+
 EPI_ACT, EPI_GRU_ZR, EPI_GRU_Q, EPI_HEAD, EPI_GLO = 0, 1, 2, 3, 4
 
 

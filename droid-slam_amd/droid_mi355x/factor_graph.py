@@ -15,7 +15,7 @@ import torch
 import droid_backends
 
 from .corr import AltCorrBlock, CorrBlock
-from .fused import PendingLookup, edge_segments
+from .fused import PendingAltLookup, PendingLookup, edge_segments
 
 
 def _coords_grid(ht, wd, device):
@@ -48,6 +48,9 @@ class FactorGraph:
         self.target_inac = torch.zeros([1, 0, ht, wd, 2], device=self.device, dtype=torch.float)
         self.weight_inac = torch.zeros([1, 0, ht, wd, 2], device=self.device, dtype=torch.float)
         self._dev_cache = {}
+        # corr_impl "pyramid" (MI355X): no per-edge volume; update() computes the
+        # correlation windows on demand from this feature pyramid of the frames
+        self._alt_pyr = None
         self.comm = None  # set for edge-sharded multi-GPU: dict(group, own=(lo,hi), t0, t1)
         # fused (MI355X) operator: per-edge hidden state kept channels-last (E,H,W,128)
         from .fused import FusedUpdateModule
@@ -69,7 +72,7 @@ class FactorGraph:
         key = (name, arr.tobytes())
         t = self._dev_cache.get(name)
         if t is None or t[0] != key:
-            t = (key, torch.as_tensor(arr, dtype=torch.long).to(self.device, non_blocking=True))
+            t = (key, torch.from_numpy(np.ascontiguousarray(arr)).to(self.device, non_blocking=True))
             self._dev_cache[name] = t
         return t[1]
 
@@ -140,6 +143,9 @@ class FactorGraph:
             fmap2 = self.video.fmaps[djj, c].to(self.device).unsqueeze(0)
             corr = CorrBlock(fmap1, fmap2)
             self.corr = corr if self.corr is None else self.corr.cat(corr)
+        if self.corr_impl == "pyramid":
+            self._alt_pyr = None   # frames may have changed: rebuilt at the next update
+        if self.corr_impl in ("volume", "pyramid"):
             inp = self._edge_state(self.video.inps[dii].to(self.device))
             self.inp = inp if self.inp is None else torch.cat([self.inp, inp], self._edim)
 
@@ -175,6 +181,7 @@ class FactorGraph:
         self.weight = self.weight[:, dkeep]
 
     def rm_keyframe(self, ix):
+        self._alt_pyr = None   # frames shift
         v = self.video
         with v.get_lock():
             for buf in (v.images, v.poses, v.disps, v.disps_sens, v.intrinsics, v.nets, v.inps, v.fmaps):
@@ -208,7 +215,10 @@ class FactorGraph:
         uniq, inverse = np.unique(self._ii, return_inverse=True)
         dinv = self._dev("inverse", inverse.astype(np.int64))
         if self.fused:
-            corr = PendingLookup(self.corr, coords1)   # lookup runs fused with corr_encoder[0]
+            if self.corr_impl == "pyramid":
+                corr = self._pending_alt_lookup(coords1)   # windows computed on demand (no volume)
+            else:
+                corr = PendingLookup(self.corr, coords1)   # lookup runs fused with corr_encoder[0]
             ptr, idx = edge_segments(inverse, len(uniq))
             segs = (self._dev("seg_ptr", ptr), self._dev("seg_idx", idx))
             self.net, delta, weight, damping = self.update_op(self.net, self.inp, corr, motn[0], dinv, len(uniq),
@@ -245,6 +255,21 @@ class FactorGraph:
                           t0, t1, itrs=itrs, lm=1e-4, ep=0.1, motion_only=motion_only,
                           ii_host=ii_h, jj_host=jj_h, comm=self.comm)
         self.age += 1
+
+    def _pending_alt_lookup(self, coords1):
+        """corr_impl "pyramid": AltCorrBlock pyramid of the frames (built once per
+        edge-set change) + per-edge pyramid rows: f1 = fmaps[ii, 0], f2 =
+        fmaps[jj, ii == jj] (the stereo edge reads the right image,
+        factor_graph.py:112-114)."""
+        num, rig = self.video.fmaps.shape[:2]
+        n = max(int(self.video.counter.value), int(max(self._ii.max(), self._jj.max())) + 1)
+        if self._alt_pyr is None or self._alt_pyr[0] != n:
+            f = self.video.fmaps[:n]
+            blk = AltCorrBlock(f.reshape((1, n * rig) + tuple(f.shape[2:])))
+            self._alt_pyr = (n, [lv.view((-1,) + tuple(lv.shape[2:])) for lv in blk.pyramid])
+        f1 = self._dev("alt_f1", (rig * self._ii).astype(np.int32))
+        f2 = self._dev("alt_f2", (rig * self._jj + ((self._ii == self._jj) & (rig > 1))).astype(np.int32))
+        return PendingAltLookup(self._alt_pyr[1], f1, f2, coords1)
 
     def update_lowmem(self, t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, steps=8):
         """factor_graph.py:245-290: alternate (on-the-fly) correlation, chunks of 8 sources."""

@@ -92,6 +92,19 @@ class PendingLookup:
         return self.block.lookup_nhwc(self.coords)
 
 
+class PendingAltLookup:
+    """A lookup of an AltCorrBlock feature pyramid (corr.py:91-139) for edges
+    (f1 rows, f2 rows) at `coords` (1,E,H,W,2): FusedUpdateModule computes the
+    correlation windows on demand on MFMA, fused with corr_encoder[0]
+    (droid_backends.corr_alt_ce0); no volume exists."""
+
+    def __init__(self, pyramid, f1, f2, coords):
+        self.pyramid = pyramid
+        self.f1 = f1
+        self.f2 = f2
+        self.coords = coords
+
+
 def edge_segments(inverse, num_unique):
     """CSR (seg_ptr (U+1), seg_idx (E)) int64 of the edges per source-frame slot.
     `inverse` may be a numpy array (built on the host) or a device tensor."""
@@ -186,7 +199,10 @@ class FusedUpdateModule(torch.nn.Module):
         e16 = lambda c: torch.empty((E, H, W, c), dtype=torch.float16, device=dev)
 
         levels = corr.block.corr_pyramid if isinstance(corr, PendingLookup) else None
-        if levels is not None and droid_backends.corr_lookup_ce0_supported(levels, H, W):
+        if isinstance(corr, PendingAltLookup):
+            coords = corr.coords.reshape(E, H, W, 2).float().contiguous()
+            c1 = droid_backends.corr_alt_ce0(corr.pyramid, corr.f1, corr.f2, coords, P["ce0_224"], P["ce0_b"])
+        elif levels is not None and droid_backends.corr_lookup_ce0_supported(levels, H, W):
             coords = corr.coords.reshape(E, H, W, 2).float().contiguous()
             c1 = droid_backends.corr_lookup_ce0(levels, coords, P["ce0_224"], P["ce0_b"])
         else:

@@ -74,6 +74,18 @@ int droid_corr_pyramid_lookup_nhwc(const void* const* levels, const int* H2s, co
 int droid_corr_lookup_ce0(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
                           const void* w, const float* bias, void* out, int E, int H, int W, hipStream_t stream);
 
+/* The same lookup + corr_encoder[0] computed WITHOUT the volume: the 4
+ * correlation levels are formed on demand on MFMA from a feature pyramid
+ * pyr[l] (NF,H_l,W_l,128) fp16 = avgpool^l(fmap/4) (the reference's
+ * AltCorrBlock pyramid, corr.py:91-104): per 8x8 query tile the union of the
+ * windows is multiplied against the query features, rounded to fp16 and read
+ * with the volume lookup's bilinear arithmetic.  f1/f2 (E) int32: pyramid row
+ * of each edge's query / target features; coords (E,H,W,2) f32; w, bias as
+ * droid_corr_lookup_ce0.  Needs H % 8 == 0 and W % 8 == 0. */
+int droid_corr_alt_ce0(const void* const* pyr, const int* Hl, const int* Wl, const int* f1, const int* f2,
+                       const float* coords, const void* w, const float* bias, void* out, int E, int H, int W,
+                       hipStream_t stream);
+
 /* ---- update operator ----------------------------------------------------
  * Implicit-GEMM convolution on MFMA (UpdateModule / ConvGRU convs,
  * droid_net.py:78-143, modules/gru.py:19-32), NHWC fp16 in, fp32 accumulate.

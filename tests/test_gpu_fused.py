@@ -284,3 +284,86 @@ def test_flow_encoder0(E, H, W):
     out = droid_backends.flow_enc0_f16(motn, pack_flow_enc0(w), b)
     ref = F.relu(F.conv2d(motn.half().float(), w.half().float(), b, padding=3)).permute(0, 2, 3, 1)
     np.testing.assert_allclose(host(out.float()), host(ref), atol=2e-3 * max(1.0, float(ref.abs().max())), rtol=2e-3)
+
+
+@pytest.mark.parametrize("noise", [1.5, 40.0])   # coherent windows / incoherent (quadrant and pixel fallbacks)
+def test_corr_alt_ce0_matches_volume_path(noise):
+    """On-demand correlation (feature pyramid, MFMA) + corr_encoder[0] == the
+    volume lookup + corr_encoder[0] up to fp16 rounding of the pooled levels
+    (modules/corr.py: CorrBlock vs AltCorrBlock semantics)."""
+    import droid_backends
+    from droid_mi355x.corr import AltCorrBlock, CorrBlock
+    rng = np.random.default_rng(31)
+    NF, H, W = 4, 16, 24
+    fm = torch.from_numpy(rng.normal(size=(NF, 128, H, W)).astype(np.float16)).to(DEV)
+    ii = np.array([0, 1, 2, 3, 1, 2], np.int64)
+    jj = np.array([1, 0, 3, 1, 1, 0], np.int64)
+    E = len(ii)
+    cb = CorrBlock(fm[ii][None], fm[jj][None])
+    pyr = [lv.view((-1,) + tuple(lv.shape[2:])) for lv in AltCorrBlock(fm[None]).pyramid]
+    grid = np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None].astype(np.float32)
+    coords = grid + rng.normal(0, noise, (E, H, W, 2)).astype(np.float32) + 2.0
+    c = torch.from_numpy(coords).to(DEV).contiguous()
+    g = torch.Generator(device=DEV).manual_seed(32)
+    w224 = torch.zeros((128, 224), device=DEV)
+    w224[:, :196] = torch.randn((128, 196), generator=g, device=DEV) / 14.0
+    w224 = w224.half().contiguous()
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    with torch.no_grad():
+        ref = droid_backends.corr_lookup_ce0(cb.corr_pyramid, c, w224, b).float()
+        out = droid_backends.corr_alt_ce0(pyr, torch.as_tensor(ii, dtype=torch.int32, device=DEV),
+                                          torch.as_tensor(jj, dtype=torch.int32, device=DEV), c, w224, b).float()
+    scale = float(ref.abs().max())
+    err = (out - ref).abs()
+    assert float(err.max()) < 2e-2 * scale, float(err.max()) / scale
+    assert float(err.mean()) < 1e-3 * scale, float(err.mean()) / scale
+    out2 = droid_backends.corr_alt_ce0(pyr, torch.as_tensor(ii, dtype=torch.int32, device=DEV),
+                                       torch.as_tensor(jj, dtype=torch.int32, device=DEV), c, w224, b).float()
+    assert torch.equal(out, out2)
+
+
+def test_factor_graph_update_pyramid_corr():
+    """FactorGraph(corr_impl="pyramid"): no volume; update() finite and its BA
+    matches the oracle on the inputs it hands over."""
+    import droid_backends
+    from droid_mi355x import DepthVideo, FactorGraph, UpdateModule, synthetic
+    from droid_mi355x.fused import FusedUpdateModule
+    from oracle import ba as oba
+    rng = np.random.default_rng(34)
+    n, H, W = 8, 16, 24
+    video = DepthVideo(image_size=(8 * H, 8 * W), buffer=n, device=DEV)
+    poses = synthetic.trajectory(n, rng)
+    poses, disps = synthetic.perturb(poses, synthetic.smooth_disps(n, H, W, rng), rng)
+    video.poses[:n] = torch.from_numpy(poses.astype(np.float32)).to(DEV)
+    video.disps[:n] = torch.from_numpy(disps.astype(np.float32)).to(DEV)
+    video.intrinsics[:n] = torch.tensor([[H / 1.5, H / 1.5, W / 2, H / 2]] * n, device=DEV)
+    video.fmaps[:n] = torch.from_numpy(rng.normal(size=(n, 1, 128, H, W)).astype(np.float16)).to(DEV)
+    video.nets[:n] = torch.from_numpy(np.tanh(rng.normal(size=(n, 128, H, W))).astype(np.float16)).to(DEV)
+    video.inps[:n] = torch.from_numpy(np.maximum(rng.normal(size=(n, 128, H, W)), 0).astype(np.float16)).to(DEV)
+    video.counter.value = n
+    m = UpdateModule().to(DEV).eval()
+    det_fill(m)
+    g = FactorGraph(video, FusedUpdateModule(m), device=DEV, corr_impl="pyramid")
+    g.add_neighborhood_factors(0, n, r=2)
+    assert g.corr is None
+    captured = {}
+    orig = droid_backends.ba
+
+    def spy(*a, **k):
+        captured["a"] = [x.detach().clone() if isinstance(x, torch.Tensor) else x for x in a]
+        return orig(*a, **k)
+
+    droid_backends.ba = spy
+    try:
+        with torch.no_grad():
+            g.update()
+            g.update()
+    finally:
+        droid_backends.ba = orig
+    a = captured["a"]
+    ref = oba.ba(poses=host(a[0]), disps=host(a[1]), intrinsics=host(a[2]), disps_sens=host(a[3]),
+                 targets=host(a[4]), weights=host(a[5]), eta=host(a[6]), ii=host(a[7]), jj=host(a[8]), t0=a[9],
+                 t1=a[10], iterations=a[11], lm=a[12], ep=a[13], motion_only=a[14])
+    np.testing.assert_allclose(host(video.poses[:n]), ref["poses"][:n], atol=1e-4)
+    np.testing.assert_allclose(host(video.disps[:n]), np.maximum(ref["disps"][:n], 1e-3), atol=1e-4)
+    assert torch.isfinite(g.net.float()).all()
