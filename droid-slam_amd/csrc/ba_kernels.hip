@@ -600,6 +600,7 @@ struct CholDev {
   float* dx;    // [n]
   int debug;    // unused (tracing is compile-time: DROID_CHOL_TRACE)
   int* marks;   // debug progress marks or null
+  long long* tprof;  // debug per-ticket timeline {wg|type<<12|i<<16|j<<32|k<<48, got, deps ok, published} (s_memrealtime) or null
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mkrs(const void* p, size_t bytes) {
@@ -629,6 +630,23 @@ __device__ __forceinline__ void tile_load(__amdgpu_buffer_rsrc_t r, int ld, int 
     const unsigned off = (rr < nr && cc < nc) ? (unsigned)(((size_t)(R0 + rr) * ld + C0 + cc) * 8) : kOobOff;
     v[q] = ld2(r, off);
   }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
+    *reinterpret_cast<dbl2*>(&T[rr * LT + cc]) = v[q];
+  }
+}
+// the same load split in two, so the global latency overlaps other work
+__device__ __forceinline__ void tile_issue(__amdgpu_buffer_rsrc_t r, int ld, int R0, int C0, int nr, int nc,
+                                           dbl2 (&v)[8]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
+    const unsigned off = (rr < nr && cc < nc) ? (unsigned)(((size_t)(R0 + rr) * ld + C0 + cc) * 8) : kOobOff;
+    v[q] = ld2(r, off);
+  }
+}
+__device__ __forceinline__ void tile_commit(const dbl2 (&v)[8], double* T) {
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
@@ -686,12 +704,13 @@ __device__ __forceinline__ void acc_store(double* T, const dbl4 (&acc)[2][2], in
 }
 
 // every storing wave drains, then one lane publishes (Guideline 16 R1)
-__device__ __forceinline__ void publish(int* w, int v, int* w2 = nullptr, int v2 = 0) {
+__device__ __forceinline__ void publish(int* w, int v, int* w2 = nullptr, int v2 = 0, int* w3 = nullptr, int v3 = 0) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (w2) __hip_atomic_store(w2, v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w3) __hip_atomic_store(w3, v3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -709,34 +728,54 @@ __device__ bool poll_ge(int* w, int target, int* abort_w, int* flag) {
   }
 }
 
+// wave-uniform lane -> every lane (two v_readlane_b32, no LDS round trip)
+__device__ __forceinline__ double bcast_lane(double v, int src) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, src);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), src);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// 1/sqrt(x) in fp64: v_rsq_f64 + two Newton steps (no division, no sqrt
+// expansion on the critical path; ~1 ulp, far inside the 1e-4 parity bar)
+__device__ __forceinline__ double rsqrt_f64(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  y = y * fma(-hx * y, y, 1.5);
+  y = y * fma(-hx * y, y, 1.5);
+  return y;
+}
+
 // 16-wide panel of the diagonal factor: wave 0, lane r owns row r's panel
-// values in registers; the scaled pivot column is broadcast through LDS.
-__device__ __forceinline__ void panel_factor(double* T, double* col, int c0, int pw, int lane, int* flag) {
-  double v[16];
+// values in registers; pivots and scaled column entries are broadcast with
+// v_readlane (wave-synchronous: no LDS, no waits, no branches).  Lanes above
+// the diagonal update their (never read) upper-triangle entries too, and
+// pivot columns past the block's Bp real columns use a unit pivot, so every
+// panel is a full, branch-free 16 columns.
+// dinv[c] = 1 / L[c][c].
+__device__ __forceinline__ void panel_factor(double* T, double* dinv, int c0, int Bp, int lane, int* flag) {
+  double v[16], invs[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) v[q] = T[lane * LT + c0 + q];
+  bool bad = false;
 #pragma unroll
   for (int jj = 0; jj < 16; ++jj) {
-    if (jj < pw) {
-      const int jr = c0 + jj;
-      if (lane == jr) col[64] = v[jj];          // pivot broadcast through LDS
-      asm volatile("" ::: "memory");
-      const double piv = col[64];
-      if (lane == 0 && !(piv > 0.0 && piv < 1e300)) atomicOr(flag, 1);
-      const double sd = sqrt(piv), inv = 1.0 / sd;
-      v[jj] = (lane == jr) ? sd : ((lane > jr) ? v[jj] * inv : v[jj]);
-      col[lane] = v[jj];
-      asm volatile("" ::: "memory");
+    const bool real = c0 + jj < Bp;  // wave-uniform
+    const double piv = real ? bcast_lane(v[jj], c0 + jj) : 1.0;
+    bad |= !(piv > 0.0 && piv < 1e300);
+    const double inv = rsqrt_f64(piv);
+    invs[jj] = inv;
+    v[jj] *= inv;  // the diagonal lane gets piv / sqrt(piv)
 #pragma unroll
-      for (int q = jj + 1; q < 16; ++q) {
-        const double lc = col[c0 + q];
-        v[q] = (c0 + q <= lane) ? fma(-v[jj], lc, v[q]) : v[q];
-      }
-      asm volatile("" ::: "memory");
-    }
+    for (int q = jj + 1; q < 16; ++q) v[q] = fma(-v[jj], bcast_lane(v[jj], c0 + q), v[q]);
   }
 #pragma unroll
   for (int q = 0; q < 16; ++q) T[lane * LT + c0 + q] = v[q];
+  double mine = 0.0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) mine = (lane == q) ? invs[q] : mine;
+  if (lane < 16) dinv[c0 + lane] = mine;
+  if (bad && lane == 0) atomicOr(flag, 1);
 }
 
 __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
@@ -768,6 +807,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
     if (tid == 0) shi[0] = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     BAR();
     const int tk = __builtin_amdgcn_readfirstlane(shi[0]);
+    const unsigned long long t_got = d.tprof ? __builtin_amdgcn_s_memrealtime() : 0ull;
     CHOL_MARK(0, tk);
     CHOL_MARK(1, 1);
     CHOL_TRACE("[chol] wg %d got ticket %d\n", (int)blockIdx.x, tk);
@@ -779,7 +819,9 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
     if (tid == 0) {
       bool ok = true;
       switch (type) {
-        case kPotrf: ok = poll_ge(&ver[k * nbc + k], k, abort_w, d.flag); break;
+        case kPotrf:  // all updates of the tile but the last (done here); L(k, k-1) is awaited below
+          ok = poll_ge(&ver[k * nbc + k], k > 0 ? k - 1 : 0, abort_w, d.flag);
+          break;
         case kTrsm:
           ok = poll_ge(&ver[i * nbc + k], k, abort_w, d.flag) && poll_ge(&ver[k * nbc + k], k + 1, abort_w, d.flag);
           break;
@@ -802,17 +844,40 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
     CHOL_TRACE("[chol] wg %d ticket %d deps %s\n", (int)blockIdx.x, tk, shi[1] ? "ok" : "ABORT");
     if (!__builtin_amdgcn_readfirstlane(shi[1])) break;
     CHOL_MARK(1, 2);
+    if (d.tprof && tid == 0) {
+      d.tprof[4 * tk + 0] = (long long)blockIdx.x | ((long long)type << 12) | ((long long)i << 16) | ((long long)j << 32) |
+                           ((long long)k << 48);
+      d.tprof[4 * tk + 1] = (long long)t_got;
+      d.tprof[4 * tk + 2] = (long long)__builtin_amdgcn_s_memrealtime();
+    }
 
     if (type == kPotrf) {
+      int ps = 0;
+#define PSTAMP() do { if (d.tprof && tid == 0) d.tprof[65536 + 16 * k + (ps < 15 ? ps : 15)] = (long long)__builtin_amdgcn_s_memrealtime(); ++ps; } while (0)
       const int R0 = 64 * k, Bp = min(64, n - R0), Br = min(64, n + 1 - R0);
-      tile_load(rM, ld, R0, R0, Br, Bp, T0);
-      BAR();
-      CHOL_TRACE("[chol] potrf %d loaded Bp %d Br %d\n", k, Bp, Br);
-      for (int c0 = 0; c0 < Bp; c0 += 16) {
-        CHOL_MARK(1, 100 + c0);
-        if (wave == 0) panel_factor(T0, vec, c0, min(16, Bp - c0), lane, d.flag);
-        if (wave == 0) CHOL_MARK(2, 100 + c0);
+      dbl2 pre[8];
+      tile_issue(rM, ld, R0, R0, Br, Bp, pre);  // A(k,k) is final but for (k,k,k-1): load while L(k,k-1) is awaited
+      if (k > 0) {  // the tile's last update (k, k, k-1): T0 -= L(k,k-1) L(k,k-1)^T
+        if (tid == 0) shi[1] = poll_ge(&ver[k * nbc + k - 1], k, abort_w, d.flag) ? 1 : 0;
         BAR();
+        if (!__builtin_amdgcn_readfirstlane(shi[1])) break;
+        tile_load(rM, ld, R0, R0 - 64, Br, 64, T1);
+        tile_commit(pre, T0);
+        BAR();
+        dbl4 acc[2][2];
+        acc_load(T0, acc, wr, wc, lane);
+        gemm_nt64(T1, T1, acc, wr, wc, lane, -1.0);
+        acc_store(T0, acc, wr, wc, lane);
+      } else {
+        tile_commit(pre, T0);
+      }
+      BAR(); PSTAMP();
+      CHOL_TRACE("[chol] potrf %d loaded Bp %d Br %d\n", k, Bp, Br);
+      for (int c0 = 0; c0 < Bp; c0 += 16) {  // whole 16-wide panels (unit-padded)
+        CHOL_MARK(1, 100 + c0);
+        if (wave == 0) panel_factor(T0, vec + 128, c0, Bp, lane, d.flag);
+        if (wave == 0) CHOL_MARK(2, 100 + c0);
+        BAR(); PSTAMP();
         CHOL_MARK(1, 200 + c0);
         CHOL_TRACE("[chol] potrf %d panel %d done\n", k, c0);
         const int s0 = c0 + 16;
@@ -829,17 +894,25 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) T0[(R + 4 * q + fk) * LT + C + fr] = acc[q];
         }
-        BAR();
+        BAR(); PSTAMP();
       }
       CHOL_TRACE("[chol] potrf %d factored\n", k);
       CHOL_MARK(1, 300);
+      const bool below = k + 1 < nbr;  // trsm(k+1, k) runs in this task
+      const int R1 = R0 + 64, nr1 = below ? min(64, n + 1 - R1) : 0;
+      if (below && tid == 0) shi[2] = poll_ge(&ver[(k + 1) * nbc + k], k, abort_w, d.flag) ? 1 : 0;
       // Linv of the Bp x Bp pivot block (unit-diagonal padding past Bp)
       for (int idx = tid; idx < 64 * 64; idx += 256) {
         const int r = idx >> 6, c = idx & 63;
         T2[r * LT + c] = (r < Bp) ? (c <= r ? T0[r * LT + c] : 0.0) : (r == c ? 1.0 : 0.0);
         T1[r * LT + c] = 0.0;
       }
-      BAR();
+      if (tid >= Bp && tid < 64) vec[128 + tid] = 1.0;  // unit padding of the pivot block
+      BAR(); PSTAMP();
+      if (below) {
+        if (!__builtin_amdgcn_readfirstlane(shi[2])) break;
+        tile_issue(rM, ld, R1, R0, nr1, Bp, pre);  // lands during the Linv work
+      }
       if (wave == 0) {  // the four 16x16 diagonal blocks; lane = 16 * block + column
         const int base = 16 * (lane >> 4), cc = lane & 15;
         double xv[16];
@@ -848,12 +921,12 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           double sacc = (t == cc) ? 1.0 : 0.0;
 #pragma unroll
           for (int u = 0; u < t; ++u) sacc = fma(-T2[(base + t) * LT + base + u], xv[u], sacc);
-          xv[t] = sacc / T2[(base + t) * LT + base + t];
+          xv[t] = sacc * vec[128 + base + t];  // 1 / L[t][t] from the panel
         }
 #pragma unroll
         for (int t = 0; t < 16; ++t) T1[(base + t) * LT + base + cc] = xv[t];
       }
-      BAR();
+      BAR(); PSTAMP();
       for (int I = 1; I < 4; ++I) {  // Linv[I][J] = -Dinv_I sum_{K=J}^{I-1} L[I][K] Linv[K][J]
         if (wave < I) {
           const int J = wave;
@@ -873,7 +946,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) T1[(16 * I + 4 * q + fk) * LT + 16 * J + fr] = R[q];
         }
-        BAR();
+        BAR(); PSTAMP();
         CHOL_TRACE("[chol] potrf %d linv row %d\n", k, I);
       }
       CHOL_MARK(1, 400);
@@ -882,8 +955,26 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       const bool rhs = Br > Bp;
       if (rhs && tid < 32) st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[Bp * LT + 2 * tid]));
       CHOL_TRACE("[chol] potrf %d stored\n", k);
-      publish(&ver[k * nbc + k], k + 1, rhs ? &yver[k] : nullptr, 1);
+      if (below) {  // trsm(k+1, k): L(k+1,k) = A(k+1,k) L_kk^-T with L_kk^-1 still in T1
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        BAR();  // T0's store reads are done
+        tile_commit(pre, T0);
+        BAR();
+        dbl4 acc[2][2] = {};
+        gemm_nt64(T0, T1, acc, wr, wc, lane, 1.0);
+        BAR();
+        acc_store(T0, acc, wr, wc, lane);
+        BAR();
+        tile_store(rM, ld, R1, R0, nr1, Bp, T0);
+        const bool rhs1 = (k + 1 == nbr - 1);
+        if (rhs1 && tid < 32) st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[(n - R1) * LT + 2 * tid]));
+        publish(&ver[k * nbc + k], k + 1, &ver[(k + 1) * nbc + k], k + 1, rhs1 ? &yver[k] : nullptr, 1);
+      } else {
+        publish(&ver[k * nbc + k], k + 1, rhs ? &yver[k] : nullptr, 1);
+      }
       CHOL_TRACE("[chol] potrf %d published\n", k);
+      PSTAMP();
+#undef PSTAMP
     } else if (type == kTrsm) {
       const int R0 = 64 * i, C0 = 64 * k, nr = min(64, n + 1 - R0), nc = min(64, n - C0);
       tile_load(rM, ld, R0, C0, nr, nc, T0);
@@ -916,9 +1007,10 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       BAR();
       tile_store(rM, ld, Ri, Rj, nri, ncj, T2);
       publish(&ver[i * nbc + j], k + 1);
-    } else if (type == kBsolve) {
+    } else if (type == kBsolve) {  // x_i = L_ii^-T y_i, then bupd(i, i-1): y_{i-1} -= L(i,i-1)^T x_i
       const int C0 = 64 * i, Bp = min(64, n - C0);
       tile_load(rL, 64, C0, 0, 64, 64, T1);
+      if (i > 0) tile_load(rM, ld, C0, C0 - 64, Bp, 64, T0);
       CHOL_TRACE("[chol] bsolve %d tile issued\n", i);
       if (tid < 32) {
         const dbl2 yv = ld2(rY, 2 * tid < Bp ? (unsigned)((C0 + 2 * tid) * 8) : kOobOff);
@@ -935,10 +1027,25 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           st1(rX, (unsigned)((C0 + lane) * 8), sacc);
           d.dx[C0 + lane] = failed ? 0.0f : (float)sacc;
         }
+        vec[64 + lane] = lane < Bp ? sacc : 0.0;
       }
       CHOL_TRACE("[chol] bsolve %d computed\n", i);
       publish(&xdone[i], 1);
       CHOL_TRACE("[chol] bsolve %d published\n", i);
+      if (i > 0) {
+        if (tid == 0) shi[1] = poll_ge(&yver[i - 1], 1 + (nbc - 1 - i), abort_w, d.flag) ? 1 : 0;
+        BAR();
+        if (!__builtin_amdgcn_readfirstlane(shi[1])) break;
+        if (tid < 64) vec[128 + tid] = ld1(rY, (unsigned)((C0 - 64 + tid) * 8));
+        BAR();
+        if (wave == 0) {
+          double sacc = vec[128 + lane];
+#pragma unroll 8
+          for (int t = 0; t < 64; ++t) sacc = fma(-T0[t * LT + lane], vec[64 + t], sacc);
+          st1(rY, (unsigned)((C0 - 64 + lane) * 8), sacc);
+        }
+        publish(&yver[i - 1], 1 + (nbc - i));
+      }
     } else {  // kBupd: y_c -= L_rc^T x_r
       const int R0 = 64 * i, C0 = 64 * j, nr = min(64, n - R0), nc = min(64, n - C0);
       tile_load(rM, ld, R0, C0, nr, nc, T0);
@@ -953,6 +1060,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       }
       publish(&yver[j], 1 + (nbc - i));
     }
+    if (d.tprof && tid == 0) d.tprof[4 * tk + 3] = (long long)__builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -1145,6 +1253,9 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, const BaDev& bd, floa
   c.dx = dx;
   static int* const marks = getenv("DROID_CHOL_MARKS") ? reinterpret_cast<int*>(strtoull(getenv("DROID_CHOL_MARKS"), nullptr, 0)) : nullptr;
   c.marks = marks;
+  static long long* const tprof =
+      getenv("DROID_CHOL_TPROF") ? reinterpret_cast<long long*>(strtoull(getenv("DROID_CHOL_TPROF"), nullptr, 0)) : nullptr;
+  c.tprof = tprof;
   static bool attr = false;
   if (!attr) {
     DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&chol_dataflow_kernel),

@@ -39,18 +39,26 @@ void build_chol_tasks(int n, int& nbc, int& nbr, std::vector<int>& out) {
     id[std::make_tuple(type, i, j, k)] = (int)t.size();
     t.push_back({type, i, j, k, cost, {}, 0, 0.0});
   };
+  // potrf(k) also applies the last update of its own tile, (k,k,k-1), and
+  // solves the tile below it, trsm(k+1,k): the diagonal chain hands off once
+  // per step instead of three times.
   for (int k = 0; k < nbc; ++k) {
-    add(kPotrf, k, k, k, 6.0);
-    for (int i = k + 1; i < nbr; ++i) add(kTrsm, i, k, k, 2.0);
+    add(kPotrf, k, k, k, 10.0);
+    for (int i = k + 2; i < nbr; ++i) add(kTrsm, i, k, k, 2.0);
     for (int j = k + 1; j < nbc; ++j)
-      for (int i = j; i < nbr; ++i) add(kUpdate, i, j, k, 2.0);
+      for (int i = j; i < nbr; ++i)
+        if (!(i == j && j == k + 1)) add(kUpdate, i, j, k, 2.0);
   }
+  // bsolve(c) also applies x_c to y_{c-1} (bupd(c, c-1)): one hand-off per
+  // step of the back-substitution chain
   for (int c = 0; c < nbc; ++c) {
-    add(kBsolve, c, c, c, 1.0);
-    for (int r = c + 1; r < nbc; ++r) add(kBupd, r, c, c, 1.0);
+    add(kBsolve, c, c, c, 2.0);
+    for (int r = c + 2; r < nbc; ++r) add(kBupd, r, c, c, 1.0);
   }
   auto get = [&](int type, int i, int j, int k) { return id.at(std::make_tuple(type, i, j, k)); };
-  auto fin = [&](int i, int k) { return i == k ? get(kPotrf, k, k, k) : get(kTrsm, i, k, k); };
+  auto fin = [&](int i, int k) { return (i == k || i == k + 1) ? get(kPotrf, k, k, k) : get(kTrsm, i, k, k); };
+  // the task that applies x_r to y_c
+  auto ychain = [&](int r, int c) { return r == c + 1 ? get(kBsolve, r, r, r) : get(kBupd, r, c, c); };
   auto edge = [&](int a, int b) {
     for (int x : t[a].succ)
       if (x == b) return;
@@ -61,7 +69,9 @@ void build_chol_tasks(int n, int& nbc, int& nbr, std::vector<int>& out) {
     const Node nd = t[v];
     switch (nd.type) {
       case kPotrf:
-        if (nd.k > 0) edge(get(kUpdate, nd.k, nd.k, nd.k - 1), v);
+        if (nd.k >= 2) edge(get(kUpdate, nd.k, nd.k, nd.k - 2), v);
+        if (nd.k >= 1) edge(get(kPotrf, nd.k - 1, nd.k - 1, nd.k - 1), v);
+        if (nd.k >= 1 && nd.k + 1 < nbr) edge(get(kUpdate, nd.k + 1, nd.k, nd.k - 1), v);
         break;
       case kTrsm:
         edge(get(kPotrf, nd.k, nd.k, nd.k), v);
@@ -74,12 +84,16 @@ void build_chol_tasks(int n, int& nbc, int& nbr, std::vector<int>& out) {
         break;
       case kBsolve:
         edge(get(kPotrf, nd.i, nd.i, nd.i), v);
-        edge(nd.i == nbc - 1 ? fin(nbr - 1, nd.i) : get(kBupd, nd.i + 1, nd.i, nd.i), v);
+        edge(nd.i == nbc - 1 ? fin(nbr - 1, nd.i) : ychain(nd.i + 1, nd.i), v);
+        if (nd.i >= 1) {
+          edge(fin(nd.i, nd.i - 1), v);
+          edge(nd.i == nbc - 1 ? fin(nbr - 1, nd.i - 1) : ychain(nd.i + 1, nd.i - 1), v);
+        }
         break;
       case kBupd:
         edge(get(kBsolve, nd.i, nd.i, nd.i), v);
         edge(fin(nd.i, nd.j), v);
-        edge(nd.i == nbc - 1 ? fin(nbr - 1, nd.j) : get(kBupd, nd.i + 1, nd.j, nd.j), v);
+        edge(nd.i == nbc - 1 ? fin(nbr - 1, nd.j) : ychain(nd.i + 1, nd.j), v);
         break;
     }
   }
