@@ -39,6 +39,19 @@ ZR_FLOPS_PER_PIXEL = 2 * 256 * 448 * 9
 ZR_KERNEL = "conv_band_kernel<256,256>"   # csrc/conv_kernels.hip, chosen for 48x64 maps
 ZR_KERNEL_MATCH = "conv_band_kernel<256, 256"   # its symbol in rocprof / PMC summaries
 LOOKUP_KERNEL = "corr_pyramid_f16_r3_kernel"
+# SURVEY.md §8d whole-iteration floors.  Update-operator convs per edge-pixel:
+# corr_encoder 1x1 196->128 + 3x3 128->128, flow_encoder 7x7 4->128 + 3x3 128->64,
+# ConvGRU convz|convr|convq 3x3 448->128 + w 1x1 128->128, delta/weight 3x3
+# 128->128 + 3x3 128->2 each, GraphAgg conv1 3x3 128->128 (droid_net.py:59-143,
+# gru.py:19-32); per unique source frame-pixel: GraphAgg conv2 3x3 128->128,
+# eta 3x3 128->1, upmask 1x1 128->576.
+CONV_FLOPS_PER_EDGE_PIXEL = 2 * (196 * 128 + 128 * 128 * 9 + 4 * 128 * 49 + 128 * 64 * 9 + 3 * 448 * 128 * 9
+                                 + 128 * 128 + 2 * (128 * 128 * 9 + 128 * 2 * 9) + 128 * 128 * 9)
+CONV_FLOPS_PER_FRAME_PIXEL = 2 * (128 * 128 * 9 + 128 * 9 + 128 * 576)
+# HBM-bound stages per update (fused lookup path): lookup 3,059,712 B/edge (§8d fused row),
+# BA 2 GN x (49,152 B/edge + 49,152 B/frame), reproject + motn 110,592 B/edge
+HBM_BYTES_PER_EDGE = 3059712 + 2 * 49152 + 110592
+HBM_BYTES_PER_FRAME = 2 * 49152
 
 
 LOOKUP_FN = ["corr_lookup_ce0"]
@@ -320,6 +333,24 @@ def main():
         }
         if lookup_roof:
             result["roofline_lookup"] = lookup_roof
+        # whole-iteration fraction: max(HBM floor, MFMA floor) / measured update()
+        hw = (args.ht // 8) * (args.wd // 8)
+        n_src = len(np.unique(ii))
+        conv_flops = (CONV_FLOPS_PER_EDGE_PIXEL * len(ii) + CONV_FLOPS_PER_FRAME_PIXEL * n_src) * hw
+        hbm_bytes = HBM_BYTES_PER_EDGE * len(ii) + HBM_BYTES_PER_FRAME * args.frames
+        mfma_floor = conv_flops / (PEAK_F16_TFLOPS * 1e12) * 1e3 / world
+        hbm_floor = hbm_bytes / (PEAK_HBM_GBS * 1e9) * 1e3 / world
+        result["iteration_roofline"] = {
+            "bound": "mfma" if mfma_floor >= hbm_floor else "hbm",
+            "mfma_floor_ms": mfma_floor, "hbm_floor_ms": hbm_floor, "measured_ms": ms,
+            "frac": max(mfma_floor, hbm_floor) / ms,
+            "conv_flops_per_update": conv_flops, "hbm_bytes_per_update": hbm_bytes}
+        if breakdown:
+            op_ms = breakdown["update_op (convs)"]
+            result["iteration_roofline"]["conv_stack"] = {
+                "achieved_tflops": conv_flops / world / (op_ms * 1e-3) / 1e12, "peak": PEAK_F16_TFLOPS,
+                "frac": conv_flops / world / (op_ms * 1e-3) / 1e12 / PEAK_F16_TFLOPS,
+                "update_op_ms": op_ms, "note": "update_op includes the fused lookup + corr_encoder[0]"}
         if breakdown:
             result["breakdown_ms"] = breakdown
         if world == 1 and not args.no_cpu_baseline:
