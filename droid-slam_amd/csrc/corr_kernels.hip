@@ -14,6 +14,7 @@
 // product rounded to half, every += rounded to half); fp32/fp64 use the fused
 // multiply-add nvcc emits for `corr += s * w`.
 #include "common.hpp"
+#include "lds_dma.hpp"
 
 // Bit-exact at::Half semantics need every product and sum rounded separately:
 // forbid fusing them into v_fma_mix / v_fma_f16 (hipcc contracts by default).
@@ -480,6 +481,7 @@ int droid_corr_pyramid_lookup_nhwc(const void* const* levels, const int* H2s, co
   return kOk;
 }
 
+extern "C++" {  // (inside the extern "C" block: the kernel below is a template)
 namespace droid {
 
 // ---------------------------------------------------------------------------
@@ -503,6 +505,7 @@ struct CorrCe0Args {
   int H2[4], W2[4];
   const float* coords;  // (E, H, W, 2)
   int fast;             // bit l: level l rows are 16-B aligned (W2 % 8 == 0)
+  int tiled;            // bit l: level l slices stored in 8x8 tiles (droid_corr_lookup_ce0_tiled)
   const __half* w;      // [128][224], columns >= 196 zero
   const float* bias;    // [128]
   __half* out;          // (E, H, W, 128)
@@ -511,15 +514,38 @@ struct CorrCe0Args {
 };
 
 constexpr int kCeTP = 128, kCeKS = 232, kCeOS = 136;
-constexpr int kCeLds = (2 * 128 * kCeKS + kCeTP * kCeOS) * 2;
+constexpr unsigned kCeOob = 0x80000000u;  // buffer offset past any descriptor: the load returns 0
+// + coordinate staging Cs [2 slots][2 pixel halves][64 px] float2 (LDS-DMA)
+constexpr int kCeLds = (2 * 128 * kCeKS + kCeTP * kCeOS) * 2 + 2 * 2 * 64 * 8;
 
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+// LDS-DMA of 4 B per lane (buffer_load_dword ... lds): lane l's dword lands at
+// LDS byte `lds` + 4 l.  Preceded by lgkmcnt(0) so that the issuing wave's
+// earlier ds_reads of the destination have returned (write-after-read).
+__device__ __forceinline__ void ce_dma4(rsrc_t rs, unsigned lds, unsigned voff) {
+  const rsrc_t r = {__builtin_amdgcn_readfirstlane(rs.x), __builtin_amdgcn_readfirstlane(rs.y),
+                    __builtin_amdgcn_readfirstlane(rs.z), __builtin_amdgcn_readfirstlane(rs.w)};
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// FAST: every level's rows are 16-B aligned (W2 % 8 == 0) - the gather is
+// branch-free buffer loads only, which keeps the compiler's vmcnt accounting
+// exact across the loop (a CFG join with the generic path makes it wait for 0)
+template <bool FAST>
 __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
   extern __shared__ __attribute__((aligned(16))) _Float16 smem_ce[];
   _Float16* Ws = smem_ce;                 // [128 co][kCeKS]
   _Float16* As = Ws + 128 * kCeKS;        // [128 px][kCeKS] lookup tile (cols 196.. zero)
   _Float16* Os = As + kCeTP * kCeKS;      // [128 px][kCeOS] output staging
+  float2* Cs = reinterpret_cast<float2*>(Os + kCeTP * kCeOS);  // [2 slots][2 halves][64 px]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int lvl = wave & 3, px = (wave >> 2) * 64 + lane;
+  // level is wave-uniform: keep it (and everything derived from it) in SGPRs
+  const int lvl = __builtin_amdgcn_readfirstlane(wave & 3), px = (wave >> 2) * 64 + lane;
   const int HW = a.HW, tpe = HW / kCeTP;  // tiles per edge
 
   for (int idx = tid; idx < 128 * 29; idx += 512) {
@@ -534,17 +560,19 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
   }
 
   const int H2 = a.H2[lvl], W2 = a.W2[lvl], nch = W2 >> 3;
-  const bool fast = (a.fast >> lvl) & 1;  // rows 16-B aligned
+  const bool fast = FAST || ((a.fast >> lvl) & 1);  // rows 16-B aligned
   const __half* vol = a.vol[lvl];
-  const long slice = (long)H2 * W2;
+  // 8x8-tiled slices (tiled bit): element (y, x) at ((y>>3) * W2/8 + (x>>3)) * 64
+  // + (y&7) * 8 + (x&7), H2 padded to a multiple of 8 - a window's 8 rows then
+  // touch ~3.5 128-B lines instead of 8 (one per row of the row-major slice)
+  const bool tiled = (a.tiled >> lvl) & 1;
+  const long slice = tiled ? (long)((H2 + 7) & ~7) * W2 : (long)H2 * W2;
   const float scl = 1.0f / (float)(1 << lvl);
 
-  // per-lane gather state of one tile
-  uint4 raw[8][2];
-  float cx = 0.f, cy = 0.f;      // coordinates of the tile being loaded
-  float ncx = 0.f, ncy = 0.f;    // coordinates of the tile after it
-  float wdx = 0.f, wdy = 0.f;    // bilinear fractions of the loaded tile
-  int woff = 0;                  // window x offset within the first chunk
+  // per-lane gather state of the two tiles in flight (slot = iteration parity)
+  uint4 raw[2][8][2];
+  float wdx[2] = {0.f, 0.f}, wdy[2] = {0.f, 0.f};  // bilinear fractions
+  int woff[2] = {0, 0};                             // window x offset within the first chunk
   auto tile_pixel = [&](long t) { return (t / tpe) * (long)HW + (t % tpe) * kCeTP + px; };
   auto load_coords = [&](long t, float& x, float& y) {
     if (t < a.ntiles) {
@@ -552,31 +580,62 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
       x = c.x; y = c.y;
     }
   };
-  auto issue = [&](long t) {
+  // Coordinates of the tile a slot issues next are staged in LDS by this wave's
+  // own LDS-DMA (its 64 pixels, 2 x 4 B per lane), issued right BEFORE the slot's
+  // window rows: when the wave has waited for those rows (the bilinear step),
+  // the coordinates have landed too (vmcnt retires in order) and no VGPR holds a
+  // load across the loop - a loop-carried loaded value costs a vmcnt wait on its
+  // copy at the back edge, which would drain the other slot's rows.
+  const int half = wave >> 2;
+  const unsigned cs_lds = lds_addr(Cs) + (unsigned)(half * 512);
+  auto stage_coords = [&](const int sl, long t) __attribute__((always_inline)) {
     if (t >= a.ntiles) return;
+    const long p0 = (t / tpe) * (long)HW + (t % tpe) * kCeTP + half * 64;
+    const rsrc_t rs = make_rsrc(a.coords + p0 * 2, 512);
+    const unsigned dst = cs_lds + (unsigned)(sl * 1024);
+    ce_dma4(rs, dst, (unsigned)lane * 4u);
+    ce_dma4(rs, dst + 256, 256u + (unsigned)lane * 4u);
+  };
+  auto issue = [&](const int sl, long t, float cx, float cy) __attribute__((always_inline)) {
+    const bool valid = t < a.ntiles;  // uniform; FAST: past the last tile every offset is out of range
+    if (!FAST && !valid) return;
     const float x0 = cx * scl, y0 = cy * scl;
     const float fx0 = floorf(x0), fy0 = floorf(y0);
-    wdx = x0 - fx0; wdy = y0 - fy0;
+    wdx[sl] = x0 - fx0; wdy[sl] = y0 - fy0;
     const int xi0 = (int)fx0, yi0 = (int)fy0;
     const int xs = xi0 - 3;
     const int c0 = (xs >= 0) ? (xs >> 3) : -((-xs + 7) >> 3);
-    woff = xs - 8 * c0;
-    const __half* base = vol + tile_pixel(t) * slice;
+    woff[sl] = xs - 8 * c0;
     if (fast) {
+      // buffer loads relative to the tile's first slice (wave-uniform descriptor;
+      // a tile never crosses an edge since HW % 128 == 0): window pieces outside
+      // the slice get an out-of-range offset and return zeros - no branches, so
+      // all 16 loads of the lane stay in flight together
+      const long tp0 = valid ? (t / tpe) * (long)HW + (t % tpe) * kCeTP : 0;
+      const unsigned long long pa = (unsigned long long)(vol + tp0 * slice);
+      const unsigned long long pu = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(pa >> 32)) << 32) |
+                                    (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)pa);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<void*>(pu), (short)0, __builtin_amdgcn_readfirstlane((int)(kCeTP * slice * 2)), 0x00020000);
+      const unsigned pbase = (unsigned)(px * slice) * 2u;
+      const bool ok0 = valid && c0 >= 0 && c0 < nch, ok1 = valid && c0 + 1 >= 0 && c0 + 1 < nch;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int y1 = yi0 - 3 + j;
         const bool yok = y1 >= 0 && y1 < H2;
-        const __half* row = base + (long)y1 * W2;
-        raw[j][0] = (yok && c0 >= 0 && c0 < nch) ? *reinterpret_cast<const uint4*>(row + 8 * c0)
-                                                 : make_uint4(0, 0, 0, 0);
-        raw[j][1] = (yok && c0 + 1 >= 0 && c0 + 1 < nch) ? *reinterpret_cast<const uint4*>(row + 8 * (c0 + 1))
-                                                          : make_uint4(0, 0, 0, 0);
+        // 16-B piece c of row y1: row-major y1*W2 + 8c, tiled ((y1>>3)*nch + c)*64 + (y1&7)*8
+        const int re = tiled ? (y1 >> 3) * nch * 64 + (y1 & 7) * 8 : y1 * W2;
+        const int cs = tiled ? 64 : 8;
+        const unsigned o0 = (yok && ok0) ? pbase + (unsigned)(re + cs * c0) * 2u : kCeOob;
+        const unsigned o1 = (yok && ok1) ? pbase + (unsigned)(re + cs * (c0 + 1)) * 2u : kCeOob;
+        raw[sl][j][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o0, 0, 0));
+        raw[sl][j][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, 0));
       }
-    } else {
+    } else if constexpr (!FAST) {
+      const __half* base = vol + tile_pixel(t) * slice;
       // rows not 16-B aligned (W2 % 8 != 0): the 8 taps one by one, packed as an
       // aligned chunk (window offset 0)
-      woff = 0;
+      woff[sl] = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int y1 = yi0 - 3 + j;
@@ -590,22 +649,23 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
           const unsigned hi = (yok && xb >= 0 && xb < W2) ? row[xb] : 0u;
           u[m] = lo | (hi << 16);
         }
-        raw[j][0] = make_uint4(u[0], u[1], u[2], u[3]);
-        raw[j][1] = make_uint4(0, 0, 0, 0);
+        raw[sl][j][0] = make_uint4(u[0], u[1], u[2], u[3]);
+        raw[sl][j][1] = make_uint4(0, 0, 0, 0);
       }
     }
   };
-  // row j of the loaded window as 8 floats (the taps x = xs .. xs+7)
-  auto row_taps = [&](int j, float* t) {
-    const unsigned u[8] = {raw[j][0].x, raw[j][0].y, raw[j][0].z, raw[j][0].w,
-                           raw[j][1].x, raw[j][1].y, raw[j][1].z, raw[j][1].w};
-    const int k = woff >> 1;
-    unsigned v[6], w[5];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) v[i] = (k & 2) ? u[i + 2] : u[i];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) w[i] = (k & 1) ? v[i + 1] : v[i];
-    const unsigned sh = (woff & 1) ? 16u : 0u;
+  // row j of slot sl's window as 8 floats (the taps x = xs .. xs+7)
+  auto row_taps = [&](const int sl, int j, float* t) __attribute__((always_inline)) {
+    // dword m + k of the two pieces, k = woff / 2 in 0..3, as explicit selects on
+    // scalars (a select over an array index becomes a dynamic index into scratch,
+    // whose vmcnt waits would drain the window loads still in flight)
+    const uint4 p0 = raw[sl][j][0], p1 = raw[sl][j][1];
+    const int k = woff[sl] >> 1;
+    const bool k2 = k & 2, k1 = k & 1;
+    const unsigned v0 = k2 ? p0.z : p0.x, v1 = k2 ? p0.w : p0.y, v2 = k2 ? p1.x : p0.z;
+    const unsigned v3 = k2 ? p1.y : p0.w, v4 = k2 ? p1.z : p1.x, v5 = k2 ? p1.w : p1.y;
+    const unsigned w[5] = {k1 ? v1 : v0, k1 ? v2 : v1, k1 ? v3 : v2, k1 ? v4 : v3, k1 ? v5 : v4};
+    const unsigned sh = (woff[sl] & 1) ? 16u : 0u;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const unsigned o = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
@@ -620,23 +680,20 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) bias[j] = a.bias[wn * 64 + j * 16 + fr];
 
-  long t = blockIdx.x;
-  load_coords(t, cx, cy);
-  load_coords(t + gridDim.x, ncx, ncy);
-  issue(t);
-  __syncthreads();  // weights and pad columns are in LDS
-  for (; t < a.ntiles; t += gridDim.x) {
+  // one tile: windows of slot sl -> As, then (with the tile two steps ahead
+  // issued into the same slot) the 1x1 conv on MFMA and the coalesced store
+  auto process = [&](const int sl, long t) __attribute__((always_inline)) {
     // (1) bilinear windows of tile t -> As (corr_pyramid_f16_r3_kernel arithmetic)
     {
-      const float w11 = rnd16(wdx * wdy);
-      const float w10 = rnd16(wdx * (1.0f - wdy));
-      const float w01 = rnd16((1.0f - wdx) * wdy);
-      const float w00 = rnd16((1.0f - wdx) * (1.0f - wdy));
+      const float w11 = rnd16(wdx[sl] * wdy[sl]);
+      const float w10 = rnd16(wdx[sl] * (1.0f - wdy[sl]));
+      const float w01 = rnd16((1.0f - wdx[sl]) * wdy[sl]);
+      const float w00 = rnd16((1.0f - wdx[sl]) * (1.0f - wdy[sl]));
       _Float16* arow = As + px * kCeKS + lvl * 49;
       float prev[8], cur[8];
 #pragma unroll
       for (int j = 0; j <= 7; ++j) {
-        row_taps(j, cur);
+        row_taps(sl, j, cur);
         if (j > 0) {
           const int b = j - 1;
 #pragma unroll
@@ -652,10 +709,11 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
         for (int i = 0; i < 8; ++i) prev[i] = cur[i];
       }
     }
-    // (2) next tiles in flight while this one is multiplied and stored
-    cx = ncx; cy = ncy;
-    issue(t + gridDim.x);
-    load_coords(t + 2L * gridDim.x, ncx, ncy);
+    // (2) the tile two steps ahead goes into this slot while this one is multiplied
+    // and stored; its coordinates were staged before the rows just consumed.
+    const float2 c2 = Cs[sl * 128 + half * 64 + lane];  // staged with the rows just consumed
+    stage_coords(sl, t + 4L * gridDim.x);
+    issue(sl, t + 2L * gridDim.x, c2.x, c2.y);
     __syncthreads();
     // (3) 128 px x 128 co x 224 on MFMA
     floatx4_t acc[2][4];
@@ -687,26 +745,53 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
           Os[(wm * 32 + f * 16 + fq * 4 + k) * kCeOS + wn * 64 + j * 16 + fr] =
               (_Float16)fmaxf(acc[f][j][k] + bias[j], 0.f);
     __syncthreads();
+    if (t >= a.ntiles) return;  // uniform: the odd step past the last tile computes but stores nothing
     const long pix0 = (t / tpe) * (long)HW + (t % tpe) * kCeTP;
     for (int idx = tid; idx < kCeTP * 16; idx += 512) {
       const int r = idx >> 4, q = idx & 15;
       *reinterpret_cast<uint4*>(a.out + (pix0 + r) * 128 + q * 8) = *reinterpret_cast<const uint4*>(&Os[r * kCeOS + q * 8]);
     }
+  };
+
+  const long g = gridDim.x;
+  long t = blockIdx.x;
+  {
+    float cx0 = 0.f, cy0 = 0.f, cx1 = 0.f, cy1 = 0.f;
+    load_coords(t, cx0, cy0);
+    load_coords(t + g, cx1, cy1);
+    stage_coords(0, t + 2 * g);
+    issue(0, t, cx0, cy0);
+    stage_coords(1, t + 3 * g);
+    issue(1, t + g, cx1, cy1);
+  }
+  __syncthreads();  // weights and pad columns are in LDS
+  // two tiles in flight per lane (16 window rows each): slot 0 holds the even
+  // steps, slot 1 the odd ones.  Both steps run unconditionally (a guarded
+  // second step would make the loop-carried coordinates a phi whose copy waits
+  // for the loads in flight); a step past the last tile loads and stores nothing.
+  for (; t < a.ntiles; t += 2 * g) {
+    process(0, t);
+    process(1, t + g);
   }
 }
 
 }  // namespace droid
+}  // extern "C++"
 
 // Fused CorrBlock lookup + corr_encoder[0] (see corr_ce0_kernel).
-int droid_corr_lookup_ce0(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
-                          const void* w, const float* bias, void* out, int E, int H, int W, hipStream_t stream) {
+static int corr_lookup_ce0_impl(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
+                                const void* w, const float* bias, void* out, int E, int H, int W, bool tiled,
+                                hipStream_t stream) {
   using namespace droid;
   if ((H * W) % kCeTP)
     return fail(kUnsupported, "corr_lookup_ce0: H*W must be a multiple of 128");
   CorrCe0Args a{};
   for (int l = 0; l < 4; ++l) {
     if (H2s[l] <= 0 || W2s[l] <= 0) return fail(kInvalidArgument, "corr_lookup_ce0: empty level");
-    if (W2s[l] % 8 == 0 && (reinterpret_cast<uintptr_t>(levels[l]) & 15) == 0) a.fast |= 1 << l;
+    const bool aligned = W2s[l] % 8 == 0 && (reinterpret_cast<uintptr_t>(levels[l]) & 15) == 0;
+    if (tiled && !aligned) return fail(kUnsupported, "corr_lookup_ce0_tiled: W2 % 8 != 0 or unaligned level");
+    if (aligned) a.fast |= 1 << l;
+    if (tiled) a.tiled |= 1 << l;
     a.vol[l] = (const __half*)levels[l];
     a.H2[l] = H2s[l];
     a.W2[l] = W2s[l];
@@ -721,14 +806,30 @@ int droid_corr_lookup_ce0(const void* const* levels, const int* H2s, const int* 
   if (a.ntiles == 0) return kOk;
   static bool attr = false;
   if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_ce0_kernel),
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_ce0_kernel<true>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kCeLds));
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_ce0_kernel<false>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kCeLds));
     attr = true;
   }
   const long grid = std::min<long>(a.ntiles, device_cu_count());
-  corr_ce0_kernel<<<dim3((unsigned)grid), 512, kCeLds, stream>>>(a);
+  if (a.fast == 15)
+    corr_ce0_kernel<true><<<dim3((unsigned)grid), 512, kCeLds, stream>>>(a);
+  else
+    corr_ce0_kernel<false><<<dim3((unsigned)grid), 512, kCeLds, stream>>>(a);
   DROID_LAUNCH_CHECK();
   return kOk;
+}
+
+int droid_corr_lookup_ce0(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
+                          const void* w, const float* bias, void* out, int E, int H, int W, hipStream_t stream) {
+  return corr_lookup_ce0_impl(levels, H2s, W2s, coords, w, bias, out, E, H, W, false, stream);
+}
+
+int droid_corr_lookup_ce0_tiled(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
+                                const void* w, const float* bias, void* out, int E, int H, int W,
+                                hipStream_t stream) {
+  return corr_lookup_ce0_impl(levels, H2s, W2s, coords, w, bias, out, E, H, W, true, stream);
 }
 
 int droid_altcorr_forward(int dtype, const void* fmap1, const void* fmap2, const float* coords,

@@ -136,10 +136,12 @@ def corr_lookup_ce0_supported(levels, H, W):
     return len(levels) == 4 and (H * W) % 128 == 0
 
 
-def corr_lookup_ce0(levels, coords, w, bias, out=None):
+def corr_lookup_ce0(levels, coords, w, bias, out=None, tiled_shapes=None):
     """Fused CorrBlock lookup + corr_encoder[0] (include/droid_backends.h:
     droid_corr_lookup_ce0): levels 4 x (E,H,W,H2,W2) fp16, coords (E,H,W,2) f32,
-    w [128][224] fp16, bias [128] f32 -> (E,H,W,128) fp16 = relu(w . lookup + b)."""
+    w [128][224] fp16, bias [128] f32 -> (E,H,W,128) fp16 = relu(w . lookup + b).
+    tiled_shapes [(H2,W2)] x 4: the levels are 8x8-tiled (corr.tile8) and go to
+    droid_corr_lookup_ce0_tiled."""
     _check_inputs(["level%d" % i for i in range(len(levels))] + ["coords", "w", "bias"],
                   list(levels) + [coords, w, bias])
     _need(coords, torch.float32, "coords")
@@ -150,11 +152,20 @@ def corr_lookup_ce0(levels, coords, w, bias, out=None):
         out = torch.empty((E, H, W, 128), dtype=torch.float16, device=coords.device)
     L = len(levels)
     ptrs = (ctypes.c_void_p * L)(*[lv.data_ptr() for lv in levels])
-    h2s = (ctypes.c_int * L)(*[lv.shape[3] for lv in levels])
-    w2s = (ctypes.c_int * L)(*[lv.shape[4] for lv in levels])
+    if tiled_shapes is not None:
+        for lv, (h2, w2) in zip(levels, tiled_shapes):
+            if tuple(lv.shape[3:]) != ((h2 + 7) // 8, w2 // 8, 8, 8):
+                raise RuntimeError("corr_lookup_ce0: level shape %s is not the 8x8 tiling of %dx%d"
+                                   % (tuple(lv.shape), h2, w2))
+        h2s = (ctypes.c_int * L)(*[h for h, _ in tiled_shapes])
+        w2s = (ctypes.c_int * L)(*[w_ for _, w_ in tiled_shapes])
+        fn, name = lib.droid_corr_lookup_ce0_tiled, "corr_lookup_ce0_tiled"
+    else:
+        h2s = (ctypes.c_int * L)(*[lv.shape[3] for lv in levels])
+        w2s = (ctypes.c_int * L)(*[lv.shape[4] for lv in levels])
+        fn, name = lib.droid_corr_lookup_ce0, "corr_lookup_ce0"
     with torch.cuda.device(coords.device):
-        check(lib.droid_corr_lookup_ce0(ptrs, h2s, w2s, _ptr(coords), _ptr(w), _ptr(bias), _ptr(out), E, H, W,
-                                        _stream(coords)), "corr_lookup_ce0")
+        check(fn(ptrs, h2s, w2s, _ptr(coords), _ptr(w), _ptr(bias), _ptr(out), E, H, W, _stream(coords)), name)
     return out
 
 

@@ -43,37 +43,77 @@ def _avg_pool2(x, max_elems=1 << 30):
     return out
 
 
-class CorrBlock:
-    """corr.py:23-71 (volume correlation pyramid)."""
+def tile8(level, chunk=256):
+    """(E,H,W,H2,W2) -> 8x8-tiled (E,H,W,ceil(H2/8),W2/8,8,8), rows past H2 zero
+    (the layout of droid_corr_lookup_ce0_tiled), in edge chunks to bound the
+    transient memory of the copy."""
+    E, H, W, H2, W2 = level.shape
+    H2p = (H2 + 7) // 8 * 8
+    out = torch.zeros((E, H, W, H2p // 8, W2 // 8, 8, 8), dtype=level.dtype, device=level.device)
+    for s in range(0, E, chunk):
+        x = level[s:s + chunk]
+        if H2p != H2:
+            x = F.pad(x, (0, 0, 0, H2p - H2))
+        n = x.shape[0]
+        out[s:s + n] = x.reshape(n, H, W, H2p // 8, 8, W2 // 8, 8).permute(0, 1, 2, 3, 5, 4, 6)
+    return out
 
-    def __init__(self, fmap1, fmap2, num_levels=4, radius=3):
+
+def untile8(level, H2, W2):
+    """inverse of tile8: (E,H,W,H2p/8,W2/8,8,8) -> (E,H,W,H2,W2)."""
+    E, H, W = level.shape[:3]
+    H2p = level.shape[3] * 8
+    x = level.permute(0, 1, 2, 3, 5, 4, 6).reshape(E, H, W, H2p, W2)
+    return x[:, :, :, :H2].contiguous()
+
+
+class CorrBlock:
+    """corr.py:23-71 (volume correlation pyramid).
+
+    tiled=True (FactorGraph with the fused operator): the levels are stored in
+    8x8 tiles (tile8) for droid_corr_lookup_ce0_tiled - same values, a layout
+    whose lookup windows touch fewer DRAM lines; the reference layout is
+    rebuilt on demand for the other lookups (reference_pyramid)."""
+
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=3, tiled=False):
         self.num_levels = num_levels
         self.radius = radius
         self.corr_pyramid = []
         vol = CorrBlock.corr(fmap1, fmap2)
         batch, num, h1, w1, h2, w2 = vol.shape
+        self.level_shapes = [(h2 // 2 ** i, w2 // 2 ** i) for i in range(num_levels)]
+        self.tiled = bool(tiled) and all(w % 8 == 0 for _, w in self.level_shapes)
         vol = vol.reshape(batch * num * h1 * w1, 1, h2, w2)
         for i in range(num_levels):
-            self.corr_pyramid.append(vol.view(batch * num, h1, w1, h2 // 2 ** i, w2 // 2 ** i))
+            lv = vol.view(batch * num, h1, w1, h2 // 2 ** i, w2 // 2 ** i)
             if i + 1 < num_levels:
                 vol = _avg_pool2(vol)
+            self.corr_pyramid.append(tile8(lv) if self.tiled else lv)
+            del lv
+
+    def reference_pyramid(self):
+        """the levels in the reference layout (E,H,W,H2,W2)."""
+        if not self.tiled:
+            return self.corr_pyramid
+        return [untile8(lv, h2, w2) for lv, (h2, w2) in zip(self.corr_pyramid, self.level_shapes)]
 
     def __call__(self, coords):
         batch, num, ht, wd, _ = coords.shape
-        if torch.is_grad_enabled() and any(v.requires_grad for v in self.corr_pyramid):
+        pyr = self.reference_pyramid()
+        if torch.is_grad_enabled() and any(v.requires_grad for v in pyr):
             c = coords.permute(0, 1, 4, 2, 3).contiguous().view(batch * num, 2, ht, wd)
-            out = [CorrSampler.apply(self.corr_pyramid[i], c / 2 ** i, self.radius).view(batch, num, -1, ht, wd)
+            out = [CorrSampler.apply(pyr[i], c / 2 ** i, self.radius).view(batch, num, -1, ht, wd)
                    for i in range(self.num_levels)]
             return torch.cat(out, dim=2)
         c = coords.reshape(batch * num, ht, wd, 2).float().contiguous()
-        out = droid_backends.corr_pyramid_lookup(self.corr_pyramid, c, self.radius)
+        out = droid_backends.corr_pyramid_lookup(pyr, c, self.radius)
         return out.view(batch, num, -1, ht, wd)
 
     def lookup_nhwc(self, coords):
         """fused-operator layout: (E,H,W,200) fp16 rows (196 used), one launch."""
         batch, num, ht, wd, _ = coords.shape
         c = coords.reshape(batch * num, ht, wd, 2).float().contiguous()
-        return droid_backends.corr_pyramid_lookup_nhwc(self.corr_pyramid, c, 200)
+        return droid_backends.corr_pyramid_lookup_nhwc(self.reference_pyramid(), c, 200)
 
     def cat(self, other):
         for i in range(self.num_levels):

@@ -9,6 +9,8 @@ scatter indices and the BA plan never need a device->host sync; the motion
 features come out of the fused reprojection kernel; the correlation lookup
 is one kernel for all levels; BA runs fully on the GPU.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -55,6 +57,8 @@ class FactorGraph:
         # fused (MI355X) operator: per-edge hidden state kept channels-last (E,H,W,128)
         from .fused import FusedUpdateModule
         self.fused = isinstance(update_op, FusedUpdateModule)
+        # CorrBlock(tiled=...) for the fused lookup (DROID_TILED_VOLUME=0: reference row-major layout)
+        self.tiled_volume = os.environ.get("DROID_TILED_VOLUME", "1") != "0"
 
     # -- per-edge state layout ------------------------------------------------
     @property
@@ -141,7 +145,8 @@ class FactorGraph:
             c = torch.as_tensor((ii == jj).astype(np.int64), device=self.device)
             fmap1 = self.video.fmaps[dii, 0].to(self.device).unsqueeze(0)
             fmap2 = self.video.fmaps[djj, c].to(self.device).unsqueeze(0)
-            corr = CorrBlock(fmap1, fmap2)
+            # the fused operator reads the volume through the 8x8-tiled layout
+            corr = CorrBlock(fmap1, fmap2, tiled=self.fused and self.tiled_volume)
             self.corr = corr if self.corr is None else self.corr.cat(corr)
         if self.corr_impl == "pyramid":
             self._alt_pyr = None   # frames may have changed: rebuilt at the next update

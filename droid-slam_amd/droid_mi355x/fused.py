@@ -199,12 +199,14 @@ class FusedUpdateModule(torch.nn.Module):
         e16 = lambda c: torch.empty((E, H, W, c), dtype=torch.float16, device=dev)
 
         levels = corr.block.corr_pyramid if isinstance(corr, PendingLookup) else None
+        tiled = levels is not None and getattr(corr.block, "tiled", False)
         if isinstance(corr, PendingAltLookup):
             coords = corr.coords.reshape(E, H, W, 2).float().contiguous()
             c1 = droid_backends.corr_alt_ce0(corr.pyramid, corr.f1, corr.f2, coords, P["ce0_224"], P["ce0_b"])
         elif levels is not None and droid_backends.corr_lookup_ce0_supported(levels, H, W):
             coords = corr.coords.reshape(E, H, W, 2).float().contiguous()
-            c1 = droid_backends.corr_lookup_ce0(levels, coords, P["ce0_224"], P["ce0_b"])
+            c1 = droid_backends.corr_lookup_ce0(levels, coords, P["ce0_224"], P["ce0_b"],
+                                                tiled_shapes=corr.block.level_shapes if tiled else None)
         else:
             if isinstance(corr, PendingLookup):
                 corr = corr.materialise()

@@ -74,6 +74,17 @@ int droid_corr_pyramid_lookup_nhwc(const void* const* levels, const int* H2s, co
 int droid_corr_lookup_ce0(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
                           const void* w, const float* bias, void* out, int E, int H, int W, hipStream_t stream);
 
+/* droid_corr_lookup_ce0 on volumes stored in 8x8 tiles: level l is
+ * (E,H,W,ceil(H2/8),W2/8,8,8) fp16 - element (y,x) of a slice at
+ * ((y/8)*(W2/8) + x/8)*64 + (y%8)*8 + x%8, rows past H2 unused - so the 8
+ * window rows of a lookup touch ~3.5 128-B lines instead of 8.  The
+ * layout is internal to this build (CorrBlock(tiled=True) writes it in
+ * add_factors); results are bit-identical to droid_corr_lookup_ce0 on the
+ * reference layout.  Needs W2 % 8 == 0 on every level. */
+int droid_corr_lookup_ce0_tiled(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
+                                const void* w, const float* bias, void* out, int E, int H, int W,
+                                hipStream_t stream);
+
 /* The same lookup + corr_encoder[0] computed WITHOUT the volume: the 4
  * correlation levels are formed on demand on MFMA from a feature pyramid
  * pyr[l] (NF,H_l,W_l,128) fp16 = avgpool^l(fmap/4) (the reference's

@@ -79,3 +79,23 @@ def test_python_layer_rejects_host_tensors():
         droid_backends.corr_index_forward(vol, coords, 3)
     with pytest.raises(RuntimeError, match="contiguous"):
         droid_backends.corr_index_forward(vol.transpose(3, 4), coords, 3)
+
+
+def test_tile8_round_trip_host_only():
+    """corr.tile8 / untile8 (the 8x8-tiled volume layout of
+    droid_corr_lookup_ce0_tiled) on CPU tensors: element (y, x) lands at
+    ((y//8)*(W2//8) + x//8)*64 + (y%8)*8 + x%8 of its slice, padded rows zero."""
+    import torch
+    from droid_mi355x.corr import tile8, untile8
+    for H2, W2 in [(48, 64), (12, 16), (6, 8), (3, 8)]:
+        lv = torch.randn(3, 2, 5, H2, W2).half()
+        t = tile8(lv, chunk=2)
+        H2p = (H2 + 7) // 8 * 8
+        assert t.shape == (3, 2, 5, H2p // 8, W2 // 8, 8, 8)
+        flat = t.reshape(3, 2, 5, -1)
+        for y, x in [(0, 0), (H2 - 1, W2 - 1), (H2 // 2, 3), (min(7, H2 - 1), 7)]:
+            k = ((y // 8) * (W2 // 8) + x // 8) * 64 + (y % 8) * 8 + x % 8
+            assert torch.equal(flat[..., k], lv[..., y, x])
+        if H2p != H2:
+            assert not t.reshape(3, 2, 5, H2p // 8, W2 // 8, 8, 8)[:, :, :, -1, :, H2 % 8:, :].any()
+        assert torch.equal(untile8(t, H2, W2), lv)

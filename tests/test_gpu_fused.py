@@ -257,6 +257,40 @@ def test_corr_lookup_ce0_fused(E, H, W):
     assert torch.equal(out, out2)
 
 
+@pytest.mark.parametrize("E,H,W", [(3, 24, 64), (2, 48, 64), (2, 16, 32)])
+def test_corr_lookup_ce0_tiled_volume_bitexact(E, H, W):
+    """The 8x8-tiled volume (CorrBlock(tiled=True), droid_corr_lookup_ce0_tiled)
+    gives bit-identical outputs to the reference row-major layout, including
+    levels whose H2 is not a multiple of 8 (padded tile rows) and windows that
+    leave the volume; (16, 32) has a W2 = 4 level, so the block stays row-major."""
+    import droid_backends
+    from droid_mi355x.corr import CorrBlock
+    rng = np.random.default_rng(23)
+    f1 = torch.from_numpy(rng.normal(size=(1, E, 128, H, W)).astype(np.float16)).to(DEV)
+    f2 = torch.from_numpy(rng.normal(size=(1, E, 128, H, W)).astype(np.float16)).to(DEV)
+    cb = CorrBlock(f1, f2)
+    cbt = CorrBlock(f1, f2, tiled=True)
+    assert cbt.tiled == all(w % 8 == 0 for _, w in cbt.level_shapes)
+    for a, b in zip(cb.corr_pyramid, cbt.reference_pyramid()):
+        assert torch.equal(a, b)
+    coords = (np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None, None]
+              + rng.normal(0, 6, (1, E, H, W, 2))).astype(np.float32)
+    coords[0, 0, :4] = rng.uniform(-12, max(H, W) + 12, (4, W, 2))   # far outside at every level
+    c = torch.from_numpy(coords).to(DEV).view(E, H, W, 2).contiguous()
+    g = torch.Generator(device=DEV).manual_seed(24)
+    w224 = torch.zeros((128, 224), device=DEV)
+    w224[:, :196] = torch.randn((128, 196), generator=g, device=DEV) / 14.0
+    w224 = w224.half().contiguous()
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    with torch.no_grad():
+        ref = droid_backends.corr_lookup_ce0(cb.corr_pyramid, c, w224, b)
+        out = droid_backends.corr_lookup_ce0(cbt.corr_pyramid, c, w224, b,
+                                             tiled_shapes=cbt.level_shapes if cbt.tiled else None)
+        assert torch.equal(out, ref)
+        # the generic lookups of a tiled block go through the reference layout
+        assert torch.equal(cbt(c.view(1, E, H, W, 2)), cb(c.view(1, E, H, W, 2)))
+
+
 @pytest.mark.parametrize("E,H,W", [(3, 8, 24), (2, 48, 64)])
 def test_gru_global_context(E, H, W):
     """glo = mean_px sigmoid(conv1x1(h) + b) * h (modules/gru.py:24-26) vs torch fp32."""
