@@ -301,7 +301,7 @@ def main():
                        "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                        "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
                        "traffic": load_traffic("corr_lookup", e_local, "corr_pyramid_f16_r3_kernel" if args.reference_op
-                                               else "corr_ce0_kernel"), "launch_ms": lookup_ms,
+                                               else "corr_ce0_kernel<true>"), "launch_ms": lookup_ms,
                        "algorithmic_bytes_per_launch": bytes_per_launch}
         if zr_ms:
             flops = ZR_FLOPS_PER_PIXEL * e_local * (args.ht // 8) * (args.wd // 8)

@@ -499,6 +499,7 @@ namespace droid {
 // ---------------------------------------------------------------------------
 typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
 typedef float floatx4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
 
 struct CorrCe0Args {
   const __half* vol[4];
@@ -655,7 +656,9 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
     }
   };
   // row j of slot sl's window as 8 floats (the taps x = xs .. xs+7)
-  auto row_taps = [&](const int sl, int j, float* t) __attribute__((always_inline)) {
+  // Row j of slot sl's window as fp16 pairs: T[m] = (tap 2m, tap 2m+1) and
+  // S[m] = (tap 2m+1, tap 2m+2) of the taps x = xs .. xs+7 (S[3].x = tap 7).
+  auto row_pairs = [&](const int sl, int j, h2_t* T, h2_t* S) __attribute__((always_inline)) {
     // dword m + k of the two pieces, k = woff / 2 in 0..3, as explicit selects on
     // scalars (a select over an array index becomes a dynamic index into scratch,
     // whose vmcnt waits would drain the window loads still in flight)
@@ -666,11 +669,13 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
     const unsigned v3 = k2 ? p1.y : p0.w, v4 = k2 ? p1.z : p1.x, v5 = k2 ? p1.w : p1.y;
     const unsigned w[5] = {k1 ? v1 : v0, k1 ? v2 : v1, k1 ? v3 : v2, k1 ? v4 : v3, k1 ? v5 : v4};
     const unsigned sh = (woff[sl] & 1) ? 16u : 0u;
+    unsigned o[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) o[m] = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      const unsigned o = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
-      t[2 * m + 0] = __half2float(__ushort_as_half((unsigned short)(o & 0xffffu)));
-      t[2 * m + 1] = __half2float(__ushort_as_half((unsigned short)(o >> 16)));
+      T[m] = __builtin_bit_cast(h2_t, o[m]);
+      S[m] = __builtin_bit_cast(h2_t, __builtin_amdgcn_alignbit(m < 3 ? o[m + 1] : 0u, o[m], 16));
     }
   };
 
@@ -684,29 +689,40 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
   // issued into the same slot) the 1x1 conv on MFMA and the coalesced store
   auto process = [&](const int sl, long t) __attribute__((always_inline)) {
     // (1) bilinear windows of tile t -> As (corr_pyramid_f16_r3_kernel arithmetic)
+    //     on packed fp16 pairs of x offsets (q, q+1).  The reference rounds every
+    //     product and sum of two halves to half through float (at::Half ops);
+    //     a native half op rounds the exact result once, and float carries 24 >=
+    //     2*11 + 2 bits, so the double rounding is innocuous: bit-identical.
+    //     No contraction (an fma would round once where the reference rounds twice).
     {
-      const float w11 = rnd16(wdx[sl] * wdy[sl]);
-      const float w10 = rnd16(wdx[sl] * (1.0f - wdy[sl]));
-      const float w01 = rnd16((1.0f - wdx[sl]) * wdy[sl]);
-      const float w00 = rnd16((1.0f - wdx[sl]) * (1.0f - wdy[sl]));
+#pragma clang fp contract(off)
+      const _Float16 h11 = (_Float16)rnd16(wdx[sl] * wdy[sl]);
+      const _Float16 h10 = (_Float16)rnd16(wdx[sl] * (1.0f - wdy[sl]));
+      const _Float16 h01 = (_Float16)rnd16((1.0f - wdx[sl]) * wdy[sl]);
+      const _Float16 h00 = (_Float16)rnd16((1.0f - wdx[sl]) * (1.0f - wdy[sl]));
+      const h2_t W00 = {h00, h00}, W01 = {h01, h01}, W10 = {h10, h10}, W11 = {h11, h11};
+      const h2_t Z = {(_Float16)0.f, (_Float16)0.f};
       _Float16* arow = As + px * kCeKS + lvl * 49;
-      float prev[8], cur[8];
+      h2_t Tp[4], Sp[4], Tc[4], Sc[4];
+      row_pairs(sl, 0, Tp, Sp);
 #pragma unroll
-      for (int j = 0; j <= 7; ++j) {
-        row_taps(sl, j, cur);
-        if (j > 0) {
-          const int b = j - 1;
+      for (int j = 1; j <= 7; ++j) {
+        row_pairs(sl, j, Tc, Sc);
+        const int b = j - 1;
 #pragma unroll
-          for (int q = 0; q < 7; ++q) {
-            float acc = 0.f + rnd16(prev[q] * w00);
-            acc = rnd16(acc + rnd16(cur[q] * w01));
-            acc = rnd16(acc + rnd16(prev[q + 1] * w10));
-            acc = rnd16(acc + rnd16(cur[q + 1] * w11));
-            arow[q * 7 + b] = (_Float16)__half2float(__float2half(acc));
-          }
+        for (int m = 0; m < 4; ++m) {
+          h2_t acc = Z + Tp[m] * W00;   // (0 + p w00: +0 for a -0 product, as in float)
+          acc = acc + Tc[m] * W01;
+          acc = acc + Sp[m] * W10;
+          acc = acc + Sc[m] * W11;
+          arow[(2 * m) * 7 + b] = acc.x;
+          if (m < 3) arow[(2 * m + 1) * 7 + b] = acc.y;
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) prev[i] = cur[i];
+        for (int m = 0; m < 4; ++m) {
+          Tp[m] = Tc[m];
+          Sp[m] = Sc[m];
+        }
       }
     }
     // (2) the tile two steps ahead goes into this slot while this one is multiplied

@@ -1,7 +1,7 @@
 """Workload for the PMC traffic passes (run under rocprofv3 --pmc; see
 scripts/pmc_traffic.sh): a 1 GiB device copy (calibration of the FETCH/WRITE
 counters on a known byte count), then the C3 ZR gate conv and the C3 4-level
-correlation lookup fused with corr_encoder[0] (corr_lookup_ce0), each launched
+correlation lookup fused with corr_encoder[0] (corr_lookup_ce0 on the 8x8-tiled volume), each launched
 3 times on synthetic data."""
 import os
 import sys
@@ -43,7 +43,7 @@ f = torch.randn((1, nf, 128, H, W), generator=g, device=dev).half()
 rng = np.random.default_rng(0)
 ii = torch.as_tensor(rng.integers(0, nf, E), device=dev)
 jj = torch.as_tensor(rng.integers(0, nf, E), device=dev)
-cb = CorrBlock(f[:, ii], f[:, jj])
+cb = CorrBlock(f[:, ii], f[:, jj], tiled=True)   # the layout FactorGraph builds for the fused operator
 coords = torch.stack(torch.meshgrid(torch.arange(W, device=dev), torch.arange(H, device=dev), indexing="xy"), -1)
 coords = (coords[None, None].float() + torch.randn((1, E, H, W, 2), generator=g, device=dev) * 3).contiguous()
 w224 = (torch.randn((128, 224), generator=g, device=dev) * 0.05).half()
@@ -51,6 +51,6 @@ b128 = torch.zeros(128, device=dev)
 c = coords.view(E, H, W, 2).contiguous()
 with torch.no_grad():
     for _ in range(3):
-        droid_backends.corr_lookup_ce0(cb.corr_pyramid, c, w224, b128)
+        droid_backends.corr_lookup_ce0(cb.corr_pyramid, c, w224, b128, tiled_shapes=cb.level_shapes)
 torch.cuda.synchronize()
 print("ok")
