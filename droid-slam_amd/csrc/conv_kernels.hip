@@ -1024,7 +1024,21 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
   }
 }
 
-template <int TMX, int TN, bool DWHEAD>
+// one MFMA then one LDS read, R times (sched_group_barrier sequence)
+template <int R>
+struct MfmaReadPairs {
+  static __device__ __forceinline__ void emit() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    MfmaReadPairs<R - 1>::emit();
+  }
+};
+template <>
+struct MfmaReadPairs<0> {
+  static __device__ __forceinline__ void emit() {}
+};
+
+template <int TMX, int TN, bool DWHEAD, bool ILV>
 __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   using BP = Band<TMX, TN>;
   constexpr int FM = BP::FM, FN = BP::FN, WN = BP::WN, NBI = BP::NBI;
@@ -1140,19 +1154,49 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
       if (st + 1 < nst) issue_b(st + 1);
       if (t == 0 && ch + 1 < nch) issue_halo(ch + 1);
       const char* Bb = Bl + (st & 1) * TN * 128;
+      if constexpr (ILV) {
+        // all fragments of the stage read up front (A0, B0..B7 first, so the
+        // first MFMA waits for two reads only); the K-half-1 reads interleave
+        // one per MFMA with the K-half-0 multiplies (sched_group_barrier), so
+        // they land long before their use and the MFMA pipe is not paced by
+        // the LDS latency
+        __builtin_amdgcn_sched_barrier(0);
+        half8 af[2][FM], bf[2][FN];
 #pragma unroll
-      for (int hk = 0; hk < 2; ++hk) {
-        const char* ap = Hb + abase[tx + 1][hk] + ty * rowb;
-        half8 af[FM], bf[FN];
+        for (int hk = 0; hk < 2; ++hk) {
+          const char* ap = Hb + abase[tx + 1][hk] + ty * rowb;
+          af[hk][0] = *reinterpret_cast<const half8*>(ap);
 #pragma unroll
-        for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const half8*>(ap + i * 8192);
+          for (int j = 0; j < FN; ++j) bf[hk][j] = *reinterpret_cast<const half8*>(Bb + bbase[hk] + j * 2048);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const half8*>(Bb + bbase[hk] + j * 2048);
+          for (int i = 1; i < FM; ++i) af[hk][i] = *reinterpret_cast<const half8*>(ap + i * 8192);
+        }
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+        for (int hk = 0; hk < 2; ++hk)
 #pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[hk][i], bf[hk][j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, FM + FN, 0);
+        MfmaReadPairs<FM + FN>::emit();
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * FM * FN - (FM + FN), 0);
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+#pragma unroll
+        for (int hk = 0; hk < 2; ++hk) {
+          const char* ap = Hb + abase[tx + 1][hk] + ty * rowb;
+          half8 af[FM], bf[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const half8*>(ap + i * 8192);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const half8*>(Bb + bbase[hk] + j * 2048);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
       }
     }
   }
@@ -1162,6 +1206,15 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   } else {
     band_epilogue<TMX, TN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid);
   }
+}
+
+// DROID_CONV_ILV=0 selects the compiler-scheduled stage body (A/B runs)
+static bool band_interleaved() {
+  static const bool on = [] {
+    const char* e = getenv("DROID_CONV_ILV");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 template <int TMX, int TN>
@@ -1190,13 +1243,22 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
   if (lds > kLdsMax) return fail(kUnsupported, "conv band: LDS");
   static bool attr = false;
   if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN, DWHEAD>),
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN, DWHEAD, false>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    if constexpr (TN != 256)
+      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN, DWHEAD, true>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     attr = true;
   }
   const long nwg = a.m_tiles * a.n_tiles;
   if (nwg > 0x7fffffffL) return fail(kUnsupported, "conv_nhwc_f16: problem too large");
-  conv_band_kernel<TMX, TN, DWHEAD><<<dim3((unsigned)nwg), 512, lds, stream>>>(a);
+  // interleaved stage body: +2-5 % on the 384-row tiles; the 256x256 tile has
+  // no registers for it (it spills), so it keeps the compiler's schedule
+  bool ilv = false;
+  if constexpr (TN != 256) ilv = band_interleaved();
+  if constexpr (TN != 256)
+    if (ilv) conv_band_kernel<TMX, TN, DWHEAD, true><<<dim3((unsigned)nwg), 512, lds, stream>>>(a);
+  if (!ilv) conv_band_kernel<TMX, TN, DWHEAD, false><<<dim3((unsigned)nwg), 512, lds, stream>>>(a);
   DROID_LAUNCH_CHECK();
   return kOk;
 }
