@@ -37,6 +37,10 @@
 #include "lds_dma.hpp"
 #include <algorithm>
 
+#ifndef DROID_CONV_PROFILE
+#define DROID_CONV_PROFILE 0
+#endif
+
 namespace droid {
 
 
@@ -78,6 +82,7 @@ struct ConvArgs {
   int nslot;  // band pixels ((TMX/W + 2) * W)
   int nhi;    // halo DMA instructions per wave per chunk
   const __half* hw;  // EPI_DWHEAD: head weights [48][256] (row = tap*4 + out channel)
+  long long* prof;   // band kernel timeline (droid_conv_set_profile): 4 stamps per workgroup, or null
 };
 
 constexpr int TM = 128, BK = 64;
@@ -872,14 +877,26 @@ __device__ __forceinline__ int frag_row(int wm, int i) {
   return CONTIG ? wm * FM * 16 + 16 * i : 16 * (wm + WM * i);
 }
 
-template <int TMX, int TN, int FM, int FN, int WM = 4, bool CONTIG = false, int NT = 512>
+// The epilogue type is a template parameter (EPI < 0: runtime a.epi, for the
+// kernels that still dispatch at run time): with a runtime switch every one of
+// the FM*FN*4 unrolled elements carried a 3-way branch and tanhf's divergent
+// range reduction, ~50 KB of straight-line code fetched cold once per tile
+// (the timeline measured 20k clocks per 384x128 epilogue).
+__device__ __forceinline__ float tanh_fast(float x) {
+  // 1 - 2 / (1 + e^(2x)): branch-free, saturates to +-1; abs error ~1e-7, far
+  // below the fp16 rounding of the gate that follows
+  return 1.0f - 2.0f / (1.0f + __expf(2.0f * x));
+}
+
+template <int TMX, int TN, int FM, int FN, int WM = 4, bool CONTIG = false, int NT = 512, int EPI = -1>
 __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
                                               int n0, int wm, int wn, int lane, int tid) {
   constexpr int ER = TN + 8, PPR = TN / 8;
   const int HW = a.H * a.W;
   const int b = (int)(m0 / HW);  // a tile never straddles two images
   const int fr = lane & 15, fq = lane >> 4;
-  const int epi = a.epi;
+  const int epi = EPI >= 0 ? EPI : a.epi;
+  const bool relu = a.act == 1;
   __syncthreads();  // main-loop LDS reads are done
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
@@ -894,14 +911,20 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
         const int r = frag_row<FM, WM, CONTIG>(wm, i) + fq * 4 + k;
         const float v = acc[i][j][k] + bv;
         float o;
-        if (epi == EPI_GRU_ZR) o = sigmoidf_(v);
+        if constexpr (EPI == EPI_GRU_ZR) o = sigmoidf_(v);
+        else if constexpr (EPI == EPI_GRU_Q) o = tanh_fast(v);
+        else if constexpr (EPI == EPI_ACT) o = relu ? fmaxf(v, 0.f) : v;
+        else if (epi == EPI_GRU_ZR) o = sigmoidf_(v);
         else if (epi == EPI_GRU_Q) o = tanhf(v);
         else o = (a.act == 1) ? fmaxf(v, 0.f) : v;
         smem[r * ER + c] = (_Float16)o;
       }
   }
   __syncthreads();
-  for (int idx = tid; idx < TMX * PPR; idx += NT) {
+  static_assert((TMX * PPR) % NT == 0, "band epilogue: whole store rounds");
+#pragma unroll  // all rounds' LDS reads (and h / z loads) in flight together
+  for (int q = 0; q < TMX * PPR / NT; ++q) {
+    const int idx = tid + q * NT;
     const int r = idx / PPR, p = idx - r * PPR;
     const long m = m0 + r;
     const int c = n0 + p * 8;
@@ -1038,7 +1061,7 @@ struct MfmaReadPairs<0> {
   static __device__ __forceinline__ void emit() {}
 };
 
-template <int TMX, int TN, bool DWHEAD, bool ILV>
+template <int TMX, int TN, bool DWHEAD, bool ILV, int EPI>
 __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   using BP = Band<TMX, TN>;
   constexpr int FM = BP::FM, FN = BP::FN, WN = BP::WN, NBI = BP::NBI;
@@ -1138,8 +1161,25 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   const int nst = a.nstage;  // nch * 9
   const int rowb = W * 128;
 
+  // timeline (profiling builds of the call only): s_memtime at entry, loop
+  // start (first stage's operands landed), loop end and exit, plus the CU id
+#if DROID_CONV_PROFILE
+  long long* const prof = a.prof ? a.prof + 6 * blockIdx.x : nullptr;
+#else
+  long long* const prof = nullptr;  // the hooks cost the 256x256 tile registers: profiling builds only
+#endif
+  if (prof && tid == 0) {
+    const unsigned hwid = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));   // HW_REG_XCC_ID
+    prof[0] = (long long)hwid | ((long long)(xcc & 15) << 32);
+    prof[1] = (long long)__builtin_amdgcn_s_memtime();
+  }
   issue_halo(0);
   issue_b(0);
+  if (prof) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) prof[2] = (long long)__builtin_amdgcn_s_memtime();
+  }
   int st = 0;
   for (int ch = 0; ch < nch; ++ch) {
     const char* Hb = Hl + (ch & 1) * hbytes;
@@ -1200,11 +1240,17 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
       }
     }
   }
+  if (prof && tid == 0) prof[3] = (long long)__builtin_amdgcn_s_memtime();
   if constexpr (DWHEAD) {
     static_assert(TMX == 256 && TN == 256, "dw/head fusion runs on the 256x256 tile");
     dwhead_epilogue<FM, FN>(a, acc, smem, m0, wm, wn, lane, tid);
   } else {
-    band_epilogue<TMX, TN, FM, FN>(a, acc, smem, m0, n0, wm, wn, lane, tid);
+    band_epilogue<TMX, TN, FM, FN, 4, false, 512, EPI>(a, acc, smem, m0, n0, wm, wn, lane, tid);
+  }
+  if (prof) {
+    if (tid == 0) prof[4] = (long long)__builtin_amdgcn_s_memtime();  // stores issued
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) prof[5] = (long long)__builtin_amdgcn_s_memtime();  // stores drained
   }
 }
 
@@ -1230,6 +1276,18 @@ static bool band_fits(int W, int* nslot, int* nhi) {
   return true;
 }
 
+template <int TMX, int TN, bool DWHEAD, bool ILV, int EPI>
+static int launch_band_kernel(const ConvArgs& a, long nwg, int lds, hipStream_t stream) {
+  static bool attr = false;  // one per instantiation
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN, DWHEAD, ILV, EPI>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    attr = true;
+  }
+  conv_band_kernel<TMX, TN, DWHEAD, ILV, EPI><<<dim3((unsigned)nwg), 512, lds, stream>>>(a);
+  return kOk;
+}
+
 template <int TMX, int TN, bool DWHEAD = false>
 static int launch_band(const ConvArgs& a0, hipStream_t stream) {
   ConvArgs a = a0;
@@ -1241,24 +1299,31 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
   const int epi_b = TMX * (TN + 8) * 2 + (DWHEAD ? 48 * 264 * 2 : 0);
   const int lds = main_b > epi_b ? main_b : epi_b;
   if (lds > kLdsMax) return fail(kUnsupported, "conv band: LDS");
-  static bool attr = false;
-  if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN, DWHEAD, false>),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-    if constexpr (TN != 256)
-      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN, DWHEAD, true>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-    attr = true;
-  }
   const long nwg = a.m_tiles * a.n_tiles;
   if (nwg > 0x7fffffffL) return fail(kUnsupported, "conv_nhwc_f16: problem too large");
   // interleaved stage body: +2-5 % on the 384-row tiles; the 256x256 tile has
   // no registers for it (it spills), so it keeps the compiler's schedule
   bool ilv = false;
   if constexpr (TN != 256) ilv = band_interleaved();
-  if constexpr (TN != 256)
-    if (ilv) conv_band_kernel<TMX, TN, DWHEAD, true><<<dim3((unsigned)nwg), 512, lds, stream>>>(a);
-  if (!ilv) conv_band_kernel<TMX, TN, DWHEAD, false><<<dim3((unsigned)nwg), 512, lds, stream>>>(a);
+  int st = kOk;
+  if constexpr (DWHEAD) {
+    st = launch_band_kernel<TMX, TN, true, false, EPI_DWHEAD>(a, nwg, lds, stream);
+  } else {
+    const int epi = a.epi == EPI_GRU_ZR ? EPI_GRU_ZR : a.epi == EPI_GRU_Q ? EPI_GRU_Q : EPI_ACT;
+    if constexpr (TN != 256) {
+      if (ilv) {
+        if (epi == EPI_GRU_ZR) st = launch_band_kernel<TMX, TN, false, true, EPI_GRU_ZR>(a, nwg, lds, stream);
+        else if (epi == EPI_GRU_Q) st = launch_band_kernel<TMX, TN, false, true, EPI_GRU_Q>(a, nwg, lds, stream);
+        else st = launch_band_kernel<TMX, TN, false, true, EPI_ACT>(a, nwg, lds, stream);
+      }
+    }
+    if (!ilv) {
+      if (epi == EPI_GRU_ZR) st = launch_band_kernel<TMX, TN, false, false, EPI_GRU_ZR>(a, nwg, lds, stream);
+      else if (epi == EPI_GRU_Q) st = launch_band_kernel<TMX, TN, false, false, EPI_GRU_Q>(a, nwg, lds, stream);
+      else st = launch_band_kernel<TMX, TN, false, false, EPI_ACT>(a, nwg, lds, stream);
+    }
+  }
+  if (st != kOk) return st;
   DROID_LAUNCH_CHECK();
   return kOk;
 }
@@ -1506,6 +1571,23 @@ extern "C" {
 //   otherwise CHUNKED, nstage = ks*ks * sum_s ceil(C_s/64), stage = (source, 64-ch chunk, tap).
 // epi: 0 act (act 0 none / 1 relu) -> out fp16 NHWC slice; 1 GRU z|r; 2 GRU q;
 // 3 head (fp32 out32, sigmoid on co >= 2); 4 GRU global mean (atomic fp32 out32, zeroed by caller).
+static long long* g_conv_prof = nullptr;
+
+// Timeline of the next band-kernel launches (debug/profiling): buf receives 6
+// int64 per workgroup (hardware id, s_memtime at entry / loop start / loop end /
+// epilogue stores issued / stores drained); null turns it off.  Only the profiling build (make prof ->
+// lib/prof/libdroid_hip.so, -DDROID_CONV_PROFILE=1) writes them; the regular
+// library reports DROID_UNSUPPORTED.  Not thread-safe by design.
+int droid_conv_set_profile(void* buf) {
+#if DROID_CONV_PROFILE
+  g_conv_prof = static_cast<long long*>(buf);
+  return droid::kOk;
+#else
+  (void)buf;
+  return droid::fail(droid::kUnsupported, "conv_set_profile: build with make prof (DROID_CONV_PROFILE=1)");
+#endif
+}
+
 int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc,
                         const void* wp, const float* bias, const float* bbias, int B, int H, int W,
                         int Cout, int ks, int act, int epi, void* out, int out_cstride, int out_coff,
@@ -1519,6 +1601,7 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
   if (epi == EPI_GLO && (H * W) % TM != 0)
     return fail(kUnsupported, "conv_nhwc_f16: global-context epilogue needs H*W % 128 == 0");
   ConvArgs a{};
+  a.prof = g_conv_prof;
   int chunks = 0;
   for (int s = 0; s < nsrc; ++s) {
     if (C[s] % 8 || cstride[s] % 8 || cstride[s] < C[s] || (reinterpret_cast<uintptr_t>(srcs[s]) & 15))

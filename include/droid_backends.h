@@ -64,6 +64,15 @@ int droid_corr_pyramid_lookup_nhwc(const void* const* levels, const int* H2s, co
                                    int num_levels, const float* coords, void* out, int out_cstride,
                                    int E, int H, int W, hipStream_t stream);
 
+/* Profiling switch for the band convolution kernel (profiling build only,
+ * `make prof`; the regular library returns DROID_UNSUPPORTED): while buf is
+ * set, each launch writes 6 int64 per workgroup (hardware id | XCC id << 32,
+ * s_memtime at entry, when the first stage's operands have landed, at the end
+ * of the main loop, when the epilogue's stores are issued and when they have
+ * drained).  buf = null switches it off.  Not part of the reference interface
+ * (scripts/conv_timeline.py). */
+int droid_conv_set_profile(void* buf);
+
 /* CorrBlock lookup fused with the update operator's corr_encoder[0]
  * (modules/corr.py:40-50 + droid_net.py:84-86): out (E,H,W,128) fp16 =
  * relu(conv1x1(lookup(coords), w) + bias), the 196-channel lookup never

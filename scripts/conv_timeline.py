@@ -1,0 +1,76 @@
+"""Per-workgroup timeline of the band conv kernel (droid_conv_set_profile):
+prologue (entry -> first stage's operands landed), main loop, epilogue, and the
+gap between consecutive workgroups on the same CU, in shader clocks.
+
+usage: python scripts/conv_timeline.py [edges] [zr|q|ce2|dw]
+(runs on the profiling build: make -C droid-slam_amd/csrc prof)"""
+import os
+import sys
+
+_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "droid-slam_amd", "lib", "prof", "libdroid_hip.so")
+os.environ.setdefault("DROID_HIP_LIB", _LIB)
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "droid-slam_amd"))
+import ctypes
+
+import numpy as np
+import torch
+
+import droid_backends
+from droid_backends._lib import lib
+from droid_mi355x.fused import pack_conv
+
+E = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+which = sys.argv[2] if len(sys.argv) > 2 else "zr"
+H, W = 48, 64
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev).manual_seed(0)
+t = lambda c: (torch.randn((E, H, W, c), generator=g, device=dev) * 0.5).half()
+net, inp, cf, ff = t(128), t(128), t(128), t(64)
+srcs4 = [(net, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)]
+cfg = {"zr": (srcs4, 256), "q": (srcs4, 128), "ce2": ([(net, 0, 128)], 128), "dw": ([(net, 0, 128)], 256)}[which]
+srcs, cout = cfg
+cin = sum(c for _, _, c in srcs)
+w = torch.randn((cout, cin, 3, 3), generator=g, device=dev) * 0.02
+wp = pack_conv(w, [c for _, _, c in srcs])
+bias = torch.zeros(cout, device=dev)
+out = torch.empty((E, H, W, cout), dtype=torch.float16, device=dev)
+run = lambda: droid_backends.conv_nhwc_f16(srcs, wp, cout, 3, bias=bias, act=1, out=out)
+for _ in range(3):
+    run()
+torch.cuda.synchronize()
+tile = {256: 256, 128: 384}[cout]
+nwg = E * H * W // tile
+prof = torch.zeros(nwg * 6, dtype=torch.int64, device=dev)
+lib.droid_conv_set_profile(ctypes.c_void_p(prof.data_ptr()))
+s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+s.record()
+run()
+e.record()
+torch.cuda.synchronize()
+lib.droid_conv_set_profile(None)
+ms = s.elapsed_time(e)
+p = prof.view(nwg, 6).cpu().numpy()
+assert (p[:, 1] > 0).all(), "profile not written (kernel not the band kernel?)"
+hw = p[:, 0]
+cu = ((hw >> 32) & 15) * 256 + ((hw >> 8) & 0xff)   # XCC id, then SE_ID[15:13] | SH_ID[12] | CU_ID[11:8]
+pro, loop, epi, drain = p[:, 2] - p[:, 1], p[:, 3] - p[:, 2], p[:, 4] - p[:, 3], p[:, 5] - p[:, 4]
+gaps = []
+for c in np.unique(cu):
+    q = p[cu == c]
+    q = q[np.argsort(q[:, 1])]
+    gaps.extend((q[1:, 1] - q[:-1, 5]).tolist())
+gaps = np.asarray(gaps)
+tot = pro + loop + epi + drain
+span_clk = np.median(tot) * nwg / len(np.unique(cu)) + np.median(gaps) * (nwg / len(np.unique(cu)) - 1)
+print("%s: %d edges, %d workgroups on %d CUs, %.3f ms (HIP events)" % (which, E, nwg, len(np.unique(cu)), ms))
+for name, v in (("prologue", pro), ("main loop", loop), ("epilogue issue", epi), ("store drain", drain),
+                ("gap to next WG", gaps)):
+    print("  %-15s median %8.0f clk  mean %8.0f  p90 %8.0f  (%.1f %% of a WG's median cycle)"
+          % (name, np.median(v), v.mean(), np.percentile(v, 90), 100 * np.median(v) / (np.median(tot) + np.median(gaps))))
+stages = (cin // 64 if cin % 64 == 0 else cin // 64 + 1) * 9
+tn = 256 if cout == 256 else 128
+floor = 64 * (tile // 64) * (tn // 32)   # 2 waves/SIMD x 2*FM*FN MFMAs x 16 clk
+print("  main loop per stage: %.0f clk (%d stages); MFMA-only floor %d clk/stage" % (np.median(loop) / stages, stages,
+                                                                                     floor))
+print("  implied clock: %.2f GHz (median WG cycle x WGs per CU / kernel time)" % (span_clk / (ms * 1e-3) / 1e9))
