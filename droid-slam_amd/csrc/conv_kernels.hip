@@ -40,6 +40,12 @@
 #ifndef DROID_CONV_PROFILE
 #define DROID_CONV_PROFILE 0
 #endif
+#ifndef DROID_CONV_ABLATE
+#define DROID_CONV_ABLATE 0
+#endif
+#if DROID_CONV_ABLATE && !DROID_CONV_PROFILE
+#error "DROID_CONV_ABLATE is for profiling builds only"
+#endif
 
 namespace droid {
 
@@ -1188,11 +1194,16 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
       const int ty = t / 3 - 1, tx = t % 3 - 1;
       // this stage's weights (and at t == 0 this chunk's band) must have landed;
       // at t == 1 the next chunk's band (issued after them) may stay in flight
-      wait_vmcnt((t == 1 && ch + 1 < nch) ? nhi : 0);
+      if (!(DROID_CONV_ABLATE & 4) || st == 0) wait_vmcnt((t == 1 && ch + 1 < nch) ? nhi : 0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (st + 1 < nst) issue_b(st + 1);
-      if (t == 0 && ch + 1 < nch) issue_halo(ch + 1);
+      // DROID_CONV_ABLATE (profiling experiments only, results invalid):
+      // bit 0 drops the stage barrier, bit 1 the DMA after the first stage,
+      // bit 2 the DMA waits after the first stage
+      if (!(DROID_CONV_ABLATE & 1)) __builtin_amdgcn_s_barrier();
+      if (!(DROID_CONV_ABLATE & 2) || st == 0) {
+        if (st + 1 < nst) issue_b(st + 1);
+        if (t == 0 && ch + 1 < nch) issue_halo(ch + 1);
+      }
       const char* Bb = Bl + (st & 1) * TN * 128;
       if constexpr (ILV) {
         // all fragments of the stage read up front (A0, B0..B7 first, so the
