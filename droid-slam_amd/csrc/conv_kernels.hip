@@ -896,7 +896,8 @@ __device__ __forceinline__ float tanh_fast(float x) {
 
 template <int TMX, int TN, int FM, int FN, int WM = 4, bool CONTIG = false, int NT = 512, int EPI = -1>
 __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
-                                              int n0, int wm, int wn, int lane, int tid) {
+                                              int n0, int wm, int wn, int lane, int tid,
+                                              const float* bpre = nullptr) {
   constexpr int ER = TN + 8, PPR = TN / 8;
   const int HW = a.H * a.W;
   const int b = (int)(m0 / HW);  // a tile never straddles two images
@@ -908,8 +909,13 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
   for (int j = 0; j < FN; ++j) {
     const int c = wn * FN * 16 + j * 16 + fr;
     const int co = n0 + c;
-    float bv = a.bias ? a.bias[co] : 0.f;
-    if (a.bbias) bv += a.bbias[(long)b * a.Cout + co];
+    float bv;
+    if (bpre) {
+      bv = bpre[j];  // loaded before the main loop
+    } else {
+      bv = a.bias ? a.bias[co] : 0.f;
+      if (a.bbias) bv += a.bbias[(long)b * a.Cout + co];
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -1182,6 +1188,21 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   }
   issue_halo(0);
   issue_b(0);
+  // the epilogue's bias (+ per-image bias) of this lane's columns, loaded now so
+  // the latency hides under the main loop (the 256-wide tile has no registers
+  // to spare: it loads them in the epilogue)
+  constexpr bool kPreBias = TN != 256 && !DWHEAD;
+  float bpre[kPreBias ? FN : 1];
+  if constexpr (kPreBias) {
+    const int bimg = (int)(m0 / HW);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int co = n0 + wn * FN * 16 + j * 16 + (lane & 15);
+      float bv = a.bias ? a.bias[co] : 0.f;
+      if (a.bbias) bv += a.bbias[(long)bimg * a.Cout + co];
+      bpre[j] = bv;
+    }
+  }
   if (prof) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tid == 0) prof[2] = (long long)__builtin_amdgcn_s_memtime();
@@ -1256,7 +1277,8 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
     static_assert(TMX == 256 && TN == 256, "dw/head fusion runs on the 256x256 tile");
     dwhead_epilogue<FM, FN>(a, acc, smem, m0, wm, wn, lane, tid);
   } else {
-    band_epilogue<TMX, TN, FM, FN, 4, false, 512, EPI>(a, acc, smem, m0, n0, wm, wn, lane, tid);
+    band_epilogue<TMX, TN, FM, FN, 4, false, 512, EPI>(a, acc, smem, m0, n0, wm, wn, lane, tid,
+                                                      kPreBias ? bpre : nullptr);
   }
   if (prof) {
     if (tid == 0) prof[4] = (long long)__builtin_amdgcn_s_memtime();  // stores issued
