@@ -932,10 +932,31 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
         smem[r * ER + c] = (_Float16)o;
       }
   }
-  __syncthreads();
   static_assert((TMX * PPR) % NT == 0, "band epilogue: whole store rounds");
-#pragma unroll  // all rounds' LDS reads (and h / z loads) in flight together
-  for (int q = 0; q < TMX * PPR / NT; ++q) {
+  constexpr int RND = TMX * PPR / NT;
+  // GRU epilogues: every round's h (and z) pieces are loaded here, all in flight
+  // together while the staging barrier waits (issued inside the store loop they
+  // were serialised behind the previous round's store: one HBM latency per round)
+  constexpr bool kPreH = EPI == EPI_GRU_ZR || EPI == EPI_GRU_Q;
+  half8 hpre[kPreH ? RND : 1], zpre[EPI == EPI_GRU_Q ? RND : 1];
+  if constexpr (kPreH) {
+#pragma unroll
+    for (int q = 0; q < RND; ++q) {
+      const int idx = tid + q * NT;
+      const int r = idx / PPR, p = idx - r * PPR;
+      const long m = m0 + r;
+      const int c = n0 + p * 8;
+      if constexpr (EPI == EPI_GRU_Q) {
+        hpre[q] = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c);
+        zpre[q] = *reinterpret_cast<const half8*>(a.z + m * a.z_cstride + c);
+      } else if (c >= a.gru_ch) {
+        hpre[q] = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c - a.gru_ch);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll  // all rounds' LDS reads in flight together
+  for (int q = 0; q < RND; ++q) {
     const int idx = tid + q * NT;
     const int r = idx / PPR, p = idx - r * PPR;
     const long m = m0 + r;
@@ -943,7 +964,9 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
     half8 v = *reinterpret_cast<const half8*>(&smem[r * ER + p * 8]);
     if (epi == EPI_GRU_ZR) {
       if (c >= a.gru_ch) {
-        const half8 h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c - a.gru_ch);
+        half8 h;
+        if constexpr (kPreH) h = hpre[q];
+        else h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c - a.gru_ch);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = (_Float16)((float)v[e] * (float)h[e]);
         *reinterpret_cast<half8*>(a.rnet + m * a.gru_ch + c - a.gru_ch) = v;
@@ -951,8 +974,14 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
         *reinterpret_cast<half8*>(a.zout + m * a.gru_ch + c) = v;
       }
     } else if (epi == EPI_GRU_Q) {
-      const half8 h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c);
-      const half8 z = *reinterpret_cast<const half8*>(a.z + m * a.z_cstride + c);
+      half8 h, z;
+      if constexpr (EPI == EPI_GRU_Q) {
+        h = hpre[q];
+        z = zpre[q];
+      } else {
+        h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c);
+        z = *reinterpret_cast<const half8*>(a.z + m * a.z_cstride + c);
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float zv = (float)z[e];
@@ -1365,30 +1394,35 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
 // ConvGRU global context (modules/gru.py:19-32, the glo branch):
 //   glo[e][co] = mean over the edge's pixels of sigmoid(w . h + b)[co] * h[co]
 // for a 1x1 128 -> 128 conv w on the hidden state h itself.  One workgroup per
-// edge streams its pixels in 64-pixel tiles (LDS-DMA, double buffered) against
-// the resident weights; wave w owns output columns 32w .. 32w+31 for every
-// pixel, so the per-column sums stay in registers and the mean is a plain
-// store - no atomics, deterministic.
+// edge streams its pixels in 64-pixel tiles by LDS-DMA through a ring of 4
+// tile buffers, three tiles in flight (one in flight left the kernel latency
+// bound at ~2.5 TB/s); wave w keeps the weight fragments of its output columns
+// 32w .. 32w+31 in registers (32 VGPRs), so the LDS holds only the ring and two
+// workgroups share a CU.  The per-column sums stay in registers and the mean
+// is a plain store - no atomics, deterministic.
 constexpr int kGloTP = 64;
-constexpr int kGloLds = 2 * 128 * 128 + 2 * 2 * kGloTP * 128;  // weights + 2 A tiles (bytes)
+constexpr int kGloRing = 4;
+constexpr int kGloLds = kGloRing * 2 * kGloTP * 128;  // the tile ring (bytes)
 
 __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__ h, const __half* __restrict__ w,
                                                       const float* __restrict__ bias, float* __restrict__ glo,
                                                       int HW) {
   extern __shared__ __attribute__((aligned(16))) _Float16 smem_glo[];
   char* lds = reinterpret_cast<char*>(smem_glo);
-  char* Wl = lds;                     // [2 k-chunks][128 co][128 B]
-  char* Al = lds + 2 * 128 * 128;     // [2 buf][2 k-chunks][64 px][128 B]
+  char* Al = lds;                     // [kGloRing buf][2 k-chunks][64 px][128 B]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int e = blockIdx.x;
   const int fr = lane & 15, fq = lane >> 4;
   const int ntile = HW / kGloTP;
-  // weights -> LDS (swizzled 16-B slots)
-  for (int idx = tid; idx < 128 * 16; idx += 256) {
-    const int co = idx >> 4, q = idx & 15, c = q >> 3, piece = q & 7;
-    *reinterpret_cast<uint4*>(Wl + c * 16384 + co * 128 + ((piece ^ (co & 7)) << 4)) =
-        *reinterpret_cast<const uint4*>(w + co * 128 + c * 64 + piece * 8);
-  }
+  // this wave's weight fragments (B operand of K-step ks, column block j)
+  half8 wf[4][2];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int co = wave * 32 + j * 16 + fr, k = (ks >> 1) * 64 + ((ks & 1) * 4 + fq) * 8;
+      wf[ks][j] = *reinterpret_cast<const half8*>(w + co * 128 + k);
+    }
   const __half* he = h + (long)e * HW * 128;
   const rsrc_t rs = make_rsrc(he, (unsigned)HW * 256);
   const unsigned Al_a = lds_addr(Al);
@@ -1401,20 +1435,27 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
     for (int i = 0; i < 4; ++i) {
       const int q = wave_u + 4 * i, c = q & 1, pr = (q >> 1) * 8;
       const unsigned off = (unsigned)(((t * kGloTP + pr + lrow) * 128 + c * 64 + lpiece * 8) * 2);
-      dma16(rs, Al_a + (t & 1) * 16384 + c * 8192 + pr * 128, off);
+      dma16(rs, Al_a + (t % kGloRing) * 16384 + c * 8192 + pr * 128, off);
     }
   };
   float bj[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bj[j] = bias[wave * 32 + j * 16 + fr];
   float colsum[2] = {0.f, 0.f};
-  issue(0);
+  // the weight and bias loads land before the ring starts (the counted vmcnt
+  // waits below assume only DMAs are outstanding)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int t = 0; t < kGloRing - 1 && t < ntile; ++t) issue(t);
   for (int t = 0; t < ntile; ++t) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // tile t landed: each later tile in flight is 4 DMA instructions of this wave
+    const int later = min(kGloRing - 2, ntile - 1 - t);
+    if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // tile t landed (all waves); tile t-1's reads done
-    if (t + 1 < ntile) issue(t + 1);
-    const char* At = Al + (t & 1) * 16384;
+    if (t + kGloRing - 1 < ntile) issue(t + kGloRing - 1);  // into tile t-1's buffer
+    const char* At = Al + (t % kGloRing) * 16384;
     floatx4 acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1423,21 +1464,17 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int c = ks >> 1, kq = (ks & 1) * 4 + fq;
-      half8 af[4], bf[2];
+      half8 af[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = i * 16 + fr;
         af[i] = *reinterpret_cast<const half8*>(At + c * 8192 + r * 128 + ((kq ^ (r & 7)) << 4));
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int co = wave * 32 + j * 16 + fr;
-        bf[j] = *reinterpret_cast<const half8*>(Wl + c * 16384 + co * 128 + ((kq ^ (co & 7)) << 4));
-      }
-#pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], wf[ks][j], acc[i][j], 0, 0, 0);
     }
     // sigmoid(. + b) * h summed over the tile's pixels (h = the tile itself: k == co)
 #pragma unroll
@@ -1469,30 +1506,40 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
 // autocast).  Persistent: one 8-wave workgroup per CU keeps the packed weights
 // (K = 52 taps x 8 channels, 4 real) in LDS and walks 128-pixel tiles; a tile's
 // input band (its rows +-3, fp16, 8 channels per pixel with zero padding) is a
-// few KB of LDS, built from registers loaded during the previous tile.  A K-step
-// of 32 = 4 taps x 8 channels, so each A fragment is one 16-B LDS read.
-constexpr int kFeTP = 128, kFeK = 416, kFeKS = kFeK + 8, kFeOS = 136;
+// few KB of LDS, built from registers loaded during the previous tile.  The
+// band holds 4 channels per pixel (8 B), so the 8 K values of an A fragment are
+// two horizontally adjacent taps x 4 channels - two neighbouring band pixels,
+// one 16-B LDS piece: a K-step of 32 is one kernel row (4 tap pairs, the
+// eighth tap of the row has zero weights) and the 7x7 conv takes 7 K-steps,
+// not the 13 of the 8-channel packing (half of whose K was zero padding).
+// The weights keep the ABI layout w[co][tap*8 + c] (K = 52 x 8) and are
+// re-packed to [co][7 rows x 4 pairs x 8] while staged into LDS.
+constexpr int kFeTP = 128, kFeK = 416, kFeK2 = 224, kFeKS = kFeK2 + 8, kFeOS = 136;
 
 __host__ __device__ constexpr int fe_lds_bytes(int W) {
-  return 128 * kFeKS * 2 + (kFeTP / W + 6) * (W + 6) * 16 + kFeTP * kFeOS * 2;
+  return 128 * kFeKS * 2 + (kFeTP / W + 6) * (W + 8) * 8 + kFeTP * kFeOS * 2;
 }
 
 __global__ void __launch_bounds__(512) flow_enc0_kernel(const float* __restrict__ motn, const __half* __restrict__ w,
                                                         const float* __restrict__ bias, __half* __restrict__ out,
                                                         int H, int W, long ntiles) {
   extern __shared__ __attribute__((aligned(16))) _Float16 smem_fe[];
-  const int RB = kFeTP / W + 6, PW = W + 6;  // band rows, padded row length (pixels)
-  _Float16* Ws = smem_fe;                    // [128][kFeKS]
-  _Float16* In = Ws + 128 * kFeKS;           // [RB][PW][8]
-  _Float16* Os = In + RB * PW * 8;           // [128][kFeOS]
+  // band rows; padded row length: 3 columns left, 5 right (the pair (6, 7) of
+  // a row reads column x + 7, whose weights are zero)
+  const int RB = kFeTP / W + 6, PW = W + 8;
+  _Float16* Ws = smem_fe;                    // [128][kFeKS]: [row 7][pair 4][tap 2][ch 4]
+  _Float16* In = Ws + 128 * kFeKS;           // [RB][PW][4]
+  _Float16* Os = In + RB * PW * 4;           // [128][kFeOS]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int HW = H * W, tpe = HW / kFeTP;
-  for (int idx = tid; idx < 128 * (kFeK / 8); idx += 512) {
-    const int r = idx / (kFeK / 8), q = idx - r * (kFeK / 8);
-    *reinterpret_cast<uint4*>(&Ws[r * kFeKS + q * 8]) = *reinterpret_cast<const uint4*>(w + r * kFeK + q * 8);
+  for (int idx = tid; idx < 128 * 28 * 2; idx += 512) {  // (co, row, pair, tap of the pair)
+    const int co = idx / 56, q = idx - co * 56, kb = q >> 1, h2 = q & 1;
+    const int ty = kb >> 2, tx = 2 * (kb & 3) + h2;
+    const uint2 v = tx < 7 ? *reinterpret_cast<const uint2*>(w + co * kFeK + (ty * 7 + tx) * 8) : make_uint2(0, 0);
+    *reinterpret_cast<uint2*>(&Ws[co * kFeKS + kb * 8 + h2 * 4]) = v;
   }
   for (int idx = tid; idx < RB * PW; idx += 512)
-    *reinterpret_cast<uint4*>(&In[idx * 8]) = make_uint4(0, 0, 0, 0);  // padding columns stay zero
+    *reinterpret_cast<uint2*>(&In[idx * 4]) = make_uint2(0, 0);  // padding columns stay zero
   // input staging: thread -> band pixel (row idx / W, column idx % W), several per thread
   const int nin = (RB * W + 511) / 512;  // <= 2 for W <= 128
   float v[2][4];
@@ -1514,10 +1561,11 @@ __global__ void __launch_bounds__(512) flow_enc0_kernel(const float* __restrict_
       const int idx = tid + 512 * u;
       const int ry = idx / W, x = idx - ry * W;
       if (u < nin && ry < RB) {
-        half8 h;
+        typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+        half4_t h;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) { h[c] = (_Float16)v[u][c]; h[c + 4] = (_Float16)0.f; }
-        *reinterpret_cast<half8*>(&In[(ry * PW + x + 3) * 8]) = h;
+        for (int c = 0; c < 4; ++c) h[c] = (_Float16)v[u][c];
+        *reinterpret_cast<half4_t*>(&In[(ry * PW + x + 3) * 4]) = h;
       }
     }
   };
@@ -1544,13 +1592,15 @@ __global__ void __launch_bounds__(512) flow_enc0_kernel(const float* __restrict_
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[f][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < kFeK / 32; ++ks) {
-      int tap = ks * 4 + fq;
-      if (tap > 48) tap = 48;  // taps 49..51 have zero weights; read any valid slot
-      const int ty = tap / 7, tx = tap - ty * 7;
+    for (int ks = 0; ks < kFeK2 / 32; ++ks) {  // K-step = kernel row ks, lane group fq = tap pair
       half8 af[2], bf[4];
 #pragma unroll
-      for (int f = 0; f < 2; ++f) af[f] = *reinterpret_cast<const half8*>(&In[(pyx[f] + ty * PW + tx) * 8]);
+      for (int f = 0; f < 2; ++f) {
+        // band pixels (x + 2 fq, x + 2 fq + 1) of row ks: 16 B at an 8-B boundary
+        const uint2* src = reinterpret_cast<const uint2*>(&In[(pyx[f] + ks * PW + 2 * fq) * 4]);
+        const uint2 lo = src[0], hi = src[1];
+        af[f] = __builtin_bit_cast(half8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         bf[j] = *reinterpret_cast<const half8*>(&Ws[(wn * 64 + j * 16 + fr) * kFeKS + ks * 32 + fq * 8]);
