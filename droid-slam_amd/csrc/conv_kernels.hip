@@ -1772,6 +1772,7 @@ int droid_conv_dw_head_f16(const void* const* srcs, const int* C, const int* cst
     return fail(kUnsupported, "conv_dw_head_f16: shape needs the band tile (W in {16,32,64}, H*W % 256 == 0)");
   if ((long)B * H * W * 8 > 0x7fffffffL) return fail(kUnsupported, "conv_dw_head_f16: too many pixels");
   ConvArgs a{};
+  a.prof = g_conv_prof;
   int chunks = 0;
   for (int s = 0; s < nsrc; ++s) {
     if (C[s] % 8 || cstride[s] % 8 || cstride[s] < C[s] || (reinterpret_cast<uintptr_t>(srcs[s]) & 15))

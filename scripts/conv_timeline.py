@@ -2,7 +2,7 @@
 prologue (entry -> first stage's operands landed), main loop, epilogue, and the
 gap between consecutive workgroups on the same CU, in shader clocks.
 
-usage: python scripts/conv_timeline.py [edges] [zr|q|ce2|dw]
+usage: python scripts/conv_timeline.py [edges] [zr|q|ce2|dw|dwh]
 (runs on the profiling build: make -C droid-slam_amd/csrc prof)"""
 import os
 import sys
@@ -28,14 +28,21 @@ g = torch.Generator(device=dev).manual_seed(0)
 t = lambda c: (torch.randn((E, H, W, c), generator=g, device=dev) * 0.5).half()
 net, inp, cf, ff = t(128), t(128), t(128), t(64)
 srcs4 = [(net, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)]
-cfg = {"zr": (srcs4, 256), "q": (srcs4, 128), "ce2": ([(net, 0, 128)], 128), "dw": ([(net, 0, 128)], 256)}[which]
+cfg = {"zr": (srcs4, 256), "q": (srcs4, 128), "ce2": ([(net, 0, 128)], 128), "dw": ([(net, 0, 128)], 256),
+       "dwh": ([(net, 0, 128)], 256)}[which]
 srcs, cout = cfg
 cin = sum(c for _, _, c in srcs)
 w = torch.randn((cout, cin, 3, 3), generator=g, device=dev) * 0.02
 wp = pack_conv(w, [c for _, _, c in srcs])
 bias = torch.zeros(cout, device=dev)
 out = torch.empty((E, H, W, cout), dtype=torch.float16, device=dev)
-run = lambda: droid_backends.conv_nhwc_f16(srcs, wp, cout, 3, bias=bias, act=1, out=out)
+if which == "dwh":   # delta.0 || weight.0 with both heads fused (EPI_DWHEAD)
+    from droid_mi355x.fused import pack_head_taps
+    hw = pack_head_taps(torch.randn((4, 256, 3, 3), generator=g, device=dev) * 0.02)
+    head = torch.zeros((E, H, W, 4), device=dev)
+    run = lambda: droid_backends.conv_dw_head_f16(srcs, wp, bias, hw, head)
+else:
+    run = lambda: droid_backends.conv_nhwc_f16(srcs, wp, cout, 3, bias=bias, act=1, out=out)
 for _ in range(3):
     run()
 torch.cuda.synchronize()
