@@ -67,7 +67,11 @@ def build_state(args, rank, world, device):
 
     H, W = args.ht // 8, args.wd // 8
     rng = np.random.default_rng(1003)
-    ii, jj = synthetic.c3_edges(args.frames, args.edges, rng=np.random.default_rng(1003))
+    stereo = args.config == "C4"
+    if stereo:   # C4: 128 KF, one stereo (i, i) edge per frame + temporal + loops
+        ii, jj = synthetic.c4_edges(args.frames, rng=np.random.default_rng(1004))
+    else:
+        ii, jj = synthetic.c3_edges(args.frames, args.edges, rng=np.random.default_rng(1003))
     comm = None
     if world > 1:
         ii_l, jj_l, own = sharding.shard_edges(ii, jj, args.frames, rank, world)
@@ -77,12 +81,12 @@ def build_state(args, rank, world, device):
     n = args.frames
     gt = synthetic.trajectory(n, rng)
     poses, disps = synthetic.perturb(gt, synthetic.smooth_disps(n, H, W, rng), rng)
-    video = DepthVideo(image_size=(args.ht, args.wd), buffer=n, device=device)
+    video = DepthVideo(image_size=(args.ht, args.wd), buffer=n, stereo=stereo, device=device)
     video.poses[:n] = torch.from_numpy(poses.astype(np.float32)).to(device)
     video.disps[:n] = torch.from_numpy(disps.astype(np.float32)).to(device)
     video.intrinsics[:n] = torch.from_numpy(np.tile(synthetic.INTRINSICS, (n, 1))).to(device)
     g = torch.Generator(device=device).manual_seed(1003)
-    video.fmaps[:n] = torch.randn((n, 1, 128, H, W), generator=g, device=device).half()
+    video.fmaps[:n] = torch.randn((n, 2 if stereo else 1, 128, H, W), generator=g, device=device).half()
     video.nets[:n] = torch.tanh(torch.randn((n, 128, H, W), generator=g, device=device)).half()
     video.inps[:n] = torch.relu(torch.randn((n, 128, H, W), generator=g, device=device)).half()
     video.counter.value = n
@@ -211,6 +215,9 @@ def load_traffic(name, e_local, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", choices=["C3", "C4"], default="C3",
+                    help="C3 (default, the metric's config): 256 KF / 2048 edges mono; "
+                         "C4: stereo, 128 KF, (i, i) stereo edges + temporal + loops (~1k edges)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=256)
@@ -226,6 +233,8 @@ def main():
     ap.add_argument("--reference-op", action="store_true",
                     help="run the reference-structured UpdateModule (torch/MIOpen convs, NCHW) instead of the fused MFMA operator")
     args = ap.parse_args()
+    if args.config == "C4" and args.frames == 256:
+        args.frames = 128
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -313,7 +322,8 @@ def main():
         else:
             roofline, lookup_roof = lookup_roof, None
         result = {
-            "metric": "factor_graph.update() iters/sec at 256 KF x 2k edges, 384x512",
+            "metric": ("factor_graph.update() iters/sec at 256 KF x 2k edges, 384x512" if args.config == "C3"
+                       else "factor_graph.update() iters/sec, C4 stereo %d KF x %d edges, 384x512" % (args.frames, len(ii))),
             "value": 1000.0 / ms,
             "unit": "iters/s",
             "n_gpus": world,
@@ -324,8 +334,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f16 (corr volume, update-operator convs) / f32 (BA linearisation, Schur) / f64 (reduced system)",
-            "data": "synthetic (SURVEY.md §8d C3 graph, random-init UpdateModule)",
-            "config": {"workload": "C3 global graph: update(itrs=2), volume corr", "keyframes": args.frames,
+            "data": "synthetic (SURVEY.md §8d %s graph, random-init UpdateModule)" % args.config,
+            "config": {"workload": ("C4 stereo graph" if args.config == "C4" else "C3 global graph")
+                                   + ": update(itrs=2), %s corr" % args.corr, "keyframes": args.frames,
                        "edges": len(ii), "image": [args.ht, args.wd], "fmap": [args.ht // 8, args.wd // 8],
                        "parallelism": "edge-sharded x%d (RCCL all-reduce of reduced camera system)" % world},
             "roofline": roofline,

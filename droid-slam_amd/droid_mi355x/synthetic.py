@@ -89,6 +89,26 @@ def c3_edges(num_kf=256, num_edges=2048, rng=None, max_out=14):
     return e[:, 0], e[:, 1]
 
 
+def c4_edges(num_kf=128, loops=100, rng=None):
+    """Stereo config: one (i, i) stereo edge per keyframe
+    (factor_graph.py:335-337; it correlates against the right image), +-1..+-3
+    temporal neighbours and ~`loops` random bidirectional loop edges |i-j| > 3."""
+    rng = rng or np.random.default_rng(1004)
+    es = [(i, i) for i in range(num_kf)]
+    es += [(i, j) for i in range(num_kf) for j in range(num_kf) if i != j and abs(i - j) <= 3]
+    have = set(es)
+    target = len(es) + loops
+    while len(es) + 2 <= target:
+        i, j = (int(x) for x in rng.integers(0, num_kf, 2))
+        if abs(i - j) <= 3 or (i, j) in have:
+            continue
+        for a, b in ((i, j), (j, i)):
+            es.append((a, b))
+            have.add((a, b))
+    e = np.asarray(es, dtype=np.int64)
+    return e[:, 0], e[:, 1]
+
+
 def c2_edges():
     """Frontend window: 16-KF buffer, optimise [8,16); |i-j|<=3 in [4,16) plus
     inactive-style edges from [8,16) into [5,8) -> 96 edges."""

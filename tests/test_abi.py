@@ -99,3 +99,16 @@ def test_tile8_round_trip_host_only():
         if H2p != H2:
             assert not t.reshape(3, 2, 5, H2p // 8, W2 // 8, 8, 8)[:, :, :, -1, :, H2 % 8:, :].any()
         assert torch.equal(untile8(t, H2, W2), lv)
+
+
+def test_c4_stereo_edges_host_only():
+    """bench.py --config C4 graph: one (i, i) edge per keyframe, +-1..+-3
+    temporal edges, bidirectional loop edges, no duplicates (~1k edges)."""
+    from droid_mi355x import synthetic
+    ii, jj = synthetic.c4_edges(128)
+    assert (ii == jj).sum() == 128
+    pairs = set(zip(ii.tolist(), jj.tolist()))
+    assert len(pairs) == len(ii) and 900 < len(ii) < 1100
+    assert all((j, i) in pairs for i, j in pairs)
+    d = np.abs(ii - jj)
+    assert ((d >= 1) & (d <= 3)).sum() == 2 * (127 + 126 + 125)

@@ -401,3 +401,68 @@ def test_factor_graph_update_pyramid_corr():
     np.testing.assert_allclose(host(video.poses[:n]), ref["poses"][:n], atol=1e-4)
     np.testing.assert_allclose(host(video.disps[:n]), np.maximum(ref["disps"][:n], 1e-3), atol=1e-4)
     assert torch.isfinite(g.net.float()).all()
+
+
+@pytest.mark.parametrize("corr_impl", ["volume", "pyramid"])
+def test_factor_graph_update_stereo(corr_impl):
+    """Stereo video: neighbourhood edges skip |i-j| <= 1
+    (factor_graph.py:334-337), one (i, i) edge per frame correlates against the
+    right image (fmaps[i, 1], factor_graph.py:112-114) and BA uses the fixed
+    stereo baseline for it.  Checks the stereo volume rows, then BA parity on the
+    inputs update() hands over (as test_factor_graph_update_fused_path)."""
+    import droid_backends
+    from droid_mi355x import DepthVideo, FactorGraph, UpdateModule, synthetic
+    from droid_mi355x.fused import FusedUpdateModule
+    from oracle import ba as oba
+    rng = np.random.default_rng(35)
+    n, H, W = 8, 16, 24
+    video = DepthVideo(image_size=(8 * H, 8 * W), buffer=n, stereo=True, device=DEV)
+    poses = synthetic.trajectory(n, rng)
+    poses, disps = synthetic.perturb(poses, synthetic.smooth_disps(n, H, W, rng), rng)
+    video.poses[:n] = torch.from_numpy(poses.astype(np.float32)).to(DEV)
+    video.disps[:n] = torch.from_numpy(disps.astype(np.float32)).to(DEV)
+    video.intrinsics[:n] = torch.tensor([[H / 1.5, H / 1.5, W / 2, H / 2]] * n, device=DEV)
+    fm = rng.normal(size=(n, 2, 128, H, W)).astype(np.float16)
+    video.fmaps[:n] = torch.from_numpy(fm).to(DEV)
+    video.nets[:n] = torch.from_numpy(np.tanh(rng.normal(size=(n, 128, H, W))).astype(np.float16)).to(DEV)
+    video.inps[:n] = torch.from_numpy(np.maximum(rng.normal(size=(n, 128, H, W)), 0).astype(np.float16)).to(DEV)
+    video.counter.value = n
+    m = UpdateModule().to(DEV).eval()
+    det_fill(m)
+    g = FactorGraph(video, FusedUpdateModule(m), device=DEV, corr_impl=corr_impl)
+    g.add_neighborhood_factors(0, n, r=3)
+    d = np.abs(g._ii - g._jj)
+    assert d.min() == 2 and d.max() == 3
+    g.add_factors(np.arange(n), np.arange(n))
+    stereo = np.nonzero(g._ii == g._jj)[0]
+    assert len(stereo) == n
+    if corr_impl == "volume":
+        lv0 = g.corr.reference_pyramid()[0]
+        for k in stereo[:3]:
+            i = int(g._ii[k])
+            f1 = fm[i, 0].astype(np.float32).reshape(128, -1) / 4
+            f2 = fm[i, 1].astype(np.float32).reshape(128, -1) / 4
+            want = (f1.T @ f2).reshape(H, W, H, W)
+            np.testing.assert_allclose(host(lv0[k]).astype(np.float32), want, atol=2e-2, rtol=1e-2)
+    captured = {}
+    orig = droid_backends.ba
+
+    def spy(*a, **k):
+        captured["a"] = [x.detach().clone() if isinstance(x, torch.Tensor) else x for x in a]
+        return orig(*a, **k)
+
+    droid_backends.ba = spy
+    try:
+        with torch.no_grad():
+            g.update()
+            g.update()
+    finally:
+        droid_backends.ba = orig
+    a = captured["a"]
+    assert (host(a[7]) == host(a[8])).sum() == n   # stereo edges reach BA
+    ref = oba.ba(poses=host(a[0]), disps=host(a[1]), intrinsics=host(a[2]), disps_sens=host(a[3]),
+                 targets=host(a[4]), weights=host(a[5]), eta=host(a[6]), ii=host(a[7]), jj=host(a[8]), t0=a[9],
+                 t1=a[10], iterations=a[11], lm=a[12], ep=a[13], motion_only=a[14])
+    np.testing.assert_allclose(host(video.poses[:n]), ref["poses"][:n], atol=1e-4)
+    np.testing.assert_allclose(host(video.disps[:n]), np.maximum(ref["disps"][:n], 1e-3), atol=1e-4)
+    assert torch.isfinite(g.net.float()).all()
