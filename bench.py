@@ -36,6 +36,9 @@ LOOKUP_BYTES_PER_EDGE = 2801664  # volume-API lookup, 4 lvl x 64
 LOOKUP_CE0_BYTES_PER_EDGE = 4 * 64 * 2 * 3072 + 2 * 4 * 3072 + 128 * 2 * 3072
 # ConvGRU z|r conv (modules/gru.py:19-32, convz+convr fused): 3x3, 448 -> 256 channels
 ZR_FLOPS_PER_PIXEL = 2 * 256 * 448 * 9
+# ... with the context features factored out per source frame (droid_conv_gru_pre_f16):
+# the per-edge z|r conv runs over net | corr | flow = 320 channels
+ZR_PRE_FLOPS_PER_PIXEL = 2 * 256 * 320 * 9
 ZR_KERNEL = "conv_band_kernel<256,256>"   # csrc/conv_kernels.hip, chosen for 48x64 maps
 ZR_KERNEL_MATCH = "conv_band_kernel<256, 256"   # its symbol in rocprof / PMC summaries
 LOOKUP_KERNEL = "corr_pyramid_f16_r3_kernel"
@@ -48,6 +51,8 @@ LOOKUP_KERNEL = "corr_pyramid_f16_r3_kernel"
 CONV_FLOPS_PER_EDGE_PIXEL = 2 * (196 * 128 + 128 * 128 * 9 + 4 * 128 * 49 + 128 * 64 * 9 + 3 * 448 * 128 * 9
                                  + 128 * 128 + 2 * (128 * 128 * 9 + 128 * 2 * 9) + 128 * 128 * 9)
 CONV_FLOPS_PER_FRAME_PIXEL = 2 * (128 * 128 * 9 + 128 * 9 + 128 * 576)
+# factored gates: 3 x 128 inp channels move from per-edge to per-source-frame pixels
+GATE_INP_FLOPS_PER_PIXEL = 2 * 3 * 128 * 128 * 9
 # HBM-bound stages per update (fused lookup path): lookup 3,059,712 B/edge (§8d fused row),
 # BA 2 GN x (49,152 B/edge + 49,152 B/frame), reproject + motn 110,592 B/edge
 HBM_BYTES_PER_EDGE = 3059712 + 2 * 49152 + 110592
@@ -263,9 +268,10 @@ def main():
     LOOKUP_FN[0] = ("corr_pyramid_lookup" if args.reference_op else
                     "corr_alt_ce0" if args.corr == "pyramid" else "corr_lookup_ce0")
     lookup = KernelTimer(droid_backends, LOOKUP_FN[0])
-    zr = None
+    zr = zrp = None
     if not args.reference_op:
         zr = KernelTimer(droid_backends, "conv_nhwc_f16", when=lambda *a, **k: k.get("epi") == droid_backends.EPI_GRU_ZR)
+        zrp = KernelTimer(droid_backends, "conv_gru_pre_f16", when=lambda *a, **k: a[5] == droid_backends.EPI_GRU_ZR)
 
     with torch.no_grad():
         t_w = time.time()
@@ -279,7 +285,7 @@ def main():
         torch.cuda.synchronize(device)
         lookup.active = True
         if zr:
-            zr.active = True
+            zr.active = zrp.active = True
         t0 = time.perf_counter()
         for _ in range(args.steps):
             graph.update()
@@ -289,7 +295,7 @@ def main():
         elapsed = time.perf_counter() - t0
         lookup.active = False
         if zr:
-            zr.active = False
+            zr.active = zrp.active = False
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -298,6 +304,9 @@ def main():
     finite = bool(torch.isfinite(video.poses).all() and torch.isfinite(video.disps).all())
     lookup_ms = lookup.mean_ms()
     zr_ms = zr.mean_ms() if zr else None
+    factored = bool(zrp and zrp.mean_ms())
+    if factored:
+        zr_ms = zrp.mean_ms()
     breakdown = stage_breakdown(graph, video) if args.breakdown else None
 
     if rank == 0:
@@ -313,9 +322,10 @@ def main():
                                                else "corr_ce0_kernel<true>"), "launch_ms": lookup_ms,
                        "algorithmic_bytes_per_launch": bytes_per_launch}
         if zr_ms:
-            flops = ZR_FLOPS_PER_PIXEL * e_local * (args.ht // 8) * (args.wd // 8)
+            flops = (ZR_PRE_FLOPS_PER_PIXEL if factored else ZR_FLOPS_PER_PIXEL) * e_local * (args.ht // 8) * (args.wd // 8)
             tf = flops / (zr_ms * 1e-3) / 1e12
-            roofline = {"kernel": "%s (ConvGRU z|r gates, 3x3 448->256, fp16 MFMA)" % ZR_KERNEL,
+            roofline = {"kernel": "%s (ConvGRU z|r gates, 3x3 %d->256, fp16 MFMA%s)"
+                                  % (ZR_KERNEL, 320 if factored else 448, ", inp term per source frame" if factored else ""),
                         "bound": "mfma", "achieved": tf, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                         "frac": tf / PEAK_F16_TFLOPS, "traffic": load_traffic("conv_zr", e_local, ZR_KERNEL_MATCH),
                         "launch_ms": zr_ms, "algorithmic_flops_per_launch": flops}
@@ -348,6 +358,8 @@ def main():
         hw = (args.ht // 8) * (args.wd // 8)
         n_src = len(np.unique(ii))
         conv_flops = (CONV_FLOPS_PER_EDGE_PIXEL * len(ii) + CONV_FLOPS_PER_FRAME_PIXEL * n_src) * hw
+        if factored:   # the algorithm run: gate inp term per source frame, not per edge
+            conv_flops -= GATE_INP_FLOPS_PER_PIXEL * (len(ii) - n_src) * hw
         hbm_bytes = HBM_BYTES_PER_EDGE * len(ii) + HBM_BYTES_PER_FRAME * args.frames
         mfma_floor = conv_flops / (PEAK_F16_TFLOPS * 1e12) * 1e3 / world
         hbm_floor = hbm_bytes / (PEAK_HBM_GBS * 1e9) * 1e3 / world

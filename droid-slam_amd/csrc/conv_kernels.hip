@@ -33,6 +33,9 @@
 //   EPI_HEAD  : fp32 out, co < 2 raw (delta), co >= 2 sigmoid (weight)
 //   EPI_GLO   : sigmoid(.) * h summed over the tile's pixels, atomically added
 //               (scaled by 1/HW) into glo[b][co]: the GRU global-context mean
+//   EPI_GRU_ZRP / EPI_GRU_QP (band tiles, droid_conv_gru_pre_f16): EPI_GRU_ZR /
+//               EPI_GRU_Q with a per-source-frame term added before the gate:
+//               gate(acc + bias + bbias[b] + pre[pre_idx[b], pixel, pre_coff + co])
 #include "common.hpp"
 #include "lds_dma.hpp"
 #include <algorithm>
@@ -50,7 +53,9 @@
 namespace droid {
 
 
-enum ConvEpi : int { EPI_ACT = 0, EPI_GRU_ZR = 1, EPI_GRU_Q = 2, EPI_HEAD = 3, EPI_GLO = 4, EPI_DWHEAD = 5 };
+enum ConvEpi : int { EPI_ACT = 0, EPI_GRU_ZR = 1, EPI_GRU_Q = 2, EPI_HEAD = 3, EPI_GLO = 4, EPI_DWHEAD = 5,
+                     EPI_GRU_ZRP = 6, EPI_GRU_QP = 7 };
+constexpr int kEpiPreShift = EPI_GRU_ZRP - EPI_GRU_ZR;  // EPI_GRU_*P -> its base epilogue
 
 struct ConvSrc {
   const __half* ptr;
@@ -89,6 +94,11 @@ struct ConvArgs {
   int nhi;    // halo DMA instructions per wave per chunk
   const __half* hw;  // EPI_DWHEAD: head weights [48][256] (row = tap*4 + out channel)
   long long* prof;   // band kernel timeline (droid_conv_set_profile): 4 stamps per workgroup, or null
+  // EPI_GRU_ZRP / EPI_GRU_QP: per-source-frame pre-activation term, NHWC fp16
+  // (frames, H, W, pre_cstride); image b reads frame pre_idx[b]
+  const __half* pre;
+  const long long* pre_idx;
+  int pre_cstride, pre_coff;
 };
 
 constexpr int TM = 128, BK = 64;
@@ -902,20 +912,38 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
   const int HW = a.H * a.W;
   const int b = (int)(m0 / HW);  // a tile never straddles two images
   const int fr = lane & 15, fq = lane >> 4;
-  const int epi = EPI >= 0 ? EPI : a.epi;
+  // kPre: the gate's argument gets the per-source term in pass (2), so pass (1)
+  // stages the pre-activation acc + bias (fp16, as the reference's autocast
+  // conv output is) and the gate is applied after the sum
+  constexpr bool kPre = EPI == EPI_GRU_ZRP || EPI == EPI_GRU_QP;
+  constexpr int EB = kPre ? EPI - kEpiPreShift : EPI;
+  const int epi = EB >= 0 ? EB : a.epi;
   const bool relu = a.act == 1;
+  // the lane's column biases: all FN loads issued before the first use (a
+  // per-column conditional load paid one L2 round trip per column)
+  float bvv[FN];
+  if (bpre) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bvv[j] = bpre[j];  // loaded before the main loop
+  } else {
+    const float* const bias = a.bias;
+    const float* const bbias = a.bbias ? a.bbias + (long)b * a.Cout : nullptr;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bvv[j] = 0.f;
+    if (bias) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bvv[j] = bias[n0 + wn * FN * 16 + j * 16 + fr];
+    }
+    if (bbias) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bvv[j] += bbias[n0 + wn * FN * 16 + j * 16 + fr];
+    }
+  }
   __syncthreads();  // main-loop LDS reads are done
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int c = wn * FN * 16 + j * 16 + fr;
-    const int co = n0 + c;
-    float bv;
-    if (bpre) {
-      bv = bpre[j];  // loaded before the main loop
-    } else {
-      bv = a.bias ? a.bias[co] : 0.f;
-      if (a.bbias) bv += a.bbias[(long)b * a.Cout + co];
-    }
+    const float bv = bvv[j];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -923,7 +951,8 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
         const int r = frag_row<FM, WM, CONTIG>(wm, i) + fq * 4 + k;
         const float v = acc[i][j][k] + bv;
         float o;
-        if constexpr (EPI == EPI_GRU_ZR) o = sigmoidf_(v);
+        if constexpr (kPre) o = v;
+        else if constexpr (EPI == EPI_GRU_ZR) o = sigmoidf_(v);
         else if constexpr (EPI == EPI_GRU_Q) o = tanh_fast(v);
         else if constexpr (EPI == EPI_ACT) o = relu ? fmaxf(v, 0.f) : v;
         else if (epi == EPI_GRU_ZR) o = sigmoidf_(v);
@@ -937,8 +966,10 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
   // GRU epilogues: every round's h (and z) pieces are loaded here, all in flight
   // together while the staging barrier waits (issued inside the store loop they
   // were serialised behind the previous round's store: one HBM latency per round)
-  constexpr bool kPreH = EPI == EPI_GRU_ZR || EPI == EPI_GRU_Q;
-  half8 hpre[kPreH ? RND : 1], zpre[EPI == EPI_GRU_Q ? RND : 1];
+  constexpr bool kPreH = EB == EPI_GRU_ZR || EB == EPI_GRU_Q;
+  half8 hpre[kPreH ? RND : 1], zpre[EB == EPI_GRU_Q ? RND : 1], ppre[kPre ? RND : 1];
+  // pixel m of image b -> pixel of its source frame in the pre map
+  const long pshift = kPre ? ((long)a.pre_idx[b] - b) * HW : 0;
   if constexpr (kPreH) {
 #pragma unroll
     for (int q = 0; q < RND; ++q) {
@@ -946,7 +977,8 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
       const int r = idx / PPR, p = idx - r * PPR;
       const long m = m0 + r;
       const int c = n0 + p * 8;
-      if constexpr (EPI == EPI_GRU_Q) {
+      if constexpr (kPre) ppre[q] = *reinterpret_cast<const half8*>(a.pre + (m + pshift) * a.pre_cstride + a.pre_coff + c);
+      if constexpr (EB == EPI_GRU_Q) {
         hpre[q] = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c);
         zpre[q] = *reinterpret_cast<const half8*>(a.z + m * a.z_cstride + c);
       } else if (c >= a.gru_ch) {
@@ -955,6 +987,11 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
     }
   }
   __syncthreads();
+  // (2a) every round's output piece computed first, (2b) then all stores: with
+  // a store inside each round, the in-order vmcnt wait for round q+1's h / z /
+  // pre pieces also drained round q's stores (gfx9 counts stores in vmcnt) -
+  // one store round trip per round, ~26k clocks per 256x256 tile measured
+  half8 outv[RND];
 #pragma unroll  // all rounds' LDS reads in flight together
   for (int q = 0; q < RND; ++q) {
     const int idx = tid + q * NT;
@@ -962,6 +999,13 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
     const long m = m0 + r;
     const int c = n0 + p * 8;
     half8 v = *reinterpret_cast<const half8*>(&smem[r * ER + p * 8]);
+    if constexpr (kPre) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = (float)v[e] + (float)ppre[q][e];
+        v[e] = (_Float16)(EB == EPI_GRU_ZR ? sigmoidf_(x) : tanh_fast(x));
+      }
+    }
     if (epi == EPI_GRU_ZR) {
       if (c >= a.gru_ch) {
         half8 h;
@@ -969,13 +1013,10 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
         else h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c - a.gru_ch);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = (_Float16)((float)v[e] * (float)h[e]);
-        *reinterpret_cast<half8*>(a.rnet + m * a.gru_ch + c - a.gru_ch) = v;
-      } else {
-        *reinterpret_cast<half8*>(a.zout + m * a.gru_ch + c) = v;
       }
     } else if (epi == EPI_GRU_Q) {
       half8 h, z;
-      if constexpr (EPI == EPI_GRU_Q) {
+      if constexpr (EB == EPI_GRU_Q) {
         h = hpre[q];
         z = zpre[q];
       } else {
@@ -987,9 +1028,25 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
         const float zv = (float)z[e];
         v[e] = (_Float16)((1.0f - zv) * (float)h[e] + zv * (float)v[e]);
       }
-      *reinterpret_cast<half8*>(a.out + m * a.out_cstride + a.out_coff + c) = v;
+    }
+    outv[q] = v;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  __half* const zout = a.zout;
+  __half* const rnet = a.rnet;
+  __half* const out = a.out;
+  const int gch = a.gru_ch, ocs = a.out_cstride, ooff = a.out_coff;
+#pragma unroll
+  for (int q = 0; q < RND; ++q) {
+    const int idx = tid + q * NT;
+    const int r = idx / PPR, p = idx - r * PPR;
+    const long m = m0 + r;
+    const int c = n0 + p * 8;
+    if (epi == EPI_GRU_ZR) {
+      if (c >= gch) *reinterpret_cast<half8*>(rnet + m * gch + c - gch) = outv[q];
+      else *reinterpret_cast<half8*>(zout + m * gch + c) = outv[q];
     } else {
-      *reinterpret_cast<half8*>(a.out + m * a.out_cstride + a.out_coff + c) = v;
+      *reinterpret_cast<half8*>(out + m * ocs + ooff + c) = outv[q];
     }
   }
 }
@@ -1371,17 +1428,24 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
   if constexpr (DWHEAD) {
     st = launch_band_kernel<TMX, TN, true, false, EPI_DWHEAD>(a, nwg, lds, stream);
   } else {
-    const int epi = a.epi == EPI_GRU_ZR ? EPI_GRU_ZR : a.epi == EPI_GRU_Q ? EPI_GRU_Q : EPI_ACT;
+    int epi = a.epi == EPI_GRU_ZR ? EPI_GRU_ZR : a.epi == EPI_GRU_Q ? EPI_GRU_Q : EPI_ACT;
+    if (a.pre && epi != EPI_ACT) epi += kEpiPreShift;
+    // the instantiations the update operator's shapes take: z|r on 256x256,
+    // q and the plain convs on the 384-row tiles
     if constexpr (TN != 256) {
       if (ilv) {
-        if (epi == EPI_GRU_ZR) st = launch_band_kernel<TMX, TN, false, true, EPI_GRU_ZR>(a, nwg, lds, stream);
-        else if (epi == EPI_GRU_Q) st = launch_band_kernel<TMX, TN, false, true, EPI_GRU_Q>(a, nwg, lds, stream);
+        if (epi == EPI_GRU_Q) st = launch_band_kernel<TMX, TN, false, true, EPI_GRU_Q>(a, nwg, lds, stream);
+        else if (epi == EPI_GRU_QP) st = launch_band_kernel<TMX, TN, false, true, EPI_GRU_QP>(a, nwg, lds, stream);
+        else if (epi == EPI_GRU_ZR) st = launch_band_kernel<TMX, TN, false, true, EPI_GRU_ZR>(a, nwg, lds, stream);
+        else if (epi == EPI_GRU_ZRP) st = launch_band_kernel<TMX, TN, false, true, EPI_GRU_ZRP>(a, nwg, lds, stream);
         else st = launch_band_kernel<TMX, TN, false, true, EPI_ACT>(a, nwg, lds, stream);
       }
     }
     if (!ilv) {
       if (epi == EPI_GRU_ZR) st = launch_band_kernel<TMX, TN, false, false, EPI_GRU_ZR>(a, nwg, lds, stream);
+      else if (epi == EPI_GRU_ZRP) st = launch_band_kernel<TMX, TN, false, false, EPI_GRU_ZRP>(a, nwg, lds, stream);
       else if (epi == EPI_GRU_Q) st = launch_band_kernel<TMX, TN, false, false, EPI_GRU_Q>(a, nwg, lds, stream);
+      else if (epi == EPI_GRU_QP) st = launch_band_kernel<TMX, TN, false, false, EPI_GRU_QP>(a, nwg, lds, stream);
       else st = launch_band_kernel<TMX, TN, false, false, EPI_ACT>(a, nwg, lds, stream);
     }
   }
@@ -1671,11 +1735,12 @@ int droid_conv_set_profile(void* buf) {
 #endif
 }
 
-int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc,
-                        const void* wp, const float* bias, const float* bbias, int B, int H, int W,
-                        int Cout, int ks, int act, int epi, void* out, int out_cstride, int out_coff,
-                        const void* h, int h_cstride, const void* z, int z_cstride, void* zout,
-                        void* rnet, int gru_ch, void* out32, hipStream_t stream) {
+static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstride, int nsrc,
+                          const void* wp, const float* bias, const float* bbias, int B, int H, int W,
+                          int Cout, int ks, int act, int epi, void* out, int out_cstride, int out_coff,
+                          const void* h, int h_cstride, const void* z, int z_cstride, void* zout,
+                          void* rnet, int gru_ch, void* out32, const void* pre, const long long* pre_idx,
+                          int pre_cstride, int pre_coff, hipStream_t stream) {
   if (nsrc < 1 || nsrc > 4 || B < 0 || H <= 0 || W <= 0 || Cout <= 0 || ks < 1 || ks > 7 || !(ks & 1) ||
       epi < EPI_ACT || epi > EPI_GLO)
     return fail(kInvalidArgument, "conv_nhwc_f16: bad arguments");
@@ -1708,6 +1773,7 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
   a.z = (const __half*)z; a.z_cstride = z_cstride;
   a.zout = (__half*)zout; a.rnet = (__half*)rnet; a.gru_ch = gru_ch;
   a.out32 = (float*)out32;
+  a.pre = (const __half*)pre; a.pre_idx = pre_idx; a.pre_cstride = pre_cstride; a.pre_coff = pre_coff;
   const int TN = Cout >= 128 ? 128 : (Cout > 16 ? 64 : 16);
   a.stage_out = (Cout % 8 == 0 && out_cstride % 8 == 0 && out_coff % 8 == 0) ? 1 : 0;
   if (epi == EPI_ACT && !out) return fail(kInvalidArgument, "conv_nhwc_f16: out is null");
@@ -1737,6 +1803,15 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
                        (epi == EPI_GRU_ZR || epi == EPI_GRU_Q || (epi == EPI_ACT && a.stage_out)) &&
                        (epi != EPI_GRU_ZR || gru_ch % 128 == 0);
   int ns_, nh_;
+  if (pre) {  // the per-source term exists on the band tiles only
+    if (band_ok && epi == EPI_GRU_ZR && Cout == 256 && 256 % W == 0 && (H * W) % 256 == 0 &&
+        band_fits<256, 256>(W, &ns_, &nh_))
+      return launch_band<256, 256>(a, stream);
+    if (band_ok && epi == EPI_GRU_Q && Cout == 128 && 384 % W == 0 && (H * W) % 384 == 0 &&
+        band_fits<384, 128>(W, &ns_, &nh_))
+      return launch_band<384, 128>(a, stream);
+    return fail(kUnsupported, "conv_gru_pre_f16: shape has no band tile");
+  }
   if (band_ok && Cout % 256 == 0 && 256 % W == 0 && (H * W) % 256 == 0 && band_fits<256, 256>(W, &ns_, &nh_))
     return launch_band<256, 256>(a, stream);
   if (band_ok && Cout % 128 == 0 && 384 % W == 0 && (H * W) % 384 == 0 && band_fits<384, 128>(W, &ns_, &nh_))
@@ -1754,6 +1829,35 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
   if (TN == 128) return launch_conv<128>(a, stream);
   if (TN == 64) return launch_conv<64>(a, stream);
   return launch_conv<16>(a, stream);
+}
+
+int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc,
+                        const void* wp, const float* bias, const float* bbias, int B, int H, int W,
+                        int Cout, int ks, int act, int epi, void* out, int out_cstride, int out_coff,
+                        const void* h, int h_cstride, const void* z, int z_cstride, void* zout,
+                        void* rnet, int gru_ch, void* out32, hipStream_t stream) {
+  return conv_nhwc_impl(srcs, C, cstride, nsrc, wp, bias, bbias, B, H, W, Cout, ks, act, epi, out, out_cstride,
+                        out_coff, h, h_cstride, z, z_cstride, zout, rnet, gru_ch, out32, nullptr, nullptr, 0, 0,
+                        stream);
+}
+
+// ConvGRU gates with the per-source-frame term factored out (EPI_GRU_ZRP /
+// EPI_GRU_QP): the srcs conv excludes the context features inp, whose part of
+// the gate argument, conv3x3(inp[frame]), is the same for every edge leaving
+// that frame and arrives precomputed in pre (frames, H, W, pre_cstride) fp16;
+// image b adds frame pre_idx[b] at channel offset pre_coff.
+int droid_conv_gru_pre_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc,
+                           const void* wp, const float* bias, const float* bbias, int B, int H, int W,
+                           int Cout, int epi, void* out, int out_cstride, int out_coff, const void* h,
+                           int h_cstride, const void* z, int z_cstride, void* zout, void* rnet, int gru_ch,
+                           const void* pre, const long long* pre_idx, int pre_cstride, int pre_coff,
+                           hipStream_t stream) {
+  if ((epi != EPI_GRU_ZR && epi != EPI_GRU_Q) || !pre || !pre_idx || pre_cstride % 8 || pre_coff % 8 ||
+      pre_coff + Cout > pre_cstride || (reinterpret_cast<uintptr_t>(pre) & 15))
+    return fail(kInvalidArgument, "conv_gru_pre_f16: needs a z|r or q epilogue and a 16-B aligned pre map");
+  return conv_nhwc_impl(srcs, C, cstride, nsrc, wp, bias, bbias, B, H, W, Cout, 3, 0, epi, out, out_cstride,
+                        out_coff, h, h_cstride, z, z_cstride, zout, rnet, gru_ch, nullptr, pre, pre_idx,
+                        pre_cstride, pre_coff, stream);
 }
 
 

@@ -225,6 +225,41 @@ def conv_nhwc_f16(sources, wp, cout, ks, bias=None, bbias=None, act=0, epi=EPI_A
     return out
 
 
+def gru_pre_supported(H, W):
+    """Shapes droid_conv_gru_pre_f16 accepts for both gates (z|r on the 256x256
+    band tile, q on the 384x128 one)."""
+    return W in (16, 32, 64) and (H * W) % 768 == 0
+
+
+def conv_gru_pre_f16(sources, wp, cout, bias, bbias, epi, pre, pre_idx, pre_coff, h, z=None, zout=None,
+                     rnet=None, out=None, gru_ch=128):
+    """ConvGRU gate conv with the per-source-frame term factored out
+    (include/droid_backends.h: droid_conv_gru_pre_f16): the gate argument is
+    conv3x3(sources) + bias + bbias[b] + pre[pre_idx[b], :, :, pre_coff:pre_coff+cout].
+    pre (F,H,W,Cp) fp16 contiguous; pre_idx (B,) int64 on the device."""
+    t0 = sources[0][0]
+    B, H, W = t0.shape[:3]
+    n = len(sources)
+    for t, _, _ in sources:
+        if t.dtype != torch.float16 or not t.is_contiguous() or t.shape[:3] != (B, H, W):
+            raise RuntimeError("conv_gru_pre_f16: sources must be contiguous fp16 (B,H,W,C) tensors")
+    _check_inputs(("pre", "pre_idx"), (pre, pre_idx))
+    _need(pre, torch.float16, "pre")
+    _need(pre_idx, torch.int64, "pre_idx")
+    if pre.dim() != 4 or tuple(pre.shape[1:3]) != (H, W) or pre_idx.numel() != B:
+        raise RuntimeError("conv_gru_pre_f16: pre must be (F,H,W,C) and pre_idx hold one frame per image")
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() + 2 * off for t, off, _ in sources])
+    cs = (ctypes.c_int * n)(*[c for _, _, c in sources])
+    strides = (ctypes.c_int * n)(*[t.shape[-1] for t, _, _ in sources])
+    with torch.cuda.device(t0.device):
+        check(lib.droid_conv_gru_pre_f16(ptrs, cs, strides, n, _ptr(wp), _ptr(bias), _ptr(bbias), B, H, W, int(cout),
+                                         int(epi), _ptr(out), out.shape[-1] if out is not None else 0, 0, _ptr(h),
+                                         h.shape[-1], _ptr(z), z.shape[-1] if z is not None else 0, _ptr(zout),
+                                         _ptr(rnet), int(gru_ch), _ptr(pre), _ptr(pre_idx), pre.shape[-1],
+                                         int(pre_coff), _stream(t0)), "conv_gru_pre_f16")
+    return out
+
+
 def dw_head_supported(H, W):
     """Shapes droid_conv_dw_head_f16 accepts (the band tile: W in {16,32,64}, H*W % 256 == 0)."""
     return W in (16, 32, 64) and (H * W) % 256 == 0

@@ -34,6 +34,8 @@ _SIGS = {
     "droid_corr_alt_ce0": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_conv_nhwc_f16": ([_p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _i, _i,
                              _p, _i, _p, _i, _p, _p, _i, _p, _p], _i),
+    "droid_conv_gru_pre_f16": ([_p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _p, _i,
+                                _p, _p, _i, _p, _p, _i, _i, _p], _i),
     "droid_conv_dw_head_f16": ([_p, _p, _p, _i, _p, _p, _i, _i, _i, _p, _p, _p], _i),
     "droid_flow_enc0_f16": ([_p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_gru_global_f16": ([_p, _p, _p, _p, _i, _i, _p], _i),

@@ -226,8 +226,14 @@ class FactorGraph:
                 corr = PendingLookup(self.corr, coords1)   # lookup runs fused with corr_encoder[0]
             ptr, idx = edge_segments(inverse, len(uniq))
             segs = (self._dev("seg_ptr", ptr), self._dev("seg_idx", idx))
+            # every edge leaving a frame holds the same context features (video.inps[ii],
+            # factor_graph.py:118): one row per source frame - the first edge of its
+            # segment - lets the gate convs compute their inp term once per frame
+            inp_frames = None
+            if self.inp is not None:
+                inp_frames = self.inp.index_select(0, self._dev("seg_first", idx[ptr[:-1]]))
             self.net, delta, weight, damping = self.update_op(self.net, self.inp, corr, motn[0], dinv, len(uniq),
-                                                              segments=segs)
+                                                              segments=segs, inp_frames=inp_frames)
         else:
             corr = self.corr(coords1)
             with torch.autocast("cuda", enabled=True):

@@ -19,6 +19,12 @@ Same parameters (state-dict names) and forward semantics as UpdateModule
   * the correlation lookup can be handed over unevaluated (PendingLookup): the
     lookup and corr_encoder[0] then run as ONE kernel (corr_lookup_ce0) and the
     196-channel lookup tensor is never materialised;
+  * the context features inp enter the z|r and q gates through a conv that is
+    the same for every edge leaving a frame (inp is video.inps[ii],
+    factor_graph.py:93): given the per-frame features (inp_frames), that term
+    is computed once per source frame (one 128 -> 384 conv) and added in the
+    gate epilogues (droid_conv_gru_pre_f16), and the per-edge gate convs run
+    over 320 instead of 448 input channels;
   * GraphAgg's upmask is not computed: update() discards it (factor_graph.py:209).
 All convs: fp16 operands, fp32 accumulation (the reference's autocast).
 """
@@ -163,6 +169,13 @@ class FusedUpdateModule(torch.nn.Module):
         P["zr_b"] = torch.cat([g.convz.bias, g.convr.bias]).float().contiguous()
         P["q"] = pack_conv(g.convq.weight, splits)
         P["q_b"] = g.convq.bias.float().contiguous()
+        # inp factored out: per-edge gates over (net | corr | flow), the inp
+        # columns (128:256) as one per-frame conv with 384 outputs (z | r | q)
+        wzr = torch.cat([g.convz.weight, g.convr.weight], 0)
+        keep = lambda w: torch.cat([w[:, :128], w[:, 256:]], 1)
+        P["zr_x"] = pack_conv(keep(wzr), [128, 128, 64])
+        P["q_x"] = pack_conv(keep(g.convq.weight), [128, 128, 64])
+        P["inp_zrq"] = pack_conv(torch.cat([wzr[:, 128:256], g.convq.weight[:, 128:256]], 0), [128])
         P["glo_w"] = torch.cat([g.convz_glo.weight, g.convr_glo.weight, g.convq_glo.weight], 0)[:, :, 0, 0].float()
         P["glo_b"] = torch.cat([g.convz_glo.bias, g.convr_glo.bias, g.convq_glo.bias]).float()
         P["dw0"] = pack_conv(torch.cat([m.delta[0].weight, m.weight[0].weight], 0), [128])
@@ -183,8 +196,10 @@ class FusedUpdateModule(torch.nn.Module):
         self._packed = P
 
     @torch.no_grad()
-    def forward(self, net, inp, corr, motn, inverse, num_unique, segments=None):
-        """net, inp (E,H,W,128) fp16; corr (E,H,W,200) fp16 (196 used) or a
+    def forward(self, net, inp, corr, motn, inverse, num_unique, segments=None, inp_frames=None):
+        """net, inp (E,H,W,128) fp16 (inp may be None when inp_frames is given);
+        inp_frames: optional (U,H,W,128) fp16 context features per source-frame
+        slot (edge e's inp is inp_frames[inverse[e]]); corr (E,H,W,200) fp16 (196 used) or a
         PendingLookup; motn
         (E,4,H,W) fp32; inverse (E) frame slot of each edge's source, num_unique
         frames; segments = optional (seg_ptr (U+1), seg_idx (E)) int64 CSR of
@@ -232,11 +247,25 @@ class FusedUpdateModule(torch.nn.Module):
         gb = torch.addmm(P["glo_b"], glo, P["glo_w"].t())          # (E, 384): z | r | q
         z = e16(128)
         rn = e16(128)
-        conv([(net, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["zr"], 256, 3, bias=P["zr_b"],
-             bbias=gb[:, :256].contiguous(), epi=EPI_GRU_ZR, h=net, zout=z, rnet=rn)
         net_new = e16(128)
-        conv([(rn, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["q"], 128, 3, bias=P["q_b"],
-             bbias=gb[:, 256:].contiguous(), epi=EPI_GRU_Q, h=net, z=z, out=net_new)
+        if inp_frames is not None and droid_backends.gru_pre_supported(H, W):
+            U = inp_frames.shape[0]
+            pre = torch.empty((U, H, W, 384), dtype=torch.float16, device=dev)
+            conv([(inp_frames, 0, 128)], P["inp_zrq"], 384, 3, out=pre)
+            pidx = inverse if inverse.dtype == torch.int64 else inverse.long()
+            droid_backends.conv_gru_pre_f16([(net, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["zr_x"], 256, P["zr_b"],
+                                            gb[:, :256].contiguous(), EPI_GRU_ZR, pre, pidx, 0, h=net, zout=z,
+                                            rnet=rn)
+            droid_backends.conv_gru_pre_f16([(rn, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["q_x"], 128, P["q_b"],
+                                            gb[:, 256:].contiguous(), EPI_GRU_Q, pre, pidx, 256, h=net, z=z,
+                                            out=net_new)
+        else:
+            if inp is None:
+                inp = inp_frames[inverse]
+            conv([(net, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["zr"], 256, 3, bias=P["zr_b"],
+                 bbias=gb[:, :256].contiguous(), epi=EPI_GRU_ZR, h=net, zout=z, rnet=rn)
+            conv([(rn, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["q"], 128, 3, bias=P["q_b"],
+                 bbias=gb[:, 256:].contiguous(), epi=EPI_GRU_Q, h=net, z=z, out=net_new)
 
         if droid_backends.dw_head_supported(H, W):
             head = torch.zeros((E, H, W, 4), dtype=torch.float32, device=dev)

@@ -124,6 +124,22 @@ int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstrid
                         const void* h, int h_cstride, const void* z, int z_cstride, void* zout,
                         void* rnet, int gru_ch, void* out32, hipStream_t stream);
 
+/* ConvGRU z|r and q gates (modules/gru.py:19-32) with the context-feature term
+ * factored out per source frame: the gate argument is conv3x3(srcs) (the srcs
+ * exclude inp) + bias + bbias[b] + pre[pre_idx[b], y, x, pre_coff + co], where
+ * pre (frames,H,W,pre_cstride) fp16 holds conv3x3(inp[frame]) with the inp
+ * columns of the gate weights - identical for every edge leaving that frame.
+ * epi is 1 (z|r gates, Cout 256) or 2 (GRU update, Cout 128); the other
+ * arguments as droid_conv_nhwc_f16 (ks 3, no act).  Runs on the band tiles
+ * only (W in {16,32,64}, H*W % 256 == 0 for z|r, % 384 for q), else returns
+ * DROID_UNSUPPORTED. */
+int droid_conv_gru_pre_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc,
+                           const void* wp, const float* bias, const float* bbias, int B, int H, int W,
+                           int Cout, int epi, void* out, int out_cstride, int out_coff, const void* h,
+                           int h_cstride, const void* z, int z_cstride, void* zout, void* rnet, int gru_ch,
+                           const void* pre, const long long* pre_idx, int pre_cstride, int pre_coff,
+                           hipStream_t stream);
+
 /* UpdateModule delta/weight heads fused (droid_net.py:95-103, 132-133): conv3x3
  * srcs -> 256 (wp, bias, ReLU; the delta.0 || weight.0 hidden map) feeding the
  * block-diagonal conv3x3 256 -> 4 (hw [48][256] fp16, row = tap*4 + c, tap =

@@ -2,7 +2,8 @@
 prologue (entry -> first stage's operands landed), main loop, epilogue, and the
 gap between consecutive workgroups on the same CU, in shader clocks.
 
-usage: python scripts/conv_timeline.py [edges] [zr|q|ce2|dw|dwh]
+usage: python scripts/conv_timeline.py [edges] [zr|q|zrp|qp|ce2|dw|dwh]
+(zrp / qp: the gates with the inp term per source frame, droid_conv_gru_pre_f16)
 (runs on the profiling build: make -C droid-slam_amd/csrc prof)"""
 import os
 import sys
@@ -28,8 +29,9 @@ g = torch.Generator(device=dev).manual_seed(0)
 t = lambda c: (torch.randn((E, H, W, c), generator=g, device=dev) * 0.5).half()
 net, inp, cf, ff = t(128), t(128), t(128), t(64)
 srcs4 = [(net, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)]
+srcs3 = [(net, 0, 128), (cf, 0, 128), (ff, 0, 64)]
 cfg = {"zr": (srcs4, 256), "q": (srcs4, 128), "ce2": ([(net, 0, 128)], 128), "dw": ([(net, 0, 128)], 256),
-       "dwh": ([(net, 0, 128)], 256)}[which]
+       "dwh": ([(net, 0, 128)], 256), "zrp": (srcs3, 256), "qp": (srcs3, 128)}[which]
 srcs, cout = cfg
 cin = sum(c for _, _, c in srcs)
 w = torch.randn((cout, cin, 3, 3), generator=g, device=dev) * 0.02
@@ -41,6 +43,16 @@ if which == "dwh":   # delta.0 || weight.0 with both heads fused (EPI_DWHEAD)
     hw = pack_head_taps(torch.randn((4, 256, 3, 3), generator=g, device=dev) * 0.02)
     head = torch.zeros((E, H, W, 4), device=dev)
     run = lambda: droid_backends.conv_dw_head_f16(srcs, wp, bias, hw, head)
+elif which in ("zrp", "qp"):   # 8 edges per source frame, as in the C3 graph
+    pre = t(384)[: E // 8].contiguous()
+    pidx = torch.arange(E, device=dev) // 8
+    if os.environ.get("TL_PIDX0"):   # experiment: every edge reads frame 0's pre map (L2-resident)
+        pidx.zero_()
+    zo, rn = t(128), t(128)
+    epi = droid_backends.EPI_GRU_ZR if which == "zrp" else droid_backends.EPI_GRU_Q
+    kw = dict(zout=zo, rnet=rn) if which == "zrp" else dict(z=zo, out=out)
+    run = lambda: droid_backends.conv_gru_pre_f16(srcs, wp, cout, bias, None, epi, pre, pidx,
+                                                  0 if which == "zrp" else 256, h=net, **kw)
 else:
     run = lambda: droid_backends.conv_nhwc_f16(srcs, wp, cout, 3, bias=bias, act=1, out=out)
 for _ in range(3):

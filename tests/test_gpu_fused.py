@@ -466,3 +466,93 @@ def test_factor_graph_update_stereo(corr_impl):
     np.testing.assert_allclose(host(video.poses[:n]), ref["poses"][:n], atol=1e-4)
     np.testing.assert_allclose(host(video.disps[:n]), np.maximum(ref["disps"][:n], 1e-3), atol=1e-4)
     assert torch.isfinite(g.net.float()).all()
+
+
+@pytest.mark.parametrize("B,H,W", [(3, 12, 64), (2, 24, 32), (4, 48, 16)])
+def test_conv_gru_pre_epilogues(B, H, W):
+    """Gates with the inp term factored per source frame (droid_conv_gru_pre_f16):
+    conv3x3 over (h | corr | flow) + pre[pre_idx[b]] with pre = conv3x3(inp_frames)
+    vs torch fp32 over the full 448-channel input (modules/gru.py:19-32)."""
+    import droid_backends
+    from droid_backends import EPI_GRU_Q, EPI_GRU_ZR
+    from droid_mi355x.fused import pack_conv
+    g = torch.Generator(device=DEV).manual_seed(13)
+    mk = lambda n, c: torch.randn((n, H, W, c), generator=g, device=DEV).half()
+    F_ = 2
+    idx = torch.tensor([1, 0, 1, 0][:B], dtype=torch.int64, device=DEV)
+    inp_f = mk(F_, 128)
+    h = torch.tanh(mk(B, 128).float()).half()
+    cf, ff = mk(B, 128), mk(B, 64)
+    xs = [h, inp_f[idx].contiguous(), cf, ff]
+    wzr = torch.randn((256, 448, 3, 3), generator=g, device=DEV) / (448 * 9) ** 0.5
+    wq = torch.randn((128, 448, 3, 3), generator=g, device=DEV) / (448 * 9) ** 0.5
+    bzr, bq = torch.randn(256, generator=g, device=DEV), torch.randn(128, generator=g, device=DEV)
+    bbzr, bbq = torch.randn((B, 256), generator=g, device=DEV), torch.randn((B, 128), generator=g, device=DEV)
+    keep = lambda w: torch.cat([w[:, :128], w[:, 256:]], 1)
+    pre = torch.empty((F_, H, W, 384), dtype=torch.float16, device=DEV)
+    droid_backends.conv_nhwc_f16([(inp_f, 0, 128)], pack_conv(torch.cat([wzr[:, 128:256], wq[:, 128:256]]), [128]),
+                                 384, 3, out=pre)
+    z = torch.empty((B, H, W, 128), dtype=torch.float16, device=DEV)
+    rn = torch.empty_like(z)
+    droid_backends.conv_gru_pre_f16([(h, 0, 128), (cf, 0, 128), (ff, 0, 64)], pack_conv(keep(wzr), [128, 128, 64]),
+                                    256, bzr, bbzr, EPI_GRU_ZR, pre, idx, 0, h=h, zout=z, rnet=rn)
+    gates = torch.sigmoid(_conv_ref(xs, wzr, bzr, bbzr))
+    np.testing.assert_allclose(host(z.float()), host(gates[..., :128]), atol=3e-3)
+    np.testing.assert_allclose(host(rn.float()), host(gates[..., 128:] * h.float()), atol=3e-3)
+    hn = torch.empty_like(z)
+    droid_backends.conv_gru_pre_f16([(rn, 0, 128), (cf, 0, 128), (ff, 0, 64)], pack_conv(keep(wq), [128, 128, 64]),
+                                    128, bq, bbq, EPI_GRU_Q, pre, idx, 256, h=h, z=z, out=hn)
+    q = torch.tanh(_conv_ref([rn] + xs[1:], wq, bq, bbq))
+    ref = (1 - z.float()) * h.float() + z.float() * q
+    np.testing.assert_allclose(host(hn.float()), host(ref), atol=4e-3)
+
+
+def test_conv_gru_pre_rejects_unsupported_shape():
+    """No band tile for the shape -> DROID_UNSUPPORTED raised, nothing silently computed."""
+    import droid_backends
+    from droid_backends import EPI_GRU_ZR
+    from droid_mi355x.fused import pack_conv
+    B, H, W = 1, 10, 24
+    t = lambda c: torch.zeros((B, H, W, c), dtype=torch.float16, device=DEV)
+    h, cf, ff = t(128), t(128), t(64)
+    pre = torch.zeros((1, H, W, 384), dtype=torch.float16, device=DEV)
+    w = pack_conv(torch.zeros((256, 320, 3, 3), device=DEV), [128, 128, 64])
+    with pytest.raises(RuntimeError):
+        droid_backends.conv_gru_pre_f16([(h, 0, 128), (cf, 0, 128), (ff, 0, 64)], w, 256, None, None, EPI_GRU_ZR,
+                                        pre, torch.zeros(1, dtype=torch.int64, device=DEV), 0, h=h, zout=t(128),
+                                        rnet=t(128))
+
+
+def test_fused_update_inp_frames_matches_per_edge_inp():
+    """FusedUpdateModule with per-frame context features (gate inp term per
+    source frame) vs the same module on per-edge inp copies, and vs UpdateModule."""
+    from droid_mi355x.fused import FusedUpdateModule
+    from droid_mi355x.update import UpdateModule
+    E, H, W = 6, 24, 32
+    m = UpdateModule().to(DEV).eval()
+    det_fill(m)
+    f = FusedUpdateModule(m)
+    g = torch.Generator(device=DEV).manual_seed(19)
+    ii = torch.tensor([0, 0, 1, 2, 2, 3], device=DEV)
+    jj = torch.tensor([1, 2, 0, 1, 3, 2], device=DEV)
+    uq, inv = torch.unique(ii, return_inverse=True)
+    net = torch.tanh(torch.randn((1, E, 128, H, W), generator=g, device=DEV)).half()
+    inpf = torch.relu(torch.randn((len(uq), 128, H, W), generator=g, device=DEV)).half()
+    inp = inpf[inv].unsqueeze(0)
+    corr = (2 * torch.randn((1, E, 196, H, W), generator=g, device=DEV)).half()
+    flow = (4 * torch.randn((1, E, 4, H, W), generator=g, device=DEV)).clamp(-64, 64)
+    nhwc = lambda t: t[0].permute(0, 2, 3, 1).contiguous()
+    c200 = torch.zeros((E, H, W, 200), dtype=torch.float16, device=DEV)
+    c200[..., :196] = nhwc(corr)
+    with torch.no_grad():
+        rn, rd, rw, re, _ = m(net.float(), inp.float(), corr.float(), flow, ii, jj)
+        an, ad, aw, ae = f(nhwc(net), nhwc(inp), c200, flow[0], inv, len(uq))
+        bn, bd, bw, be = f(nhwc(net), None, c200, flow[0], inv, len(uq),
+                           inp_frames=inpf.permute(0, 2, 3, 1).contiguous())
+    np.testing.assert_allclose(host(bn.float()), host(an.float()), atol=4e-3)
+    np.testing.assert_allclose(host(bd), host(ad), atol=1e-2 * max(1.0, float(ad.abs().max())))
+    np.testing.assert_allclose(host(bw), host(aw), atol=4e-3)
+    np.testing.assert_allclose(host(bn.float()), host(nhwc(rn)), atol=1.5e-2)
+    np.testing.assert_allclose(host(bd), host(rd), atol=3e-2 * max(1.0, float(rd.abs().max())))
+    np.testing.assert_allclose(host(bw), host(rw), atol=1.5e-2)
+    np.testing.assert_allclose(host(be), host(re), atol=1e-3 + 2e-2 * float(re.abs().max()))
