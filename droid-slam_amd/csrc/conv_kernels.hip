@@ -864,6 +864,10 @@ struct Band {
   static_assert(WM * WN == 8 && FM * 16 * WM == TMX, "band tile");
 };
 constexpr int kLdsMax = 163840;
+// profiling builds: int64 slots per workgroup (hw id, entry, loop start, loop end,
+// epilogue stores issued, drained (wave 0), pass 1 written, pass-2 loads issued,
+// staging barrier passed, last wave drained)
+constexpr int kProfSlots = 10;
 
 __device__ __forceinline__ void wait_vmcnt(int n) {
   // n is wave-uniform; s_waitcnt takes an immediate
@@ -899,15 +903,19 @@ __device__ __forceinline__ int frag_row(int wm, int i) {
 // range reduction, ~50 KB of straight-line code fetched cold once per tile
 // (the timeline measured 20k clocks per 384x128 epilogue).
 __device__ __forceinline__ float tanh_fast(float x) {
-  // 1 - 2 / (1 + e^(2x)): branch-free, saturates to +-1; abs error ~1e-7, far
-  // below the fp16 rounding of the gate that follows
-  return 1.0f - 2.0f / (1.0f + __expf(2.0f * x));
+  // 1 - 2 / (1 + e^(2x)) with the hardware reciprocal (v_rcp_f32, 1 ulp) in
+  // place of the IEEE division sequence (10 VALU ops, the band epilogue's
+  // largest cost): branch-free, saturates to +-1; abs error ~1e-7, far below
+  // the fp16 rounding of the gate that follows
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x));
 }
+// sigmoid for fp16-rounded gates: 1 / (1 + e^-x) with the hardware reciprocal
+__device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
 template <int TMX, int TN, int FM, int FN, int WM = 4, bool CONTIG = false, int NT = 512, int EPI = -1>
 __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
                                               int n0, int wm, int wn, int lane, int tid,
-                                              const float* bpre = nullptr) {
+                                              const float* bpre = nullptr, long long* prof = nullptr) {
   constexpr int ER = TN + 8, PPR = TN / 8;
   const int HW = a.H * a.W;
   const int b = (int)(m0 / HW);  // a tile never straddles two images
@@ -952,7 +960,7 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
         const float v = acc[i][j][k] + bv;
         float o;
         if constexpr (kPre) o = v;
-        else if constexpr (EPI == EPI_GRU_ZR) o = sigmoidf_(v);
+        else if constexpr (EPI == EPI_GRU_ZR) o = sigmoid_fast(v);
         else if constexpr (EPI == EPI_GRU_Q) o = tanh_fast(v);
         else if constexpr (EPI == EPI_ACT) o = relu ? fmaxf(v, 0.f) : v;
         else if (epi == EPI_GRU_ZR) o = sigmoidf_(v);
@@ -961,53 +969,61 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
         smem[r * ER + c] = (_Float16)o;
       }
   }
+  if (prof && tid == 0) prof[6] = (long long)__builtin_amdgcn_s_memtime();  // pass 1 written
   static_assert((TMX * PPR) % NT == 0, "band epilogue: whole store rounds");
   constexpr int RND = TMX * PPR / NT;
   // GRU epilogues: every round's h (and z) pieces are loaded here, all in flight
   // together while the staging barrier waits (issued inside the store loop they
   // were serialised behind the previous round's store: one HBM latency per round)
   constexpr bool kPreH = EB == EPI_GRU_ZR || EB == EPI_GRU_Q;
+  // round q of thread tid: tile row r0 + q*RQ, 16-B piece p (NT % PPR == 0), so
+  // every global address is a per-thread base plus q times a uniform row step
+  static_assert(NT % PPR == 0, "band epilogue: rounds are whole rows");
+  constexpr int RQ = NT / PPR;
+  const int r0 = tid / PPR, p = tid % PPR;
+  const int c = n0 + p * 8;
+  const long mrow = m0 + r0;
+  const bool rhalf = epi == EPI_GRU_ZR && c >= a.gru_ch;
   half8 hpre[kPreH ? RND : 1], zpre[EB == EPI_GRU_Q ? RND : 1], ppre[kPre ? RND : 1];
-  // pixel m of image b -> pixel of its source frame in the pre map
-  const long pshift = kPre ? ((long)a.pre_idx[b] - b) * HW : 0;
   if constexpr (kPreH) {
+    // pixel m of image b -> pixel of its source frame in the pre map
+    const long pshift = kPre ? ((long)a.pre_idx[b] - b) * HW : 0;
+    const __half* const pp = kPre ? a.pre + (mrow + pshift) * a.pre_cstride + a.pre_coff + c : nullptr;
+    const __half* const hp = a.h + mrow * a.h_cstride + c - (EB == EPI_GRU_ZR ? a.gru_ch : 0);
+    const __half* const zp = EB == EPI_GRU_Q ? a.z + mrow * a.z_cstride + c : nullptr;
+    const long pstep = (long)RQ * a.pre_cstride, hstep = (long)RQ * a.h_cstride, zstep = (long)RQ * a.z_cstride;
 #pragma unroll
     for (int q = 0; q < RND; ++q) {
-      const int idx = tid + q * NT;
-      const int r = idx / PPR, p = idx - r * PPR;
-      const long m = m0 + r;
-      const int c = n0 + p * 8;
-      if constexpr (kPre) ppre[q] = *reinterpret_cast<const half8*>(a.pre + (m + pshift) * a.pre_cstride + a.pre_coff + c);
+      if constexpr (kPre) ppre[q] = *reinterpret_cast<const half8*>(pp + q * pstep);
       if constexpr (EB == EPI_GRU_Q) {
-        hpre[q] = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c);
-        zpre[q] = *reinterpret_cast<const half8*>(a.z + m * a.z_cstride + c);
-      } else if (c >= a.gru_ch) {
-        hpre[q] = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c - a.gru_ch);
+        hpre[q] = *reinterpret_cast<const half8*>(hp + q * hstep);
+        zpre[q] = *reinterpret_cast<const half8*>(zp + q * zstep);
+      } else if (rhalf) {
+        hpre[q] = *reinterpret_cast<const half8*>(hp + q * hstep);
       }
     }
   }
+  if (prof && tid == 0) prof[7] = (long long)__builtin_amdgcn_s_memtime();  // pass-2 loads issued
   __syncthreads();
+  if (prof && tid == 0) prof[8] = (long long)__builtin_amdgcn_s_memtime();  // staging barrier passed
   // (2a) every round's output piece computed first, (2b) then all stores: with
   // a store inside each round, the in-order vmcnt wait for round q+1's h / z /
   // pre pieces also drained round q's stores (gfx9 counts stores in vmcnt) -
-  // one store round trip per round, ~26k clocks per 256x256 tile measured
+  // one store round trip per round
   half8 outv[RND];
 #pragma unroll  // all rounds' LDS reads in flight together
   for (int q = 0; q < RND; ++q) {
-    const int idx = tid + q * NT;
-    const int r = idx / PPR, p = idx - r * PPR;
-    const long m = m0 + r;
-    const int c = n0 + p * 8;
-    half8 v = *reinterpret_cast<const half8*>(&smem[r * ER + p * 8]);
+    const long m = mrow + q * RQ;
+    half8 v = *reinterpret_cast<const half8*>(&smem[(r0 + q * RQ) * ER + p * 8]);
     if constexpr (kPre) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float x = (float)v[e] + (float)ppre[q][e];
-        v[e] = (_Float16)(EB == EPI_GRU_ZR ? sigmoidf_(x) : tanh_fast(x));
+        v[e] = (_Float16)(EB == EPI_GRU_ZR ? sigmoid_fast(x) : tanh_fast(x));
       }
     }
     if (epi == EPI_GRU_ZR) {
-      if (c >= a.gru_ch) {
+      if (rhalf) {
         half8 h;
         if constexpr (kPreH) h = hpre[q];
         else h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c - a.gru_ch);
@@ -1032,23 +1048,17 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
     outv[q] = v;
   }
   __builtin_amdgcn_sched_barrier(0);
-  __half* const zout = a.zout;
-  __half* const rnet = a.rnet;
-  __half* const out = a.out;
-  const int gch = a.gru_ch, ocs = a.out_cstride, ooff = a.out_coff;
-#pragma unroll
-  for (int q = 0; q < RND; ++q) {
-    const int idx = tid + q * NT;
-    const int r = idx / PPR, p = idx - r * PPR;
-    const long m = m0 + r;
-    const int c = n0 + p * 8;
-    if (epi == EPI_GRU_ZR) {
-      if (c >= gch) *reinterpret_cast<half8*>(rnet + m * gch + c - gch) = outv[q];
-      else *reinterpret_cast<half8*>(zout + m * gch + c) = outv[q];
-    } else {
-      *reinterpret_cast<half8*>(out + m * ocs + ooff + c) = outv[q];
-    }
+  __half* dst;
+  long dstep;
+  if (epi == EPI_GRU_ZR) {
+    dst = rhalf ? a.rnet + mrow * a.gru_ch + c - a.gru_ch : a.zout + mrow * a.gru_ch + c;
+    dstep = (long)RQ * a.gru_ch;
+  } else {
+    dst = a.out + mrow * a.out_cstride + a.out_coff + c;
+    dstep = (long)RQ * a.out_cstride;
   }
+#pragma unroll
+  for (int q = 0; q < RND; ++q) *reinterpret_cast<half8*>(dst + q * dstep) = outv[q];
 }
 
 // EPI_DWHEAD (band <256,256> only): the delta/weight heads (droid_net.py:
@@ -1262,7 +1272,7 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   // timeline (profiling builds of the call only): s_memtime at entry, loop
   // start (first stage's operands landed), loop end and exit, plus the CU id
 #if DROID_CONV_PROFILE
-  long long* const prof = a.prof ? a.prof + 6 * blockIdx.x : nullptr;
+  long long* const prof = a.prof ? a.prof + kProfSlots * blockIdx.x : nullptr;
 #else
   long long* const prof = nullptr;  // the hooks cost the 256x256 tile registers: profiling builds only
 #endif
@@ -1364,12 +1374,15 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
     dwhead_epilogue<FM, FN>(a, acc, smem, m0, wm, wn, lane, tid);
   } else {
     band_epilogue<TMX, TN, FM, FN, 4, false, 512, EPI>(a, acc, smem, m0, n0, wm, wn, lane, tid,
-                                                      kPreBias ? bpre : nullptr);
+                                                      kPreBias ? bpre : nullptr, prof);
   }
   if (prof) {
     if (tid == 0) prof[4] = (long long)__builtin_amdgcn_s_memtime();  // stores issued
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tid == 0) prof[5] = (long long)__builtin_amdgcn_s_memtime();  // stores drained
+    // the last wave's drain (the workgroup's resources free only then)
+    if (lane == 0) atomicMax(reinterpret_cast<unsigned long long*>(prof + 9),
+                             (unsigned long long)__builtin_amdgcn_s_memtime());
   }
 }
 

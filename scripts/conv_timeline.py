@@ -60,7 +60,7 @@ for _ in range(3):
 torch.cuda.synchronize()
 tile = {256: 256, 128: 384}[cout]
 nwg = E * H * W // tile
-prof = torch.zeros(nwg * 6, dtype=torch.int64, device=dev)
+prof = torch.zeros(nwg * 10, dtype=torch.int64, device=dev)
 lib.droid_conv_set_profile(ctypes.c_void_p(prof.data_ptr()))
 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 s.record()
@@ -69,7 +69,7 @@ e.record()
 torch.cuda.synchronize()
 lib.droid_conv_set_profile(None)
 ms = s.elapsed_time(e)
-p = prof.view(nwg, 6).cpu().numpy()
+p = prof.view(nwg, 10).cpu().numpy()
 assert (p[:, 1] > 0).all(), "profile not written (kernel not the band kernel?)"
 hw = p[:, 0]
 cu = ((hw >> 32) & 15) * 256 + ((hw >> 8) & 0xff)   # XCC id, then SE_ID[15:13] | SH_ID[12] | CU_ID[11:8]
@@ -78,7 +78,7 @@ gaps = []
 for c in np.unique(cu):
     q = p[cu == c]
     q = q[np.argsort(q[:, 1])]
-    gaps.extend((q[1:, 1] - q[:-1, 5]).tolist())
+    gaps.extend((q[1:, 1] - np.maximum(q[:-1, 5], q[:-1, 9])).tolist())
 gaps = np.asarray(gaps)
 tot = pro + loop + epi + drain
 span_clk = np.median(tot) * nwg / len(np.unique(cu)) + np.median(gaps) * (nwg / len(np.unique(cu)) - 1)
@@ -90,6 +90,11 @@ for name, v in (("prologue", pro), ("main loop", loop), ("epilogue issue", epi),
 stages = (cin // 64 if cin % 64 == 0 else cin // 64 + 1) * 9
 tn = 256 if cout == 256 else 128
 floor = 64 * (tile // 64) * (tn // 32)   # 2 waves/SIMD x 2*FM*FN MFMAs x 16 clk
+if (p[:, 6] > 0).all():   # band_epilogue sub-phases (wave 0) and the last wave's drain
+    for name, v in (("  pass 1 (acc -> LDS)", p[:, 6] - p[:, 3]), ("  pass-2 load issue", p[:, 7] - p[:, 6]),
+                    ("  staging barrier", p[:, 8] - p[:, 7]), ("  pass 2 + stores", p[:, 4] - p[:, 8]),
+                    ("last wave drained after wave 0", p[:, 9] - p[:, 5])):
+        print("  %-30s median %8.0f clk  p90 %8.0f" % (name, np.median(v), np.percentile(v, 90)))
 print("  main loop per stage: %.0f clk (%d stages); MFMA-only floor %d clk/stage" % (np.median(loop) / stages, stages,
                                                                                      floor))
 print("  implied clock: %.2f GHz (median WG cycle x WGs per CU / kernel time)" % (span_clk / (ms * 1e-3) / 1e9))
