@@ -40,7 +40,8 @@ ZR_FLOPS_PER_PIXEL = 2 * 256 * 448 * 9
 # the per-edge z|r conv runs over net | corr | flow = 320 channels
 ZR_PRE_FLOPS_PER_PIXEL = 2 * 256 * 320 * 9
 ZR_KERNEL = "conv_band_kernel<256,256>"   # csrc/conv_kernels.hip, chosen for 48x64 maps
-ZR_KERNEL_MATCH = "conv_band_kernel<256, 256"   # its symbol in rocprof / PMC summaries
+ZR_KERNEL_MATCH = "conv_band_kernel<256, 256, false, false, 1>"   # its symbol in rocprof / PMC summaries
+ZRP_KERNEL_MATCH = "conv_band_kernel<256, 256, false, false, 6>"  # ... the factored-gate instantiation
 LOOKUP_KERNEL = "corr_pyramid_f16_r3_kernel"
 # SURVEY.md §8d whole-iteration floors.  Update-operator convs per edge-pixel:
 # corr_encoder 1x1 196->128 + 3x3 128->128, flow_encoder 7x7 4->128 + 3x3 128->64,
@@ -327,7 +328,8 @@ def main():
             roofline = {"kernel": "%s (ConvGRU z|r gates, 3x3 %d->256, fp16 MFMA%s)"
                                   % (ZR_KERNEL, 320 if factored else 448, ", inp term per source frame" if factored else ""),
                         "bound": "mfma", "achieved": tf, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-                        "frac": tf / PEAK_F16_TFLOPS, "traffic": load_traffic("conv_zr", e_local, ZR_KERNEL_MATCH),
+                        "frac": tf / PEAK_F16_TFLOPS, "traffic": load_traffic("conv_zr", e_local,
+                                                                                ZRP_KERNEL_MATCH if factored else ZR_KERNEL_MATCH),
                         "launch_ms": zr_ms, "algorithmic_flops_per_launch": flops}
         else:
             roofline, lookup_roof = lookup_roof, None

@@ -28,7 +28,7 @@ def per_kernel(counter):
             continue
         name = r["Kernel_Name"]
         key = ("copy" if name.startswith("__amd_rocclr_copyBuffer") and len(out.get("copy", [])) < 3 else
-               "zr" if ("conv_band_kernel<256, 256," in name or "conv_rows_kernel" in name) else
+               "zr" if "conv_band_kernel<256, 256, false, false, 6>" in name else
                "lookup" if ("corr_ce0_kernel" in name or "corr_pyramid_f16_r3_kernel" in name) else None)
         if key:
             out.setdefault(key, []).append(float(r["Counter_Value"]))
@@ -45,7 +45,8 @@ res = {"calibration": {"fetch_bytes_per_unit": kf, "write_bytes_per_unit": kw,
                        "raw_fetch": fetch["copy"], "raw_write": write["copy"]}}
 # fused lookup + corr_encoder[0]: window reads + coords + 128-channel fp16 output per edge
 LOOKUP_CE0 = 4 * 64 * 2 * 3072 + 2 * 4 * 3072 + 128 * 2 * 3072
-for key, name, algo in (("zr", "conv_zr", 2 * 256 * 448 * 9 * 3072 * E), ("lookup", "corr_lookup", LOOKUP_CE0 * E)):
+# z|r gates with the inp term per source frame: 3x3 over net | corr | flow (320 channels)
+for key, name, algo in (("zr", "conv_zr", 2 * 256 * 320 * 9 * 3072 * E), ("lookup", "corr_lookup", LOOKUP_CE0 * E)):
     fb = kf * min(fetch[key])
     wb = kw * min(write[key])
     d = {"edges": E, "kernel": KNAME.get(key), "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,

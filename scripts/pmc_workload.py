@@ -1,6 +1,8 @@
 """Workload for the PMC traffic passes (run under rocprofv3 --pmc; see
 scripts/pmc_traffic.sh): a 1 GiB device copy (calibration of the FETCH/WRITE
-counters on a known byte count), then the C3 ZR gate conv and the C3 4-level
+counters on a known byte count), then the C3 ZR gate conv as update() runs it
+(over net | corr | flow, the inp term per source frame of bench.py's C3 edge
+list: droid_conv_gru_pre_f16) and the C3 4-level
 correlation lookup fused with corr_encoder[0] (corr_lookup_ce0 on the 8x8-tiled volume), each launched
 3 times on synthetic data."""
 import os
@@ -12,6 +14,7 @@ import torch
 
 import droid_backends
 from droid_mi355x.corr import CorrBlock
+from droid_mi355x import synthetic
 from droid_mi355x.fused import pack_conv
 
 E, H, W = 2048, 48, 64
@@ -26,17 +29,21 @@ torch.cuda.synchronize()
 del x, y
 
 t = lambda c: (torch.randn((E, H, W, c), generator=g, device=dev) * 0.5).half()
-net, inp, cf, ff = t(128), t(128), t(128), t(64)
-w = torch.randn((256, 448, 3, 3), generator=g, device=dev) * 0.02
-wp = pack_conv(w, [128, 128, 128, 64])
+net, cf, ff = t(128), t(128), t(64)
+ii_c3, _ = synthetic.c3_edges(256, E, rng=np.random.default_rng(1003))   # bench.py's C3 graph
+uniq, inverse = np.unique(ii_c3, return_inverse=True)
+pre = (torch.randn((len(uniq), H, W, 384), generator=g, device=dev) * 0.5).half()
+pidx = torch.as_tensor(inverse.astype(np.int64), device=dev)
+w = torch.randn((256, 320, 3, 3), generator=g, device=dev) * 0.02
+wp = pack_conv(w, [128, 128, 64])
 bias = torch.zeros(256, device=dev)
 bb = torch.zeros((E, 256), device=dev)
 z, rn = torch.empty_like(net), torch.empty_like(net)
 for _ in range(3):
-    droid_backends.conv_nhwc_f16([(net, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)], wp, 256, 3, bias=bias,
-                                 bbias=bb, epi=droid_backends.EPI_GRU_ZR, h=net, zout=z, rnet=rn)
+    droid_backends.conv_gru_pre_f16([(net, 0, 128), (cf, 0, 128), (ff, 0, 64)], wp, 256, bias, bb,
+                                    droid_backends.EPI_GRU_ZR, pre, pidx, 0, h=net, zout=z, rnet=rn)
 torch.cuda.synchronize()
-del net, inp, cf, ff, z, rn
+del net, cf, ff, z, rn, pre
 
 nf = 256
 f = torch.randn((1, nf, 128, H, W), generator=g, device=dev).half()
