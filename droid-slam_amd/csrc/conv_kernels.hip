@@ -912,10 +912,18 @@ __device__ __forceinline__ float tanh_fast(float x) {
 // sigmoid for fp16-rounded gates: 1 / (1 + e^-x) with the hardware reciprocal
 __device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
+// kBandSwap: the main loop multiplies weights x pixels (MFMA A = weight
+// fragment), so a lane's accumulators are 4 consecutive channels of one pixel
+// and the epilogue's LDS staging writes 8 B per fragment instead of four 2-B
+// writes (pass 1 1.6-2x faster).  The 256x256 tile keeps pixels x weights: with
+// the operands swapped its register allocation spills (256 VGPRs + scratch).
+template <int TN>
+constexpr bool kBandSwap = TN != 256;
+
 template <int TMX, int TN, int FM, int FN, int WM = 4, bool CONTIG = false, int NT = 512, int EPI = -1>
 __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
-                                              int n0, int wm, int wn, int lane, int tid,
-                                              const float* bpre = nullptr, long long* prof = nullptr) {
+                                              int n0, int wm, int wn, int lane, int tid, float bcol,
+                                              long long* prof = nullptr) {
   constexpr int ER = TN + 8, PPR = TN / 8;
   const int HW = a.H * a.W;
   const int b = (int)(m0 / HW);  // a tile never straddles two images
@@ -927,47 +935,50 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
   constexpr int EB = kPre ? EPI - kEpiPreShift : EPI;
   const int epi = EB >= 0 ? EB : a.epi;
   const bool relu = a.act == 1;
-  // the lane's column biases: all FN loads issued before the first use (a
-  // per-column conditional load paid one L2 round trip per column)
-  float bvv[FN];
-  if (bpre) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bvv[j] = bpre[j];  // loaded before the main loop
-  } else {
-    const float* const bias = a.bias;
-    const float* const bbias = a.bbias ? a.bbias + (long)b * a.Cout : nullptr;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bvv[j] = 0.f;
-    if (bias) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bvv[j] = bias[n0 + wn * FN * 16 + j * 16 + fr];
-    }
-    if (bbias) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bvv[j] += bbias[n0 + wn * FN * 16 + j * 16 + fr];
-    }
-  }
+  // the tile's column biases (bias + per-image bias, loaded by thread t < TN
+  // before the main loop) go through LDS: with kBandSwap a lane's accumulators
+  // are 4 consecutive channels of one pixel, so each lane needs 4 x FN of them
+  float* const bl = reinterpret_cast<float*>(smem + TMX * ER);
   __syncthreads();  // main-loop LDS reads are done
+  if (tid < TN) bl[tid] = bcol;
+  __syncthreads();
+  auto act = [&](float v) -> float {
+    if constexpr (kPre) return v;
+    else if constexpr (EPI == EPI_GRU_ZR) return sigmoid_fast(v);
+    else if constexpr (EPI == EPI_GRU_Q) return tanh_fast(v);
+    else if constexpr (EPI == EPI_ACT) return relu ? fmaxf(v, 0.f) : v;
+    else if (epi == EPI_GRU_ZR) return sigmoidf_(v);
+    else if (epi == EPI_GRU_Q) return tanhf(v);
+    else return (a.act == 1) ? fmaxf(v, 0.f) : v;
+  };
+  if constexpr (kBandSwap<TN>) {
+    // (1) lane (fr, fq) of fragment (i, j) holds channels 16 j + 4 fq .. + 3 of
+    // pixel row frag_row(i) + fr: one 8-B LDS write per fragment
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int c = wn * FN * 16 + j * 16 + fr;
-    const float bv = bvv[j];
+    for (int j = 0; j < FN; ++j) {
+      const int c = wn * FN * 16 + j * 16 + fq * 4;
+      const floatx4 bv = *reinterpret_cast<const floatx4*>(bl + c);
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i) {
+        half4_t o;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int r = frag_row<FM, WM, CONTIG>(wm, i) + fq * 4 + k;
-        const float v = acc[i][j][k] + bv;
-        float o;
-        if constexpr (kPre) o = v;
-        else if constexpr (EPI == EPI_GRU_ZR) o = sigmoid_fast(v);
-        else if constexpr (EPI == EPI_GRU_Q) o = tanh_fast(v);
-        else if constexpr (EPI == EPI_ACT) o = relu ? fmaxf(v, 0.f) : v;
-        else if (epi == EPI_GRU_ZR) o = sigmoidf_(v);
-        else if (epi == EPI_GRU_Q) o = tanhf(v);
-        else o = (a.act == 1) ? fmaxf(v, 0.f) : v;
-        smem[r * ER + c] = (_Float16)o;
+        for (int k = 0; k < 4; ++k) o[k] = (_Float16)act(acc[i][j][k] + bv[k]);
+        *reinterpret_cast<half4_t*>(&smem[(frag_row<FM, WM, CONTIG>(wm, i) + fr) * ER + c]) = o;
       }
+    }
+  } else {
+    // (1) lane (fr, fq) of fragment (i, j) holds pixel rows frag_row(i) + 4 fq .. + 3
+    // of channel 16 j + fr
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int c = wn * FN * 16 + j * 16 + fr;
+      const float bv = bl[c];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          smem[(frag_row<FM, WM, CONTIG>(wm, i) + fq * 4 + k) * ER + c] = (_Float16)act(acc[i][j][k] + bv);
+    }
   }
   if (prof && tid == 0) prof[6] = (long long)__builtin_amdgcn_s_memtime();  // pass 1 written
   static_assert((TMX * PPR) % NT == 0, "band epilogue: whole store rounds");
@@ -1076,7 +1087,7 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
 //       the caller.
 template <int FM, int FN, int WM = 4, bool CONTIG = false>
 __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
-                                                int wm, int wn, int lane, int tid) {
+                                                int wm, int wn, int lane, int tid, float bcol) {
   constexpr int TMX = 256, TS = 264, YS = 37, NT = 512;
   const int W = a.W, H = a.H, HW = H * W;
   const int R = TMX / W;
@@ -1085,11 +1096,15 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
   const int fr = lane & 15, fq = lane >> 4;
   _Float16* T = smem;             // [256][TS]
   _Float16* Bh = smem + TMX * TS; // [48][TS]
+  float* const bl = reinterpret_cast<float*>(smem + TMX * TS + 48 * TS);  // [256] column biases
   __syncthreads();  // main-loop LDS reads are done
+  if (tid < 256) bl[tid] = bcol;
+  __syncthreads();
+  // lane (fr, fq) of fragment (i, j): pixels frag_row(i) + 4 fq .. + 3 of channel 16 j + fr
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int c = wn * FN * 16 + j * 16 + fr;
-    const float bv = a.bias ? a.bias[c] : 0.f;
+    const float bv = bl[c];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -1284,20 +1299,13 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   }
   issue_halo(0);
   issue_b(0);
-  // the epilogue's bias (+ per-image bias) of this lane's columns, loaded now so
-  // the latency hides under the main loop (the 256-wide tile has no registers
-  // to spare: it loads them in the epilogue)
-  constexpr bool kPreBias = TN != 256 && !DWHEAD;
-  float bpre[kPreBias ? FN : 1];
-  if constexpr (kPreBias) {
-    const int bimg = (int)(m0 / HW);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int co = n0 + wn * FN * 16 + j * 16 + (lane & 15);
-      float bv = a.bias ? a.bias[co] : 0.f;
-      if (a.bbias) bv += a.bbias[(long)bimg * a.Cout + co];
-      bpre[j] = bv;
-    }
+  // column tid's bias (+ per-image bias), loaded now so the latency hides under
+  // the main loop; the epilogue shares them through LDS
+  float bcol = 0.f;
+  if (tid < TN) {
+    const int co = n0 + tid;
+    if (a.bias) bcol = a.bias[co];
+    if (a.bbias) bcol += a.bbias[(long)(m0 / HW) * a.Cout + co];
   }
   if (prof) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1328,6 +1336,7 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
         // one per MFMA with the K-half-0 multiplies (sched_group_barrier), so
         // they land long before their use and the MFMA pipe is not paced by
         // the LDS latency
+        static_assert(kBandSwap<TN>, "the interleaved body runs on the swapped (384-row) tiles");
         __builtin_amdgcn_sched_barrier(0);
         half8 af[2][FM], bf[2][FN];
 #pragma unroll
@@ -1345,7 +1354,7 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
           for (int i = 0; i < FM; ++i)
 #pragma unroll
             for (int j = 0; j < FN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[hk][i], bf[hk][j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[hk][j], af[hk][i], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, FM + FN, 0);
         MfmaReadPairs<FM + FN>::emit();
         __builtin_amdgcn_sched_group_barrier(0x008, 2 * FM * FN - (FM + FN), 0);
@@ -1363,7 +1372,8 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
           for (int i = 0; i < FM; ++i)
 #pragma unroll
             for (int j = 0; j < FN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = kBandSwap<TN> ? __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0)
+                                        : __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
         }
       }
     }
@@ -1371,10 +1381,9 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   if (prof && tid == 0) prof[3] = (long long)__builtin_amdgcn_s_memtime();
   if constexpr (DWHEAD) {
     static_assert(TMX == 256 && TN == 256, "dw/head fusion runs on the 256x256 tile");
-    dwhead_epilogue<FM, FN>(a, acc, smem, m0, wm, wn, lane, tid);
+    dwhead_epilogue<FM, FN>(a, acc, smem, m0, wm, wn, lane, tid, bcol);
   } else {
-    band_epilogue<TMX, TN, FM, FN, 4, false, 512, EPI>(a, acc, smem, m0, n0, wm, wn, lane, tid,
-                                                      kPreBias ? bpre : nullptr, prof);
+    band_epilogue<TMX, TN, FM, FN, 4, false, 512, EPI>(a, acc, smem, m0, n0, wm, wn, lane, tid, bcol, prof);
   }
   if (prof) {
     if (tid == 0) prof[4] = (long long)__builtin_amdgcn_s_memtime();  // stores issued
@@ -1401,7 +1410,7 @@ static bool band_fits(int W, int* nslot, int* nhi) {
   const int nh = ceil_div(ns, 64);
   if (nh > Band<TMX, TN>::MAX_NHI) return false;
   const int lds = 2 * TN * 128 + 2 * nh * 8 * 1024;
-  const int epi = TMX * (TN + 8) * 2;
+  const int epi = TMX * (TN + 8) * 2 + TN * 4;  // staging tile + column biases
   if (lds > kLdsMax || epi > kLdsMax) return false;
   *nslot = ns;
   *nhi = nh;
@@ -1428,7 +1437,7 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
   a.m_tiles = (long)a.B * a.H * a.W / TMX;
   const int main_b = 2 * TN * 128 + 2 * a.nhi * 8 * 1024;
   // EPI_DWHEAD keeps the head weights [48][264] beside the hidden-map tile
-  const int epi_b = TMX * (TN + 8) * 2 + (DWHEAD ? 48 * 264 * 2 : 0);
+  const int epi_b = TMX * (TN + 8) * 2 + TN * 4 + (DWHEAD ? 48 * 264 * 2 : 0);
   const int lds = main_b > epi_b ? main_b : epi_b;
   if (lds > kLdsMax) return fail(kUnsupported, "conv band: LDS");
   const long nwg = a.m_tiles * a.n_tiles;
@@ -1638,7 +1647,6 @@ __global__ void __launch_bounds__(512) flow_enc0_kernel(const float* __restrict_
       const int idx = tid + 512 * u;
       const int ry = idx / W, x = idx - ry * W;
       if (u < nin && ry < RB) {
-        typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
         half4_t h;
 #pragma unroll
         for (int c = 0; c < 4; ++c) h[c] = (_Float16)v[u][c];

@@ -7,6 +7,7 @@ namespace droid {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
 
 constexpr unsigned kOob = 0x80000000u;  // buffer offset past any descriptor: loads return 0
 constexpr int kBufFlags = 0x00020000;   // raw buffer descriptor word 3 (gfx950)
