@@ -939,6 +939,34 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
   // before the main loop) go through LDS: with kBandSwap a lane's accumulators
   // are 4 consecutive channels of one pixel, so each lane needs 4 x FN of them
   float* const bl = reinterpret_cast<float*>(smem + TMX * ER);
+  static_assert((TMX * PPR) % NT == 0, "band epilogue: whole store rounds");
+  constexpr int RND = TMX * PPR / NT;
+  // GRU epilogues: every round's h (and z) pieces are loaded after pass 1, all
+  // in flight together while the staging barrier waits (issued inside the store
+  // loop they were serialised behind the previous round's store)
+  constexpr bool kPreH = EB == EPI_GRU_ZR || EB == EPI_GRU_Q;
+  // round q of thread tid: tile row r0 + q*RQ, 16-B piece p (NT % PPR == 0), so
+  // every global address is a per-thread base plus q times a uniform row step
+  static_assert(NT % PPR == 0, "band epilogue: rounds are whole rows");
+  constexpr int RQ = NT / PPR;
+  const int r0 = tid / PPR, p = tid % PPR;
+  const int c = n0 + p * 8;
+  const long mrow = m0 + r0;
+  const bool rhalf = epi == EPI_GRU_ZR && c >= a.gru_ch;
+  half8 hpre[kPreH ? RND : 1], zpre[EB == EPI_GRU_Q ? RND : 1], ppre[kPre ? RND : 1];
+  // the per-frame term's pieces (pixel m of image b -> pixel of its source
+  // frame): on the 384-row tiles they go out before pass 1 - the accumulators
+  // leave room for them there - so their latency and L1 bandwidth overlap the
+  // staging writes; the 256x256 tile (2 VGPRs short) issues them after pass 1
+  constexpr bool kEarlyPre = kPre && TN != 256;
+  auto load_pre = [&]() {
+    const long pshift = ((long)a.pre_idx[b] - b) * HW;
+    const __half* const pp = a.pre + (mrow + pshift) * a.pre_cstride + a.pre_coff + c;
+    const long pstep = (long)RQ * a.pre_cstride;
+#pragma unroll
+    for (int q = 0; q < RND; ++q) ppre[q] = *reinterpret_cast<const half8*>(pp + q * pstep);
+  };
+  if constexpr (kEarlyPre) load_pre();
   __syncthreads();  // main-loop LDS reads are done
   if (tid < TN) bl[tid] = bcol;
   __syncthreads();
@@ -981,31 +1009,13 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
     }
   }
   if (prof && tid == 0) prof[6] = (long long)__builtin_amdgcn_s_memtime();  // pass 1 written
-  static_assert((TMX * PPR) % NT == 0, "band epilogue: whole store rounds");
-  constexpr int RND = TMX * PPR / NT;
-  // GRU epilogues: every round's h (and z) pieces are loaded here, all in flight
-  // together while the staging barrier waits (issued inside the store loop they
-  // were serialised behind the previous round's store: one HBM latency per round)
-  constexpr bool kPreH = EB == EPI_GRU_ZR || EB == EPI_GRU_Q;
-  // round q of thread tid: tile row r0 + q*RQ, 16-B piece p (NT % PPR == 0), so
-  // every global address is a per-thread base plus q times a uniform row step
-  static_assert(NT % PPR == 0, "band epilogue: rounds are whole rows");
-  constexpr int RQ = NT / PPR;
-  const int r0 = tid / PPR, p = tid % PPR;
-  const int c = n0 + p * 8;
-  const long mrow = m0 + r0;
-  const bool rhalf = epi == EPI_GRU_ZR && c >= a.gru_ch;
-  half8 hpre[kPreH ? RND : 1], zpre[EB == EPI_GRU_Q ? RND : 1], ppre[kPre ? RND : 1];
+  if constexpr (kPre && !kEarlyPre) load_pre();
   if constexpr (kPreH) {
-    // pixel m of image b -> pixel of its source frame in the pre map
-    const long pshift = kPre ? ((long)a.pre_idx[b] - b) * HW : 0;
-    const __half* const pp = kPre ? a.pre + (mrow + pshift) * a.pre_cstride + a.pre_coff + c : nullptr;
     const __half* const hp = a.h + mrow * a.h_cstride + c - (EB == EPI_GRU_ZR ? a.gru_ch : 0);
     const __half* const zp = EB == EPI_GRU_Q ? a.z + mrow * a.z_cstride + c : nullptr;
-    const long pstep = (long)RQ * a.pre_cstride, hstep = (long)RQ * a.h_cstride, zstep = (long)RQ * a.z_cstride;
+    const long hstep = (long)RQ * a.h_cstride, zstep = (long)RQ * a.z_cstride;
 #pragma unroll
     for (int q = 0; q < RND; ++q) {
-      if constexpr (kPre) ppre[q] = *reinterpret_cast<const half8*>(pp + q * pstep);
       if constexpr (EB == EPI_GRU_Q) {
         hpre[q] = *reinterpret_cast<const half8*>(hp + q * hstep);
         zpre[q] = *reinterpret_cast<const half8*>(zp + q * zstep);
