@@ -182,8 +182,28 @@ def ba_sharded(poses, disps, intrinsics, disps_sens, target, weight, eta, ii_hos
                                    poses.device, own=tuple(comm["own"]))
     dx = torch.empty((plan.P, 6), dtype=torch.float32, device=poses.device)
     dz = None if motion_only else torch.empty((plan.K, H * W), dtype=torch.float32, device=poses.device)
+    flat = plan.system.view(-1)
+    idx = reduced_system_index(plan)
     for _ in range(itrs):
         plan.build_system(poses, disps, intrinsics, disps_sens, target, weight, eta)
-        dist.all_reduce(plan.system, op=dist.ReduceOp.SUM, group=comm.get("group"))
+        # only what the Cholesky reads crosses the links: the lower triangle of
+        # A - S and the rhs row, packed (n(n+1)/2 + n doubles, about half of the
+        # (n+1) x ld region)
+        packed = flat.index_select(0, idx)
+        dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=comm.get("group"))
+        flat.index_copy_(0, idx, packed)
         plan.solve_update(poses, disps, intrinsics, disps_sens, target, weight, eta, lm, ep, dx, dz)
     return [dx, dz]
+
+
+def reduced_system_index(plan):
+    """flat positions (row * ld + col) of the augmented system's lower triangle
+    (col <= row < n) and of the rhs row (row n, col < n); cached on the plan."""
+    idx = getattr(plan, "_tri_index", None)
+    if idx is None:
+        n, ld = plan.n, plan.ld
+        r, c = np.tril_indices(n)
+        flat = np.concatenate([r.astype(np.int64) * ld + c, n * ld + np.arange(n, dtype=np.int64)])
+        idx = torch.as_tensor(flat, device=plan.system.device)
+        plan._tri_index = idx
+    return idx

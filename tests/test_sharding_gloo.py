@@ -110,3 +110,23 @@ def test_allreduced_shard_systems_equal_full_system():
     dx_ref, ok2 = oba.solve(A, b, 1e-4, 0.1)
     assert ok1 and ok2
     np.testing.assert_allclose(dx_sum, dx_ref, atol=1e-9)
+
+
+def test_reduced_system_index_covers_lower_triangle_and_rhs():
+    """ba_sharded all-reduces only what the Cholesky reads: the packed index
+    holds every (row, col <= row) of A - S and the rhs row, nothing else."""
+    from types import SimpleNamespace
+    from droid_mi355x.depth_video import reduced_system_index
+    n, ld = 12, 16
+    plan = SimpleNamespace(n=n, ld=ld, system=torch.zeros((n + 1, ld), dtype=torch.float64))
+    idx = reduced_system_index(plan).numpy()
+    assert len(idx) == n * (n + 1) // 2 + n == len(np.unique(idx))
+    r, c = idx // ld, idx % ld
+    assert ((r < n) & (c <= r) | (r == n) & (c < n)).all()
+    # a packed sum over two "ranks" equals the full sum on those positions
+    a, b = torch.randn(n + 1, ld, dtype=torch.float64), torch.randn(n + 1, ld, dtype=torch.float64)
+    out = a.clone().view(-1)
+    out.index_copy_(0, torch.as_tensor(idx), a.view(-1)[idx] + b.view(-1)[idx])
+    full = (a + b).view(-1)
+    assert torch.equal(out[idx], full[idx])
+    assert reduced_system_index(plan) is plan._tri_index   # cached on the plan
