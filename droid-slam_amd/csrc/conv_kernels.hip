@@ -1534,10 +1534,13 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
       dma16(rs, Al_a + (t % kGloRing) * 16384 + c * 8192 + pr * 128, off);
     }
   };
-  float bj[2];
+  // the MFMA multiplies weights x pixels: lane (fr, fq) of block (i, j) holds
+  // channels wave*32 + 16 j + 4 fq .. + 3 of pixel 16 i + fr, so its h values
+  // are one 8-B LDS read and its column sums 4 per j
+  floatx4 bj[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) bj[j] = bias[wave * 32 + j * 16 + fr];
-  float colsum[2] = {0.f, 0.f};
+  for (int j = 0; j < 2; ++j) bj[j] = *reinterpret_cast<const floatx4*>(bias + wave * 32 + j * 16 + fq * 4);
+  floatx4 colsum[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
   // the weight and bias loads land before the ring starts (the counted vmcnt
   // waits below assume only DMAs are outstanding)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1570,30 +1573,35 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], wf[ks][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][j], af[i], acc[i][j], 0, 0, 0);
     }
     // sigmoid(. + b) * h summed over the tile's pixels (h = the tile itself: k == co)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int co = wave * 32 + j * 16 + fr, c = co >> 6, kk = co & 63;
+      const int co = wave * 32 + j * 16 + fq * 4, c = co >> 6, kk = co & 63;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
+        const int r = i * 16 + fr;
+        const half4_t hv = *reinterpret_cast<const half4_t*>(
+            At + c * 8192 + r * 128 + ((((kk >> 3) ^ (r & 7)) << 4) | ((kk & 7) << 1)));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int r = i * 16 + fq * 4 + k;
-          const float hv = (float)*reinterpret_cast<const _Float16*>(
-              At + c * 8192 + r * 128 + ((((kk >> 3) ^ (r & 7)) << 4) | ((kk & 7) << 1)));
-          colsum[j] += sigmoidf_(acc[i][j][k] + bj[j]) * hv;
-        }
+        for (int k = 0; k < 4; ++k)  // v_rcp_f32 sigmoid: no IEEE division
+          colsum[j][k] += sigmoid_fast(acc[i][j][k] + bj[j][k]) * (float)hv[k];
+      }
     }
   }
+  // sum over the 16 pixel lanes (fr) of each channel quadruple
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    float v = colsum[j];
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    if (fq == 0) glo[(long)e * 128 + wave * 32 + j * 16 + fr] = v / (float)HW;
-  }
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float v = colsum[j][k];
+      v += __shfl_xor(v, 1);
+      v += __shfl_xor(v, 2);
+      v += __shfl_xor(v, 4);
+      v += __shfl_xor(v, 8);
+      if (fr == 0) glo[(long)e * 128 + wave * 32 + j * 16 + fq * 4 + k] = v / (float)HW;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1936,7 +1944,7 @@ int droid_gru_global_f16(const void* h, const void* w, const float* bias, float*
                          hipStream_t stream) {
   if (E < 0 || HW <= 0 || !h || !w || !bias || !glo) return fail(kInvalidArgument, "gru_global_f16: bad arguments");
   if (HW % kGloTP || (long)HW * 256 > 0x7fffffffL || (reinterpret_cast<uintptr_t>(h) & 15) ||
-      (reinterpret_cast<uintptr_t>(w) & 15))
+      (reinterpret_cast<uintptr_t>(w) & 15) || (reinterpret_cast<uintptr_t>(bias) & 15))
     return fail(kUnsupported, "gru_global_f16: needs H*W % 64 == 0 and 16-B aligned operands");
   if (E == 0) return kOk;
   static bool attr = false;
