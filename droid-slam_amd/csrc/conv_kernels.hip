@@ -1673,9 +1673,11 @@ __global__ void __launch_bounds__(512) flow_enc0_kernel(const float* __restrict_
     }
   };
   const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fq = lane >> 4;
-  float bj[4];
+  // weights x pixels: lane (fr, fq) of block (f, j) holds channels
+  // wn*64 + 16 j + 4 fq .. + 3 of pixel wm*32 + 16 f + fr (one 8-B LDS write)
+  floatx4 bj[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) bj[j] = bias[wn * 64 + j * 16 + fr];
+  for (int j = 0; j < 4; ++j) bj[j] = *reinterpret_cast<const floatx4*>(bias + wn * 64 + j * 16 + fq * 4);
   int pyx[2];  // band slot of the lane's pixel in fragment f, at tap (-3,-3)
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
@@ -1710,15 +1712,17 @@ __global__ void __launch_bounds__(512) flow_enc0_kernel(const float* __restrict_
 #pragma unroll
       for (int f = 0; f < 2; ++f)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[f], bf[j], acc[f][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[f], acc[f][j], 0, 0, 0);
     }
 #pragma unroll
     for (int f = 0; f < 2; ++f)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 4; ++j) {
+        half4_t o;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          Os[(wm * 32 + f * 16 + fq * 4 + k) * kFeOS + wn * 64 + j * 16 + fr] = (_Float16)fmaxf(acc[f][j][k] + bj[j], 0.f);
+        for (int k = 0; k < 4; ++k) o[k] = (_Float16)fmaxf(acc[f][j][k] + bj[j][k], 0.f);
+        *reinterpret_cast<half4_t*>(&Os[(wm * 32 + f * 16 + fr) * kFeOS + wn * 64 + j * 16 + fq * 4]) = o;
+      }
     __syncthreads();
     const long e = t / tpe;
     const long pix0 = e * HW + (t - e * tpe) * kFeTP;
@@ -1963,8 +1967,8 @@ int droid_gru_global_f16(const void* h, const void* w, const float* bias, float*
 // [128] f32 -> out (E,H,W,128) fp16 = relu(conv7x7(motn) + bias).
 int droid_flow_enc0_f16(const float* motn, const void* w, const float* bias, void* out, int E, int H, int W,
                         hipStream_t stream) {
-  if (E < 0 || H <= 0 || W <= 0 || !motn || !w || !bias || !out)
-    return fail(kInvalidArgument, "flow_enc0_f16: bad arguments");
+  if (E < 0 || H <= 0 || W <= 0 || !motn || !w || !bias || !out || (reinterpret_cast<uintptr_t>(bias) & 15))
+    return fail(kInvalidArgument, "flow_enc0_f16: bad arguments (bias must be 16-B aligned)");
   if (W % 16 || kFeTP % W || (H * W) % kFeTP || (long)E * H * W * 4 > 0x7fffffffL)
     return fail(kUnsupported, "flow_enc0_f16: needs W in {16,32,64,128} and H*W % 128 == 0");
   if (E == 0) return kOk;
