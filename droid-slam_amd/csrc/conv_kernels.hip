@@ -2001,8 +2001,19 @@ __global__ void __launch_bounds__(256) segment_mean_f16_kernel(const __half* __r
   if (q * 8 >= row) return;
   const long e0 = seg_ptr[u], e1 = seg_ptr[u + 1];
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (long e = e0; e < e1; ++e) {
-    const half8 v = *reinterpret_cast<const half8*>(src + seg_idx[e] * row + q * 8);
+  long e = e0;
+  // four rows in flight per thread; summed in edge order (same rounding)
+  for (; e + 4 <= e1; e += 4) {
+    half8 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = __builtin_nontemporal_load(reinterpret_cast<const half8*>(src + seg_idx[e + i] * row + q * 8));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += (float)v[i][k];
+  }
+  for (; e < e1; ++e) {
+    const half8 v = __builtin_nontemporal_load(reinterpret_cast<const half8*>(src + seg_idx[e] * row + q * 8));
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] += (float)v[k];
   }
