@@ -1491,13 +1491,13 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
 //   glo[e][co] = mean over the edge's pixels of sigmoid(w . h + b)[co] * h[co]
 // for a 1x1 128 -> 128 conv w on the hidden state h itself.  One workgroup per
 // edge streams its pixels in 64-pixel tiles by LDS-DMA through a ring of 4
-// tile buffers, three tiles in flight (one in flight left the kernel latency
+// tile buffers, four tiles in flight (one in flight left the kernel latency
 // bound at ~2.5 TB/s); wave w keeps the weight fragments of its output columns
 // 32w .. 32w+31 in registers (32 VGPRs), so the LDS holds only the ring and two
 // workgroups share a CU.  The per-column sums stay in registers and the mean
 // is a plain store - no atomics, deterministic.
 constexpr int kGloTP = 64;
-constexpr int kGloRing = 4;
+constexpr int kGloRing = 5;  // 80 KB: two workgroups fill a CU's 160 KB LDS
 constexpr int kGloLds = kGloRing * 2 * kGloTP * 128;  // the tile ring (bytes)
 
 __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__ h, const __half* __restrict__ w,
@@ -1548,7 +1548,8 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
   for (int t = 0; t < ntile; ++t) {
     // tile t landed: each later tile in flight is 4 DMA instructions of this wave
     const int later = min(kGloRing - 2, ntile - 1 - t);
-    if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if (later >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (later == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
