@@ -81,7 +81,9 @@ def build_state(args, rank, world, device):
     comm = None
     if world > 1:
         ii_l, jj_l, own = sharding.shard_edges(ii, jj, args.frames, rank, world)
-        comm = dict(group=None, own=own, t0=max(1, int(ii.min()) + 1), t1=int(max(ii.max(), jj.max())) + 1)
+        # the global edge list: every rank derives the same reduced-system tile structure from it
+        comm = dict(group=None, own=own, t0=max(1, int(ii.min()) + 1), t1=int(max(ii.max(), jj.max())) + 1,
+                    edges=(ii, jj))
     else:
         ii_l, jj_l = ii, jj
     n = args.frames

@@ -21,15 +21,18 @@ struct BaDev {
   float* dz;                // (K,HW) out
   // plan
   const int *ii, *jj, *kx, *feptr, *fedges, *frptr, *rpose, *redge, *fnb, *fgoff;
-  const int *blka, *blkb, *blkcptr, *rhscptr;
+  const int *blka, *blkb, *blkcptr, *rhscptr, *rhspos;
   const int4 *contrib, *rhscontrib;
+  const int *widef, *wideeoff, *widetasks;  // wide-path frames, their Ei image offsets, (w, IB, JB) tasks
+  const int* slot;                          // tile slot map of the factor [nbr*nbc]
   float* hpart;
   float* gram;
   float* qw;
-  double* M;
+  float* ei;                                // Ei images of the wide-path frames (6 x HW each)
+  double* M;                                // factor tiles, slot s at M + kTile*s
   double* x;
   int* flag;
-  int E, N, H, W, HW, t0, t1, P, K, n, ld, eta_rows, nsplit, nchunk, gpw, nblk;
+  int E, N, H, W, HW, t0, t1, P, K, n, nbc, eta_rows, nsplit, nchunk, gpw, nblk, nwide;
   float lm, ep;
 };
 
@@ -187,6 +190,7 @@ __global__ void __launch_bounds__(256) ba_frame_schur_kernel(BaDev d) {
   const bool has_ei = nrows > 0 && d.redge[r0] < 0;
   const int ei_off = has_ei ? 1 : 0;
   const int nb = d.fnb[f];
+  if (nb > NB) return;  // a wide-path frame (ba_frame_prep + ba_frame_gram_wide)
   const int nv = 6 * nrows + 1;
   const int wcol = 6 * nrows;
   float* m = lds + wave * (NB * 16 * kLdsRow);
@@ -307,8 +311,219 @@ __global__ void __launch_bounds__(256) ba_frame_schur_kernel(BaDev d) {
 }
 
 // ---------------------------------------------------------------------------
+// Wide path, for frames whose Gram [E w]^T Q [E w] is larger than kNbMax
+// 16-row tiles a side (more than 20 outgoing edges; the reference has no
+// degree limit).  Kernel B1: per pixel of each wide frame, C / w / Q over all
+// of its edges (any count: the relative poses are staged 256 edges at a time)
+// and the Ei row; grid = (ceil(HW/256), nwide).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void stash_rel_pose(const BaDev& d, int kf, int e, float* o) {
+  const int jx = d.jj[e];
+  const SE3f T = (jx == kf) ? stereo_se3() : rel_se3(d.poses + 7 * kf, d.poses + 7 * jx);
+  o[0] = T.t[0]; o[1] = T.t[1]; o[2] = T.t[2];
+  o[3] = T.q[0]; o[4] = T.q[1]; o[5] = T.q[2]; o[6] = T.q[3];
+  o[7] = (jx == kf) ? 1.0f : 0.0f;
+}
+__device__ __forceinline__ SE3f unstash_rel_pose(const float* to, bool& stereo) {
+  SE3f T;
+  T.t[0] = to[0]; T.t[1] = to[1]; T.t[2] = to[2];
+  T.q[0] = to[3]; T.q[1] = to[4]; T.q[2] = to[5]; T.q[3] = to[6];
+  stereo = to[7] != 0.0f;
+  return T;
+}
+
+__global__ void __launch_bounds__(256) ba_frame_prep_kernel(BaDev d) {
+  __shared__ float Tsh[256 * 8];
+  const int wf = blockIdx.y;
+  const int f = d.widef[wf];
+  const int HW = d.HW;
+  const int kf = d.kx[f];
+  const int e0 = d.feptr[f], e1 = d.feptr[f + 1];
+  const bool has_ei = d.redge[d.frptr[f]] < 0;
+  const int px = blockIdx.x * 256 + threadIdx.x;
+  const bool live = px < HW;
+  const float fx = d.intr[0], fy = d.intr[1], cx = d.intr[2], cy = d.intr[3];
+  const float u = (float)(px % d.W), v = (float)(px / d.W);
+  const float disp = live ? d.disps[(long)kf * HW + px] : 0.0f;
+  float C = 0.f, w = 0.f;
+  float Ei[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int base = e0; base < e1; base += 256) {
+    const int cnt = min(256, e1 - base);
+    __syncthreads();
+    if ((int)threadIdx.x < cnt) stash_rel_pose(d, kf, d.fedges[base + threadIdx.x], Tsh + 8 * threadIdx.x);
+    __syncthreads();
+    if (!live) continue;
+    for (int q = 0; q < cnt; ++q) {
+      const int e = d.fedges[base + q];
+      bool stereo;
+      const SE3f T = unstash_rel_pose(Tsh + 8 * q, stereo);
+      const float* tg = d.targets + (long)e * 2 * HW;
+      const float* wt = d.weights + (long)e * 2 * HW;
+      PixLin L;
+      linearize_pixel(T, stereo, fx, fy, cx, cy, u, v, disp, tg[px], tg[HW + px], wt[px], wt[HW + px], L);
+      C += L.C;
+      w += L.bz;
+      if (has_ei) {
+        const float au = L.wu * L.Jzu, av = L.wv * L.Jzv;
+        float Ji[6];
+        ji_from_jj(T, L.Jju, Ji);
+#pragma unroll
+        for (int nn = 0; nn < 6; ++nn) Ei[nn] += au * Ji[nn];
+        ji_from_jj(T, L.Jjv, Ji);
+#pragma unroll
+        for (int nn = 0; nn < 6; ++nn) Ei[nn] += av * Ji[nn];
+      }
+    }
+  }
+  if (!live) return;
+  const int er = (d.eta_rows == 1) ? 0 : f;
+  const float ds = d.disps_sens[(long)kf * HW + px];
+  const bool msk = ds > 0.0f;
+  const float alpha = 0.05f;
+  C = msk ? (C + alpha) : (C + d.eta[(long)er * HW + px]);
+  if (msk) w = w - alpha * (disp - ds);
+  d.qw[(long)f * HW + px] = 1.0f / C;
+  d.qw[(long)d.K * HW + (long)f * HW + px] = w;
+  if (has_ei) {
+    float* eo = d.ei + d.wideeoff[wf];
+#pragma unroll
+    for (int nn = 0; nn < 6; ++nn) eo[(long)nn * HW + px] = Ei[nn];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel B2: one 64x64-variable block pair (IB <= JB) of a wide frame's Gram,
+// per pixel chunk.  Each wave images the scaled variables of both blocks for
+// 64 pixels in LDS (an edge row is re-linearised only by the blocks that hold
+// its variables; the Ei row comes from B1's image) and multiplies them on f32
+// MFMA 16x16x4; the result goes to the same per-frame tile layout as Kernel B,
+// so the assembly is unchanged.  grid = (nchunk, #block pairs),
+// dynamic LDS = 4 waves x 128 rows x kLdsRow floats.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) ba_frame_gram_wide_kernel(BaDev d) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ float Tsh[32 * 8];
+  __shared__ int rsh[32];
+  const int task = blockIdx.y, chunk = blockIdx.x;
+  const int wf = d.widetasks[3 * task], IB = d.widetasks[3 * task + 1], JB = d.widetasks[3 * task + 2];
+  const int f = d.widef[wf];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int HW = d.HW;
+  const int kf = d.kx[f];
+  const int e0 = d.feptr[f];
+  const int r0 = d.frptr[f], r1 = d.frptr[f + 1];
+  const int nrows = r1 - r0;
+  const bool has_ei = d.redge[r0] < 0;
+  const int ei_off = has_ei ? 1 : 0;
+  const int nb = d.fnb[f];
+  const int wcol = 6 * nrows, nv = wcol + 1;
+  const bool same = IB == JB;
+  // rows (0..nrows; row nrows = the w column) holding the variables of each block
+  const int va0 = 64 * IB, vb0 = 64 * JB;
+  const int ra0 = va0 / 6, ra1 = min((va0 + 63) / 6, nrows);
+  const int rb0 = vb0 / 6, rb1 = min((vb0 + 63) / 6, nrows);
+  const int na = ra1 - ra0 + 1, nbr_ = same ? 0 : rb1 - rb0 + 1;
+  if ((int)threadIdx.x < na + nbr_) {
+    const int q = threadIdx.x;
+    const int rho = q < na ? ra0 + q : rb0 + (q - na);
+    rsh[q] = rho;
+    if (rho >= ei_off && rho < nrows) stash_rel_pose(d, kf, d.fedges[e0 + rho - ei_off], Tsh + 8 * q);
+  }
+  float* m = lds + wave * (128 * kLdsRow);
+  float* mb = same ? m : m + 64 * kLdsRow;
+  __syncthreads();
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const float fx = d.intr[0], fy = d.intr[1], cx = d.intr[2], cy = d.intr[3];
+  const float* eo = d.ei + d.wideeoff[wf];
+  for (int g = 0; g < d.gpw; ++g) {
+    const int px = (chunk * d.gpw + g) * 256 + wave * 64 + lane;
+    const bool live = px < HW;
+    const float sq = live ? sqrtf(d.qw[(long)f * HW + px]) : 0.0f;
+    const float u = (float)(px % d.W), v = (float)(px / d.W);
+    const float disp = live ? d.disps[(long)kf * HW + px] : 0.0f;
+    for (int q = 0; q < na + nbr_; ++q) {
+      const int rho = rsh[q];
+      float val[6];
+      int nval = 6;
+      if (rho == nrows) {  // the w column
+        val[0] = live ? sq * d.qw[(long)d.K * HW + (long)f * HW + px] : 0.0f;
+        nval = 1;
+      } else if (rho < ei_off) {  // the Ei row
+#pragma unroll
+        for (int nn = 0; nn < 6; ++nn) val[nn] = live ? sq * eo[(long)nn * HW + px] : 0.0f;
+      } else {
+        const int e = d.fedges[e0 + rho - ei_off];
+        bool stereo;
+        const SE3f T = unstash_rel_pose(Tsh + 8 * q, stereo);
+        PixLin L;
+        if (live) {
+          const float* tg = d.targets + (long)e * 2 * HW;
+          const float* wt = d.weights + (long)e * 2 * HW;
+          linearize_pixel(T, stereo, fx, fy, cx, cy, u, v, disp, tg[px], tg[HW + px], wt[px], wt[HW + px], L);
+        }
+        const float au = live ? L.wu * L.Jzu : 0.0f, av = live ? L.wv * L.Jzv : 0.0f;
+#pragma unroll
+        for (int nn = 0; nn < 6; ++nn) val[nn] = live ? sq * (au * L.Jju[nn] + av * L.Jjv[nn]) : 0.0f;
+      }
+      const int vbase = (rho == nrows) ? wcol : 6 * rho;
+      float* dst = q < na ? m : mb;
+      const int b0 = q < na ? va0 : vb0;
+      for (int c = 0; c < nval; ++c) {
+        const int l = vbase + c - b0;
+        if (l >= 0 && l < 64) dst[l * kLdsRow + lane] = val[c];
+      }
+    }
+    // variables past the frame's last one are zero rows
+    for (int l = max(0, nv - va0); l < 64; ++l) m[l * kLdsRow + lane] = 0.0f;
+    if (!same)
+      for (int l = max(0, nv - vb0); l < 64; ++l) mb[l * kLdsRow + lane] = 0.0f;
+    __syncthreads();
+    const int ar = lane & 15, ak = lane >> 4;
+#pragma unroll
+    for (int I = 0; I < 4; ++I) {
+#pragma unroll
+      for (int J = 0; J < 4; ++J) {
+        if (same && J < I) continue;
+        const float* pa = m + (16 * I + ar) * kLdsRow + ak;
+        const float* pb = mb + (16 * J + ar) * kLdsRow + ak;
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+          acc[I][J] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[4 * s], pb[4 * s], acc[I][J], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // cross-wave reduction and store (lane l, reg k -> row 4*(l>>4)+k, col l&15)
+  float* red = lds;
+  const int Tf = nb * (nb + 1) / 2;
+#pragma unroll
+  for (int I = 0; I < 4; ++I) {
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+      const int GI = 4 * IB + I, GJ = 4 * JB + J;
+      if ((same && J < I) || GI >= nb || GJ >= nb) continue;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) red[wave * 256 + (4 * (lane >> 4) + k) * 16 + (lane & 15)] = acc[I][J][k];
+      __syncthreads();
+      const int tf = GI * nb - GI * (GI - 1) / 2 + (GJ - GI);
+      const int idx = threadIdx.x;
+      const float s = (red[idx] + red[256 + idx]) + (red[512 + idx] + red[768 + idx]);
+      d.gram[(long)d.fgoff[f] + ((long)chunk * Tf + tf) * 256 + idx] = s;
+      __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Kernel C: deterministic assembly of the lower triangle of A - S (fp64) and
-// of the rhs b - E Q w into row n of the augmented matrix.
+// of the rhs b - E Q w into row n, in the permuted pose order, into the 64x64
+// tiles of the factor.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float hess_val(const float* H, int r, int c) {
   if (r < c) { int t = r; r = c; c = t; }
@@ -327,6 +542,12 @@ __device__ __forceinline__ double gram_sum(const BaDev& d, int f, int i, int j) 
   return s;
 }
 
+// element (v, u), v >= u, of the permuted system
+__device__ __forceinline__ double& sys_at(const BaDev& d, int v, int u) {
+  const int sl = d.slot[(v >> 6) * d.nbc + (u >> 6)];
+  return d.M[(size_t)sl * kTile + (v & 63) * 64 + (u & 63)];
+}
+
 __global__ void __launch_bounds__(64) ba_assemble_kernel(BaDev d) {
   const int b = blockIdx.x;
   const int t = threadIdx.x;
@@ -343,7 +564,13 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaDev d) {
         s -= gram_sum(d, q.y, 6 * q.z + r, 6 * q.w + c);
       }
     }
-    d.M[(long)(6 * d.blka[b] + r) * d.ld + 6 * d.blkb[b] + c] = s;
+    // block (a, b) of the original order (a >= b) sits at permuted positions
+    // (pa, pb); its (r, c) element is M'(v, u), stored as M'(u, v) when above
+    // the diagonal (a diagonal block's upper half is its lower half mirrored)
+    const int pa = d.blka[b], pb = d.blkb[b];
+    const int v = 6 * pa + r, u = 6 * pb + c;
+    if (v >= u) sys_at(d, v, u) = s;
+    else if (pa != pb) sys_at(d, u, v) = s;
   } else {
     const int a = b - d.nblk;
     if (t >= 6) return;
@@ -358,209 +585,54 @@ __global__ void __launch_bounds__(64) ba_assemble_kernel(BaDev d) {
         s -= gram_sum(d, q.y, 6 * q.z + t, wcol);
       }
     }
-    d.M[(long)d.n * d.ld + 6 * a + t] = s;
+    sys_at(d, d.n, 6 * d.rhspos[a] + t) = s;
   }
 }
 
 // diag += ep + lm * diag  (SparseBlock::solve :1197) and reset the failure flag
-__global__ void ba_damp_kernel(double* M, int n, int ld, float lm, float ep, int* flag) {
+__global__ void ba_damp_kernel(double* M, const int* slot, int nbc, int n, float lm, float ep, int* flag) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) *flag = 0;
   if (i < n) {
-    const double dg = M[(long)i * ld + i];
-    M[(long)i * ld + i] = dg + ((double)ep + (double)lm * dg);
+    double& dg = M[(size_t)slot[(i >> 6) * nbc + (i >> 6)] * kTile + (i & 63) * 65];
+    dg = dg + ((double)ep + (double)lm * dg);
   }
 }
 
-// ---------------------------------------------------------------------------
-// Blocked right-looking Cholesky, lower, in place, on the augmented matrix of
-// n_aug = n+1 rows (rhs as row n) and n pivot columns: after factorisation,
-// row n holds y = L^-1 b.
-// ---------------------------------------------------------------------------
-constexpr int CB = kCholBlock;
-
-__device__ __forceinline__ double readlane_f64(double v, int lane) {
-  const unsigned long long u = __double_as_longlong(v);
-  const unsigned lo = __builtin_amdgcn_readlane((unsigned)(u & 0xffffffffu), lane);
-  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), lane);
-  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-}
-
-// Diagonal block: one wave, lane i owns row i of the 64x64 block in
-// registers; column j is broadcast with v_readlane (no LDS, no barriers).
-__global__ void __launch_bounds__(64) chol_diag_kernel(double* M, int n, int ld, int k0, int* flag) {
-  const int i = threadIdx.x;
-  const int Br = min(CB, n + 1 - k0);
-  const int Bp = min(CB, n - k0);
-  double r[CB];
-  const double* src = M + (long)(k0 + i) * ld + k0;
-#pragma unroll
-  for (int c = 0; c < CB; ++c) r[c] = (i < Br && c <= i && c < Bp) ? src[c] : 0.0;
-#pragma unroll
-  for (int j = 0; j < CB; ++j) {
-    if (j < Bp) {
-      const double piv = readlane_f64(r[j], j);
-      if (i == 0 && !(piv > 0.0 && piv < 1e300)) atomicOr(flag, 1);
-      const double sd = sqrt(piv);
-      if (i == j) r[j] = sd;
-      else if (i > j) r[j] = r[j] / sd;
-      const double lij = r[j];
-#pragma unroll
-      for (int c = j + 1; c < CB; ++c) {
-        const double lcj = readlane_f64(lij, c);
-        r[c] = (c <= i) ? fma(-lij, lcj, r[c]) : r[c];
-      }
-    }
-  }
-  if (i < Br) {
-    double* dst = M + (long)(k0 + i) * ld + k0;
-#pragma unroll
-    for (int c = 0; c < CB; ++c)
-      if (c <= i && c < Bp) dst[c] = r[c];
-  }
-}
-
-// rows below the diagonal block: X = A_ik L_kk^-T.  L_kk and the rows of X
-// live in LDS; column-oriented elimination keeps every inner-loop update of a
-// lane independent (pipelined LDS traffic, broadcast reads of L).
-__global__ void __launch_bounds__(64) chol_trsm_kernel(double* M, int n, int ld, int k0) {
-  __shared__ double L[CB][CB + 1];
-  __shared__ double X[CB][CB + 1];
-  const int i = threadIdx.x;
-  const int Bp = min(CB, n - k0);
-  const int row = k0 + CB * (blockIdx.x + 1) + i;
-  for (int r = 0; r < CB; ++r) L[r][i] = (r < Bp && i <= r) ? M[(long)(k0 + r) * ld + k0 + i] : (r == i ? 1.0 : 0.0);
-  const bool live = row <= n;
-  const double* src = M + (long)row * ld + k0;
-  for (int c = 0; c < CB; ++c) X[i][c] = (live && c < Bp) ? src[c] : 0.0;
-  __syncthreads();
-  for (int c = 0; c < CB; ++c) {
-    const double xc = X[i][c] / L[c][c];
-    X[i][c] = xc;
-#pragma unroll 8
-    for (int t = c + 1; t < CB; ++t) X[i][t] = fma(-xc, L[t][c], X[i][t]);
-  }
-  if (!live) return;
-  double* dst = M + (long)row * ld + k0;
-  for (int c = 0; c < Bp; ++c) dst[c] = X[i][c];
-}
-
-// trailing update: M[rb][cb] -= L[rb][k] L[cb][k]^T for k0 < cb <= rb
-__global__ void __launch_bounds__(256) chol_update_kernel(double* M, int n, int ld, int k0) {
-  __shared__ double Lr[CB][CB + 1];
-  __shared__ double Lc[CB][CB + 1];
-  const int kb = k0 / CB;
-  const int rb = kb + 1 + blockIdx.y;
-  const int cb = kb + 1 + blockIdx.x;
-  const int nrowblk = ceil_div(n + 1, CB);
-  const int ncolblk = ceil_div(n, CB);
-  if (cb > rb || rb >= nrowblk || cb >= ncolblk) return;
-  const int Bp = min(CB, n - k0);
-  const int R0 = CB * rb, C0 = CB * cb;
-  const int Br = min(CB, n + 1 - R0), Bc = min(CB, n - C0);
-  for (int idx = threadIdx.x; idx < CB * CB; idx += 256) {
-    const int r = idx / CB, t = idx % CB;
-    Lr[r][t] = (r < Br && t < Bp) ? M[(long)(R0 + r) * ld + k0 + t] : 0.0;
-    Lc[r][t] = (r < Bc && t < Bp) ? M[(long)(C0 + r) * ld + k0 + t] : 0.0;
-  }
-  __syncthreads();
-  const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
-  double acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
-  for (int t = 0; t < Bp; ++t) {
-    double ra[4], cbv[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) ra[a] = Lr[4 * ty + a][t];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) cbv[b] = Lc[tx + 16 * b][t];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] += ra[a] * cbv[b];
-  }
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int r = 4 * ty + a;
-    if (r >= Br) continue;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int c = tx + 16 * b;
-      if (c >= Bc) continue;
-      if (rb == cb && c > r) continue;
-      M[(long)(R0 + r) * ld + C0 + c] -= acc[a][b];
-    }
-  }
-}
-
-// back substitution L^T x = y (y = row n), one workgroup; writes dx (fp32),
-// zeroed when the factorisation failed (SparseBlock::solve :1207-1210).
-// Per 64-column block: stage L_bb in LDS, wave 0 solves it with register
-// broadcasts, then all 1024 threads update the rhs of the earlier blocks with
-// coalesced reads of the block's 64 rows.
-__global__ void __launch_bounds__(1024) chol_backsolve_kernel(const double* M, int n, int ld,
-                                                              const int* flag, double* xout,
-                                                              float* dx) {
-  extern __shared__ __attribute__((aligned(16))) double y[];
-  __shared__ double Lb[CB][CB + 1];
-  for (int k = threadIdx.x; k < n; k += blockDim.x) y[k] = M[(long)n * ld + k];
-  const int ncolblk = ceil_div(n, CB);
-  for (int cb = ncolblk - 1; cb >= 0; --cb) {
-    const int c0 = CB * cb;
-    const int Bc = min(CB, n - c0);
-    for (int idx = threadIdx.x; idx < CB * CB; idx += blockDim.x) {
-      const int r = idx / CB, c = idx % CB;
-      Lb[r][c] = (r < Bc && c <= r) ? M[(long)(c0 + r) * ld + c0 + c] : (r == c ? 1.0 : 0.0);
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-      const int i = threadIdx.x;
-      double yi = (i < Bc) ? y[c0 + i] : 0.0;
-#pragma unroll
-      for (int c = CB - 1; c >= 0; --c) {
-        const double xc = readlane_f64(yi, c) / Lb[c][c];
-        if (i == c) yi = xc;
-        else if (i < c) yi = fma(-Lb[c][i], xc, yi);
-      }
-      if (i < Bc) y[c0 + i] = yi;
-    }
-    __syncthreads();
-    for (int jx = threadIdx.x; jx < c0; jx += blockDim.x) {
-      double s = 0.0;
-      for (int c = 0; c < Bc; ++c) s = fma(M[(long)(c0 + c) * ld + jx], y[c0 + c], s);
-      y[jx] -= s;
-    }
-    __syncthreads();
-  }
-  const bool failed = *flag != 0;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    xout[k] = y[k];
-    dx[k] = failed ? 0.0f : (float)y[k];
-  }
+// dense lower triangle of A (n x n, lda) and b -> the tiles of a chol plan
+__global__ void chol_scatter_kernel(double* M, const int* slot, int nbc, int n, const double* A, int lda,
+                                    const double* b) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)(n + 1) * n;
+  if (idx >= total) return;
+  const int v = (int)(idx / n), u = (int)(idx % n);
+  if (u > v) return;
+  const double val = v < n ? A[(long)v * lda + u] : b[u];
+  M[(size_t)slot[(v >> 6) * nbc + (u >> 6)] * kTile + (v & 63) * 64 + (u & 63)] = val;
 }
 
 // ---------------------------------------------------------------------------
 // Dataflow Cholesky + solve: ONE persistent launch.
 //
-// The augmented system (n pivots, rhs as row n, rows of ld doubles) is cut
-// into 64x64 tiles.  Workgroups (one per CU) take tasks by ticket in the
-// host's critical-path order (ba_plan.cpp build_chol_tasks) and wait for
-// their inputs on per-tile version counters: ver(i,j) = number of updates
-// applied, +1 when the tile is final.  A task that is handed out only after
-// all its predecessors were handed out never waits on a workgroup that has
-// not started, so progress does not depend on residency.
+// The augmented system (n pivots, rhs as row n) is stored as the structurally
+// nonzero 64x64 tiles of its factor (slot map from the plan).  Workgroups (one
+// per CU) take tasks by ticket in the host's critical-path order
+// (ba_plan.cpp build_chol_structure) and wait for their inputs on per-tile
+// version counters: ver(tile) = number of updates applied, fin(tile) = that
+// count + 1 once the tile is final.  A task is handed out only after all its
+// predecessors were, so it never waits on a workgroup that has not started and
+// progress does not depend on residency.
 //
 // Cross-workgroup hand-off follows cdna_hip_programming.md Guideline 16 R1:
 // every handed-off byte (tiles, Linv, y, x) is stored AND loaded with sc1
 // buffer operations (write-through / L1 bypass), every storing wave drains
 // vmcnt before the workgroup barrier, then one lane stores the counter with
 // an agent-scope atomic; consumers poll relaxed.  Spins are bounded (an
-// abort word stops every workgroup).  Tiles are products of f64 MFMA
-// (v_mfma_f64_16x16x4f64); the diagonal factor is panel-blocked (16 wide)
-// with register rows and LDS column broadcasts, and also returns L_kk^-1 so
-// the off-diagonal solves are GEMMs.
+// abort word stops every workgroup and flag bit 1 is raised; the host then
+// reports the timeout and leaves poses and disparities untouched).  Tiles are
+// products of f64 MFMA (v_mfma_f64_16x16x4f64); the diagonal factor is
+// panel-blocked (16 wide) with register rows and LDS column broadcasts, and
+// also returns L_kk^-1 so the off-diagonal solves are GEMMs.
 // ---------------------------------------------------------------------------
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef double dbl2 __attribute__((ext_vector_type(2)));
@@ -572,35 +644,24 @@ constexpr unsigned kOobOff = 0x80000000u;
 constexpr unsigned kSpinLimit = 1u << 24;
 constexpr unsigned long long kSpinTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 constexpr int kCholLds = (3 * 64 * LT + 256 + 4 * 272) * 8 + 16;
-#ifdef DROID_CHOL_TRACE
-#define CHOL_TRACE(...) do { if (threadIdx.x == 0) printf(__VA_ARGS__); } while (0)
-#else
-#define CHOL_TRACE(...) do { } while (0)
-#endif
-// debug-only progress marks (DROID_CHOL_MARKS=<device address of an int[grid*4]>):
-// per workgroup {ticket, phase, wave-0 phase, heartbeat}, system-scope stores a
-// host copy engine can read while the kernel runs
-#define CHOL_MARK(slot, v)                                                                          \
-  do {                                                                                              \
-    if (d.marks && (threadIdx.x & 63) == 0)                                                         \
-      __hip_atomic_store(d.marks + 16 * blockIdx.x + 4 * (threadIdx.x >> 6) + (slot), (v),          \
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);                              \
-  } while (0)
 
 struct CholDev {
-  double* M;
-  int n, ld, nbc, nbr;
-  const int4* tasks;
+  double* M;          // factor tiles: slot s at M + kTile * s, row-major 64 x 64
+  int n, nbc, nbr;
+  const int* tasks;   // kTaskInts per task
   int ntasks;
-  int* sync;    // [0] ticket [1] abort [4..] ver[nbr*nbc] | yver[nbc] | xdone[nbc]
+  const int* slot;    // [nbr * nbc] tile -> slot, -1 = structural zero
+  const int* fin;     // [nslots] final version per slot
+  const int* ycnt;    // [nbc] final version of y_c
+  const int* outmap;  // [n] permuted variable -> dx index
+  int nslots;
+  int* sync;    // [0] ticket [1] abort [4..] ver[nslots] | yver[nbc] | xdone[nbc]
   int* flag;    // bit 0: factorisation failed (dx = 0), bit 1: spin timeout
   double* linv; // [nbc][64][64]
   double* ybuf; // [nbc*64]
-  double* x;    // [n]
+  double* x;    // [n] (permuted order)
   float* dx;    // [n]
-  int debug;    // unused (tracing is compile-time: DROID_CHOL_TRACE)
-  int* marks;   // debug progress marks or null
-  long long* tprof;  // debug per-ticket timeline {wg|type<<12|i<<16|j<<32|k<<48, got, deps ok, published} (s_memrealtime) or null
+  int inject;   // test hook (DROID_CHOL_FAULT_INJECT=1): raise the abort at once, as a timeout would
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mkrs(const void* p, size_t bytes) {
@@ -619,31 +680,16 @@ __device__ __forceinline__ void st1(__amdgpu_buffer_rsrc_t r, unsigned off, doub
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)off, 0, kSc1);
 }
 
-// rows [R0,R0+nr) x cols [C0,C0+nc) of a row-major matrix with `ld` doubles per
-// row -> LDS T[64][LT]; zeros elsewhere (out-of-range offsets read 0).  nc even.
-__device__ __forceinline__ void tile_load(__amdgpu_buffer_rsrc_t r, int ld, int R0, int C0, int nr, int nc,
-                                          double* T) {
-  dbl2 v[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
-    const unsigned off = (rr < nr && cc < nc) ? (unsigned)(((size_t)(R0 + rr) * ld + C0 + cc) * 8) : kOobOff;
-    v[q] = ld2(r, off);
-  }
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
-    *reinterpret_cast<dbl2*>(&T[rr * LT + cc]) = v[q];
-  }
+// rows [0,nr) x cols [0,nc) of stored tile `s` -> LDS T[64][LT]; zeros
+// elsewhere (out-of-range offsets read 0).  nc even.
+__device__ __forceinline__ unsigned tile_off(int s, int rr, int cc, int nr, int nc) {
+  return (rr < nr && cc < nc) ? (unsigned)(((size_t)s * kTile + rr * 64 + cc) * 8) : kOobOff;
 }
-// the same load split in two, so the global latency overlaps other work
-__device__ __forceinline__ void tile_issue(__amdgpu_buffer_rsrc_t r, int ld, int R0, int C0, int nr, int nc,
-                                           dbl2 (&v)[8]) {
+__device__ __forceinline__ void tile_issue(__amdgpu_buffer_rsrc_t r, int s, int nr, int nc, dbl2 (&v)[8]) {
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
-    const unsigned off = (rr < nr && cc < nc) ? (unsigned)(((size_t)(R0 + rr) * ld + C0 + cc) * 8) : kOobOff;
-    v[q] = ld2(r, off);
+    v[q] = ld2(r, tile_off(s, rr, cc, nr, nc));
   }
 }
 __device__ __forceinline__ void tile_commit(const dbl2 (&v)[8], double* T) {
@@ -653,13 +699,17 @@ __device__ __forceinline__ void tile_commit(const dbl2 (&v)[8], double* T) {
     *reinterpret_cast<dbl2*>(&T[rr * LT + cc]) = v[q];
   }
 }
-__device__ __forceinline__ void tile_store(__amdgpu_buffer_rsrc_t r, int ld, int R0, int C0, int nr, int nc,
-                                           const double* T) {
+__device__ __forceinline__ void tile_load(__amdgpu_buffer_rsrc_t r, int s, int nr, int nc, double* T) {
+  dbl2 v[8];
+  tile_issue(r, s, nr, nc, v);
+  tile_commit(v, T);
+}
+__device__ __forceinline__ void tile_store(__amdgpu_buffer_rsrc_t r, int s, int nr, int nc, const double* T) {
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
     if (rr < nr && cc < nc)
-      st2(r, (unsigned)(((size_t)(R0 + rr) * ld + C0 + cc) * 8), *reinterpret_cast<const dbl2*>(&T[rr * LT + cc]));
+      st2(r, (unsigned)(((size_t)s * kTile + rr * 64 + cc) * 8), *reinterpret_cast<const dbl2*>(&T[rr * LT + cc]));
   }
 }
 
@@ -790,80 +840,80 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: wave-conditional code branches, never masks
   const int fr = lane & 15, fk = lane >> 4;
   const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
-  const int n = d.n, ld = d.ld, nbc = d.nbc, nbr = d.nbr;
-  const __amdgpu_buffer_rsrc_t rM = mkrs(d.M, (size_t)(n + 1) * ld * 8);
-  const __amdgpu_buffer_rsrc_t rL = mkrs(d.linv, (size_t)nbc * 4096 * 8);
+  const int n = d.n, nbc = d.nbc, nbr = d.nbr;
+  const __amdgpu_buffer_rsrc_t rM = mkrs(d.M, (size_t)d.nslots * kTile * 8);
+  const __amdgpu_buffer_rsrc_t rL = mkrs(d.linv, (size_t)nbc * kTile * 8);
   const __amdgpu_buffer_rsrc_t rY = mkrs(d.ybuf, (size_t)nbc * 64 * 8);
   const __amdgpu_buffer_rsrc_t rX = mkrs(d.x, (size_t)n * 8);
   int* ticket = d.sync;
   int* abort_w = d.sync + 1;
   int* ver = d.sync + 4;
-  int* yver = ver + nbr * nbc;
+  int* yver = ver + d.nslots;
   int* xdone = yver + nbc;
+  auto SL = [&](int i, int j) { return d.slot[i * nbc + j]; };
+  if (d.inject && blockIdx.x == 0 && tid == 0) {
+    __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    atomicOr(d.flag, 2);
+  }
 
-  int nbar = 0;
-#define BAR() do { ++nbar; CHOL_MARK(3, nbar); __syncthreads(); } while (0)
   for (;;) {
     if (tid == 0) shi[0] = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    BAR();
+    __syncthreads();
     const int tk = __builtin_amdgcn_readfirstlane(shi[0]);
-    const unsigned long long t_got = d.tprof ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    CHOL_MARK(0, tk);
-    CHOL_MARK(1, 1);
-    CHOL_TRACE("[chol] wg %d got ticket %d\n", (int)blockIdx.x, tk);
     if (tk >= d.ntasks) break;
-    const int4 tsk = d.tasks[tk];
-    const int type = __builtin_amdgcn_readfirstlane(tsk.x), i = __builtin_amdgcn_readfirstlane(tsk.y);
-    const int j = __builtin_amdgcn_readfirstlane(tsk.z), k = __builtin_amdgcn_readfirstlane(tsk.w);
-    CHOL_TRACE("[chol] wg %d ticket %d task %d (%d,%d,%d)\n", (int)blockIdx.x, tk, type, i, j, k);
+    const int* tsk = d.tasks + kTaskInts * tk;
+    const int type = __builtin_amdgcn_readfirstlane(tsk[0]), i = __builtin_amdgcn_readfirstlane(tsk[1]);
+    const int j = __builtin_amdgcn_readfirstlane(tsk[2]), k = __builtin_amdgcn_readfirstlane(tsk[3]);
+    const int ta = __builtin_amdgcn_readfirstlane(tsk[4]), tb = __builtin_amdgcn_readfirstlane(tsk[5]);
     if (tid == 0) {
       bool ok = true;
       switch (type) {
-        case kPotrf:  // all updates of the tile but the last (done here); L(k, k-1) is awaited below
-          ok = poll_ge(&ver[k * nbc + k], k > 0 ? k - 1 : 0, abort_w, d.flag);
+        case kPotrf: {  // all updates of the tile but the last (applied here); L(k, klast) is awaited below
+          const int s = SL(k, k);
+          ok = poll_ge(&ver[s], ta >= 0 ? d.fin[s] - 2 : 0, abort_w, d.flag);
           break;
-        case kTrsm:
-          ok = poll_ge(&ver[i * nbc + k], k, abort_w, d.flag) && poll_ge(&ver[k * nbc + k], k + 1, abort_w, d.flag);
+        }
+        case kTrsm: {
+          const int s = SL(i, k), sk = SL(k, k);
+          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&ver[sk], d.fin[sk], abort_w, d.flag);
           break;
-        case kUpdate:
-          ok = poll_ge(&ver[i * nbc + j], k, abort_w, d.flag) && poll_ge(&ver[i * nbc + k], k + 1, abort_w, d.flag) &&
-               poll_ge(&ver[j * nbc + k], k + 1, abort_w, d.flag);
+        }
+        case kUpdate: {
+          const int s = SL(i, j), si = SL(i, k), sj = SL(j, k);
+          ok = poll_ge(&ver[s], ta, abort_w, d.flag) && poll_ge(&ver[si], d.fin[si], abort_w, d.flag) &&
+               poll_ge(&ver[sj], d.fin[sj], abort_w, d.flag);
           break;
-        case kBsolve:
-          ok = poll_ge(&ver[i * nbc + i], i + 1, abort_w, d.flag) &&
-               poll_ge(&yver[i], 1 + (nbc - 1 - i), abort_w, d.flag);
+        }
+        case kBsolve: {
+          const int s = SL(i, i);
+          ok = poll_ge(&ver[s], d.fin[s], abort_w, d.flag) && poll_ge(&yver[i], d.ycnt[i], abort_w, d.flag);
           break;
-        default:  // kBupd (r = i, c = j)
-          ok = poll_ge(&xdone[i], 1, abort_w, d.flag) && poll_ge(&ver[i * nbc + j], j + 1, abort_w, d.flag) &&
-               poll_ge(&yver[j], 1 + (nbc - 1 - i), abort_w, d.flag);
+        }
+        default: {  // kBupd (r = i, c = j)
+          const int s = SL(i, j);
+          ok = poll_ge(&xdone[i], 1, abort_w, d.flag) && poll_ge(&ver[s], d.fin[s], abort_w, d.flag) &&
+               poll_ge(&yver[j], 1 + ta, abort_w, d.flag);
           break;
+        }
       }
       shi[1] = ok ? 1 : 0;
     }
-    BAR();
-    CHOL_TRACE("[chol] wg %d ticket %d deps %s\n", (int)blockIdx.x, tk, shi[1] ? "ok" : "ABORT");
+    __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(shi[1])) break;
-    CHOL_MARK(1, 2);
-    if (d.tprof && tid == 0) {
-      d.tprof[4 * tk + 0] = (long long)blockIdx.x | ((long long)type << 12) | ((long long)i << 16) | ((long long)j << 32) |
-                           ((long long)k << 48);
-      d.tprof[4 * tk + 1] = (long long)t_got;
-      d.tprof[4 * tk + 2] = (long long)__builtin_amdgcn_s_memrealtime();
-    }
 
     if (type == kPotrf) {
-      int ps = 0;
-#define PSTAMP() do { if (d.tprof && tid == 0) d.tprof[65536 + 16 * k + (ps < 15 ? ps : 15)] = (long long)__builtin_amdgcn_s_memrealtime(); ++ps; } while (0)
       const int R0 = 64 * k, Bp = min(64, n - R0), Br = min(64, n + 1 - R0);
+      const int skk = SL(k, k);
       dbl2 pre[8];
-      tile_issue(rM, ld, R0, R0, Br, Bp, pre);  // A(k,k) is final but for (k,k,k-1): load while L(k,k-1) is awaited
-      if (k > 0) {  // the tile's last update (k, k, k-1): T0 -= L(k,k-1) L(k,k-1)^T
-        if (tid == 0) shi[1] = poll_ge(&ver[k * nbc + k - 1], k, abort_w, d.flag) ? 1 : 0;
-        BAR();
+      tile_issue(rM, skk, Br, Bp, pre);  // A(k,k) is final but for (k,k,klast): load while L(k,klast) is awaited
+      if (ta >= 0) {  // the tile's last update (k, k, klast): T0 -= L(k,klast) L(k,klast)^T
+        const int sl = SL(k, ta);
+        if (tid == 0) shi[1] = poll_ge(&ver[sl], d.fin[sl], abort_w, d.flag) ? 1 : 0;
+        __syncthreads();
         if (!__builtin_amdgcn_readfirstlane(shi[1])) break;
-        tile_load(rM, ld, R0, R0 - 64, Br, 64, T1);
+        tile_load(rM, sl, Br, 64, T1);
         tile_commit(pre, T0);
-        BAR();
+        __syncthreads();
         dbl4 acc[2][2];
         acc_load(T0, acc, wr, wc, lane);
         gemm_nt64(T1, T1, acc, wr, wc, lane, -1.0);
@@ -871,15 +921,10 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       } else {
         tile_commit(pre, T0);
       }
-      BAR(); PSTAMP();
-      CHOL_TRACE("[chol] potrf %d loaded Bp %d Br %d\n", k, Bp, Br);
+      __syncthreads();
       for (int c0 = 0; c0 < Bp; c0 += 16) {  // whole 16-wide panels (unit-padded)
-        CHOL_MARK(1, 100 + c0);
         if (wave == 0) panel_factor(T0, vec + 128, c0, Bp, lane, d.flag);
-        if (wave == 0) CHOL_MARK(2, 100 + c0);
-        BAR(); PSTAMP();
-        CHOL_MARK(1, 200 + c0);
-        CHOL_TRACE("[chol] potrf %d panel %d done\n", k, c0);
+        __syncthreads();
         const int s0 = c0 + 16;
         const int nt = (64 - s0) / 16;
         for (int ti = wave; ti < nt * nt; ti += 4) {
@@ -894,13 +939,12 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) T0[(R + 4 * q + fk) * LT + C + fr] = acc[q];
         }
-        BAR(); PSTAMP();
+        __syncthreads();
       }
-      CHOL_TRACE("[chol] potrf %d factored\n", k);
-      CHOL_MARK(1, 300);
-      const bool below = k + 1 < nbr;  // trsm(k+1, k) runs in this task
+      const bool below = tb != 0;  // trsm(k+1, k) runs in this task
       const int R1 = R0 + 64, nr1 = below ? min(64, n + 1 - R1) : 0;
-      if (below && tid == 0) shi[2] = poll_ge(&ver[(k + 1) * nbc + k], k, abort_w, d.flag) ? 1 : 0;
+      const int sb = below ? SL(k + 1, k) : 0;
+      if (below && tid == 0) shi[2] = poll_ge(&ver[sb], d.fin[sb] - 1, abort_w, d.flag) ? 1 : 0;
       // Linv of the Bp x Bp pivot block (unit-diagonal padding past Bp)
       for (int idx = tid; idx < 64 * 64; idx += 256) {
         const int r = idx >> 6, c = idx & 63;
@@ -908,10 +952,10 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         T1[r * LT + c] = 0.0;
       }
       if (tid >= Bp && tid < 64) vec[128 + tid] = 1.0;  // unit padding of the pivot block
-      BAR(); PSTAMP();
+      __syncthreads();
       if (below) {
         if (!__builtin_amdgcn_readfirstlane(shi[2])) break;
-        tile_issue(rM, ld, R1, R0, nr1, Bp, pre);  // lands during the Linv work
+        tile_issue(rM, sb, nr1, Bp, pre);  // lands during the Linv work
       }
       if (wave == 0) {  // the four 16x16 diagonal blocks; lane = 16 * block + column
         const int base = 16 * (lane >> 4), cc = lane & 15;
@@ -926,7 +970,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
 #pragma unroll
         for (int t = 0; t < 16; ++t) T1[(base + t) * LT + base + cc] = xv[t];
       }
-      BAR(); PSTAMP();
+      __syncthreads();
       for (int I = 1; I < 4; ++I) {  // Linv[I][J] = -Dinv_I sum_{K=J}^{I-1} L[I][K] Linv[K][J]
         if (wave < I) {
           const int J = wave;
@@ -946,78 +990,69 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) T1[(16 * I + 4 * q + fk) * LT + 16 * J + fr] = R[q];
         }
-        BAR(); PSTAMP();
-        CHOL_TRACE("[chol] potrf %d linv row %d\n", k, I);
+        __syncthreads();
       }
-      CHOL_MARK(1, 400);
-      tile_store(rM, ld, R0, R0, Br, Bp, T0);
-      tile_store(rL, 64, R0, 0, 64, 64, T1);
+      tile_store(rM, skk, Br, Bp, T0);
+      tile_store(rL, k, 64, 64, T1);
       const bool rhs = Br > Bp;
       if (rhs && tid < 32) st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[Bp * LT + 2 * tid]));
-      CHOL_TRACE("[chol] potrf %d stored\n", k);
       if (below) {  // trsm(k+1, k): L(k+1,k) = A(k+1,k) L_kk^-T with L_kk^-1 still in T1
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        BAR();  // T0's store reads are done
+        __syncthreads();  // T0's store reads are done
         tile_commit(pre, T0);
-        BAR();
+        __syncthreads();
         dbl4 acc[2][2] = {};
         gemm_nt64(T0, T1, acc, wr, wc, lane, 1.0);
-        BAR();
+        __syncthreads();
         acc_store(T0, acc, wr, wc, lane);
-        BAR();
-        tile_store(rM, ld, R1, R0, nr1, Bp, T0);
+        __syncthreads();
+        tile_store(rM, sb, nr1, Bp, T0);
         const bool rhs1 = (k + 1 == nbr - 1);
         if (rhs1 && tid < 32) st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[(n - R1) * LT + 2 * tid]));
-        publish(&ver[k * nbc + k], k + 1, &ver[(k + 1) * nbc + k], k + 1, rhs1 ? &yver[k] : nullptr, 1);
+        publish(&ver[skk], d.fin[skk], &ver[sb], d.fin[sb], rhs1 ? &yver[k] : nullptr, 1);
       } else {
-        publish(&ver[k * nbc + k], k + 1, rhs ? &yver[k] : nullptr, 1);
+        publish(&ver[skk], d.fin[skk], rhs ? &yver[k] : nullptr, 1);
       }
-      CHOL_TRACE("[chol] potrf %d published\n", k);
-      PSTAMP();
-#undef PSTAMP
     } else if (type == kTrsm) {
       const int R0 = 64 * i, C0 = 64 * k, nr = min(64, n + 1 - R0), nc = min(64, n - C0);
-      tile_load(rM, ld, R0, C0, nr, nc, T0);
-      tile_load(rL, 64, C0, 0, 64, 64, T1);
-      BAR();
-      CHOL_TRACE("[chol] trsm %d,%d loaded\n", i, k);
+      const int s = SL(i, k);
+      tile_load(rM, s, nr, nc, T0);
+      tile_load(rL, k, 64, 64, T1);
+      __syncthreads();
       dbl4 acc[2][2] = {};
       gemm_nt64(T0, T1, acc, wr, wc, lane, 1.0);
-      BAR();
-      CHOL_TRACE("[chol] trsm %d,%d gemm\n", i, k);
+      __syncthreads();
       acc_store(T0, acc, wr, wc, lane);
-      BAR();
-      tile_store(rM, ld, R0, C0, nr, nc, T0);
+      __syncthreads();
+      tile_store(rM, s, nr, nc, T0);
       const bool rhs = (i == nbr - 1);
       if (rhs && tid < 32) st2(rY, (unsigned)((C0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[(n - R0) * LT + 2 * tid]));
-      CHOL_TRACE("[chol] trsm %d,%d stored\n", i, k);
-      publish(&ver[i * nbc + k], k + 1, rhs ? &yver[k] : nullptr, 1);
-      CHOL_TRACE("[chol] trsm %d,%d published\n", i, k);
+      publish(&ver[s], d.fin[s], rhs ? &yver[k] : nullptr, 1);
     } else if (type == kUpdate) {
       const int Ri = 64 * i, Rj = 64 * j, Ck = 64 * k;
       const int nri = min(64, n + 1 - Ri), ncj = min(64, n - Rj), nck = min(64, n - Ck);
-      tile_load(rM, ld, Ri, Ck, nri, nck, T0);
-      tile_load(rM, ld, Rj, Ck, ncj, nck, T1);
-      tile_load(rM, ld, Ri, Rj, nri, ncj, T2);
-      BAR();
+      const int s = SL(i, j);
+      tile_load(rM, SL(i, k), nri, nck, T0);
+      tile_load(rM, SL(j, k), ncj, nck, T1);
+      tile_load(rM, s, nri, ncj, T2);
+      __syncthreads();
       dbl4 acc[2][2];
       acc_load(T2, acc, wr, wc, lane);
       gemm_nt64(T0, T1, acc, wr, wc, lane, -1.0);
       acc_store(T2, acc, wr, wc, lane);
-      BAR();
-      tile_store(rM, ld, Ri, Rj, nri, ncj, T2);
-      publish(&ver[i * nbc + j], k + 1);
-    } else if (type == kBsolve) {  // x_i = L_ii^-T y_i, then bupd(i, i-1): y_{i-1} -= L(i,i-1)^T x_i
+      __syncthreads();
+      tile_store(rM, s, nri, ncj, T2);
+      publish(&ver[s], ta + 1);
+    } else if (type == kBsolve) {  // x_i = L_ii^-T y_i, then (fused) y_{i-1} -= L(i,i-1)^T x_i
       const int C0 = 64 * i, Bp = min(64, n - C0);
-      tile_load(rL, 64, C0, 0, 64, 64, T1);
-      if (i > 0) tile_load(rM, ld, C0, C0 - 64, Bp, 64, T0);
-      CHOL_TRACE("[chol] bsolve %d tile issued\n", i);
+      tile_load(rL, i, 64, 64, T1);
+      if (ta) tile_load(rM, SL(i, i - 1), Bp, 64, T0);
       if (tid < 32) {
         const dbl2 yv = ld2(rY, 2 * tid < Bp ? (unsigned)((C0 + 2 * tid) * 8) : kOobOff);
         vec[2 * tid] = yv[0];
         vec[2 * tid + 1] = yv[1];
       }
-      BAR();
+      __syncthreads();
       if (wave == 0) {
         double sacc = 0.0;
 #pragma unroll 8
@@ -1025,109 +1060,106 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         const bool failed = (__hip_atomic_load(d.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1) != 0;
         if (lane < Bp) {
           st1(rX, (unsigned)((C0 + lane) * 8), sacc);
-          d.dx[C0 + lane] = failed ? 0.0f : (float)sacc;
+          d.dx[d.outmap[C0 + lane]] = failed ? 0.0f : (float)sacc;
         }
         vec[64 + lane] = lane < Bp ? sacc : 0.0;
       }
-      CHOL_TRACE("[chol] bsolve %d computed\n", i);
       publish(&xdone[i], 1);
-      CHOL_TRACE("[chol] bsolve %d published\n", i);
-      if (i > 0) {
-        if (tid == 0) shi[1] = poll_ge(&yver[i - 1], 1 + (nbc - 1 - i), abort_w, d.flag) ? 1 : 0;
-        BAR();
+      if (ta) {
+        if (tid == 0) shi[1] = poll_ge(&yver[i - 1], d.ycnt[i - 1] - 1, abort_w, d.flag) ? 1 : 0;
+        __syncthreads();
         if (!__builtin_amdgcn_readfirstlane(shi[1])) break;
         if (tid < 64) vec[128 + tid] = ld1(rY, (unsigned)((C0 - 64 + tid) * 8));
-        BAR();
+        __syncthreads();
         if (wave == 0) {
           double sacc = vec[128 + lane];
 #pragma unroll 8
           for (int t = 0; t < 64; ++t) sacc = fma(-T0[t * LT + lane], vec[64 + t], sacc);
           st1(rY, (unsigned)((C0 - 64 + lane) * 8), sacc);
         }
-        publish(&yver[i - 1], 1 + (nbc - i));
+        publish(&yver[i - 1], d.ycnt[i - 1]);
       }
     } else {  // kBupd: y_c -= L_rc^T x_r
       const int R0 = 64 * i, C0 = 64 * j, nr = min(64, n - R0), nc = min(64, n - C0);
-      tile_load(rM, ld, R0, C0, nr, nc, T0);
+      tile_load(rM, SL(i, j), nr, nc, T0);
       if (tid < 64) vec[tid] = ld1(rX, tid < nr ? (unsigned)((R0 + tid) * 8) : kOobOff);
       else if (tid < 128) vec[tid] = ld1(rY, tid - 64 < nc ? (unsigned)((C0 + tid - 64) * 8) : kOobOff);
-      BAR();
+      __syncthreads();
       if (wave == 0) {
         double sacc = vec[64 + lane];
 #pragma unroll 8
         for (int t = 0; t < 64; ++t) sacc = fma(-T0[t * LT + lane], vec[t], sacc);
         if (lane < nc) st1(rY, (unsigned)((C0 + lane) * 8), sacc);
       }
-      publish(&yver[j], 1 + (nbc - i));
+      publish(&yver[j], 2 + ta);
     }
-    if (d.tprof && tid == 0) d.tprof[4 * tk + 3] = (long long)__builtin_amdgcn_s_memrealtime();
   }
 }
 
 // ---------------------------------------------------------------------------
 // Kernel D: back substitution dz = Q (w - sum_rows E_row . dx[pose]) with the
 // EvT6x1 skip of rows whose pose index is <= 0 (:1105), then disps += dz.
-// grid = (ceil(HW/256), K).
+// A timed-out factorisation (flag bit 1) leaves disparities untouched.
+// grid = (ceil(HW/256), K); the frame's edges are staged 256 at a time.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) ba_backsub_kernel(BaDev d) {
-  __shared__ float Tsh[24 * 8];
-  __shared__ float dxs[24 * 8];
+  __shared__ float Tsh[256 * 8];
+  __shared__ float dxs[256 * 8];
+  if (*d.flag & 2) return;
   const int f = blockIdx.y;
   const int HW = d.HW;
   const int px = blockIdx.x * 256 + threadIdx.x;
+  const bool live = px < HW;
   const int kf = d.kx[f];
   const int e0 = d.feptr[f], e1 = d.feptr[f + 1];
   const int t = threadIdx.x;
-  if (t < e1 - e0) {
-    const int e = d.fedges[e0 + t];
-    const int jx = d.jj[e];
-    SE3f T = (jx == kf) ? stereo_se3() : rel_se3(d.poses + 7 * kf, d.poses + 7 * jx);
-    float* o = Tsh + 8 * t;
-    o[0] = T.t[0]; o[1] = T.t[1]; o[2] = T.t[2];
-    o[3] = T.q[0]; o[4] = T.q[1]; o[5] = T.q[2]; o[6] = T.q[3];
-    o[7] = (jx == kf) ? 1.0f : 0.0f;
-    const int pr = jx - d.t0;
-    for (int k = 0; k < 6; ++k) dxs[8 * t + k] = (pr > 0 && pr < d.P) ? d.dx[6 * pr + k] : 0.0f;
-    dxs[8 * t + 6] = (pr > 0 && pr < d.P) ? 1.0f : 0.0f;
-  }
-  __syncthreads();
-  if (px >= HW) return;
   const float fx = d.intr[0], fy = d.intr[1], cx = d.intr[2], cy = d.intr[3];
   const float u = (float)(px % d.W), v = (float)(px / d.W);
-  const float disp = d.disps[(long)kf * HW + px];
+  const float disp = live ? d.disps[(long)kf * HW + px] : 0.0f;
   const int pi = kf - d.t0;
   const bool use_ei = pi > 0 && pi < d.P;
   float Ei[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float acc = 0.f;
-  for (int k = e0; k < e1; ++k) {
-    const int e = d.fedges[k];
-    const float* to = Tsh + 8 * (k - e0);
-    SE3f T;
-    T.t[0] = to[0]; T.t[1] = to[1]; T.t[2] = to[2];
-    T.q[0] = to[3]; T.q[1] = to[4]; T.q[2] = to[5]; T.q[3] = to[6];
-    const bool stereo = to[7] != 0.0f;
-    const float* tg = d.targets + (long)e * 2 * HW;
-    const float* wt = d.weights + (long)e * 2 * HW;
-    PixLin L;
-    linearize_pixel(T, stereo, fx, fy, cx, cy, u, v, disp, tg[px], tg[HW + px], wt[px], wt[HW + px], L);
-    const float au = L.wu * L.Jzu, av = L.wv * L.Jzv;
-    const float* dxe = dxs + 8 * (k - e0);
-    if (dxe[6] != 0.0f) {
-      float dw = 0.f;
-#pragma unroll
-      for (int nn = 0; nn < 6; ++nn) dw += (au * L.Jju[nn] + av * L.Jjv[nn]) * dxe[nn];
-      acc += dw;
+  for (int base = e0; base < e1; base += 256) {
+    const int cnt = min(256, e1 - base);
+    __syncthreads();
+    if (t < cnt) {
+      const int e = d.fedges[base + t];
+      stash_rel_pose(d, kf, e, Tsh + 8 * t);
+      const int pr = d.jj[e] - d.t0;
+      for (int k = 0; k < 6; ++k) dxs[8 * t + k] = (pr > 0 && pr < d.P) ? d.dx[6 * pr + k] : 0.0f;
+      dxs[8 * t + 6] = (pr > 0 && pr < d.P) ? 1.0f : 0.0f;
     }
-    if (use_ei) {
-      float Ji[6];
-      ji_from_jj(T, L.Jju, Ji);
+    __syncthreads();
+    if (!live) continue;
+    for (int q = 0; q < cnt; ++q) {
+      const int e = d.fedges[base + q];
+      bool stereo;
+      const SE3f T = unstash_rel_pose(Tsh + 8 * q, stereo);
+      const float* tg = d.targets + (long)e * 2 * HW;
+      const float* wt = d.weights + (long)e * 2 * HW;
+      PixLin L;
+      linearize_pixel(T, stereo, fx, fy, cx, cy, u, v, disp, tg[px], tg[HW + px], wt[px], wt[HW + px], L);
+      const float au = L.wu * L.Jzu, av = L.wv * L.Jzv;
+      const float* dxe = dxs + 8 * q;
+      if (dxe[6] != 0.0f) {
+        float dw = 0.f;
 #pragma unroll
-      for (int nn = 0; nn < 6; ++nn) Ei[nn] += au * Ji[nn];
-      ji_from_jj(T, L.Jjv, Ji);
+        for (int nn = 0; nn < 6; ++nn) dw += (au * L.Jju[nn] + av * L.Jjv[nn]) * dxe[nn];
+        acc += dw;
+      }
+      if (use_ei) {
+        float Ji[6];
+        ji_from_jj(T, L.Jju, Ji);
 #pragma unroll
-      for (int nn = 0; nn < 6; ++nn) Ei[nn] += av * Ji[nn];
+        for (int nn = 0; nn < 6; ++nn) Ei[nn] += au * Ji[nn];
+        ji_from_jj(T, L.Jjv, Ji);
+#pragma unroll
+        for (int nn = 0; nn < 6; ++nn) Ei[nn] += av * Ji[nn];
+      }
     }
   }
+  if (!live) return;
   if (use_ei) {
     float dw = 0.f;
 #pragma unroll
@@ -1141,9 +1173,10 @@ __global__ void __launch_bounds__(256) ba_backsub_kernel(BaDev d) {
   d.disps[(long)kf * HW + px] = disp + dzv;
 }
 
-__global__ void ba_retract_kernel(float* poses, const float* dx, int t0, int P) {
+// poses <- Exp(dx) poses; a timed-out factorisation (flag bit 1) changes nothing
+__global__ void ba_retract_kernel(float* poses, const float* dx, int t0, int P, const int* flag) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= P) return;
+  if (k >= P || (*flag & 2)) return;
   float xi[6];
   for (int n = 0; n < 6; ++n) xi[n] = dx[6 * k + n];
   retr_se3(xi, poses + 7 * (t0 + k));
@@ -1178,6 +1211,22 @@ static int schur_dispatch(int nb, const BaDev& d, hipStream_t s) {
   return kOk;
 }
 
+static int launch_wide(const BaPlan& p, const BaDev& d, hipStream_t s) {
+  if (p.wide_f.empty()) return kOk;
+  ba_frame_prep_kernel<<<dim3(ceil_div(p.HW, 256), (int)p.wide_f.size()), 256, 0, s>>>(d);
+  DROID_LAUNCH_CHECK();
+  const int lds = 4 * 128 * kLdsRow * (int)sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&ba_frame_gram_wide_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr = true;
+  }
+  ba_frame_gram_wide_kernel<<<dim3(p.nchunk, (int)p.wide_tasks.size() / 3), 256, lds, s>>>(d);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
 static BaDev make_dev(BaPlan& p, char* ws) {
   BaDev d{};
   const int* I = reinterpret_cast<const int*>(ws + p.off_ints);
@@ -1186,76 +1235,45 @@ static BaDev make_dev(BaPlan& p, char* ws) {
   d.frptr = I + p.o_frptr; d.rpose = I + p.o_rpose; d.redge = I + p.o_redge;
   d.fnb = I + p.o_fnb; d.fgoff = I + p.o_fgoff;
   d.blka = I + p.o_blka; d.blkb = I + p.o_blkb; d.blkcptr = I + p.o_blkcptr;
-  d.rhscptr = I + p.o_rhscptr;
+  d.rhscptr = I + p.o_rhscptr; d.rhspos = I + p.o_rhspos;
   d.contrib = reinterpret_cast<const int4*>(I + p.o_contrib);
   d.rhscontrib = reinterpret_cast<const int4*>(I + p.o_rhscontrib);
+  d.widef = I + p.o_widef; d.wideeoff = I + p.o_wideeoff; d.widetasks = I + p.o_widetasks;
+  d.slot = I + p.o_slot;
   d.hpart = reinterpret_cast<float*>(ws + p.off_hpart);
   d.gram = reinterpret_cast<float*>(ws + p.off_gram);
   d.qw = reinterpret_cast<float*>(ws + p.off_qw);
+  d.ei = reinterpret_cast<float*>(ws + p.off_ei);
   d.M = reinterpret_cast<double*>(ws + p.off_M);
   d.x = reinterpret_cast<double*>(ws + p.off_x);
   d.flag = reinterpret_cast<int*>(ws + p.off_flag);
   d.E = p.E; d.N = p.N; d.H = p.H; d.W = p.W; d.HW = p.HW;
-  d.t0 = p.t0; d.t1 = p.t1; d.P = p.P; d.K = p.K; d.n = p.n; d.ld = p.ld;
+  d.t0 = p.t0; d.t1 = p.t1; d.P = p.P; d.K = p.K; d.n = p.n; d.nbc = p.cs.nbc;
   d.eta_rows = p.eta_rows; d.nsplit = p.nsplit; d.nchunk = p.nchunk; d.gpw = p.group_per_wave;
   d.nblk = (int)p.blk_a.size();
+  d.nwide = (int)p.wide_f.size();
   return d;
-}
-
-// the previous launch-per-step blocked factorisation (A/B reference: DROID_CHOL=blocked)
-static int chol_blocked(const BaDev& d, int n, int ld, float* dx, hipStream_t stream) {
-  const int ncolblk = ceil_div(n, CB), nrowblk = ceil_div(n + 1, CB);
-  for (int kb = 0; kb < ncolblk; ++kb) {
-    const int k0 = CB * kb;
-    chol_diag_kernel<<<1, 64, 0, stream>>>(d.M, n, ld, k0, d.flag);
-    const int below = nrowblk - kb - 1;
-    if (below > 0) {
-      chol_trsm_kernel<<<below, 64, 0, stream>>>(d.M, n, ld, k0);
-      chol_update_kernel<<<dim3(below, below), 256, 0, stream>>>(d.M, n, ld, k0);
-    }
-  }
-  DROID_LAUNCH_CHECK();
-  static int backsolve_lds = 0;
-  const int need = n * (int)sizeof(double);
-  if (need > backsolve_lds) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&chol_backsolve_kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, need));
-    backsolve_lds = need;
-  }
-  if (need > 160 * 1024) return fail(kUnsupported, "ba: reduced system too large for the single-WG back solve");
-  chol_backsolve_kernel<<<1, 1024, (size_t)n * sizeof(double), stream>>>(d.M, n, ld, d.flag, d.x, dx);
-  DROID_LAUNCH_CHECK();
-  return kOk;
-}
-
-static bool use_dataflow_chol() {
-  static const bool on = [] {
-    const char* e = getenv("DROID_CHOL");
-    return !(e && std::string(e) == "blocked");
-  }();
-  return on;
 }
 
 static int num_cus() { return device_cu_count(); }
 
-static int launch_chol_dataflow(const BaPlan& p, char* ws, const BaDev& bd, float* dx, hipStream_t stream) {
-  if ((size_t)(p.n + 1) * p.ld * 8 >= 0x80000000ull)
-    return fail(kUnsupported, "ba: reduced system exceeds the 2 GB dense-solver limit");
+static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_t stream) {
+  const int* I = reinterpret_cast<const int*>(ws + p.off_ints);
   CholDev c{};
-  c.M = bd.M; c.n = p.n; c.ld = p.ld; c.nbc = p.nbc; c.nbr = p.nbr;
-  c.tasks = reinterpret_cast<const int4*>(reinterpret_cast<const int*>(ws + p.off_ints) + p.o_tasks);
-  c.ntasks = p.ntasks;
+  c.M = reinterpret_cast<double*>(ws + p.off_M);
+  c.n = p.n; c.nbc = p.cs.nbc; c.nbr = p.cs.nbr;
+  c.tasks = I + p.o_tasks;
+  c.ntasks = p.cs.ntasks;
+  c.slot = I + p.o_slot; c.fin = I + p.o_fin; c.ycnt = I + p.o_ycnt; c.outmap = I + p.o_outmap;
+  c.nslots = p.cs.nslots;
   c.sync = reinterpret_cast<int*>(ws + p.off_sync);
-  c.flag = bd.flag;
+  c.flag = reinterpret_cast<int*>(ws + p.off_flag);
   c.linv = reinterpret_cast<double*>(ws + p.off_linv);
   c.ybuf = reinterpret_cast<double*>(ws + p.off_ybuf);
-  c.x = bd.x;
+  c.x = reinterpret_cast<double*>(ws + p.off_x);
   c.dx = dx;
-  static int* const marks = getenv("DROID_CHOL_MARKS") ? reinterpret_cast<int*>(strtoull(getenv("DROID_CHOL_MARKS"), nullptr, 0)) : nullptr;
-  c.marks = marks;
-  static long long* const tprof =
-      getenv("DROID_CHOL_TPROF") ? reinterpret_cast<long long*>(strtoull(getenv("DROID_CHOL_TPROF"), nullptr, 0)) : nullptr;
-  c.tprof = tprof;
+  const char* inj = getenv("DROID_CHOL_FAULT_INJECT");
+  c.inject = (inj && atoi(inj) != 0) ? 1 : 0;
   static bool attr = false;
   if (!attr) {
     DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&chol_dataflow_kernel),
@@ -1263,7 +1281,7 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, const BaDev& bd, floa
     attr = true;
   }
   DROID_HIP_CHECK(hipMemsetAsync(c.sync, 0, p.sync_bytes, stream));
-  const int grid = std::min(p.ntasks, num_cus());
+  const int grid = std::min(p.cs.ntasks, num_cus());
   chol_dataflow_kernel<<<grid, 256, kCholLds, stream>>>(c);
   DROID_LAUNCH_CHECK();
   return kOk;
@@ -1280,6 +1298,8 @@ int droid_ba_plan_upload(void* plan, void* workspace, hipStream_t stream) {
   if (!p || !workspace) return fail(kInvalidArgument, "ba_plan_upload: null argument");
   DROID_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(workspace) + p->off_ints, p->ints.data(),
                                  p->ints.size() * sizeof(int), hipMemcpyHostToDevice, stream));
+  // the status word reads "no failure" until a solve runs
+  DROID_HIP_CHECK(hipMemsetAsync(static_cast<char*>(workspace) + p->off_flag, 0, 64, stream));
   p->uploaded = true;
   p->uploaded_to = workspace;
   return kOk;
@@ -1308,13 +1328,19 @@ int droid_ba_build_system(void* plan, void* workspace, float* poses, float* disp
     DROID_LAUNCH_CHECK();
   }
   if (!p->motion_only && p->K > 0) {
-    st = schur_dispatch(p->nb_max, d, stream);
+    if (p->wide_f.size() < (size_t)p->K) {
+      st = schur_dispatch(p->nb_max, d, stream);
+      if (st) return st;
+      DROID_LAUNCH_CHECK();
+    }
+    st = launch_wide(*p, d, stream);
     if (st) return st;
+  }
+  DROID_HIP_CHECK(hipMemsetAsync(d.M, 0, (size_t)p->cs.nslots * kTile * sizeof(double), stream));
+  if (d.nblk + p->P > 0) {
+    ba_assemble_kernel<<<d.nblk + p->P, 64, 0, stream>>>(d);
     DROID_LAUNCH_CHECK();
   }
-  DROID_HIP_CHECK(hipMemsetAsync(d.M, 0, (size_t)(p->n + 1) * p->ld * sizeof(double), stream));
-  ba_assemble_kernel<<<d.nblk + p->P, 64, 0, stream>>>(d);
-  DROID_LAUNCH_CHECK();
   return kOk;
 }
 
@@ -1331,14 +1357,11 @@ int droid_ba_solve_update(void* plan, void* workspace, float* poses, float* disp
   d.poses = poses; d.disps = disps; d.intr = intrinsics; d.disps_sens = disps_sens;
   d.targets = targets; d.weights = weights; d.eta = eta; d.dx = dx; d.dz = dz;
   d.lm = lm; d.ep = ep;
-  const int n = p->n, ld = p->ld;
-  ba_damp_kernel<<<ceil_div(std::max(n, 1), 256), 256, 0, stream>>>(d.M, n, ld, lm, ep, d.flag);
+  const int n = p->n;
+  ba_damp_kernel<<<ceil_div(std::max(n, 1), 256), 256, 0, stream>>>(d.M, d.slot, d.nbc, n, lm, ep, d.flag);
   DROID_LAUNCH_CHECK();
-  if (n > 0 && use_dataflow_chol()) {
-    st = launch_chol_dataflow(*p, static_cast<char*>(workspace), d, dx, stream);
-    if (st) return st;
-  } else if (n > 0) {
-    st = chol_blocked(d, n, ld, dx, stream);
+  if (n > 0) {
+    st = launch_chol_dataflow(*p, static_cast<char*>(workspace), dx, stream);
     if (st) return st;
   }
   if (!p->motion_only && p->K > 0) {
@@ -1346,29 +1369,56 @@ int droid_ba_solve_update(void* plan, void* workspace, float* poses, float* disp
     ba_backsub_kernel<<<dim3(ceil_div(p->HW, 256), p->K), 256, 0, stream>>>(d);
     DROID_LAUNCH_CHECK();
   }
-  ba_retract_kernel<<<ceil_div(std::max(p->P, 1), 64), 64, 0, stream>>>(poses, dx, p->t0, p->P);
+  if (p->P > 0) {
+    ba_retract_kernel<<<ceil_div(p->P, 64), 64, 0, stream>>>(poses, dx, p->t0, p->P, d.flag);
+    DROID_LAUNCH_CHECK();
+  }
+  return kOk;
+}
+
+// Byte offset of the status word in a plan's workspace: bit 0 = the last
+// factorisation was not positive definite (dx = 0, as the reference), bit 1 =
+// the dataflow solve timed out (poses / disparities left unchanged).
+int droid_ba_plan_flag_offset(const void* plan, size_t* offset) {
+  auto* p = static_cast<const BaPlan*>(plan);
+  if (!p || !offset) return fail(kInvalidArgument, "ba_plan_flag_offset: null argument");
+  *offset = p->off_flag;
+  return kOk;
+}
+
+// Dense lower triangle of A (n x n, row stride lda doubles) and b (n) into the
+// tiles of a chol plan (droid_chol_plan_create), both fp64 device pointers.
+int droid_chol_set_system(void* plan, void* workspace, const double* A, int lda, const double* b,
+                          hipStream_t stream) {
+  auto* p = static_cast<BaPlan*>(plan);
+  int st = check_ready(p, workspace);
+  if (st) return st;
+  if (lda < p->n) return fail(kInvalidArgument, "chol_set_system: lda < n");
+  char* ws = static_cast<char*>(workspace);
+  double* M = reinterpret_cast<double*>(ws + p->off_M);
+  DROID_HIP_CHECK(hipMemsetAsync(M, 0, (size_t)std::max(p->cs.nslots, 1) * kTile * sizeof(double), stream));
+  if (p->n == 0) return kOk;
+  const long total = (long)(p->n + 1) * p->n;
+  chol_scatter_kernel<<<(int)((total + 255) / 256), 256, 0, stream>>>(
+      M, reinterpret_cast<const int*>(ws + p->off_ints) + p->o_slot, p->cs.nbc, p->n, A, lda, b);
   DROID_LAUNCH_CHECK();
   return kOk;
 }
 
-
-// Dense damped SPD solve on a chol plan (droid_chol_plan_create): diag += ep +
-// lm*diag, factor, dx = solution (0 and flag bit 0 set if not SPD).
+// Dense damped SPD solve on a chol plan: diag += ep + lm*diag, factor,
+// dx = solution (0 and flag bit 0 set if not SPD).
 int droid_chol_solve(void* plan, void* workspace, float lm, float ep, float* dx, hipStream_t stream) {
   auto* p = static_cast<BaPlan*>(plan);
   int st = check_ready(p, workspace);
   if (st) return st;
   char* ws = static_cast<char*>(workspace);
-  BaDev d{};
-  d.M = reinterpret_cast<double*>(ws + p->off_M);
-  d.x = reinterpret_cast<double*>(ws + p->off_x);
-  d.flag = reinterpret_cast<int*>(ws + p->off_flag);
-  d.n = p->n;
-  d.ld = p->ld;
-  ba_damp_kernel<<<ceil_div(std::max(p->n, 1), 256), 256, 0, stream>>>(d.M, p->n, p->ld, lm, ep, d.flag);
+  double* M = reinterpret_cast<double*>(ws + p->off_M);
+  const int* slot = reinterpret_cast<const int*>(ws + p->off_ints) + p->o_slot;
+  int* flag = reinterpret_cast<int*>(ws + p->off_flag);
+  ba_damp_kernel<<<ceil_div(std::max(p->n, 1), 256), 256, 0, stream>>>(M, slot, p->cs.nbc, p->n, lm, ep, flag);
   DROID_LAUNCH_CHECK();
   if (p->n == 0) return kOk;
-  return use_dataflow_chol() ? launch_chol_dataflow(*p, ws, d, dx, stream) : chol_blocked(d, p->n, p->ld, dx, stream);
+  return launch_chol_dataflow(*p, ws, dx, stream);
 }
 
 // Full ba(): `iterations` GN steps on one device (droid_backends.ba).

@@ -1,14 +1,15 @@
 // Host-side structure analysis for one ba() call (the part of ba_cuda that
 // depends only on ii, jj, t0, t1): droid_kernels.cu:1336-1345 (ts, kx, kk),
 // :1241-1272 (Schur row graph) and the triplet lists of
-// SparseBlock::update_lhs/rhs (:1131-1173).  Unlike the reference, this runs
-// once per edge set (cached by the caller), never inside the GN loop.
+// SparseBlock::update_lhs/rhs (:1131-1173), plus what SimplicialLLT's analyse
+// step does for the reference (:1192-1213): a fill-reducing pose order and the
+// symbolic factor, here at 64x64-tile granularity.  Unlike the reference, this
+// runs once per edge set (cached by the caller), never inside the GN loop.
 #include <algorithm>
 #include <cstring>
-#include <functional>
 #include <map>
 #include <queue>
-#include <tuple>
+#include <unordered_map>
 #include <utility>
 
 #include "ba.hpp"
@@ -18,47 +19,166 @@ namespace droid {
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Task DAG of the dataflow Cholesky (ba_kernels.hip: chol_dataflow_kernel) for
-// the augmented system with n pivots and the rhs as row n:
-//   POTRF(k)     factor tile (k,k) (+ the rhs row when it lies in that tile), Linv_k
-//   TRSM(i,k)    tile (i,k) <- A_ik Linv_k^T
-//   UPD(i,j,k)   tile (i,j) -= L_ik L_jk^T               (k < j <= i)
-//   BSOLVE(c)    x_c = Linv_c^T y_c
-//   BUPD(r,c)    y_c -= L_rc^T x_r                       (c < r, applied in order r = nbc-1 .. c+1)
-// Tickets are handed out in a list-scheduling order: among ready tasks, the
-// longest remaining path (estimated microseconds incl. one hop per edge) first.
-void build_chol_tasks(int n, int& nbc, int& nbr, std::vector<int>& out) {
-  nbc = (n + 63) / 64;
-  nbr = (n + 1 + 63) / 64;
-  out.clear();
+// ---------------------------------------------------------------------------
+// Tile-level symbolic Cholesky.  Bitset per tile column: rows i >= j with
+// nonzero (i, j).  Eliminating column k makes (i, j) nonzero for every pair of
+// nonzero rows i >= j > k of column k.
+// ---------------------------------------------------------------------------
+struct TileBits {
+  int nbc = 0, nbr = 0, nw = 0;
+  std::vector<uint64_t> col;  // nbc x nw
+  bool get(int i, int j) const { return (col[(size_t)j * nw + (i >> 6)] >> (i & 63)) & 1; }
+  void set(int i, int j) { col[(size_t)j * nw + (i >> 6)] |= 1ull << (i & 63); }
+};
+
+static void init_bits(TileBits& tb, int n) {
+  tb.nbc = (n + 63) / 64;
+  tb.nbr = (n + 1 + 63) / 64;
+  tb.nw = (tb.nbr + 63) / 64;
+  tb.col.assign((size_t)tb.nbc * tb.nw, 0);
+}
+
+// diagonal tiles and the rhs row (row n: every column) are always present
+static void close_bits(TileBits& tb) {
+  for (int k = 0; k < tb.nbc; ++k) {
+    tb.set(k, k);
+    tb.set(tb.nbr - 1, k);
+  }
+  for (int k = 0; k < tb.nbc; ++k) {
+    const uint64_t* ck = &tb.col[(size_t)k * tb.nw];
+    for (int w = 0; w < tb.nw; ++w) {
+      uint64_t bits = ck[w];
+      while (bits) {
+        const int i = 64 * w + __builtin_ctzll(bits);
+        bits &= bits - 1;
+        if (i <= k || i >= tb.nbc) continue;  // rows of column k that are also pivot columns j = i
+        uint64_t* cj = &tb.col[(size_t)i * tb.nw];
+        for (int w2 = i >> 6; w2 < tb.nw; ++w2) {
+          uint64_t m = ck[w2];
+          if (w2 == (i >> 6)) m &= ~0ull << (i & 63);
+          cj[w2] |= m;
+        }
+      }
+    }
+  }
+}
+
+// number of tile updates the factorisation performs (its dominant work)
+static long count_updates(const TileBits& tb) {
+  long u = 0;
+  for (int k = 0; k < tb.nbc; ++k) {
+    long c = 0;
+    for (int w = 0; w < tb.nw; ++w) c += __builtin_popcountll(tb.col[(size_t)k * tb.nw + w]);
+    c -= 1;  // rows strictly below the diagonal
+    u += c * (c + 1) / 2;
+  }
+  return u;
+}
+
+void build_chol_structure(int n, const std::vector<char>& pattern, CholStructure& cs) {
+  TileBits tb;
+  init_bits(tb, n);
+  const int nbc = tb.nbc, nbr = tb.nbr;
+  cs.n = n; cs.nbc = nbc; cs.nbr = nbr;
+  cs.slot.assign((size_t)nbr * nbc, -1);
+  cs.tasks.clear();
+  cs.fin.clear(); cs.ycnt.assign(nbc, 1);
+  cs.nslots = cs.nslots_a = 0;
+  cs.ntasks = 0;
   if (n <= 0) return;
-  struct Node { int type, i, j, k; double cost; std::vector<int> succ; int npred; double bl; };
-  std::vector<Node> t;
-  std::map<std::tuple<int, int, int, int>, int> id;
-  auto add = [&](int type, int i, int j, int k, double cost) {
-    id[std::make_tuple(type, i, j, k)] = (int)t.size();
-    t.push_back({type, i, j, k, cost, {}, 0, 0.0});
+  std::vector<char> input((size_t)nbr * nbc, 0);
+  for (int i = 0; i < nbr; ++i)
+    for (int j = 0; j <= std::min(i, nbc - 1); ++j)
+      if (pattern[(size_t)i * nbc + j] || i == j || i == nbr - 1) { input[(size_t)i * nbc + j] = 1; tb.set(i, j); }
+  close_bits(tb);
+  // slots: input tiles first (the region a sharded caller all-reduces), then fill
+  for (int i = 0; i < nbr; ++i)
+    for (int j = 0; j <= std::min(i, nbc - 1); ++j)
+      if (input[(size_t)i * nbc + j]) cs.slot[(size_t)i * nbc + j] = cs.nslots++;
+  cs.nslots_a = cs.nslots;
+  for (int i = 0; i < nbr; ++i)
+    for (int j = 0; j <= std::min(i, nbc - 1); ++j)
+      if (tb.get(i, j) && cs.slot[(size_t)i * nbc + j] < 0) cs.slot[(size_t)i * nbc + j] = cs.nslots++;
+  auto nz = [&](int i, int j) { return i >= 0 && j >= 0 && i < nbr && j < nbc && j <= i && cs.slot[(size_t)i * nbc + j] >= 0; };
+  auto sl = [&](int i, int j) { return cs.slot[(size_t)i * nbc + j]; };
+  // row bitsets (columns k of row i) for the update lists U(i,j) = {k < j : (i,k), (j,k) nonzero}
+  const int cw = (nbc + 63) / 64;
+  std::vector<uint64_t> rowb((size_t)nbr * cw, 0);
+  for (int i = 0; i < nbr; ++i)
+    for (int j = 0; j <= std::min(i, nbc - 1); ++j)
+      if (nz(i, j)) rowb[(size_t)i * cw + (j >> 6)] |= 1ull << (j & 63);
+  auto ulist = [&](int i, int j, std::vector<int>& out) {
+    out.clear();
+    for (int w = 0; w <= ((j - 1) >> 6) && j > 0; ++w) {
+      uint64_t m = rowb[(size_t)i * cw + w] & rowb[(size_t)j * cw + w];
+      if (w == (j >> 6)) m &= (1ull << (j & 63)) - 1;
+      while (m) { out.push_back(64 * w + __builtin_ctzll(m)); m &= m - 1; }
+    }
   };
-  // potrf(k) also applies the last update of its own tile, (k,k,k-1), and
-  // solves the tile below it, trsm(k+1,k): the diagonal chain hands off once
-  // per step instead of three times.
-  for (int k = 0; k < nbc; ++k) {
-    add(kPotrf, k, k, k, 10.0);
-    for (int i = k + 2; i < nbr; ++i) add(kTrsm, i, k, k, 2.0);
-    for (int j = k + 1; j < nbc; ++j)
-      for (int i = j; i < nbr; ++i)
-        if (!(i == j && j == k + 1)) add(kUpdate, i, j, k, 2.0);
-  }
-  // bsolve(c) also applies x_c to y_{c-1} (bupd(c, c-1)): one hand-off per
-  // step of the back-substitution chain
+  cs.fin.assign(cs.nslots, 1);
+  std::vector<int> nupd(cs.nslots, 0), klast(nbc, -1);
+  std::vector<int> U;
+  for (int i = 0; i < nbr; ++i)
+    for (int j = 0; j <= std::min(i, nbc - 1); ++j)
+      if (nz(i, j)) {
+        ulist(i, j, U);
+        nupd[sl(i, j)] = (int)U.size();
+        cs.fin[sl(i, j)] = (int)U.size() + 1;
+        if (i == j && !U.empty()) klast[i] = U.back();
+      }
+  // back-solve rows of each y_c, descending
+  std::vector<std::vector<int>> yrows(nbc);
   for (int c = 0; c < nbc; ++c) {
-    add(kBsolve, c, c, c, 2.0);
-    for (int r = c + 2; r < nbc; ++r) add(kBupd, r, c, c, 1.0);
+    for (int r = nbc - 1; r > c; --r)
+      if (nz(r, c)) yrows[c].push_back(r);
+    cs.ycnt[c] = 1 + (int)yrows[c].size();
   }
-  auto get = [&](int type, int i, int j, int k) { return id.at(std::make_tuple(type, i, j, k)); };
-  auto fin = [&](int i, int k) { return (i == k || i == k + 1) ? get(kPotrf, k, k, k) : get(kTrsm, i, k, k); };
-  // the task that applies x_r to y_c
-  auto ychain = [&](int r, int c) { return r == c + 1 ? get(kBsolve, r, r, r) : get(kBupd, r, c, c); };
+
+  // ---- task graph ----
+  struct Node { int rec[kTaskInts]; double cost; std::vector<int> succ; int npred; double bl; };
+  std::vector<Node> t;
+  std::unordered_map<uint64_t, int> id;
+  auto key = [](int type, int i, int j, int k) {
+    return (uint64_t)type | ((uint64_t)(uint32_t)i << 4) | ((uint64_t)(uint32_t)j << 24) | ((uint64_t)(uint32_t)k << 44);
+  };
+  auto add = [&](int type, int i, int j, int k, int a, int b, double cost) {
+    id[key(type, i, j, k)] = (int)t.size();
+    Node nd{{type, i, j, k, a, b, 0, 0}, cost, {}, 0, 0.0};
+    t.push_back(std::move(nd));
+  };
+  std::vector<char> below(nbc, 0);
+  for (int k = 0; k < nbc; ++k) {
+    below[k] = (k + 1 < nbr && nz(k + 1, k)) ? 1 : 0;
+    add(kPotrf, k, k, k, klast[k], below[k], 10.0);
+    for (int i = k + 1; i < nbr; ++i)
+      if (nz(i, k) && !(i == k + 1 && below[k])) add(kTrsm, i, k, k, 0, 0, 2.0);
+  }
+  for (int i = 0; i < nbr; ++i)
+    for (int j = 0; j <= std::min(i, nbc - 1); ++j)
+      if (nz(i, j)) {
+        ulist(i, j, U);
+        for (int s = 0; s < (int)U.size(); ++s)
+          if (!(i == j && U[s] == klast[i])) add(kUpdate, i, j, U[s], s, 0, 2.0);
+      }
+  for (int c = 0; c < nbc; ++c) {
+    add(kBsolve, c, c, c, (c >= 1 && nz(c, c - 1)) ? 1 : 0, 0, 2.0);
+    for (int s = 0; s < (int)yrows[c].size(); ++s)
+      if (yrows[c][s] != c + 1) add(kBupd, yrows[c][s], c, c, s, 0, 1.0);
+  }
+  auto get = [&](int type, int i, int j, int k) { return id.at(key(type, i, j, k)); };
+  auto fin_task = [&](int i, int k) {  // the task that makes tile (i,k) final
+    if (i == k || (i == k + 1 && below[k])) return get(kPotrf, k, k, k);
+    return get(kTrsm, i, k, k);
+  };
+  auto upd_task = [&](int i, int j, int s) {  // the task that publishes version s+1 of (i,j)
+    ulist(i, j, U);
+    return get(kUpdate, i, j, U[s]);
+  };
+  auto yprod = [&](int c, int v) {  // the task that publishes version v of y_c
+    if (v == 1) return fin_task(nbr - 1, c);
+    const int r = yrows[c][v - 2];
+    return r == c + 1 ? get(kBsolve, r, r, r) : get(kBupd, r, c, c);
+  };
   auto edge = [&](int a, int b) {
     for (int x : t[a].succ)
       if (x == b) return;
@@ -66,34 +186,36 @@ void build_chol_tasks(int n, int& nbc, int& nbr, std::vector<int>& out) {
     t[b].npred++;
   };
   for (int v = 0; v < (int)t.size(); ++v) {
-    const Node nd = t[v];
-    switch (nd.type) {
-      case kPotrf:
-        if (nd.k >= 2) edge(get(kUpdate, nd.k, nd.k, nd.k - 2), v);
-        if (nd.k >= 1) edge(get(kPotrf, nd.k - 1, nd.k - 1, nd.k - 1), v);
-        if (nd.k >= 1 && nd.k + 1 < nbr) edge(get(kUpdate, nd.k + 1, nd.k, nd.k - 1), v);
+    const int type = t[v].rec[0], i = t[v].rec[1], j = t[v].rec[2], k = t[v].rec[3], a = t[v].rec[4];
+    switch (type) {
+      case kPotrf: {
+        const int nu = nupd[sl(k, k)];
+        if (nu >= 2) edge(upd_task(k, k, nu - 2), v);
+        if (a >= 0) edge(fin_task(k, a), v);
+        if (t[v].rec[5] && nupd[sl(k + 1, k)] >= 1) edge(upd_task(k + 1, k, nupd[sl(k + 1, k)] - 1), v);
         break;
+      }
       case kTrsm:
-        edge(get(kPotrf, nd.k, nd.k, nd.k), v);
-        if (nd.k > 0) edge(get(kUpdate, nd.i, nd.k, nd.k - 1), v);
+        edge(get(kPotrf, k, k, k), v);
+        if (nupd[sl(i, k)] >= 1) edge(upd_task(i, k, nupd[sl(i, k)] - 1), v);
         break;
       case kUpdate:
-        edge(fin(nd.i, nd.k), v);
-        edge(fin(nd.j, nd.k), v);
-        if (nd.k > 0) edge(get(kUpdate, nd.i, nd.j, nd.k - 1), v);
+        if (a >= 1) edge(upd_task(i, j, a - 1), v);
+        edge(fin_task(i, k), v);
+        edge(fin_task(j, k), v);
         break;
       case kBsolve:
-        edge(get(kPotrf, nd.i, nd.i, nd.i), v);
-        edge(nd.i == nbc - 1 ? fin(nbr - 1, nd.i) : ychain(nd.i + 1, nd.i), v);
-        if (nd.i >= 1) {
-          edge(fin(nd.i, nd.i - 1), v);
-          edge(nd.i == nbc - 1 ? fin(nbr - 1, nd.i - 1) : ychain(nd.i + 1, nd.i - 1), v);
+        edge(get(kPotrf, i, i, i), v);
+        edge(yprod(i, cs.ycnt[i]), v);
+        if (a) {
+          edge(fin_task(i, i - 1), v);
+          edge(yprod(i - 1, cs.ycnt[i - 1] - 1), v);
         }
         break;
-      case kBupd:
-        edge(get(kBsolve, nd.i, nd.i, nd.i), v);
-        edge(fin(nd.i, nd.j), v);
-        edge(nd.i == nbc - 1 ? fin(nbr - 1, nd.j) : ychain(nd.i + 1, nd.j), v);
+      default:  // kBupd (r = i, c = j)
+        edge(get(kBsolve, i, i, i), v);
+        edge(fin_task(i, j), v);
+        edge(yprod(j, 1 + a), v);
         break;
     }
   }
@@ -111,7 +233,8 @@ void build_chol_tasks(int n, int& nbc, int& nbr, std::vector<int>& out) {
     for (int s2 : nd.succ) m = std::max(m, 1.0 + t[s2].bl);
     nd.bl = nd.cost + m;
   }
-  // list scheduling by bottom level
+  // list scheduling by bottom level: tickets are a topological order, so a
+  // task never waits on one that has not been handed out
   auto cmp = [&](int a, int b) { return t[a].bl != t[b].bl ? t[a].bl < t[b].bl : a > b; };
   std::priority_queue<int, std::vector<int>, decltype(cmp)> ready(cmp);
   for (size_t v = 0; v < t.size(); ++v) {
@@ -121,15 +244,188 @@ void build_chol_tasks(int n, int& nbc, int& nbr, std::vector<int>& out) {
   while (!ready.empty()) {
     const int v = ready.top();
     ready.pop();
-    out.push_back(t[v].type); out.push_back(t[v].i); out.push_back(t[v].j); out.push_back(t[v].k);
+    cs.tasks.insert(cs.tasks.end(), t[v].rec, t[v].rec + kTaskInts);
     for (int s2 : t[v].succ)
       if (--indeg[s2] == 0) ready.push(s2);
   }
+  cs.ntasks = (int)cs.tasks.size() / kTaskInts;
 }
 
-static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, int N, int H, int W,
-                      int t0, int t1, int eta_rows, int motion_only, int own_lo, int own_hi) {
-  if (E < 0 || N <= 0 || H <= 0 || W <= 0) return fail(kInvalidArgument, "ba: bad sizes");
+// ---------------------------------------------------------------------------
+// Pose orderings for the reduced system (adjacency of poses sharing a block).
+// ---------------------------------------------------------------------------
+static std::vector<int> order_rcm(int P, const std::vector<std::vector<int>>& adj) {
+  std::vector<int> deg(P), out;
+  for (int a = 0; a < P; ++a) deg[a] = (int)adj[a].size();
+  std::vector<char> done(P, 0);
+  std::vector<int> lvl(P);
+  auto bfs = [&](int s, std::vector<int>& seq, bool mark) {
+    std::vector<char> seen(P, 0);
+    seq.clear();
+    seq.push_back(s); seen[s] = 1; lvl[s] = 0;
+    for (size_t q = 0; q < seq.size(); ++q) {
+      std::vector<int> nb;
+      for (int b : adj[seq[q]]) if (!seen[b] && !done[b]) nb.push_back(b);
+      std::sort(nb.begin(), nb.end(), [&](int x, int y) { return deg[x] != deg[y] ? deg[x] < deg[y] : x < y; });
+      for (int b : nb) { seen[b] = 1; lvl[b] = lvl[seq[q]] + 1; seq.push_back(b); }
+    }
+    if (mark) for (int v : seq) done[v] = 1;
+  };
+  std::vector<int> seq;
+  for (int s0 = 0; s0 < P; ++s0) {
+    if (done[s0]) continue;
+    // pseudo-peripheral start: repeat BFS from the farthest, lowest-degree node
+    int s = s0, ecc = -1;
+    for (int it = 0; it < 4; ++it) {
+      bfs(s, seq, false);
+      const int e = lvl[seq.back()];
+      if (e <= ecc) break;
+      ecc = e;
+      int best = seq.back();
+      for (int v : seq) if (lvl[v] == e && deg[v] < deg[best]) best = v;
+      s = best;
+    }
+    bfs(s, seq, true);
+    out.insert(out.end(), seq.begin(), seq.end());
+  }
+  std::reverse(out.begin(), out.end());
+  std::vector<int> perm(P);
+  for (int q = 0; q < P; ++q) perm[out[q]] = q;
+  return perm;
+}
+
+static std::vector<int> order_mindeg(int P, const std::vector<std::vector<int>>& adj) {
+  const int nw = (P + 63) / 64;
+  std::vector<uint64_t> g((size_t)P * nw, 0);
+  for (int a = 0; a < P; ++a)
+    for (int b : adj[a]) g[(size_t)a * nw + (b >> 6)] |= 1ull << (b & 63);
+  std::vector<int> deg(P), perm(P, -1);
+  std::vector<char> alive(P, 1);
+  for (int a = 0; a < P; ++a) deg[a] = (int)adj[a].size();
+  std::vector<int> nb;
+  for (int q = 0; q < P; ++q) {
+    int v = -1;
+    for (int a = 0; a < P; ++a)
+      if (alive[a] && (v < 0 || deg[a] < deg[v])) v = a;
+    perm[v] = q;
+    alive[v] = 0;
+    nb.clear();
+    for (int w = 0; w < nw; ++w) {
+      uint64_t m = g[(size_t)v * nw + w];
+      while (m) { const int b = 64 * w + __builtin_ctzll(m); m &= m - 1; if (alive[b]) nb.push_back(b); }
+    }
+    for (int b : nb) {
+      uint64_t* gb = &g[(size_t)b * nw];
+      const uint64_t* gv = &g[(size_t)v * nw];
+      int d = 0;
+      for (int w = 0; w < nw; ++w) gb[w] |= gv[w];
+      gb[b >> 6] &= ~(1ull << (b & 63));
+      gb[v >> 6] &= ~(1ull << (v & 63));
+      for (int w = 0; w < nw; ++w) {
+        uint64_t m = gb[w];
+        while (m) { const int c = 64 * w + __builtin_ctzll(m); m &= m - 1; d += alive[c]; }
+      }
+      deg[b] = d;
+    }
+  }
+  return perm;
+}
+
+static void tile_pattern(int n, int P, const std::vector<int>& perm, const std::vector<std::pair<int, int>>& pairs,
+                         std::vector<char>& pat) {
+  const int nbc = (n + 63) / 64, nbr = (n + 1 + 63) / 64;
+  pat.assign((size_t)nbr * nbc, 0);
+  auto mark = [&](int pa, int pb) {  // 6x6 block at permuted pose positions pa >= pb
+    for (int ti = (6 * pa) >> 6; ti <= (6 * pa + 5) >> 6; ++ti)
+      for (int tj = (6 * pb) >> 6; tj <= (6 * pb + 5) >> 6; ++tj)
+        if (tj <= ti) pat[(size_t)ti * nbc + tj] = 1;
+  };
+  for (int a = 0; a < P; ++a) mark(perm[a], perm[a]);
+  for (auto& pr : pairs) {
+    const int pa = perm[pr.first], pb = perm[pr.second];
+    mark(std::max(pa, pb), std::min(pa, pb));
+  }
+}
+
+static long order_cost(int n, int P, const std::vector<int>& perm, const std::vector<std::pair<int, int>>& pairs) {
+  std::vector<char> pat;
+  tile_pattern(n, P, perm, pairs, pat);
+  TileBits tb;
+  init_bits(tb, n);
+  for (int i = 0; i < tb.nbr; ++i)
+    for (int j = 0; j <= std::min(i, tb.nbc - 1); ++j)
+      if (pat[(size_t)i * tb.nbc + j]) tb.set(i, j);
+  close_bits(tb);
+  return count_updates(tb);
+}
+
+// the reduced system's pose-pair pattern: edge blocks (i,j) and Schur blocks of
+// every pair of optimised rows sharing a depth frame (the global graph, so every
+// rank of a sharded BA derives the same structure)
+static void pose_pairs(const std::vector<int>& gi, const std::vector<int>& gj, int t0, int t1,
+                       std::vector<std::pair<int, int>>& pairs, int motion_only) {
+  const int P = t1 - t0;
+  std::vector<std::vector<int>> rows;  // optimised poses per depth frame
+  std::map<int, int> fidx;
+  pairs.clear();
+  for (size_t e = 0; e < gi.size(); ++e) {
+    const int a = gi[e] - t0, b = gj[e] - t0;
+    if (a >= 0 && a < P && b >= 0 && b < P && a != b) pairs.push_back({std::max(a, b), std::min(a, b)});
+  }
+  if (!motion_only) {
+    for (size_t e = 0; e < gi.size(); ++e) {
+      auto it = fidx.find(gi[e]);
+      int f;
+      if (it == fidx.end()) {
+        f = (int)rows.size();
+        fidx[gi[e]] = f;
+        rows.push_back({});
+        if (gi[e] >= t0 && gi[e] < t1) rows[f].push_back(gi[e] - t0);
+      } else {
+        f = it->second;
+      }
+      if (gj[e] >= t0 && gj[e] < t1) rows[f].push_back(gj[e] - t0);
+    }
+    for (auto& r : rows) {
+      std::sort(r.begin(), r.end());
+      r.erase(std::unique(r.begin(), r.end()), r.end());
+      for (size_t x = 0; x < r.size(); ++x)
+        for (size_t y = 0; y < x; ++y) pairs.push_back({r[x], r[y]});
+    }
+  }
+  std::sort(pairs.begin(), pairs.end());
+  pairs.erase(std::unique(pairs.begin(), pairs.end()), pairs.end());
+}
+
+static void choose_order(BaPlan& p, const std::vector<std::pair<int, int>>& pairs) {
+  const int P = p.P, n = p.n;
+  std::vector<int> ident(P);
+  for (int a = 0; a < P; ++a) ident[a] = a;
+  p.perm = ident;
+  p.order_kind = 0;
+  const char* force = getenv("DROID_BA_ORDER");  // identity | rcm | mindeg (A/B and tests)
+  if (P <= 32 && !force) return;                  // a handful of tiles: nothing to gain
+  std::vector<std::vector<int>> adj(P);
+  for (auto& pr : pairs) { adj[pr.first].push_back(pr.second); adj[pr.second].push_back(pr.first); }
+  if (force) {
+    const std::string f(force);
+    if (f == "rcm") { p.perm = order_rcm(P, adj); p.order_kind = 1; }
+    else if (f == "mindeg") { p.perm = order_mindeg(P, adj); p.order_kind = 2; }
+    return;
+  }
+  long best = order_cost(n, P, ident, pairs);
+  // the identity is kept unless an ordering saves more than 5 % of the tile updates
+  for (int kind = 1; kind <= 2; ++kind) {
+    std::vector<int> perm = kind == 1 ? order_rcm(P, adj) : order_mindeg(P, adj);
+    const long c = order_cost(n, P, perm, pairs);
+    if (c * 20 < best * 19) { best = c; p.perm = perm; p.order_kind = kind; }
+  }
+}
+
+static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, const int64_t* gii,
+                      const int64_t* gjj, int gE, int N, int H, int W, int t0, int t1, int eta_rows,
+                      int motion_only, int own_lo, int own_hi) {
+  if (E < 0 || gE < 0 || N <= 0 || H <= 0 || W <= 0) return fail(kInvalidArgument, "ba: bad sizes");
   if (t0 < 0 || t1 <= t0 || t1 > N)
     return fail(kInvalidArgument, "ba: need 0 <= t0 < t1 <= num_frames");
   p.E = E; p.N = N; p.H = H; p.W = W; p.HW = H * W;
@@ -141,6 +437,13 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, in
       return fail(kInvalidArgument, "ba: edge index out of range");
     p.ii[e] = (int)ii[e];
     p.jj[e] = (int)jj[e];
+  }
+  std::vector<int> gi(gE), gj(gE);
+  for (int e = 0; e < gE; ++e) {
+    if (gii[e] < 0 || gii[e] >= N || gjj[e] < 0 || gjj[e] >= N)
+      return fail(kInvalidArgument, "ba: global edge index out of range");
+    gi[e] = (int)gii[e];
+    gj[e] = (int)gjj[e];
   }
   const int HW = p.HW;
 
@@ -175,12 +478,15 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, in
   p.group_per_wave = std::max(1, std::min(rounds, (int)((long)p.K * rounds / 1024)));
   p.nchunk = ceil_div(rounds, p.group_per_wave);
 
-  // Schur rows per frame: [Ei row if the frame's pose is optimised] + one Eij row per edge
+  // Schur rows per frame: [Ei row if the frame's pose is optimised] + one Eij row per edge.
+  // Frames whose Gram fits the register tile (<= kNbMax tiles a side) take the
+  // one-kernel path; the others the wide (prep + blocked Gram) path.
   p.f_rptr.assign(p.K + 1, 0);
   p.r_pose.clear(); p.r_edge.clear();
   p.f_nb.assign(p.K, 0); p.f_goff.assign(p.K, 0);
-  p.nb_max = 1;
-  p.gram_floats = 0;
+  p.wide_f.clear(); p.wide_eoff.clear(); p.wide_tasks.clear();
+  p.nb_max = 1; p.nb_all = 1;
+  p.gram_floats = 0; p.ei_floats = 0;
   for (int f = 0; f < p.K; ++f) {
     const int kf = p.kx[f];
     if (kf >= t0 && kf < t1) { p.r_pose.push_back(kf - t0); p.r_edge.push_back(-1); }
@@ -193,20 +499,46 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, in
     p.f_rptr[f + 1] = (int)p.r_pose.size();
     const int nrows = p.f_rptr[f + 1] - p.f_rptr[f];
     const int nb = ceil_div(6 * nrows + 1, 16);
-    if (!motion_only && nb > kNbMax)
-      return fail(kUnsupported, "ba: a depth frame has " + std::to_string(nrows - 1) +
-                                    " outgoing edges; the Schur kernel supports up to 20");
     p.f_nb[f] = nb;
-    p.nb_max = std::max(p.nb_max, nb);
+    p.nb_all = std::max(p.nb_all, nb);
+    if (nb > kNbMax) {
+      const int w = (int)p.wide_f.size();
+      p.wide_f.push_back(f);
+      p.wide_eoff.push_back((int)p.ei_floats);
+      p.ei_floats += 6L * HW;
+      const int nblk = ceil_div(nb, kWideBlk);
+      for (int a = 0; a < nblk; ++a)
+        for (int b = a; b < nblk; ++b) { p.wide_tasks.push_back(w); p.wide_tasks.push_back(a); p.wide_tasks.push_back(b); }
+    } else {
+      p.nb_max = std::max(p.nb_max, nb);
+    }
     p.f_goff[f] = (int)p.gram_floats;
     p.gram_floats += (long)p.nchunk * (nb * (nb + 1) / 2) * 256;
   }
-  if (motion_only) p.gram_floats = 0;
+  if (p.gram_floats > 0x7fffffffL || p.ei_floats > 0x7fffffffL)
+    return fail(kUnsupported, "ba: Schur workspace exceeds 2^31 floats");
+  if (motion_only) { p.gram_floats = 0; p.ei_floats = 0; p.wide_f.clear(); p.wide_eoff.clear(); p.wide_tasks.clear(); }
 
-  // Block contribution lists for the lower triangle of the reduced system.
-  std::map<std::pair<int, int>, std::vector<Contrib>> blocks;
-  std::vector<std::vector<Contrib>> rhs(p.P);
+  // pose order + tile structure of the factor (from the global graph)
   const int P = p.P;
+  std::vector<std::pair<int, int>> pairs;
+  pose_pairs(gi, gj, t0, t1, pairs, motion_only);
+  choose_order(p, pairs);
+  {
+    std::vector<char> pat;
+    tile_pattern(p.n, P, p.perm, pairs, pat);
+    build_chol_structure(p.n, pat, p.cs);
+  }
+  std::vector<int> iperm(P);
+  for (int a = 0; a < P; ++a) iperm[p.perm[a]] = a;
+  p.outmap.assign(p.n, 0);
+  for (int v = 0; v < p.n; ++v) p.outmap[v] = 6 * iperm[v / 6] + v % 6;
+  p.rhs_pos = p.perm;
+
+  // Block contribution lists for the lower triangle of the reduced system
+  // (original pose indices r >= c; the kernel maps them to permuted positions).
+  std::map<std::pair<int, int>, std::vector<Contrib>> blocks;
+  std::vector<std::vector<Contrib>> rhs(P);
   for (int e = 0; e < E; ++e) {
     const int i = p.ii[e] - t0, j = p.jj[e] - t0;
     const int idx[2] = {i, j};
@@ -236,8 +568,8 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, in
   }
   p.blk_a.clear(); p.blk_b.clear(); p.blk_cptr.assign(1, 0); p.contrib.clear();
   for (auto& kv : blocks) {
-    p.blk_a.push_back(kv.first.first);
-    p.blk_b.push_back(kv.first.second);
+    p.blk_a.push_back(p.perm[kv.first.first]);
+    p.blk_b.push_back(p.perm[kv.first.second]);
     for (auto& c : kv.second) p.contrib.push_back(c);
     p.blk_cptr.push_back((int)p.contrib.size());
   }
@@ -265,14 +597,17 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, in
   p.o_frptr = put(p.f_rptr); p.o_rpose = put(p.r_pose); p.o_redge = put(p.r_edge);
   p.o_fnb = put(p.f_nb); p.o_fgoff = put(p.f_goff);
   p.o_blka = put(p.blk_a); p.o_blkb = put(p.blk_b); p.o_blkcptr = put(p.blk_cptr);
-  p.o_rhscptr = put(p.rhs_cptr);
+  p.o_rhscptr = put(p.rhs_cptr); p.o_rhspos = put(p.rhs_pos);
   p.o_contrib = putc(p.contrib); p.o_rhscontrib = putc(p.rhs_contrib);
-  build_chol_tasks(p.n, p.nbc, p.nbr, p.tasks);
-  p.ntasks = (int)p.tasks.size() / 4;
-  p.o_tasks = put(p.tasks);
+  p.o_tasks = put(p.cs.tasks);
+  p.o_slot = put(p.cs.slot); p.o_fin = put(p.cs.fin); p.o_ycnt = put(p.cs.ycnt);
+  p.o_outmap = put(p.outmap);
+  p.o_widef = put(p.wide_f); p.o_wideeoff = put(p.wide_eoff); p.o_widetasks = put(p.wide_tasks);
   if (p.ints.empty()) p.ints.push_back(0);
-  p.ld = (p.n + 1 + 7) / 8 * 8;
-  p.sync_bytes = align_up((size_t)(4 + p.nbr * p.nbc + 2 * p.nbc) * 4, 16);
+  const int nbc = p.cs.nbc;
+  p.sync_bytes = align_up((size_t)(4 + p.cs.nslots + 2 * nbc) * 4, 16);
+  if ((size_t)std::max(p.cs.nslots, 1) * kTile * 8 >= 0x80000000ull)
+    return fail(kUnsupported, "ba: factor tiles exceed the 2 GB buffer-resource range");
 
   // workspace layout
   size_t off = 0;
@@ -280,12 +615,13 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, in
   p.off_hpart = off; off = align_up(off + (size_t)std::max(E, 1) * p.nsplit * kHessStride * 4, 256);
   p.off_gram = off; off = align_up(off + (size_t)std::max(p.gram_floats, 1L) * 4, 256);
   p.off_qw = off; off = align_up(off + (size_t)2 * p.K * HW * 4 + 4, 256);
-  p.off_M = off; off = align_up(off + (size_t)(p.n + 1) * p.ld * 8, 256);
+  p.off_ei = off; off = align_up(off + (size_t)std::max(p.ei_floats, 1L) * 4, 256);
+  p.off_M = off; off = align_up(off + (size_t)std::max(p.cs.nslots, 1) * kTile * 8, 256);
   p.off_x = off; off = align_up(off + (size_t)(p.n + 1) * 8, 256);
   p.off_flag = off; off = align_up(off + 64, 256);
   p.off_sync = off; off = align_up(off + p.sync_bytes, 256);
-  p.off_linv = off; off = align_up(off + (size_t)std::max(p.nbc, 1) * 64 * 64 * 8, 256);
-  p.off_ybuf = off; off = align_up(off + (size_t)std::max(p.nbc, 1) * 64 * 8, 256);
+  p.off_linv = off; off = align_up(off + (size_t)std::max(nbc, 1) * kTile * 8, 256);
+  p.off_ybuf = off; off = align_up(off + (size_t)std::max(nbc, 1) * 64 * 8, 256);
   p.total = off;
   return kOk;
 }
@@ -296,62 +632,95 @@ using namespace droid;
 
 extern "C" {
 
-int droid_ba_plan_create(const int64_t* ii, const int64_t* jj, int num_edges, int num_frames,
-                         int ht, int wd, int t0, int t1, int eta_rows, int motion_only,
-                         int own_lo, int own_hi, void** plan_out) {
+// Sharded BA: ii/jj are this rank's edges; gii/gjj the global edge list, from
+// which the pose order and the factor's tile structure are derived (identical
+// on every rank, so the reduced systems line up for the all-reduce).
+int droid_ba_plan_create_sharded(const int64_t* ii, const int64_t* jj, int num_edges, const int64_t* gii,
+                                 const int64_t* gjj, int num_global_edges, int num_frames, int ht, int wd, int t0,
+                                 int t1, int eta_rows, int motion_only, int own_lo, int own_hi, void** plan_out) {
   if (!plan_out) return fail(kInvalidArgument, "ba_plan_create: null output");
   *plan_out = nullptr;
   auto* p = new BaPlan();
-  int st = build_plan(*p, ii, jj, num_edges, num_frames, ht, wd, t0, t1, eta_rows, motion_only,
-                      own_lo, own_hi);
+  int st = build_plan(*p, ii, jj, num_edges, gii, gjj, num_global_edges, num_frames, ht, wd, t0, t1, eta_rows,
+                      motion_only, own_lo, own_hi);
   if (st != kOk) { delete p; return st; }
   *plan_out = p;
   return kOk;
 }
 
-// Dense SPD solve of an augmented system on the dataflow Cholesky alone (no
-// BA): n pivots, ld = n+1 rounded up to 8; rows 0..n-1 hold the lower
-// triangle of A, row n the rhs b (droid_ba_plan_system_region locates it).
+int droid_ba_plan_create(const int64_t* ii, const int64_t* jj, int num_edges, int num_frames,
+                         int ht, int wd, int t0, int t1, int eta_rows, int motion_only,
+                         int own_lo, int own_hi, void** plan_out) {
+  return droid_ba_plan_create_sharded(ii, jj, num_edges, ii, jj, num_edges, num_frames, ht, wd, t0, t1, eta_rows,
+                                      motion_only, own_lo, own_hi, plan_out);
+}
+
+// Dense SPD solve of an n x n system on the dataflow Cholesky alone (no BA):
+// every lower tile present, identity order.  droid_chol_set_system loads A, b.
 int droid_chol_plan_create(int n, void** plan_out) {
   if (!plan_out || n < 0) return fail(kInvalidArgument, "chol_plan_create: bad arguments");
   auto* p = new BaPlan();
   p->n = n;
   p->P = 0;
   p->motion_only = 1;
-  build_chol_tasks(n, p->nbc, p->nbr, p->tasks);
-  p->ntasks = (int)p->tasks.size() / 4;
-  p->ints = p->tasks;
-  p->o_tasks = 0;
+  const int nbc = (n + 63) / 64, nbr = (n + 1 + 63) / 64;
+  std::vector<char> pat((size_t)nbr * nbc, 1);
+  build_chol_structure(n, pat, p->cs);
+  p->outmap.resize(n);
+  for (int v = 0; v < n; ++v) p->outmap[v] = v;
+  p->ints.clear();
+  auto put = [&](const std::vector<int>& v) {
+    size_t o = p->ints.size();
+    p->ints.insert(p->ints.end(), v.begin(), v.end());
+    while (p->ints.size() % 4) p->ints.push_back(0);
+    return o;
+  };
+  p->o_tasks = put(p->cs.tasks);
+  p->o_slot = put(p->cs.slot); p->o_fin = put(p->cs.fin); p->o_ycnt = put(p->cs.ycnt);
+  p->o_outmap = put(p->outmap);
   if (p->ints.empty()) p->ints.push_back(0);
-  p->ld = (n + 1 + 7) / 8 * 8;
-  p->sync_bytes = align_up((size_t)(4 + p->nbr * p->nbc + 2 * p->nbc) * 4, 16);
+  p->sync_bytes = align_up((size_t)(4 + p->cs.nslots + 2 * nbc) * 4, 16);
   size_t off = 0;
   p->off_ints = off; off = align_up(off + p->ints.size() * 4, 256);
-  p->off_M = off; off = align_up(off + (size_t)(n + 1) * p->ld * 8, 256);
+  p->off_M = off; off = align_up(off + (size_t)std::max(p->cs.nslots, 1) * kTile * 8, 256);
   p->off_x = off; off = align_up(off + (size_t)(n + 1) * 8, 256);
   p->off_flag = off; off = align_up(off + 64, 256);
   p->off_sync = off; off = align_up(off + p->sync_bytes, 256);
-  p->off_linv = off; off = align_up(off + (size_t)std::max(p->nbc, 1) * 64 * 64 * 8, 256);
-  p->off_ybuf = off; off = align_up(off + (size_t)std::max(p->nbc, 1) * 64 * 8, 256);
+  p->off_linv = off; off = align_up(off + (size_t)std::max(nbc, 1) * kTile * 8, 256);
+  p->off_ybuf = off; off = align_up(off + (size_t)std::max(nbc, 1) * 64 * 8, 256);
   p->total = off;
   *plan_out = p;
   return kOk;
 }
 
-int droid_chol_plan_info(const void* plan, int* ld, int* ntasks, int* flag_offset) {
+// ntasks, the flag word's byte offset in the workspace, tile slots (all / input region)
+int droid_chol_plan_info(const void* plan, int* ntasks, int* flag_offset, int* nslots, int* nslots_input) {
   auto* p = static_cast<const BaPlan*>(plan);
   if (!p) return fail(kInvalidArgument, "chol_plan_info: null plan");
-  if (ld) *ld = p->ld;
-  if (ntasks) *ntasks = p->ntasks;
+  if (ntasks) *ntasks = p->cs.ntasks;
   if (flag_offset) *flag_offset = (int)p->off_flag;
+  if (nslots) *nslots = p->cs.nslots;
+  if (nslots_input) *nslots_input = p->cs.nslots_a;
   return kOk;
 }
 
-// the plan's Cholesky task list in ticket order (4 ints per task: type, i, j, k)
+// the plan's Cholesky task list in ticket order (kTaskInts ints per task)
 int droid_chol_plan_tasks(const void* plan, int* out) {
   auto* p = static_cast<const BaPlan*>(plan);
   if (!p || !out) return fail(kInvalidArgument, "chol_plan_tasks: null argument");
-  std::copy(p->tasks.begin(), p->tasks.end(), out);
+  std::copy(p->cs.tasks.begin(), p->cs.tasks.end(), out);
+  return kOk;
+}
+
+// slot map (nbr*nbc ints, -1 = structural zero), final tile versions (nslots),
+// final y versions (nbc), and the permuted-var -> dx index map (n)
+int droid_chol_plan_structure(const void* plan, int* slot, int* fin, int* ycnt, int* outmap) {
+  auto* p = static_cast<const BaPlan*>(plan);
+  if (!p) return fail(kInvalidArgument, "chol_plan_structure: null plan");
+  if (slot) std::copy(p->cs.slot.begin(), p->cs.slot.end(), slot);
+  if (fin) std::copy(p->cs.fin.begin(), p->cs.fin.end(), fin);
+  if (ycnt) std::copy(p->cs.ycnt.begin(), p->cs.ycnt.end(), ycnt);
+  if (outmap) std::copy(p->outmap.begin(), p->outmap.end(), outmap);
   return kOk;
 }
 
@@ -367,7 +736,19 @@ int droid_ba_plan_info(const void* plan, int* K, int* P, int* nblocks, int* nb_m
   if (K) *K = p->K;
   if (P) *P = p->P;
   if (nblocks) *nblocks = (int)p->blk_a.size();
-  if (nb_max) *nb_max = p->nb_max;
+  if (nb_max) *nb_max = p->nb_all;
+  return kOk;
+}
+
+// order kind (0 identity, 1 RCM, 2 min degree), the pose order (P ints),
+// number of wide-path frames and tile tasks
+int droid_ba_plan_order(const void* plan, int* kind, int* perm, int* num_wide, int* ntasks) {
+  auto* p = static_cast<const BaPlan*>(plan);
+  if (!p) return fail(kInvalidArgument, "ba_plan_order: null plan");
+  if (kind) *kind = p->order_kind;
+  if (perm) std::copy(p->perm.begin(), p->perm.end(), perm);
+  if (num_wide) *num_wide = (int)p->wide_f.size();
+  if (ntasks) *ntasks = p->cs.ntasks;
   return kOk;
 }
 
@@ -378,14 +759,15 @@ int droid_ba_plan_kx(const void* plan, int64_t* out) {
   return kOk;
 }
 
-// Byte offset/size of the reduced system (augmented, n+1 rows of ld fp64 with
-// ld = n+1 rounded up to 8, rhs in the last row) inside the workspace: the
-// buffer a multi-GPU caller all-reduces.
+// Byte offset/size of the reduced system's input tiles (the 64x64 fp64 tiles
+// the assembly writes, rhs row included) inside the workspace: the contiguous
+// buffer a multi-GPU caller all-reduces.  Fill tiles follow it and are zero
+// before the factorisation.
 int droid_ba_plan_system_region(const void* plan, size_t* offset, size_t* bytes) {
   auto* p = static_cast<const BaPlan*>(plan);
   if (!p) return fail(kInvalidArgument, "ba_plan_system_region: null plan");
   *offset = p->off_M;
-  *bytes = (size_t)(p->n + 1) * p->ld * 8;
+  *bytes = (size_t)p->cs.nslots_a * kTile * 8;
   return kOk;
 }
 

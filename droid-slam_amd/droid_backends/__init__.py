@@ -22,7 +22,7 @@ from ._lib import EXPORTS, check, lib
 
 __all__ = ["ba", "frame_distance", "projmap", "depth_filter", "iproj", "altcorr_forward",
            "altcorr_backward", "corr_index_forward", "corr_index_backward",
-           "corr_pyramid_lookup", "projective_transform", "BaPlan", "EXPORTS"]
+           "corr_pyramid_lookup", "projective_transform", "BaPlan", "check_status", "EXPORTS"]
 
 _DTYPES = {torch.float16: 0, torch.float32: 1, torch.float64: 2}
 
@@ -474,17 +474,28 @@ class BaPlan:
 
     Built from host copies of ii/jj (no device sync), uploaded once; reused by
     every ba() with the same edge set.  `own` = (lo, hi) restricts the depth
-    rows to poses owned by this rank (edge-sharded multi-GPU BA)."""
+    rows to poses owned by this rank (edge-sharded multi-GPU BA); `gedges` =
+    (gii, gjj) is then the global edge list the pose order and the factor's
+    tile structure derive from, identical on every rank."""
 
-    def __init__(self, ii, jj, num_frames, ht, wd, t0, t1, eta_rows, motion_only, device, own=None):
+    def __init__(self, ii, jj, num_frames, ht, wd, t0, t1, eta_rows, motion_only, device, own=None, gedges=None):
         ii = np.ascontiguousarray(np.asarray(ii, dtype=np.int64))
         jj = np.ascontiguousarray(np.asarray(jj, dtype=np.int64))
         lo, hi = own if own is not None else (0, 2 ** 31 - 1)
         h = ctypes.c_void_p()
-        check(lib.droid_ba_plan_create(ii.ctypes.data_as(ctypes.c_void_p), jj.ctypes.data_as(ctypes.c_void_p),
-                                       len(ii), int(num_frames), int(ht), int(wd), int(t0), int(t1),
-                                       int(eta_rows), int(bool(motion_only)), int(lo), int(hi),
-                                       ctypes.byref(h)), "ba plan")
+        if gedges is None:
+            check(lib.droid_ba_plan_create(ii.ctypes.data_as(ctypes.c_void_p), jj.ctypes.data_as(ctypes.c_void_p),
+                                           len(ii), int(num_frames), int(ht), int(wd), int(t0), int(t1),
+                                           int(eta_rows), int(bool(motion_only)), int(lo), int(hi),
+                                           ctypes.byref(h)), "ba plan")
+        else:
+            gii = np.ascontiguousarray(np.asarray(gedges[0], dtype=np.int64))
+            gjj = np.ascontiguousarray(np.asarray(gedges[1], dtype=np.int64))
+            check(lib.droid_ba_plan_create_sharded(
+                ii.ctypes.data_as(ctypes.c_void_p), jj.ctypes.data_as(ctypes.c_void_p), len(ii),
+                gii.ctypes.data_as(ctypes.c_void_p), gjj.ctypes.data_as(ctypes.c_void_p), len(gii),
+                int(num_frames), int(ht), int(wd), int(t0), int(t1), int(eta_rows), int(bool(motion_only)),
+                int(lo), int(hi), ctypes.byref(h)), "ba plan")
         self._h = h
         self.device = torch.device(device)
         self.t0, self.t1, self.motion_only = int(t0), int(t1), bool(motion_only)
@@ -495,14 +506,25 @@ class BaPlan:
         kx = np.zeros(max(self.K, 1), dtype=np.int64)
         check(lib.droid_ba_plan_kx(h, kx.ctypes.data_as(ctypes.c_void_p)), "ba plan kx")
         self.kx = kx[:self.K]
+        kind, nwide, ntasks = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        perm = np.zeros(max(self.P, 1), dtype=np.int32)
+        check(lib.droid_ba_plan_order(h, ctypes.byref(kind), perm.ctypes.data_as(ctypes.c_void_p),
+                                      ctypes.byref(nwide), ctypes.byref(ntasks)), "ba plan order")
+        self.order = ("identity", "rcm", "mindeg")[kind.value]
+        self.perm = perm[:self.P]
+        self.num_wide, self.ntasks = nwide.value, ntasks.value
         nbytes = lib.droid_ba_plan_workspace_bytes(h)
         self.workspace = torch.empty((nbytes,), dtype=torch.uint8, device=self.device)
-        off, sz = ctypes.c_size_t(), ctypes.c_size_t()
+        off, sz, foff = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
         check(lib.droid_ba_plan_system_region(h, ctypes.byref(off), ctypes.byref(sz)), "ba plan region")
+        check(lib.droid_ba_plan_flag_offset(h, ctypes.byref(foff)), "ba plan flag")
         self.n = 6 * self.P
-        self.ld = sz.value // (8 * (self.n + 1))     # row stride (doubles): n+1 rounded up to 8
-        # augmented reduced system (rows 0..n-1 = A - S lower triangle, row n = rhs); all-reduce THIS
-        self.system = self.workspace[off.value:off.value + sz.value].view(torch.float64).view(self.n + 1, self.ld)
+        # the reduced system's input tiles (64x64 fp64, permuted lower triangle of
+        # A - S, rhs as row n): the contiguous region a multi-GPU caller all-reduces
+        self.system = self.workspace[off.value:off.value + sz.value].view(torch.float64).view(-1, 64, 64)
+        self._flag = self.workspace[foff.value:foff.value + 4].view(torch.int32)
+        self._status = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._status_evt = None
         with torch.cuda.device(self.device):
             check(lib.droid_ba_plan_upload(h, _ptr(self.workspace), _stream(self.workspace)), "ba plan upload")
 
@@ -512,16 +534,37 @@ class BaPlan:
             lib.droid_ba_plan_destroy(h)
             self._h = None
 
+    def _record_status(self):
+        """queue a copy of the status word of the solve just enqueued (checked lazily)."""
+        self._status.copy_(self._flag, non_blocking=True)
+        self._status_evt = torch.cuda.Event()
+        self._status_evt.record(torch.cuda.current_stream(self.device))
+
+    def check_status(self):
+        """Raise if the last solve's dataflow Cholesky timed out (status bit 1):
+        that solve left poses and disparities unchanged.  Waits for that solve."""
+        evt, self._status_evt = self._status_evt, None
+        if evt is None:
+            return
+        evt.synchronize()
+        if int(self._status[0]) & 2:
+            raise RuntimeError("ba: the dataflow Cholesky timed out (dependency wait exceeded); "
+                               "poses and disparities were left unchanged")
+
     def build_system(self, poses, disps, intrinsics, disps_sens, targets, weights, eta):
-        check(lib.droid_ba_build_system(self._h, _ptr(self.workspace), _ptr(poses), _ptr(disps), _ptr(intrinsics),
-                                        _ptr(disps_sens), _ptr(targets), _ptr(weights), _ptr(eta),
-                                        _stream(poses)), "ba build_system")
+        with torch.cuda.device(self.device):
+            check(lib.droid_ba_build_system(self._h, _ptr(self.workspace), _ptr(poses), _ptr(disps),
+                                            _ptr(intrinsics), _ptr(disps_sens), _ptr(targets), _ptr(weights),
+                                            _ptr(eta), _stream(poses)), "ba build_system")
 
     def solve_update(self, poses, disps, intrinsics, disps_sens, targets, weights, eta, lm, ep, dx, dz):
-        check(lib.droid_ba_solve_update(self._h, _ptr(self.workspace), _ptr(poses), _ptr(disps), _ptr(intrinsics),
-                                        _ptr(disps_sens), _ptr(targets), _ptr(weights), _ptr(eta),
-                                        float(lm), float(ep), _ptr(dx), _ptr(dz), _stream(poses)),
-              "ba solve_update")
+        self.check_status()
+        with torch.cuda.device(self.device):
+            check(lib.droid_ba_solve_update(self._h, _ptr(self.workspace), _ptr(poses), _ptr(disps),
+                                            _ptr(intrinsics), _ptr(disps_sens), _ptr(targets), _ptr(weights),
+                                            _ptr(eta), float(lm), float(ep), _ptr(dx), _ptr(dz), _stream(poses)),
+                  "ba solve_update")
+            self._record_status()
 
     def run(self, poses, disps, intrinsics, disps_sens, targets, weights, eta, iterations, lm, ep):
         dx = torch.empty((self.P, 6), dtype=torch.float32, device=poses.device)
@@ -529,15 +572,24 @@ class BaPlan:
                                                       dtype=torch.float32, device=poses.device)
         if iterations <= 0:
             return dx.zero_(), dz
+        self.check_status()
         with torch.cuda.device(poses.device):
             check(lib.droid_ba_run(self._h, _ptr(self.workspace), _ptr(poses), _ptr(disps), _ptr(intrinsics),
                                    _ptr(disps_sens), _ptr(targets), _ptr(weights), _ptr(eta), int(iterations),
                                    float(lm), float(ep), _ptr(dx), _ptr(dz), _stream(poses)), "ba")
+            self._record_status()
         return dx, dz
 
 
 _PLAN_CACHE = OrderedDict()
 _PLAN_CACHE_SIZE = 8
+
+
+def check_status():
+    """Raise RuntimeError if a cached BA plan's last solve timed out (see
+    BaPlan.check_status); waits for the solves still in flight."""
+    for plan in list(_PLAN_CACHE.values()):
+        plan.check_status()
 
 
 def dense_spd_solve(A, b, lm=0.0, ep=0.0):
@@ -548,38 +600,41 @@ def dense_spd_solve(A, b, lm=0.0, ep=0.0):
     _need(A, torch.float64, "A")
     _need(b, torch.float64, "b")
     n = int(b.numel())
+    if tuple(A.shape) != (n, n):
+        raise RuntimeError("dense_spd_solve: A must be (n, n) with n = len(b)")
     h = ctypes.c_void_p()
     check(lib.droid_chol_plan_create(n, ctypes.byref(h)), "chol plan")
     try:
-        ld, nt, foff = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        check(lib.droid_chol_plan_info(h, ctypes.byref(ld), ctypes.byref(nt), ctypes.byref(foff)), "chol plan info")
+        nt, foff, ns, nsa = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib.droid_chol_plan_info(h, ctypes.byref(nt), ctypes.byref(foff), ctypes.byref(ns), ctypes.byref(nsa)),
+              "chol plan info")
         ws = torch.zeros((lib.droid_ba_plan_workspace_bytes(h),), dtype=torch.uint8, device=A.device)
-        off, sz = ctypes.c_size_t(), ctypes.c_size_t()
-        check(lib.droid_ba_plan_system_region(h, ctypes.byref(off), ctypes.byref(sz)), "chol region")
-        sysm = ws[off.value:off.value + sz.value].view(torch.float64).view(n + 1, ld.value)
-        sysm[:n, :n] = torch.tril(A)
-        sysm[n, :n] = b
         dx = torch.empty(n, dtype=torch.float32, device=A.device)
         with torch.cuda.device(A.device):
             check(lib.droid_ba_plan_upload(h, _ptr(ws), _stream(A)), "chol upload")
+            check(lib.droid_chol_set_system(h, _ptr(ws), _ptr(A), n, _ptr(b), _stream(A)), "chol set_system")
             check(lib.droid_chol_solve(h, _ptr(ws), float(lm), float(ep), _ptr(dx), _stream(A)), "chol solve")
         flag = int(ws[foff.value:foff.value + 4].view(torch.int32).item())
+        if flag & 2:
+            raise RuntimeError("dense_spd_solve: the dataflow Cholesky timed out")
         return dx, bool(flag & 1)
     finally:
         lib.droid_ba_plan_destroy(h)
 
 
-def get_plan(ii_host, jj_host, num_frames, ht, wd, t0, t1, eta_rows, motion_only, device, own=None):
+def get_plan(ii_host, jj_host, num_frames, ht, wd, t0, t1, eta_rows, motion_only, device, own=None, gedges=None):
     ii_host = np.ascontiguousarray(np.asarray(ii_host, dtype=np.int64))
     jj_host = np.ascontiguousarray(np.asarray(jj_host, dtype=np.int64))
+    gkey = None if gedges is None else (np.asarray(gedges[0], np.int64).tobytes(),
+                                        np.asarray(gedges[1], np.int64).tobytes())
     key = (ii_host.tobytes(), jj_host.tobytes(), int(num_frames), int(ht), int(wd), int(t0), int(t1),
-           int(eta_rows), bool(motion_only), str(device), own)
+           int(eta_rows), bool(motion_only), str(device), own, gkey)
     plan = _PLAN_CACHE.get(key)
     if plan is None:
-        plan = BaPlan(ii_host, jj_host, num_frames, ht, wd, t0, t1, eta_rows, motion_only, device, own)
+        plan = BaPlan(ii_host, jj_host, num_frames, ht, wd, t0, t1, eta_rows, motion_only, device, own, gedges)
         _PLAN_CACHE[key] = plan
         while len(_PLAN_CACHE) > _PLAN_CACHE_SIZE:
-            _PLAN_CACHE.popitem(last=False)
+            _PLAN_CACHE.popitem(last=False)[1].check_status()
     else:
         _PLAN_CACHE.move_to_end(key)
     return plan
@@ -604,6 +659,11 @@ def ba(poses, disps, intrinsics, disps_sens, targets, weights, eta, ii, jj, t0, 
     E = ii.shape[0]
     if targets.shape != (E, 2, H, W) or weights.shape != (E, 2, H, W):
         raise RuntimeError("targets/weights must be (E,2,H,W)")
+    # the reference-style call (no host copies of the edge list) synchronises
+    # like the reference's ba (its D2H copies) and reports a failed solve at
+    # once; with ii_host/jj_host the check is deferred to the next solve on the
+    # plan (or droid_backends.check_status()) so update() never stalls the host
+    sync = ii_host is None or jj_host is None
     if ii_host is None:
         ii_host = ii.cpu().numpy()
     if jj_host is None:
@@ -611,4 +671,6 @@ def ba(poses, disps, intrinsics, disps_sens, targets, weights, eta, ii, jj, t0, 
     eta_rows = eta.numel() // (H * W) if eta.numel() else 0
     plan = get_plan(ii_host, jj_host, N, H, W, int(t0), int(t1), eta_rows, motion_only, poses.device)
     dx, dz = plan.run(poses, disps, intrinsics, disps_sens, targets, weights, eta, int(iterations), lm, ep)
+    if sync:
+        plan.check_status()
     return [dx, dz]

@@ -48,6 +48,10 @@ _SIGS = {
     "droid_iproj": ([_p, _p, _p, _i, _i, _i, _p, _p], _i),
     "droid_depth_filter": ([_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p], _i),
     "droid_ba_plan_create": ([_p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, ctypes.POINTER(_p)], _i),
+    "droid_ba_plan_create_sharded": ([_p, _p, _i, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i,
+                                      ctypes.POINTER(_p)], _i),
+    "droid_ba_plan_order": ([_p, ctypes.POINTER(_i), _p, ctypes.POINTER(_i), ctypes.POINTER(_i)], _i),
+    "droid_ba_plan_flag_offset": ([_p, ctypes.POINTER(_sz)], _i),
     "droid_ba_plan_destroy": ([_p], None),
     "droid_ba_plan_workspace_bytes": ([_p], _sz),
     "droid_ba_plan_info": ([_p, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),
@@ -58,9 +62,12 @@ _SIGS = {
     "droid_ba_build_system": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _p], _i),
     "droid_ba_solve_update": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p], _i),
     "droid_chol_plan_create": ([_i, ctypes.POINTER(_p)], _i),
-    "droid_chol_plan_info": ([_p, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)], _i),
+    "droid_chol_plan_info": ([_p, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),
+                              ctypes.POINTER(_i)], _i),
+    "droid_chol_set_system": ([_p, _p, _p, _i, _p, _p], _i),
     "droid_chol_solve": ([_p, _p, _f, _f, _p, _p], _i),
     "droid_chol_plan_tasks": ([_p, _p], _i),
+    "droid_chol_plan_structure": ([_p, _p, _p, _p, _p], _i),
     "droid_ba_run": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _f, _f, _p, _p, _p], _i),
 }
 

@@ -164,7 +164,10 @@ class FactorGraph:
         self.weight = torch.cat([self.weight, weight], 1)
 
     def rm_factors(self, mask, store=False):
-        mask = np.asarray(mask, dtype=bool)
+        # the reference frontend passes device bool tensors (droid_frontend.py:42,106)
+        if isinstance(mask, torch.Tensor):
+            mask = mask.detach().cpu().numpy()
+        mask = np.asarray(mask, dtype=bool).reshape(-1)
         keep = ~mask
         dmask = torch.as_tensor(mask, device=self.device)
         dkeep = ~dmask

@@ -69,9 +69,29 @@ def perturb(poses, disps, rng):
     return p, np.clip(d, 0.05, None)
 
 
-def c3_edges(num_kf=256, num_edges=2048, rng=None, max_out=14):
-    """±1..±3 temporal neighbours plus random bidirectional loop edges |i-j| > 3."""
+def trajectory_laps(n, lap, rng):
+    """world->cam poses of a camera driving `n / lap` laps of a circle (0.05 m
+    per KF, heading along the tangent, a few cm / mrad of lap-to-lap jitter):
+    keyframe i revisits the place of i - lap, as loop closures need."""
+    R = 0.05 * lap / (2 * np.pi)
+    th = 2 * np.pi * np.arange(n) / lap
+    poses = np.zeros((n, 7))
+    for k in range(n):
+        r = R + 0.02 * rng.normal()
+        c = np.array([r * (1 - np.cos(th[k])), 0.01 * rng.normal(), r * np.sin(th[k])])   # camera centre
+        q = _quat_from_rotvec(np.array([0.0, -(th[k] + 0.01 * rng.normal()), 0.0]))     # cam<-world
+        qv, qw = q[:3], q[3]
+        uv = 2 * np.cross(qv, c)
+        poses[k, :3] = -(c + qw * uv + np.cross(qv, uv))
+        poses[k, 3:] = q
+    return poses
+
+
+def c3_edges(num_kf=256, num_edges=2048, rng=None, max_out=None):
+    """±1..±3 temporal neighbours plus random bidirectional loop edges |i-j| > 3
+    (no out-degree cap unless max_out is given)."""
     rng = rng or np.random.default_rng(1003)
+    max_out = max_out or num_kf
     es = [(i, j) for i in range(num_kf) for j in range(num_kf) if i != j and abs(i - j) <= 3]
     have = set(es)
     out = {}
@@ -105,6 +125,47 @@ def c4_edges(num_kf=128, loops=100, rng=None):
         for a, b in ((i, j), (j, i)):
             es.append((a, b))
             have.add((a, b))
+    e = np.asarray(es, dtype=np.int64)
+    return e[:, 0], e[:, 1]
+
+
+def c5_edges(num_kf=2048, lap=256, loop_pairs=None, rng=None):
+    """Sharded config: 2048 KFs driving 8 laps of a circuit
+    (trajectory_laps), ±1..±3 temporal neighbours plus bidirectional revisit
+    loops i <-> i - m*lap + d (m >= 1, |d| <= 2) - the proximity edges
+    frame_distance finds when a trajectory returns to a place - up to ~8 edges
+    per KF (16k edges at 2048 KF)."""
+    rng = rng or np.random.default_rng(1005)
+    es = [(i, j) for i in range(num_kf) for j in range(max(0, i - 3), min(num_kf, i + 4)) if i != j]
+    if loop_pairs is None:
+        loop_pairs = max(0, (8 * num_kf - len(es)) // 2)
+    have = set(es)
+    added = 0
+    while added < loop_pairs and num_kf > lap:
+        i = int(rng.integers(lap, num_kf))
+        m = int(rng.integers(1, i // lap + 1))
+        j = i - m * lap + int(rng.integers(-2, 3))
+        if j < 0 or j >= num_kf or abs(i - j) <= 3 or (i, j) in have:
+            continue
+        for a, b in ((i, j), (j, i)):
+            es.append((a, b))
+            have.add((a, b))
+        added += 1
+    e = np.asarray(es, dtype=np.int64)
+    return e[:, 0], e[:, 1]
+
+
+def dense_edges(num_kf=48, out_degree=42, rng=None):
+    """High-degree graph (the backend's max_factors = 16 t regime and beyond,
+    droid_backend.py:31): every frame links to `out_degree` others, always
+    including its ±1..±3 neighbours."""
+    rng = rng or np.random.default_rng(1006)
+    es = []
+    for i in range(num_kf):
+        near = [j for j in range(max(0, i - 3), min(num_kf, i + 4)) if j != i]
+        far = [j for j in range(num_kf) if j != i and j not in near]
+        pick = rng.choice(far, size=min(len(far), out_degree - len(near)), replace=False)
+        es += [(i, j) for j in near] + [(i, int(j)) for j in sorted(pick)]
     e = np.asarray(es, dtype=np.int64)
     return e[:, 0], e[:, 1]
 
@@ -154,7 +215,7 @@ def reproject_np(poses, disps, intr, ii, jj):
 def ba_problem(config="C2", H=48, W=64, seed=None, edges=None, num_frames=None, t0=None, t1=None,
                sens_fraction=0.0):
     """Inputs of one droid_backends.ba() call for a config (numpy, float32)."""
-    cid = {"C2": 2, "C3": 3, "C4": 4}.get(config, 9)
+    cid = {"C2": 2, "C3": 3, "C4": 4, "C5": 5}.get(config, 9)
     rng = np.random.default_rng(1000 + cid if seed is None else seed)
     if edges is not None:
         ii, jj = edges
@@ -162,6 +223,8 @@ def ba_problem(config="C2", H=48, W=64, seed=None, edges=None, num_frames=None, 
         ii, jj = c2_edges()
     elif config == "C3":
         ii, jj = c3_edges(rng=np.random.default_rng(1003))
+    elif config == "C5":
+        ii, jj = c5_edges()
     else:
         raise ValueError(config)
     N = num_frames or int(max(ii.max(), jj.max())) + 1
@@ -169,7 +232,7 @@ def ba_problem(config="C2", H=48, W=64, seed=None, edges=None, num_frames=None, 
         t0 = 8 if config == "C2" else 1
     if t1 is None:
         t1 = int(max(ii.max(), jj.max())) + 1
-    gt_poses = trajectory(N, rng)
+    gt_poses = trajectory_laps(N, 256, rng) if config == "C5" else trajectory(N, rng)
     gt_disps = smooth_disps(N, H, W, rng)
     targets = reproject_np(gt_poses, gt_disps, INTRINSICS.astype(np.float64), ii, jj)
     targets += rng.normal(0, 0.5, targets.shape)

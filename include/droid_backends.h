@@ -225,21 +225,41 @@ int droid_depth_filter(const float* poses, const float* disps, const float* intr
  * replaces ba (src/droid.cpp:88-117 -> ba_cuda droid_kernels.cu:1314-1434).
  *
  * A plan captures everything of one ba() call that depends only on the edge
- * list (kx = unique([t0,t1) U ii), per-frame edge lists, Schur row graph and
- * the assembly lists of the reduced camera system).  Build it on the host
- * from host copies of ii/jj, upload it once into a caller-allocated device
- * workspace, then run any number of solves with no host synchronisation.
- * own_lo/own_hi restrict which optimised poses get a depth row on this rank
- * (edge-sharded multi-GPU BA); pass 0 / INT32_MAX for a single device. */
+ * list (kx = unique([t0,t1) U ii), per-frame edge lists, Schur row graph, the
+ * assembly lists of the reduced camera system, a fill-reducing pose order and
+ * the tile-sparse structure of its Cholesky factor - SimplicialLLT's analyse
+ * step, droid_kernels.cu:1192-1213).  Build it on the host from host copies of
+ * ii/jj, upload it once into a caller-allocated device workspace, then run any
+ * number of solves with no host synchronisation.  Frames of any out-degree are
+ * accepted.  own_lo/own_hi restrict which optimised poses get a depth row on
+ * this rank (edge-sharded multi-GPU BA); pass 0 / INT32_MAX for a single
+ * device. */
 int droid_ba_plan_create(const int64_t* ii_host, const int64_t* jj_host, int num_edges,
                          int num_frames, int ht, int wd, int t0, int t1, int eta_rows,
                          int motion_only, int own_lo, int own_hi, void** plan_out);
+/* the same for one rank of an edge-sharded BA: ii/jj this rank's edges,
+ * gii/gjj the global edge list the pose order and factor structure come from
+ * (identical on every rank, so the reduced systems add up tile by tile) */
+int droid_ba_plan_create_sharded(const int64_t* ii_host, const int64_t* jj_host, int num_edges,
+                                 const int64_t* gii_host, const int64_t* gjj_host, int num_global_edges,
+                                 int num_frames, int ht, int wd, int t0, int t1, int eta_rows,
+                                 int motion_only, int own_lo, int own_hi, void** plan_out);
 void droid_ba_plan_destroy(void* plan);
 size_t droid_ba_plan_workspace_bytes(const void* plan);
+/* nb_max = largest Schur Gram tile count (16 variables) of any depth frame */
 int droid_ba_plan_info(const void* plan, int* K, int* P, int* nblocks, int* nb_max);
 int droid_ba_plan_kx(const void* plan, int64_t* kx_host);
-/* the augmented (6P+1)^2 fp64 reduced system (rhs = last row) inside the workspace */
+/* kind 0 identity / 1 reverse Cuthill-McKee / 2 minimum degree; perm[pose] =
+ * elimination position (P ints); frames on the wide Schur path; tile tasks */
+int droid_ba_plan_order(const void* plan, int* kind, int* perm, int* num_wide, int* ntasks);
+/* the reduced system's input tiles inside the workspace: 64x64 fp64 tiles of
+ * the permuted lower triangle of A - S with the rhs as row n; the contiguous
+ * region a multi-GPU caller all-reduces (SUM) between build and solve */
 int droid_ba_plan_system_region(const void* plan, size_t* offset, size_t* bytes);
+/* byte offset of the int32 status word: bit 0 = last factorisation not SPD
+ * (dx = 0, as the reference), bit 1 = dataflow solve timed out (poses and
+ * disparities left unchanged; the caller must report an error) */
+int droid_ba_plan_flag_offset(const void* plan, size_t* offset);
 int droid_ba_plan_upload(void* plan, void* workspace, hipStream_t stream);
 
 /* one GN linearisation -> reduced system in the workspace (all-reduce it here for multi-GPU) */
@@ -261,18 +281,25 @@ int droid_ba_run(void* plan, void* workspace, float* poses, float* disps, const 
                  const float* eta, int iterations, float lm, float ep, float* dx, float* dz,
                  hipStream_t stream);
 
-/* Dense damped SPD solve on the same dataflow Cholesky (used by the BA; exposed
- * for direct testing and for callers with their own reduced systems).  The
- * plan's workspace holds the augmented system at droid_ba_plan_system_region:
- * n+1 rows of ld doubles (ld from droid_chol_plan_info), lower triangle of A in
- * rows 0..n-1, rhs b in row n.  droid_chol_solve adds ep + lm*diag, factors in
- * place and writes dx (n, fp32; zero and flag bit 0 set when A is not SPD).
- * Upload with droid_ba_plan_upload; free with droid_ba_plan_destroy. */
+/* Dense damped SPD solve on the same dataflow Cholesky (every lower tile
+ * present, identity order; used for direct testing and by callers with their
+ * own systems).  droid_chol_set_system loads the lower triangle of A (n x n
+ * fp64, row stride lda) and b (n) from device memory into the plan's tiles;
+ * droid_chol_solve adds ep + lm*diag, factors and writes dx (n, fp32; zero and
+ * flag bit 0 set when A is not SPD).  Upload with droid_ba_plan_upload; free
+ * with droid_ba_plan_destroy. */
 int droid_chol_plan_create(int n, void** plan_out);
-int droid_chol_plan_info(const void* plan, int* ld, int* ntasks, int* flag_offset);
+int droid_chol_plan_info(const void* plan, int* ntasks, int* flag_offset, int* nslots, int* nslots_input);
+int droid_chol_set_system(void* plan, void* workspace, const double* A, int lda, const double* b,
+                          hipStream_t stream);
 int droid_chol_solve(void* plan, void* workspace, float lm, float ep, float* dx, hipStream_t stream);
-/* host copy of the task list (4 ints per task: type 0 POTRF 1 TRSM 2 UPDATE 3 BSOLVE 4 BUPD, i, j, k) */
+/* host copy of the task list (8 ints per task: type 0 POTRF 1 TRSM 2 UPDATE 3
+ * BSOLVE 4 BUPD, i, j, k, a, b, 0, 0 - see csrc/ba.hpp) */
 int droid_chol_plan_tasks(const void* plan, int* out);
+/* tile structure of a plan's factor: slot map (nbr*nbc, -1 = zero tile), final
+ * tile versions (nslots), final y versions (nbc), permuted var -> dx index (n);
+ * any pointer may be NULL */
+int droid_chol_plan_structure(const void* plan, int* slot, int* fin, int* ycnt, int* outmap);
 
 #ifdef __cplusplus
 }

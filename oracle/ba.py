@@ -94,8 +94,9 @@ def _linearize(poses, disps, intrinsics, targets, weights, ii, jj):
 
     Ju = np.concatenate([Ji_u, Jj_u], axis=-1)   # (E,HW,12)
     Jv = np.concatenate([Ji_v, Jj_v], axis=-1)
-    H12 = np.einsum("ep,epn,epm->enm", wu, Ju, Ju) + np.einsum("ep,epn,epm->enm", wv, Jv, Jv)
-    v12 = np.einsum("ep,epn->en", wu * ru, Ju) + np.einsum("ep,epn->en", wv * rv, Jv)
+    # sum_p w_p J_p J_p^T as batched matmuls (same sums as the reference's per-pixel accumulation)
+    H12 = np.matmul((wu[..., None] * Ju).transpose(0, 2, 1), Ju) + np.matmul((wv[..., None] * Jv).transpose(0, 2, 1), Jv)
+    v12 = np.matmul((wu * ru)[:, None, :], Ju)[:, 0] + np.matmul((wv * rv)[:, None, :], Jv)[:, 0]
 
     Hs = np.stack([H12[:, :6, :6], H12[:, :6, 6:], H12[:, 6:, :6], H12[:, 6:, 6:]], axis=0)
     vs = np.stack([v12[:, :6], v12[:, 6:]], axis=0)
@@ -133,16 +134,20 @@ def _add_rhs(b, vecs, ii, P):
 
 
 def solve(A, b, lm, ep):
-    """SparseBlock::solve :1192-1213: diag += ep + lm*diag, LLT; dx = 0 on failure."""
+    """SparseBlock::solve :1192-1213: diag += ep + lm*diag, LLT; dx = 0 on failure.
+    (LAPACK potrf + two triangular solves: the same exact factorisation as
+    Eigen's SimplicialLLT up to fp64 roundoff, whatever the ordering.)"""
+    from scipy.linalg import LinAlgError, cho_factor, cho_solve
     L = A.copy()
     idx = np.arange(A.shape[0])
     L[idx, idx] += ep + lm * L[idx, idx]
+    if A.shape[0] == 0:
+        return np.zeros(0), True
     try:
-        C = np.linalg.cholesky(L)
-    except np.linalg.LinAlgError:
+        c = cho_factor(L, lower=True, overwrite_a=True, check_finite=False)
+    except LinAlgError:
         return np.zeros(A.shape[0]), False
-    y = np.linalg.solve(C, b)
-    return np.linalg.solve(C.T, y), True
+    return cho_solve(c, b, check_finite=False), True
 
 
 def ba(poses, disps, intrinsics, disps_sens, targets, weights, eta, ii, jj, t0, t1,
@@ -205,7 +210,8 @@ def ba(poses, disps, intrinsics, disps_sens, targets, weights, eta, ii, jj, t0, 
             if len(rows) == 0:
                 continue
             Ek = Erows[rows]                          # (r,6,HW)
-            G = np.einsum("anp,p,bmp->abnm", Ek, Q[k], Ek)
+            Ef = Ek.reshape(-1, Ek.shape[-1])                 # (r*6, HW)
+            G = ((Ef * Q[k]) @ Ef.T).reshape(len(rows), 6, len(rows), 6).transpose(0, 2, 1, 3)
             for a, ra in enumerate(rows):
                 for c, rc in enumerate(rows):
                     i, j = rowpose[ra], rowpose[rc]

@@ -1,11 +1,14 @@
-"""Host-side check of the dataflow Cholesky's task list (ba_plan.cpp
-build_chol_tasks): executed sequentially in ticket order by a numpy model of
-each task (the kernel's tile algebra, chol_dataflow_kernel; potrf(k) also
-applies its tile's last update and solves trsm(k+1,k); bsolve(c) also applies
-bupd(c,c-1)), every dependency
-the kernel polls for must already hold, every task must run exactly once, and
-the result must be the damped SPD solution.  No GPU needed."""
+"""Host-side check of the dataflow Cholesky's plan (ba_plan.cpp
+build_chol_structure): the task list is executed sequentially in ticket order
+by a numpy model of each task (the kernel's tile algebra, chol_dataflow_kernel;
+potrf(k) also applies its tile's last update and solves tile (k+1,k); bsolve(c)
+also applies bupd(c,c-1)); every version the kernel polls for must already
+hold, every tile's updates must arrive in sequence, every task must run exactly
+once, and the result must be the damped SPD solution.  Dense systems (the
+chol-only plan) and the tile-sparse, pose-permuted reduced systems of BA plans
+(C2, C3 and a C5-shaped 2048-keyframe graph) are covered.  No GPU needed."""
 import ctypes
+import time
 
 import numpy as np
 import pytest
@@ -13,24 +16,69 @@ import pytest
 POTRF, TRSM, UPD, BSOLVE, BUPD = range(5)
 
 
-def tasks_for(n):
+def _lib():
     from droid_backends._lib import check, lib
+    return check, lib
+
+
+def structure(h, n):
+    check, lib = _lib()
+    nt, fo, ns, nsa = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    check(lib.droid_chol_plan_info(h, ctypes.byref(nt), ctypes.byref(fo), ctypes.byref(ns), ctypes.byref(nsa)),
+          "info")
+    nbc, nbr = (n + 63) // 64, (n + 64) // 64
+    tasks = np.zeros(max(8 * nt.value, 1), np.int32)
+    check(lib.droid_chol_plan_tasks(h, tasks.ctypes.data_as(ctypes.c_void_p)), "tasks")
+    slot = np.zeros(max(nbr * nbc, 1), np.int32)
+    fin = np.zeros(max(ns.value, 1), np.int32)
+    ycnt = np.zeros(max(nbc, 1), np.int32)
+    outmap = np.zeros(max(n, 1), np.int32)
+    check(lib.droid_chol_plan_structure(h, slot.ctypes.data_as(ctypes.c_void_p), fin.ctypes.data_as(ctypes.c_void_p),
+                                        ycnt.ctypes.data_as(ctypes.c_void_p), outmap.ctypes.data_as(ctypes.c_void_p)),
+          "structure")
+    return dict(tasks=tasks[:8 * nt.value].reshape(-1, 8), slot=slot[:nbr * nbc].reshape(nbr, nbc),
+                fin=fin[:ns.value], ycnt=ycnt[:nbc], outmap=outmap[:n], nslots=ns.value, nslots_input=nsa.value,
+                nbc=nbc, nbr=nbr)
+
+
+def chol_plan(n):
+    check, lib = _lib()
     h = ctypes.c_void_p()
     check(lib.droid_chol_plan_create(n, ctypes.byref(h)), "chol plan")
     try:
-        ld, nt, fo = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        check(lib.droid_chol_plan_info(h, ctypes.byref(ld), ctypes.byref(nt), ctypes.byref(fo)), "info")
-        out = np.zeros(max(4 * nt.value, 1), np.int32)
-        check(lib.droid_chol_plan_tasks(h, out.ctypes.data_as(ctypes.c_void_p)), "tasks")
-        return out[:4 * nt.value].reshape(-1, 4), ld.value
+        return structure(h, n)
     finally:
         lib.droid_ba_plan_destroy(h)
 
 
-def emulate(M, n, tasks):
-    """M: (n+1, n) augmented (rows 0..n-1 lower A, row n = b). Returns x."""
-    nbc, nbr = (n + 63) // 64, (n + 64) // 64
-    ver = np.zeros((nbr, nbc), int)
+def ba_plan(ii, jj, N, t0, t1, H=4, W=8):
+    check, lib = _lib()
+    ii = np.ascontiguousarray(ii, np.int64)
+    jj = np.ascontiguousarray(jj, np.int64)
+    h = ctypes.c_void_p()
+    kx = np.unique(np.concatenate([np.arange(t0, t1), ii]))
+    t = time.perf_counter()
+    check(lib.droid_ba_plan_create(ii.ctypes.data_as(ctypes.c_void_p), jj.ctypes.data_as(ctypes.c_void_p), len(ii),
+                                   N, H, W, t0, t1, len(kx), 0, 0, 2 ** 31 - 1, ctypes.byref(h)), "ba plan")
+    secs = time.perf_counter() - t
+    try:
+        P = t1 - t0
+        kind, nwide, ntasks = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        perm = np.zeros(max(P, 1), np.int32)
+        check(lib.droid_ba_plan_order(h, ctypes.byref(kind), perm.ctypes.data_as(ctypes.c_void_p),
+                                      ctypes.byref(nwide), ctypes.byref(ntasks)), "order")
+        s = structure(h, 6 * P)
+        s.update(perm=perm[:P], kind=kind.value, nwide=nwide.value, plan_seconds=secs)
+        return s
+    finally:
+        lib.droid_ba_plan_destroy(h)
+
+
+def emulate(M, n, st):
+    """M: (n+1, n) augmented (rows 0..n-1 lower A, row n = b), modified in
+    place on the plan's tiles only.  Returns x (permuted order)."""
+    nbc, nbr, slot, fin, ycnt = st["nbc"], st["nbr"], st["slot"], st["fin"], st["ycnt"]
+    ver = np.zeros(st["nslots"], int)
     yver = np.zeros(nbc, int)
     xdone = np.zeros(nbc, int)
     linv = {}
@@ -38,19 +86,21 @@ def emulate(M, n, tasks):
     x = np.zeros(n)
     blk = lambda i: slice(64 * i, min(64 * i + 64, n + 1))
     col = lambda k: slice(64 * k, min(64 * k + 64, n))
+    S = lambda i, j: slot[i, j]
     seen = set()
-    for t, i, j, k in tasks:
+    for t, i, j, k, a, b, _, _ in st["tasks"]:
         key = (t, i, j, k)
         assert key not in seen
         seen.add(key)
-        if t == POTRF:                       # + the tile's last update (k,k,k-1) and trsm(k+1,k)
-            assert ver[k, k] >= max(k - 1, 0)
+        if t == POTRF:
+            s = S(k, k)
+            assert s >= 0 and ver[s] >= (fin[s] - 2 if a >= 0 else 0)
             R = blk(k)
             Bp = col(k).stop - col(k).start
             T = M[R, col(k)].copy()
-            if k > 0:
-                assert ver[k, k - 1] >= k
-                T -= M[R, col(k - 1)] @ M[col(k), col(k - 1)].T
+            if a >= 0:                                               # the tile's last update (k,k,a)
+                assert ver[s] == fin[s] - 2 and ver[S(k, a)] >= fin[S(k, a)]
+                T -= M[R, col(a)] @ M[col(k), col(a)].T
             L = np.linalg.cholesky(np.tril(T[:Bp]) + np.tril(T[:Bp], -1).T)
             T[:Bp] = L
             if T.shape[0] > Bp:                                      # rhs row inside the diagonal tile
@@ -59,58 +109,184 @@ def emulate(M, n, tasks):
                 yver[k] = 1
             M[R, col(k)] = T
             linv[k] = np.linalg.inv(L)
-            ver[k, k] = k + 1
-            if k + 1 < nbr:
-                assert ver[k + 1, k] >= k
+            ver[s] = fin[s]
+            if b:                                                    # trsm(k+1, k)
+                sb = S(k + 1, k)
+                assert sb >= 0 and ver[sb] >= fin[sb] - 1
                 M[blk(k + 1), col(k)] = M[blk(k + 1), col(k)] @ linv[k].T
                 if k + 1 == nbr - 1:
                     y[64 * k:64 * k + Bp] = M[n, col(k)]
                     yver[k] = 1
-                ver[k + 1, k] = k + 1
+                ver[sb] = fin[sb]
+            else:
+                assert k + 1 >= nbr or S(k + 1, k) < 0
         elif t == TRSM:
-            assert ver[i, k] >= k and ver[k, k] >= k + 1
+            s = S(i, k)
+            assert s >= 0 and ver[s] >= fin[s] - 1 and ver[S(k, k)] >= fin[S(k, k)]
             M[blk(i), col(k)] = M[blk(i), col(k)] @ linv[k].T
             if i == nbr - 1:
                 y[64 * k:64 * k + (col(k).stop - col(k).start)] = M[n, col(k)]
                 yver[k] = 1
-            ver[i, k] = k + 1
+            ver[s] = fin[s]
         elif t == UPD:
-            assert ver[i, j] >= k and ver[i, k] >= k + 1 and ver[j, k] >= k + 1
+            s = S(i, j)
+            assert s >= 0 and ver[s] == a                           # updates arrive in sequence
+            assert ver[S(i, k)] >= fin[S(i, k)] and ver[S(j, k)] >= fin[S(j, k)]
             M[blk(i), col(j)] -= M[blk(i), col(k)] @ M[col(j), col(k)].T
-            ver[i, j] = k + 1
-        elif t == BSOLVE:                    # + bupd(c, c-1)
+            ver[s] = a + 1
+        elif t == BSOLVE:                                            # + bupd(c, c-1) when fused
             c = i
-            assert ver[c, c] >= c + 1 and yver[c] >= 1 + (nbc - 1 - c)
+            assert ver[S(c, c)] >= fin[S(c, c)] and yver[c] >= ycnt[c]
             Bp = col(c).stop - col(c).start
             x[col(c)] = linv[c].T @ y[64 * c:64 * c + Bp]
             xdone[c] = 1
-            if c > 0:
-                assert ver[c, c - 1] >= c and yver[c - 1] >= 1 + (nbc - 1 - c)
+            if a:
+                assert S(c, c - 1) >= 0 and ver[S(c, c - 1)] >= fin[S(c, c - 1)] and yver[c - 1] == ycnt[c - 1] - 1
                 y[64 * (c - 1):64 * c] -= M[col(c), col(c - 1)].T @ x[col(c)]
-                yver[c - 1] = 1 + (nbc - c)
+                yver[c - 1] = ycnt[c - 1]
         else:
             r, c = i, j
-            assert xdone[r] and ver[r, c] >= c + 1 and yver[c] >= 1 + (nbc - 1 - r)
+            assert xdone[r] and ver[S(r, c)] >= fin[S(r, c)] and yver[c] == 1 + a
             y[64 * c:64 * c + 64] -= M[col(r), col(c)].T @ x[col(r)]
-            yver[c] = 1 + (nbc - r)
+            yver[c] = 2 + a
+    assert np.all(ver == fin) and np.all(yver == ycnt) and np.all(xdone == 1)
     return x, len(seen)
 
 
+def _spd_with_blocks(P, pairs, rng):
+    """random SPD 6P x 6P matrix with nonzero 6x6 blocks only on the diagonal and `pairs`."""
+    A = np.zeros((6 * P, 6 * P))
+    for a, b in pairs:
+        B = rng.normal(size=(6, 6))
+        A[6 * a:6 * a + 6, 6 * b:6 * b + 6] = B
+        A[6 * b:6 * b + 6, 6 * a:6 * a + 6] = B.T
+    A += np.diag(np.abs(A).sum(1) + 1.0 + rng.uniform(0, 1, 6 * P))
+    return A
+
+
+def _pose_pairs(ii, jj, t0, t1):
+    """blocks of the reduced system: edge (i,j) plus every pair of optimised
+    rows sharing a depth frame (droid_kernels.cu:1241-1272)."""
+    P = t1 - t0
+    pairs = set()
+    rows = {}
+    for i, j in zip(ii.tolist(), jj.tolist()):
+        if t0 <= i < t1 and t0 <= j < t1 and i != j:
+            pairs.add((max(i, j) - t0, min(i, j) - t0))
+        r = rows.setdefault(i, {i - t0} if t0 <= i < t1 else set())
+        if t0 <= j < t1:
+            r.add(j - t0)
+    for r in rows.values():
+        r = sorted(r)
+        for x in range(len(r)):
+            for y in range(x):
+                pairs.add((r[x], r[y]))
+    return sorted(pairs), P
+
+
+def _check_solves(st, A, perm, rng):
+    n = A.shape[0]
+    b = rng.normal(size=n)
+    pos = (6 * np.repeat(perm, 6) + np.tile(np.arange(6), len(perm)))   # var v -> permuted index
+    Ap = np.zeros_like(A)
+    Ap[np.ix_(pos, pos)] = A
+    bp = np.zeros(n)
+    bp[pos] = b
+    # every nonzero of the permuted lower triangle lies in a tile of the plan
+    tiles = {(r // 64, c // 64) for r, c in zip(*np.nonzero(np.tril(Ap)))}
+    assert all(st["slot"][i, j] >= 0 for i, j in tiles)
+    M = np.zeros((n + 1, n))
+    M[:n] = np.tril(Ap)
+    M[n] = bp
+    x, ran = emulate(M, n, st)
+    assert ran == len(st["tasks"])
+    dx = np.zeros(n)
+    dx[st["outmap"]] = x
+    np.testing.assert_allclose(dx, np.linalg.solve(A, b), rtol=1e-8, atol=1e-10)
+
+
 @pytest.mark.parametrize("n", [6, 63, 64, 65, 128, 130, 300, 1530])
-def test_task_list_solves_spd(n):
+def test_dense_task_list_solves_spd(n):
     rng = np.random.default_rng(n)
-    tasks, ld = tasks_for(n)
-    assert ld % 8 == 0 and ld >= n + 1
+    st = chol_plan(n)
     nbc, nbr = (n + 63) // 64, (n + 64) // 64
+    # the dense DAG: potrf + trsm below the fused one + updates but the fused
+    # ones + bsolve + bupd but the fused ones
     expect = nbc + sum(max(0, nbr - k - 2) for k in range(nbc)) \
         + sum((nbr - jb) * jb for jb in range(1, nbc)) - (nbc - 1) + nbc + nbc * (nbc - 1) // 2 - (nbc - 1)
-    assert len(tasks) == expect
+    assert len(st["tasks"]) == expect
+    assert st["nslots"] == st["nslots_input"] == sum(min(i + 1, nbc) for i in range(nbr))
     Q, _ = np.linalg.qr(rng.normal(size=(n, n)))
     A = (Q * np.geomspace(1, 1e3, n)) @ Q.T
     b = rng.normal(size=n)
     M = np.zeros((n + 1, n))
     M[:n] = np.tril(A)
     M[n] = b
-    x, ran = emulate(M, n, tasks)
-    assert ran == len(tasks)
-    np.testing.assert_allclose(x, np.linalg.solve(A, b), rtol=1e-8, atol=1e-10)
+    x, ran = emulate(M, n, st)
+    assert ran == len(st["tasks"])
+    np.testing.assert_allclose(x[st["outmap"]], np.linalg.solve(A, b), rtol=1e-8, atol=1e-10)
+
+
+def _graph(name):
+    from droid_mi355x import synthetic
+    if name == "C2":
+        ii, jj = synthetic.c2_edges()
+        return ii, jj, 16, 8, 16
+    if name == "C3":
+        ii, jj = synthetic.c3_edges()
+        return ii, jj, 256, 1, 256
+    if name == "C5":
+        ii, jj = synthetic.c5_edges()
+        return ii, jj, 2048, 1, 2048
+    if name == "band":   # +-1..+-3 only: block-tridiagonal in tiles after any sane order
+        ii, jj = synthetic.c5_edges(num_kf=600, loop_pairs=0)
+        return ii, jj, 600, 1, 600
+    raise ValueError(name)
+
+
+@pytest.mark.parametrize("name", ["C2", "C3", "band"])
+def test_ba_plan_task_list_solves_reduced_system(name):
+    ii, jj, N, t0, t1 = _graph(name)
+    st = ba_plan(ii, jj, N, t0, t1)
+    pairs, P = _pose_pairs(ii, jj, t0, t1)
+    rng = np.random.default_rng(7)
+    _check_solves(st, _spd_with_blocks(P, pairs, rng), st["perm"], rng)
+
+
+def test_c5_plan_is_tile_sparse():
+    """2048 KF / ~16k edges with revisit loops: the chosen
+    pose order keeps the factor far from dense, and the plan builds in well
+    under a second."""
+    ii, jj, N, t0, t1 = _graph("C5")
+    assert 15000 <= len(ii) <= 17500
+    st = ba_plan(ii, jj, N, t0, t1)
+    nbc = st["nbc"]
+    dense = sum(min(i + 1, nbc) for i in range(st["nbr"]))
+    assert st["kind"] != 0 and st["nslots"] < 0.15 * dense
+    assert st["plan_seconds"] < 5.0
+    # the all-reduced region (input tiles) of a sharded C5 BA
+    assert st["nslots_input"] * 64 * 64 * 8 < 150e6
+
+
+@pytest.mark.parametrize("order", ["rcm", "mindeg"])
+def test_forced_orders_solve(order, monkeypatch):
+    monkeypatch.setenv("DROID_BA_ORDER", order)
+    ii, jj, N, t0, t1 = _graph("C2")
+    st = ba_plan(ii, jj, N, t0, t1)
+    assert st["kind"] == {"rcm": 1, "mindeg": 2}[order]
+    assert sorted(st["perm"].tolist()) == list(range(t1 - t0))
+    pairs, P = _pose_pairs(ii, jj, t0, t1)
+    rng = np.random.default_rng(8)
+    _check_solves(st, _spd_with_blocks(P, pairs, rng), st["perm"], rng)
+
+
+def test_high_degree_frames_plan():
+    """frames with 40+ outgoing edges (the backend's max_factors = 16 t regime,
+    droid_backend.py:31) are planned on the wide Schur path, no error."""
+    from droid_mi355x import synthetic
+    ii, jj = synthetic.dense_edges(num_kf=48, out_degree=42, rng=np.random.default_rng(3))
+    st = ba_plan(ii, jj, 48, 1, 48)
+    assert st["nwide"] > 0
+    pairs, P = _pose_pairs(ii, jj, 1, 48)
+    rng = np.random.default_rng(9)
+    _check_solves(st, _spd_with_blocks(P, pairs, rng), st["perm"], rng)

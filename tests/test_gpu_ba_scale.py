@@ -1,0 +1,144 @@
+"""BA beyond the C2/C3 shapes, on the GPU vs the fp64 oracle (1e-4 abs, the
+north star's bar):
+
+* high-degree frames (40+ outgoing edges, the backend's max_factors = 16 t
+  regime, droid_backend.py:31): the wide Schur path (ba_frame_prep +
+  ba_frame_gram_wide), no out-degree limit;
+* the C5-shaped global BA (2048 KF / ~16k edges with revisit loops, SURVEY.md
+  §8d) on one device: fill-reducing pose order + tile-sparse dataflow
+  Cholesky on the 12282-variable reduced system;
+* the same BA edge-sharded over 2 ranks (gloo, both on cuda:0): per-rank
+  Schur terms, all-reduce of the input tiles, identical solves.
+The C5 tests use 16x24 depth maps: the graph, not the image, is what C5
+scales, and the fp64 oracle then finishes in well under a minute."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from droid_mi355x import synthetic
+from gpu_util import dev, host
+from oracle import ba as oba
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+KEYS = ("poses", "disps", "intrinsics", "disps_sens", "targets", "weights", "eta", "ii", "jj", "t0", "t1")
+HERE = os.path.dirname(os.path.abspath(__file__))
+C5_HW = (16, 24)
+
+
+def _gpu_ba(prob, iterations, lm, ep):
+    import droid_backends
+    poses, disps = dev(prob["poses"]), dev(prob["disps"])
+    dx, dz = droid_backends.ba(poses, disps, dev(prob["intrinsics"]), dev(prob["disps_sens"]), dev(prob["targets"]),
+                               dev(prob["weights"]), dev(prob["eta"]), dev(prob["ii"]), dev(prob["jj"]), prob["t0"],
+                               prob["t1"], iterations, lm, ep, False)
+    torch.cuda.synchronize()
+    return dict(dx=host(dx), dz=host(dz), poses=host(poses), disps=host(disps))
+
+
+def _check(got, ref, tol=TOL):
+    for k in ("dx", "dz", "poses", "disps"):
+        np.testing.assert_allclose(got[k], ref[k], atol=tol, rtol=0, err_msg=k)
+
+
+@pytest.mark.parametrize("out_degree", [24, 42])
+def test_ba_high_degree_frames(out_degree):
+    import droid_backends
+    ii, jj = synthetic.dense_edges(num_kf=48, out_degree=out_degree, rng=np.random.default_rng(out_degree))
+    prob = synthetic.ba_problem("X", H=24, W=32, seed=90 + out_degree, edges=(ii, jj), sens_fraction=0.2)
+    plan = droid_backends.get_plan(prob["ii"], prob["jj"], 48, 24, 32, 1, 48, prob["eta"].shape[0], False, "cuda:0")
+    assert plan.num_wide > 0 and np.bincount(prob["ii"]).max() >= out_degree
+    got = _gpu_ba(prob, 2, 1e-4, 0.1)
+    ref = oba.ba(**{k: prob[k] for k in KEYS}, iterations=2, lm=1e-4, ep=0.1, motion_only=False)
+    _check(got, ref)
+    assert np.abs(ref["dx"]).max() > 1e-4
+
+
+def test_ba_mixed_narrow_and_wide_frames():
+    """a C3-like graph where a few hub frames carry 30+ loop edges: both Schur paths in one solve."""
+    ii, jj = synthetic.c3_edges(num_kf=64, num_edges=512, rng=np.random.default_rng(5))
+    hubs = [10, 40]
+    extra = [(h, j) for h in hubs for j in range(64) if abs(h - j) > 3 and j % 2 == 0][:56]
+    have = set(zip(ii.tolist(), jj.tolist()))
+    extra = [e for e in extra if e not in have]
+    ii = np.concatenate([ii, [e[0] for e in extra]]).astype(np.int64)
+    jj = np.concatenate([jj, [e[1] for e in extra]]).astype(np.int64)
+    prob = synthetic.ba_problem("X", H=24, W=32, seed=95, edges=(ii, jj))
+    got = _gpu_ba(prob, 2, 1e-5, 1e-2)
+    ref = oba.ba(**{k: prob[k] for k in KEYS}, iterations=2, lm=1e-5, ep=1e-2, motion_only=False)
+    _check(got, ref)
+
+
+@pytest.fixture(scope="module")
+def c5():
+    prob = synthetic.ba_problem("C5", H=C5_HW[0], W=C5_HW[1])
+    ref = oba.ba(**{k: prob[k] for k in KEYS}, iterations=2, lm=1e-5, ep=1e-2, motion_only=False)
+    return prob, ref
+
+
+@pytest.mark.timeout(240)
+def test_ba_c5_scale_unsharded(c5):
+    import droid_backends
+    prob, ref = c5
+    assert prob["t1"] - prob["t0"] == 2047 and len(prob["ii"]) >= 15000
+    plan = droid_backends.get_plan(prob["ii"], prob["jj"], 2048, C5_HW[0], C5_HW[1], 1, 2048,
+                                   prob["eta"].shape[0], False, "cuda:0")
+    assert plan.order != "identity"
+    got = _gpu_ba(prob, 2, 1e-5, 1e-2)
+    _check(got, ref)
+    assert np.abs(ref["dx"]).max() > 1e-4
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.timeout(300)
+def test_ba_c5_sharded_two_ranks(c5, tmp_path):
+    prob, ref = c5
+    env = dict(os.environ, PYTHONUNBUFFERED="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = str(tmp_path / "c5")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(HERE, "sharded_ba_worker.py"), out, str(C5_HW[0]), str(C5_HW[1])],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=280)
+    assert r.returncode == 0, r.stdout.decode(errors="replace")[-3000:]
+    covered = np.zeros(2048, bool)
+    edges = 0
+    for rank in range(2):
+        d = np.load(out + ".rank%d.npz" % rank)
+        lo, hi = (int(x) for x in d["own"])
+        edges += int(d["edges"])
+        np.testing.assert_allclose(d["dx"], ref["dx"], atol=TOL, rtol=0)
+        np.testing.assert_allclose(d["poses"], ref["poses"], atol=TOL, rtol=0)
+        np.testing.assert_allclose(d["disps"][lo:hi], ref["disps"][lo:hi], atol=TOL, rtol=0)
+        covered[lo:hi] = True
+    assert covered.all() and edges == len(prob["ii"])
+
+
+def test_chol_timeout_is_reported_and_state_untouched(monkeypatch):
+    """The dataflow solve's safety net (bounded spins -> abort, flag bit 1):
+    forced here with the test hook, ba() must raise and leave poses/disps as
+    they were (the abort used to corrupt them silently)."""
+    import droid_backends
+    prob = synthetic.ba_problem("C3", H=16, W=24)
+    poses, disps = dev(prob["poses"]), dev(prob["disps"])
+    monkeypatch.setenv("DROID_CHOL_FAULT_INJECT", "1")
+    with pytest.raises(RuntimeError, match="timed out"):
+        droid_backends.ba(poses, disps, dev(prob["intrinsics"]), dev(prob["disps_sens"]), dev(prob["targets"]),
+                          dev(prob["weights"]), dev(prob["eta"]), dev(prob["ii"]), dev(prob["jj"]), prob["t0"],
+                          prob["t1"], 1, 1e-4, 0.1, False)
+    np.testing.assert_array_equal(host(poses), prob["poses"])
+    np.testing.assert_array_equal(host(disps), prob["disps"])
+    monkeypatch.delenv("DROID_CHOL_FAULT_INJECT")
+    got = _gpu_ba(prob, 1, 1e-4, 0.1)          # and the next solve on the same plan is clean
+    assert np.isfinite(got["dx"]).all()

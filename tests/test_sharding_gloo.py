@@ -112,21 +112,69 @@ def test_allreduced_shard_systems_equal_full_system():
     np.testing.assert_allclose(dx_sum, dx_ref, atol=1e-9)
 
 
-def test_reduced_system_index_covers_lower_triangle_and_rhs():
-    """ba_sharded all-reduces only what the Cholesky reads: the packed index
-    holds every (row, col <= row) of A - S and the rhs row, nothing else."""
-    from types import SimpleNamespace
-    from droid_mi355x.depth_video import reduced_system_index
-    n, ld = 12, 16
-    plan = SimpleNamespace(n=n, ld=ld, system=torch.zeros((n + 1, ld), dtype=torch.float64))
-    idx = reduced_system_index(plan).numpy()
-    assert len(idx) == n * (n + 1) // 2 + n == len(np.unique(idx))
-    r, c = idx // ld, idx % ld
-    assert ((r < n) & (c <= r) | (r == n) & (c < n)).all()
-    # a packed sum over two "ranks" equals the full sum on those positions
-    a, b = torch.randn(n + 1, ld, dtype=torch.float64), torch.randn(n + 1, ld, dtype=torch.float64)
-    out = a.clone().view(-1)
-    out.index_copy_(0, torch.as_tensor(idx), a.view(-1)[idx] + b.view(-1)[idx])
-    full = (a + b).view(-1)
-    assert torch.equal(out[idx], full[idx])
-    assert reduced_system_index(plan) is plan._tri_index   # cached on the plan
+def _plan_structure(ii, jj, gii, gjj, N, t0, t1, own):
+    """pose order + factor tile map of a (sharded) BA plan, via the C ABI (no GPU)."""
+    import ctypes
+    from droid_backends._lib import check, lib
+    ii, jj, gii, gjj = (np.ascontiguousarray(a, np.int64) for a in (ii, jj, gii, gjj))
+    kx = np.unique(np.concatenate([np.arange(max(t0, own[0]), min(t1, own[1])), ii]))
+    h = ctypes.c_void_p()
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    check(lib.droid_ba_plan_create_sharded(vp(ii), vp(jj), len(ii), vp(gii), vp(gjj), len(gii), N, H, W, t0, t1,
+                                           len(kx), 0, own[0], own[1], ctypes.byref(h)), "plan")
+    try:
+        P = t1 - t0
+        n = 6 * P
+        nbc, nbr = (n + 63) // 64, (n + 64) // 64
+        perm = np.zeros(P, np.int32)
+        slot = np.zeros(nbr * nbc, np.int32)
+        kind, nw, nt = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib.droid_ba_plan_order(h, ctypes.byref(kind), vp(perm), ctypes.byref(nw), ctypes.byref(nt)), "order")
+        check(lib.droid_chol_plan_structure(h, vp(slot), None, None, None), "structure")
+        return perm, slot
+    finally:
+        lib.droid_ba_plan_destroy(h)
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from droid_mi355x.depth_video import global_edges
+        ii, jj = synthetic.c5_edges(num_kf=512, lap=128)
+        N = 512
+        ii_l, jj_l, own = sharding.shard_edges(ii, jj, N, rank, world)
+        comm = dict(group=None, own=own)
+        gii, gjj = global_edges(ii_l, jj_l, comm)
+        assert global_edges(ii_l, jj_l, comm)[0] is gii          # cached per edge set
+        perm, slot = _plan_structure(ii_l, jj_l, gii, gjj, N, 1, N, own)
+        parts = [None] * world
+        dist.all_gather_object(parts, (np.sort(gii * N + gjj), perm, slot))
+        if rank == 0:
+            q.put(parts)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_sharded_plans_share_one_factor_structure():
+    """Every rank gathers the same global edge list and derives the same pose
+    order and tile map from it, so the per-rank reduced systems add up tile by
+    tile in ba_sharded's all-reduce."""
+    ii, jj = synthetic.c5_edges(num_kf=512, lap=128)
+    ref_perm, ref_slot = _plan_structure(ii, jj, ii, jj, 512, 1, 512, (0, 2 ** 31 - 1))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    parts = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for edges, perm, slot in parts:
+        np.testing.assert_array_equal(edges, np.sort(ii * 512 + jj))
+        np.testing.assert_array_equal(perm, ref_perm)
+        np.testing.assert_array_equal(slot, ref_slot)
