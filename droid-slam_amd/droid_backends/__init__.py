@@ -530,7 +530,7 @@ class BaPlan:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        if h is not None and h.value and lib is not None:   # lib is None during interpreter teardown
             lib.droid_ba_plan_destroy(h)
             self._h = None
 
