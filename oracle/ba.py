@@ -40,7 +40,13 @@ def linearize(poses, disps, intrinsics, targets, weights, ii, jj, chunk=64):
     return _linearize(poses, disps, intrinsics, targets, weights, ii, jj)
 
 
-def _linearize(poses, disps, intrinsics, targets, weights, ii, jj):
+def jacobians(poses, disps, intrinsics, ii, jj):
+    """Per-pixel reprojection and Jacobians of projective_transform_kernel
+    (droid_kernels.cu:281-330): Xj = Tij Xi, d = 1/z (0 where z < MIN_DEPTH),
+    Jj rows for u and v, Ji = -Adj(Tij)^T Jj (adjSE3 :147-175), Jz.  Stereo
+    edges use Tij = (-0.1,0,0 | identity).  Arrays are (E,HW[,6]); pinned
+    against the reference's geom/projective_ops.py (jacobian=True) by
+    tests/golden/projective_ops.npz."""
     E = len(ii)
     _, H, W = disps.shape
     HW = H * W
@@ -68,29 +74,39 @@ def _linearize(poses, disps, intrinsics, targets, weights, ii, jj):
     with np.errstate(divide="ignore"):
         d = np.where(bad, 0.0, 1.0 / np.where(bad, 1.0, z))
     d2 = d * d
+    zero = np.zeros_like(d)
+    Jj_u = fx * np.stack([h * d, zero, -x * h * d2, -x * y * d2, 1 + x * x * d2, -y * d], axis=-1)
+    Jj_v = fy * np.stack([zero, h * d, -y * h * d2, -1 - y * y * d2, x * y * d2, x * d], axis=-1)
+    Jz_u = fx * (tij[:, 0:1] * d - tij[:, 2:3] * (x * d2))
+    Jz_v = fy * (tij[:, 1:2] * d - tij[:, 2:3] * (y * d2))
+    TT = np.broadcast_to(T, (E, HW, 3))
+    QQ = np.broadcast_to(Q, (E, HW, 4))
+    Ji_u = -adj_se3(TT, QQ, Jj_u)
+    Ji_v = -adj_se3(TT, QQ, Jj_v)
+    return dict(x=x, y=y, z=z, h=h, d=d, bad=bad, stereo=stereo, Jj_u=Jj_u, Jj_v=Jj_v, Ji_u=Ji_u, Ji_v=Ji_v,
+                Jz_u=Jz_u, Jz_v=Jz_v, coords=np.stack([fx * d * x + cx, fy * d * y + cy], -1))
+
+
+def _linearize(poses, disps, intrinsics, targets, weights, ii, jj):
+    E = len(ii)
+    _, H, W = disps.shape
+    HW = H * W
+    fx, fy, cx, cy = [float(v) for v in intrinsics]
+    J = jacobians(poses, disps, intrinsics, ii, jj)
+    x, y, d, bad, stereo = J["x"], J["y"], J["d"], J["bad"], J["stereo"]
+    Jj_u, Jj_v, Ji_u, Ji_v, Jz_u, Jz_v = J["Jj_u"], J["Jj_v"], J["Ji_u"], J["Ji_v"], J["Jz_u"], J["Jz_v"]
     tg = targets.reshape(E, 2, HW)
     wt = weights.reshape(E, 2, HW)
     wu = np.where(bad, 0.0, 0.001 * wt[:, 0])
     wv = np.where(bad, 0.0, 0.001 * wt[:, 1])
     ru = tg[:, 0] - (fx * d * x + cx)
     rv = tg[:, 1] - (fy * d * y + cy)
-    zero = np.zeros_like(d)
-
-    Jj_u = fx * np.stack([h * d, zero, -x * h * d2, -x * y * d2, 1 + x * x * d2, -y * d], axis=-1)
-    Jj_v = fy * np.stack([zero, h * d, -y * h * d2, -1 - y * y * d2, x * y * d2, x * d], axis=-1)
-    Jz_u = fx * (tij[:, 0:1] * d - tij[:, 2:3] * (x * d2))
-    Jz_v = fy * (tij[:, 1:2] * d - tij[:, 2:3] * (y * d2))
 
     Cii = wu * Jz_u * Jz_u + wv * Jz_v * Jz_v
     bz = wu * ru * Jz_u + wv * rv * Jz_v
 
     wu = np.where(stereo[:, None], 0.0, wu)
     wv = np.where(stereo[:, None], 0.0, wv)
-
-    TT = np.broadcast_to(T, (E, HW, 3))
-    QQ = np.broadcast_to(Q, (E, HW, 4))
-    Ji_u = -adj_se3(TT, QQ, Jj_u)
-    Ji_v = -adj_se3(TT, QQ, Jj_v)
 
     Ju = np.concatenate([Ji_u, Jj_u], axis=-1)   # (E,HW,12)
     Jv = np.concatenate([Ji_v, Jj_v], axis=-1)

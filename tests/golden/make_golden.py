@@ -15,6 +15,19 @@ computed in fp32 on CPU by the reference code itself:
   update_module.npz  UpdateModule.forward(...)              (droid_net.py:111-143, gru.py:19-32)
   convgru.npz        ConvGRU.forward(...)                   (modules/gru.py:19-32)
   cvx_upsample.npz   cvx_upsample(...)                      (droid_net.py:21-35)
+  projective_ops.npz projective_transform(..., jacobian=True) (geom/projective_ops.py:96-125)
+
+lietorch (un-vendored, v0.2) is needed by geom/projective_ops.py as a working
+group: `LieStandIn.SE3` below restates the lietorch SE3 operations that file
+uses (compose, inverse, action on homogeneous points, adjT) from lietorch's
+published definitions, data layout [tx, ty, tz, qx, qy, qz, qw].  The fixture
+therefore pins the reference's projective composition and Jacobian chain
+(iproj / actp / proj, the stereo override, the depth clamps) against the
+oracle's restatement of droid_kernels.cu; the SE3 primitives themselves stay
+pinned only by scipy / finite differences.  The reference's
+`device="cuda"` literal (projective_ops.py:105) is served by mapping that
+device to the CPU while the fixture is computed (torch.as_tensor wrapper);
+the reference file itself is imported unmodified.
 
 Weights come from tests/golden/fill.py (RNG-free), inputs from a seeded numpy
 generator; both are stored in the fixture so the tests never re-derive them.
@@ -55,6 +68,103 @@ def _install_stubs():
     ts = sys.modules["torch_scatter"]
     ts.scatter_mean = scatter_mean
     ts.scatter_sum = None
+
+
+class LieStandIn:
+    """lietorch SE3 semantics (data [t, q_xyzw]) for geom/projective_ops.py."""
+
+    @staticmethod
+    def _qmul(a, b):
+        av, aw = a[..., :3], a[..., 3:]
+        bv, bw = b[..., :3], b[..., 3:]
+        return torch.cat([aw * bv + bw * av + torch.cross(av, bv, dim=-1),
+                          aw * bw - (av * bv).sum(-1, keepdim=True)], -1)
+
+    @staticmethod
+    def _rot(q, X):
+        qv, qw = q[..., :3], q[..., 3:]
+        uv = 2 * torch.cross(qv.expand_as(X), X, dim=-1)
+        return X + qw * uv + torch.cross(qv.expand_as(X), uv, dim=-1)
+
+    class SE3:
+        def __init__(self, data):
+            self.data = data
+
+        def __getitem__(self, idx):
+            return LieStandIn.SE3(self.data[idx])
+
+        def inv(self):
+            t, q = self.data[..., :3], self.data[..., 3:]
+            qi = torch.cat([-q[..., :3], q[..., 3:]], -1)
+            return LieStandIn.SE3(torch.cat([-LieStandIn._rot(qi, t), qi], -1))
+
+        def __mul__(self, other):
+            t, q = self.data[..., :3], self.data[..., 3:]
+            if isinstance(other, LieStandIn.SE3):      # group product
+                t2, q2 = other.data[..., :3], other.data[..., 3:]
+                return LieStandIn.SE3(torch.cat([t + LieStandIn._rot(q, t2), LieStandIn._qmul(q, q2)], -1))
+            X, w = other[..., :3], other[..., 3:]      # action on homogeneous points [X, w] -> [R X + t w, w]
+            return torch.cat([LieStandIn._rot(q, X) + t * w, w], -1)
+
+        def adjT(self, a):
+            """Adj(T)^T a for a cotangent a = [a_t, a_r] (lietorch tangent order)."""
+            t, q = self.data[..., :3], self.data[..., 3:]
+            qi = torch.cat([-q[..., :3], q[..., 3:]], -1)
+            at, ar = a[..., :3], a[..., 3:]
+            tt = t.expand_as(at)
+            return torch.cat([LieStandIn._rot(qi, at), LieStandIn._rot(qi, ar + torch.cross(at, tt, dim=-1))], -1)
+
+    class Sim3:
+        pass
+
+
+def projective_fixture(rng):
+    """geom/projective_ops.py:96-125 with jacobian=True on a small graph with
+    temporal, loop and stereo (i == j) edges."""
+    sys.modules["lietorch"].SE3 = LieStandIn.SE3
+    sys.modules["lietorch"].Sim3 = LieStandIn.Sim3
+    import importlib
+    import geom.projective_ops as pops
+    pops = importlib.reload(pops)   # bind the working SE3 (an earlier import saw the name-only stub)
+
+    N, H, W = 5, 6, 8
+    ang = 0.05 * rng.standard_normal((N, 3))
+    th = np.linalg.norm(ang, axis=-1, keepdims=True)
+    q = np.concatenate([np.sin(th / 2) * ang / th, np.cos(th / 2)], -1)
+    t = 0.1 * rng.standard_normal((N, 3)) + np.array([0.0, 0.0, 0.05]) * np.arange(N)[:, None]
+    poses = np.concatenate([t, q], -1).astype(np.float32)   # the reference pipeline is fp32 (:105 literal)
+    disps = rng.uniform(0.2, 1.0, (N, H, W)).astype(np.float32)
+    intr = (np.tile(np.array([6.0, 6.0, 4.0, 3.0]), (N, 1)) * (1 + 0.02 * rng.standard_normal((N, 4)))).astype(np.float32)
+    ii = np.array([0, 1, 1, 2, 3, 4, 0, 2], dtype=np.int64)
+    jj = np.array([1, 0, 2, 2, 1, 3, 4, 2], dtype=np.int64)     # (2, 2) is a stereo edge
+    orig = torch.as_tensor
+
+    def as_tensor_cpu(*a, **k):
+        if k.get("device") == "cuda":
+            k["device"] = "cpu"
+        return orig(*a, **k)
+
+    torch.as_tensor = as_tensor_cpu
+    try:
+        x1, valid, (Ji, Jj, Jz) = pops.projective_transform(
+            LieStandIn.SE3(torch.from_numpy(poses)[None]), torch.from_numpy(disps)[None],
+            torch.from_numpy(intr)[None], torch.from_numpy(ii), torch.from_numpy(jj), jacobian=True)
+    finally:
+        torch.as_tensor = orig
+    # the BA kernel takes one intrinsics vector (droid.cpp:88-117): the same graph with intrinsics[0] everywhere
+    intr1 = np.tile(intr[:1], (N, 1))
+    torch.as_tensor = as_tensor_cpu
+    try:
+        x1s, valids, (Jis, Jjs, Jzs) = pops.projective_transform(
+            LieStandIn.SE3(torch.from_numpy(poses)[None]), torch.from_numpy(disps)[None],
+            torch.from_numpy(intr1)[None], torch.from_numpy(ii), torch.from_numpy(jj), jacobian=True)
+    finally:
+        torch.as_tensor = orig
+    np.savez_compressed(os.path.join(HERE, "projective_ops.npz"), poses=poses, disps=disps, intrinsics=intr,
+                        ii=ii, jj=jj, coords=x1[0].numpy(), valid=valid[0].numpy(), Ji=Ji[0].numpy(),
+                        Jj=Jj[0].numpy(), Jz=Jz[0].numpy(), coords_shared=x1s[0].numpy(),
+                        valid_shared=valids[0].numpy(), Ji_shared=Jis[0].numpy(), Jj_shared=Jjs[0].numpy(),
+                        Jz_shared=Jzs[0].numpy())
 
 
 def main():
@@ -111,6 +221,9 @@ def main():
     mask = rng.standard_normal((2, 576, 6, 8)).astype(np.float32)
     up = droid_net.cvx_upsample(torch.from_numpy(data), torch.from_numpy(mask))
     np.savez_compressed(os.path.join(HERE, "cvx_upsample.npz"), data=data, mask=mask, up=up.numpy())
+
+    # --- projective transform + Jacobians (BA linearisation) -----------------
+    projective_fixture(np.random.default_rng(2025))
     print("golden fixtures written to", HERE)
 
 

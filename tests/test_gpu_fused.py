@@ -556,3 +556,37 @@ def test_fused_update_inp_frames_matches_per_edge_inp():
     np.testing.assert_allclose(host(bd), host(rd), atol=3e-2 * max(1.0, float(rd.abs().max())))
     np.testing.assert_allclose(host(bw), host(rw), atol=1.5e-2)
     np.testing.assert_allclose(host(be), host(re), atol=1e-3 + 2e-2 * float(re.abs().max()))
+
+
+def test_fused_update_matches_reference_module_48x64():
+    """The bench shape (48x64: W=64 band tiles, the per-frame gate term, fused
+    delta/weight heads) with E=10 edges over 4 source frames."""
+    from droid_mi355x.fused import FusedUpdateModule
+    from droid_mi355x.update import UpdateModule
+    E, H, W = 10, 48, 64
+    m = UpdateModule().to(DEV).eval()
+    det_fill(m)
+    f = FusedUpdateModule(m)
+    g = torch.Generator(device=DEV).manual_seed(19)
+    net = torch.tanh(torch.randn((1, E, 128, H, W), generator=g, device=DEV)).half()
+    ii = torch.tensor([0, 0, 0, 1, 1, 2, 2, 2, 3, 3], device=DEV)
+    jj = torch.tensor([1, 2, 3, 0, 2, 0, 1, 3, 1, 2], device=DEV)
+    inp_f = torch.relu(torch.randn((4, 128, H, W), generator=g, device=DEV)).half()
+    inp = inp_f[ii][None]                                   # every edge of a frame shares its context
+    corr = (2 * torch.randn((1, E, 196, H, W), generator=g, device=DEV)).half()
+    flow = (4 * torch.randn((1, E, 4, H, W), generator=g, device=DEV)).clamp(-64, 64)
+    with torch.no_grad():
+        rn, rd, rw, re, _ = m(net.float(), inp.float(), corr.float(), flow, ii, jj)
+        nhwc = lambda t: t[0].permute(0, 2, 3, 1).contiguous()
+        c200 = torch.zeros((E, H, W, 200), dtype=torch.float16, device=DEV)
+        c200[..., :196] = nhwc(corr)
+        uq, inv = torch.unique(ii, return_inverse=True)
+        from droid_mi355x.fused import edge_segments
+        ptr, idx = edge_segments(inv.cpu().numpy(), len(uq))
+        segs = (torch.as_tensor(ptr, device=DEV), torch.as_tensor(idx, device=DEV))
+        inp_frames = nhwc(inp).index_select(0, torch.as_tensor(idx[ptr[:-1]], device=DEV))
+        fn, fd, fw, fe = f(nhwc(net), nhwc(inp), c200, flow[0], inv, len(uq), segments=segs, inp_frames=inp_frames)
+    np.testing.assert_allclose(host(fn.float()), host(nhwc(rn)), atol=1.5e-2)
+    np.testing.assert_allclose(host(fd), host(rd), atol=3e-2 * max(1.0, float(rd.abs().max())))
+    np.testing.assert_allclose(host(fw), host(rw), atol=1.5e-2)
+    np.testing.assert_allclose(host(fe), host(re), atol=1e-3 + 2e-2 * float(re.abs().max()))

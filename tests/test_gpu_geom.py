@@ -61,3 +61,16 @@ def test_depth_filter():
     cnt = droid_backends.depth_filter(dev(poses), dev(disps), dev(k), dev(ix), dev(thresh))
     ref = og.depth_filter(poses, disps, k, ix, thresh)
     assert np.mean(host(cnt) == ref) > 0.995
+
+
+def test_projective_transform_matches_reference_fixture(golden_dir):
+    """The fused HIP reprojection vs the reference's own geom/projective_ops.py
+    output (tests/golden/projective_ops.npz, lietorch SE3 stand-in): per-frame
+    intrinsics, a stereo edge, the Z clamp and the valid mask."""
+    import os
+    import droid_backends
+    g = np.load(os.path.join(golden_dir, "projective_ops.npz"))
+    coords, valid = droid_backends.projective_transform(dev(g["poses"]), dev(g["disps"]), dev(g["intrinsics"]),
+                                                        dev(g["ii"]), dev(g["jj"]))
+    np.testing.assert_allclose(host(coords), g["coords"], rtol=1e-5, atol=2e-4)
+    np.testing.assert_array_equal(host(valid), g["valid"])

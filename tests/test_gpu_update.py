@@ -81,3 +81,99 @@ def test_update_lowmem_runs():
     with torch.no_grad():
         g.update_lowmem(steps=1)
     assert np.isfinite(host(video.poses)).all() and np.isfinite(host(video.disps)).all()
+
+
+def _c2_video(H=48, W=64, seed=51):
+    """C2 frontend shape: 16-KF buffer, fmaps/net/inp ~ N / tanh / relu."""
+    from droid_mi355x import DepthVideo, synthetic
+    n = 16
+    rng = np.random.default_rng(seed)
+    video = DepthVideo(image_size=(8 * H, 8 * W), buffer=n, device="cuda")
+    gt = synthetic.trajectory(n, rng)
+    poses, disps = synthetic.perturb(gt, synthetic.smooth_disps(n, H, W, rng), rng)
+    video.poses[:n] = dev(poses.astype(np.float32))
+    video.disps[:n] = dev(disps.astype(np.float32))
+    video.intrinsics[:n] = dev(np.tile(synthetic.INTRINSICS * np.float32(W / 64.0), (n, 1)))
+    video.fmaps[:n] = dev(rng.normal(size=(n, 1, 128, H, W)).astype(np.float16))
+    video.nets[:n] = dev(np.tanh(rng.normal(size=(n, 128, H, W))).astype(np.float16))
+    video.inps[:n] = dev(np.maximum(rng.normal(size=(n, 128, H, W)), 0).astype(np.float16))
+    video.counter.value = n
+    return video
+
+
+def test_update_unit_matches_oracle_composition():
+    """FactorGraph.update() as a unit (factor_graph.py:196-242) against the
+    oracle composition (oracle/factor_graph.py: reproject -> lookup ->
+    UpdateModule fp32 -> coords1 + delta -> damping scatter -> inactive-edge
+    concat -> BA) on a C2-shaped graph at 48x64 with use_inactive=True: the
+    fused operator (W=64 band tiles, fused lookup + corr_encoder[0] on the
+    tiled volume, fused delta/weight heads) for target, weight, damping and
+    net at fp16 tolerance; the BA inputs it builds (edge lists exactly); and
+    the BA result on those inputs at the north star's 1e-4."""
+    import droid_backends
+    from droid_mi355x import FactorGraph, UpdateModule, synthetic
+    from droid_mi355x.fused import FusedUpdateModule
+    from oracle import factor_graph as ofg
+    H, W = 48, 64
+    video = _c2_video(H, W)
+    m = UpdateModule().to("cuda").eval()
+    det_fill(m)
+    g = FactorGraph(video, FusedUpdateModule(m), device="cuda")
+    ii, jj = synthetic.c2_edges()
+    with torch.no_grad():
+        g.add_factors(ii, jj)
+        g.update()                                  # non-trivial targets / weights / damping
+        g.rm_factors(g.ii < 7, store=True)          # device-tensor mask, as droid_frontend.py:42 passes
+    assert len(g._ii_inac) > 0 and g._ii.min() == 7
+    n = video.counter.value
+    st = dict(poses=host(video.poses[:n]), disps=host(video.disps[:n]), disps_sens=host(video.disps_sens[:n]),
+              intrinsics=host(video.intrinsics[:n]), fmaps=host(video.fmaps[:n].float()),
+              ii=g._ii.copy(), jj=g._jj.copy(), net=host(g.net.float()).transpose(0, 3, 1, 2),
+              inp=host(g.inp.float()).transpose(0, 3, 1, 2), target=host(g.target[0]), weight=host(g.weight[0]),
+              damping=host(g.damping[:n]))
+    inactive = (g._ii_inac.copy(), g._jj_inac.copy(), host(g.target_inac[0]), host(g.weight_inac[0]))
+    params = {k: host(v.float()) for k, v in m.state_dict().items()}
+    captured = {}
+    orig = droid_backends.ba
+
+    def spy(*a, **k):
+        captured["a"] = [x.detach().clone() if isinstance(x, torch.Tensor) else x for x in a]
+        return orig(*a, **k)
+
+    droid_backends.ba = spy
+    try:
+        with torch.no_grad():
+            g.update(use_inactive=True)
+    finally:
+        droid_backends.ba = orig
+    torch.cuda.synchronize()
+    ref = ofg.update(params, st["poses"], st["disps"], st["disps_sens"], st["intrinsics"], st["fmaps"], st["ii"],
+                     st["jj"], st["net"], st["inp"], st["target"], st["weight"], st["damping"], use_inactive=True,
+                     inactive=inactive)
+    # the update operator's outputs (fp16 storage / fp16 convs vs fp32)
+    np.testing.assert_allclose(host(g.net.float()).transpose(0, 3, 1, 2), ref["net"], atol=2e-2)
+    dmax = max(1.0, float(np.abs(ref["target"] - ref["coords1"]).max()))
+    np.testing.assert_allclose(host(g.target[0]), ref["target"], atol=3e-2 * dmax)
+    np.testing.assert_allclose(host(g.weight[0]), ref["weight"], atol=1.5e-2)
+    u = np.unique(st["ii"])
+    np.testing.assert_allclose(host(g.damping[u]), ref["damping"][u], atol=1e-3 + 2e-2 * np.abs(ref["damping"][u]).max())
+    untouched = np.setdiff1d(np.arange(n), u)
+    np.testing.assert_array_equal(host(g.damping[untouched]), st["damping"][untouched])
+    # the BA call it makes: inactive edges with ii, jj >= t0 - 3 first, then the active ones
+    a = captured["a"]
+    tgt, wgt, eta, ii_ba, jj_ba, t0, t1 = ref["ba_in"]
+    np.testing.assert_array_equal(host(a[7]), ii_ba)
+    np.testing.assert_array_equal(host(a[8]), jj_ba)
+    assert (a[9], a[10]) == (t0, t1) and (a[11], a[12], a[13]) == (2, 1e-4, 0.1)
+    assert len(ii_ba) > len(st["ii"])               # some inactive edges joined
+    np.testing.assert_allclose(host(a[4]), tgt, atol=3e-2 * dmax)
+    np.testing.assert_allclose(host(a[5]), wgt, atol=1.5e-2)
+    np.testing.assert_allclose(host(a[6]), eta, atol=1e-3 + 2e-2 * np.abs(eta).max())
+    # BA on the inputs update() built (the 1e-4 bar) and the disparity clamp
+    ba_ref = oba.ba(poses=host(a[0]), disps=host(a[1]), intrinsics=host(a[2]), disps_sens=host(a[3]),
+                    targets=host(a[4]), weights=host(a[5]), eta=host(a[6]), ii=host(a[7]), jj=host(a[8]), t0=a[9],
+                    t1=a[10], iterations=a[11], lm=a[12], ep=a[13], motion_only=a[14])
+    np.testing.assert_allclose(host(video.poses[:n]), ba_ref["poses"][:n], atol=1e-4)
+    np.testing.assert_allclose(host(video.disps[:n]), np.maximum(ba_ref["disps"][:n], 0.001), atol=1e-4)
+    # and the whole composition lands close to the oracle's own BA result
+    np.testing.assert_allclose(host(video.poses[:n]), ref["poses"][:n], atol=2e-3)

@@ -125,3 +125,43 @@ def test_lookup_edge_cases():
     for i in range(3):
         for j in range(3):
             np.testing.assert_allclose(out[0, i, j], vol[0, :, :, 2 - 1 + j, 3 - 1 + i], atol=1e-6)
+
+
+# --- geom/projective_ops.py (reference, with a lietorch SE3 stand-in) -------
+def _pops(golden_dir):
+    return np.load(os.path.join(golden_dir, "projective_ops.npz"))
+
+
+def test_oracle_projective_transform_matches_reference(golden_dir):
+    """oracle/geometry.py (the reprojection the fused HIP kernel is checked
+    against) vs projective_ops.projective_transform (:96-125): per-frame
+    intrinsics, a stereo edge (the :105 override), the Z clamp and valid mask."""
+    from oracle import geometry as og
+    g = _pops(golden_dir)
+    coords, valid = og.projective_transform(g["poses"], g["disps"], g["intrinsics"], g["ii"], g["jj"])
+    np.testing.assert_array_equal(valid, g["valid"])
+    np.testing.assert_allclose(coords, g["coords"], rtol=1e-5, atol=1e-4)
+
+
+def test_oracle_ba_jacobians_match_reference(golden_dir):
+    """The BA linearisation's per-pixel Jacobians (oracle/ba.py jacobians,
+    restating droid_kernels.cu:281-330 incl. adjSE3) equal the reference's
+    autograd-free Jacobian chain of projective_ops (jacobian=True: Jj = Jp Ja,
+    Ji = -Gij.adjT(Jj), Jz = Jp (Gij * [0,0,0,1])) wherever both count the point
+    (Z > 0.25, the kernel's MIN_DEPTH; the reference's own valid mask)."""
+    from oracle import ba as oba
+    g = _pops(golden_dir)
+    E, H, W = g["Jj_shared"].shape[:3]
+    J = oba.jacobians(g["poses"].astype(np.float64), g["disps"].astype(np.float64),
+                      g["intrinsics"][0].astype(np.float64), g["ii"], g["jj"])
+    use = (~J["bad"]).reshape(E, H, W) & (g["valid_shared"][..., 0] > 0)
+    assert use.sum() > 0.7 * use.size
+    ref_jj, ref_ji, ref_jz = g["Jj_shared"][use], g["Ji_shared"][use], g["Jz_shared"][use]   # (n,2,6), (n,2,1)
+    ours_jj = np.stack([J["Jj_u"], J["Jj_v"]], -2).reshape(E, H, W, 2, 6)[use]
+    ours_ji = np.stack([J["Ji_u"], J["Ji_v"]], -2).reshape(E, H, W, 2, 6)[use]
+    ours_jz = np.stack([J["Jz_u"], J["Jz_v"]], -1).reshape(E, H, W, 2)[use]
+    scale = max(1.0, np.abs(ref_jj).max())
+    np.testing.assert_allclose(ours_jj, ref_jj, atol=1e-5 * scale)
+    np.testing.assert_allclose(ours_ji, ref_ji, atol=1e-5 * scale)
+    np.testing.assert_allclose(ours_jz, ref_jz[..., 0], atol=1e-5 * scale)
+    np.testing.assert_allclose(J["coords"].reshape(E, H, W, 2)[use], g["coords_shared"][use], rtol=1e-5, atol=1e-4)
