@@ -76,6 +76,8 @@ def build_state(args, rank, world, device):
     stereo = args.config == "C4"
     if stereo:   # C4: 128 KF, one stereo (i, i) edge per frame + temporal + loops
         ii, jj = synthetic.c4_edges(args.frames, rng=np.random.default_rng(1004))
+    elif args.config == "C2":   # frontend window: 16-KF buffer, 96 edges
+        ii, jj = synthetic.c2_edges()
     else:
         ii, jj = synthetic.c3_edges(args.frames, args.edges, rng=np.random.default_rng(1003))
     comm = None
@@ -107,8 +109,14 @@ def build_state(args, rank, world, device):
     graph.comm = comm
     with torch.no_grad():
         graph.add_factors(ii_l, jj_l)
+        if args.config == "C2":
+            # the frontend's state: edges older than the window stored inactive
+            # (droid_frontend.py:42,106) - update(use_inactive=True) then optimises
+            # [8, 16) with the stored edges into [5, 8) joining the BA
+            graph.update(use_inactive=False)
+            graph.rm_factors(graph.ii < 7, store=True)
     torch.cuda.synchronize(device)
-    return video, graph, (ii, jj), len(ii_l)
+    return video, graph, (ii, jj), len(graph._ii)
 
 
 class KernelTimer:
@@ -182,25 +190,79 @@ def stage_breakdown(graph, video, steps=3):
     return out
 
 
+def frontend_edge_change(graph, video, changes=5):
+    """The frontend changes its edge set once per keyframe (droid_frontend.py:
+    __update: rm_factors + add_proximity_factors, then 4-6 update() calls on the
+    new set).  Host cost of the BA plan rebuild (kx, Schur rows, assembly lists,
+    pose order, tile tasks) and the wall time of the first update() after an
+    edge change (new plan + edge-list uploads + the new edges' corr volumes)."""
+    import droid_backends
+    ii_h, jj_h = graph._ii.copy(), graph._jj.copy()
+    N, H, W = video.disps.shape
+    t0 = max(1, int(ii_h.min()) + 1)
+    m = (graph._ii_inac >= t0 - 3) & (graph._jj_inac >= t0 - 3)
+    ii_ba, jj_ba = np.concatenate([graph._ii_inac[m], ii_h]), np.concatenate([graph._jj_inac[m], jj_h])
+    t1 = int(max(ii_ba.max(), jj_ba.max())) + 1
+    plan_ms, step_ms = [], []
+    with torch.no_grad():
+        for c in range(changes):
+            h0 = time.perf_counter()
+            droid_backends.BaPlan(ii_ba, jj_ba, N, H, W, t0, t1, len(np.unique(ii_ba)), False, video.disps.device)
+            plan_ms.append(1000 * (time.perf_counter() - h0))
+            # drop one edge pair and add it back: a new edge set each time (plan cache cleared)
+            torch.cuda.synchronize()
+            h0 = time.perf_counter()
+            sel = (graph._ii == 15) & (graph._jj == 12) | (graph._ii == 12) & (graph._jj == 15)
+            graph.rm_factors(sel, store=False)
+            graph.add_factors(np.array([15, 12]), np.array([12, 15]))
+            droid_backends._PLAN_CACHE.clear()
+            graph.update(use_inactive=True)
+            torch.cuda.synchronize()
+            step_ms.append(1000 * (time.perf_counter() - h0))
+    return {"plan_build_ms_host": float(np.median(plan_ms)), "edge_change_plus_update_ms": float(np.median(step_ms)),
+            "ba_edges": int(len(ii_ba)), "note": "median of %d edge-set changes (rm + add one edge pair, "
+                                                 "its corr volume, plan rebuild, one update)" % changes}
+
+
 def cpu_baseline(graph, video, args):
+    """BASELINE.md's CPU baseline, full runs (no extrapolation): C1 (2-frame
+    CorrBlock, median of 3), C2 (one full update() of the frontend graph,
+    median of 3) and C3 (ONE full update() of this run's 256-KF / 2048-edge
+    graph, with this run's features and weights) through the oracle
+    restatement (oracle/update_cpu.py) on the host cores, ms per stage."""
     from droid_mi355x import synthetic
     from oracle import update_cpu
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    prob = synthetic.ba_problem("C3", H=args.ht // 8, W=args.wd // 8)
-    n = args.frames
-    fm = video.fmaps[:n, 0].float().cpu().numpy()
-    nets = video.nets[:n].float().cpu().numpy()
-    inps = video.inps[:n].float().cpu().numpy()
     params = {k: v.detach().float().cpu().numpy() for k, v in graph.update_op.state_dict().items()}
-    r = update_cpu.time_update(prob, fm, nets, inps, params, sample_edges=args.cpu_sample_edges, iterations=2,
-                               threads=threads)
-    return {"value": 1.0 / r["seconds_per_update"], "unit": "iters/s", "cores": r["threads"], "kind": "port",
-            "sample": ("oracle restatement (numpy/torch fp32+fp64, %d threads): per-edge stages "
-                       "(reproject, CorrBlock volume + 4-level lookup, UpdateModule fp32) timed on %d edges "
-                       "(%.2f s) scaled x%.0f to 2048 edges; BA (ba_cuda semantics) timed for 1 GN iteration on "
-                       "the full 256-KF/2048-edge C3 system (%.2f s) x2"
-                       % (r["threads"], r["sample_edges"], r["t_edge_sample"], args.edges / r["sample_edges"],
-                          r["t_ba_iter"]))}
+    H, W = args.ht // 8, args.wd // 8
+    t_all = time.time()
+    c1 = update_cpu.time_c1(threads, H, W)
+    rng = np.random.default_rng(1002)
+    p2 = synthetic.ba_problem("C2", H=H, W=W)
+    n2 = p2["disps"].shape[0]
+    f2 = (rng.normal(size=(n2, 128, H, W)).astype(np.float16), np.tanh(rng.normal(size=(n2, 128, H, W))).astype(np.float16),
+          np.maximum(rng.normal(size=(n2, 128, H, W)), 0).astype(np.float16))
+    c2 = [update_cpu.time_update(p2, *f2, params, threads) for _ in range(3)]
+    c2 = sorted(c2, key=lambda r: r["seconds_per_update"])[1]
+    p3 = synthetic.ba_problem("C3", H=H, W=W)
+    n = args.frames
+    f3 = (video.fmaps[:n, 0].cpu().numpy(), video.nets[:n].cpu().numpy(), video.inps[:n].cpu().numpy())
+    c3 = update_cpu.time_update(p3, *f3, params, threads)
+    info = update_cpu.cpu_info()
+    r = lambda d: {k: round(v, 1) for k, v in d.items()}
+    return {"value": 1.0 / c3["seconds_per_update"], "unit": "iters/s", "cores": c3["threads"], "kind": "port",
+            "sample": ("full runs, no extrapolation: ONE complete C3 update() (2048 edges, 256 KF, 48x64: "
+                       "reprojection, 4-level lookup, UpdateModule fp32, BA itrs=2 fp64) through the oracle "
+                       "restatement on %d host threads; corr volumes built per chunk and timed apart (they belong "
+                       "to add_factors)" % c3["threads"]),
+            "cpu": info, "threads": c3["threads"],
+            "C1": {"ms": round(c1["ms"], 2), "median_of": c1["repeats"],
+                   "what": "2 frames / 1 edge CorrBlock 48x64 r=3 (volume + pyramid + lookup)"},
+            "C2": {"iters_per_s": 1.0 / c2["seconds_per_update"], "ms_per_stage": r(c2["ms"]), "median_of": 3,
+                   "edges": c2["edges"]},
+            "C3": {"iters_per_s": 1.0 / c3["seconds_per_update"], "ms_per_stage": r(c3["ms"]), "runs": 1,
+                   "edges": c3["edges"]},
+            "wall_s": round(time.time() - t_all, 1)}
 
 
 def load_traffic(name, e_local, kernel):
@@ -223,9 +285,10 @@ def load_traffic(name, e_local, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=["C3", "C4"], default="C3",
+    ap.add_argument("--config", choices=["C2", "C3", "C4"], default="C3",
                     help="C3 (default, the metric's config): 256 KF / 2048 edges mono; "
-                         "C4: stereo, 128 KF, (i, i) stereo edges + temporal + loops (~1k edges)")
+                         "C4: stereo, 128 KF, (i, i) stereo edges + temporal + loops (~1k edges); "
+                         "C2: frontend window, 16-KF buffer, 96 edges, update(use_inactive=True)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=256)
@@ -236,13 +299,14 @@ def main():
                     help="correlation: 'volume' = CorrBlock's all-pairs volume (built in add_factors), "
                          "'pyramid' = windows computed on demand on MFMA from the feature pyramid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-edges", type=int, default=8)
     ap.add_argument("--breakdown", action="store_true")
     ap.add_argument("--reference-op", action="store_true",
                     help="run the reference-structured UpdateModule (torch/MIOpen convs, NCHW) instead of the fused MFMA operator")
     args = ap.parse_args()
     if args.config == "C4" and args.frames == 256:
         args.frames = 128
+    if args.config == "C2":
+        args.frames = 16
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -278,8 +342,9 @@ def main():
 
     with torch.no_grad():
         t_w = time.time()
+        upd = dict(use_inactive=True) if args.config == "C2" else {}
         for _ in range(args.warmup):
-            graph.update()
+            graph.update(**upd)
         torch.cuda.synchronize(device)
         if rank == 0:
             log("warmup %.1fs" % (time.time() - t_w))
@@ -291,7 +356,7 @@ def main():
             zr.active = zrp.active = True
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            graph.update()
+            graph.update(**upd)
         torch.cuda.synchronize(device)
         if world > 1:
             dist.barrier()
@@ -311,6 +376,7 @@ def main():
     if factored:
         zr_ms = zrp.mean_ms()
     breakdown = stage_breakdown(graph, video) if args.breakdown else None
+    frontend = frontend_edge_change(graph, video) if args.config == "C2" else None
 
     if rank == 0:
         ms = 1000.0 * elapsed / args.steps
@@ -337,7 +403,10 @@ def main():
             roofline, lookup_roof = lookup_roof, None
         result = {
             "metric": ("factor_graph.update() iters/sec at 256 KF x 2k edges, 384x512" if args.config == "C3"
-                       else "factor_graph.update() iters/sec, C4 stereo %d KF x %d edges, 384x512" % (args.frames, len(ii))),
+                       else "factor_graph.update() iters/sec, C4 stereo %d KF x %d edges, 384x512" % (args.frames, len(ii))
+                       if args.config == "C4" else
+                       "factor_graph.update(use_inactive=True) iters/sec, C2 frontend 16-KF buffer x %d edges, 384x512"
+                       % len(ii)),
             "value": 1000.0 / ms,
             "unit": "iters/s",
             "n_gpus": world,
@@ -349,7 +418,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f16 (corr volume, update-operator convs) / f32 (BA linearisation, Schur) / f64 (reduced system)",
             "data": "synthetic (SURVEY.md §8d %s graph, random-init UpdateModule)" % args.config,
-            "config": {"workload": ("C4 stereo graph" if args.config == "C4" else "C3 global graph")
+            "config": {"workload": {"C4": "C4 stereo graph", "C3": "C3 global graph",
+                                    "C2": "C2 frontend window (use_inactive=True)"}[args.config]
                                    + ": update(itrs=2), %s corr" % args.corr, "keyframes": args.frames,
                        "edges": len(ii), "image": [args.ht, args.wd], "fmap": [args.ht // 8, args.wd // 8],
                        "parallelism": "edge-sharded x%d (RCCL all-reduce of reduced camera system)" % world},
@@ -360,11 +430,13 @@ def main():
             result["roofline_lookup"] = lookup_roof
         # whole-iteration fraction: max(HBM floor, MFMA floor) / measured update()
         hw = (args.ht // 8) * (args.wd // 8)
-        n_src = len(np.unique(ii))
-        conv_flops = (CONV_FLOPS_PER_EDGE_PIXEL * len(ii) + CONV_FLOPS_PER_FRAME_PIXEL * n_src) * hw
+        # edges the update operator runs on (C2: the active window; the stored ones only join the BA)
+        e_op = e_local if args.config == "C2" else len(ii)
+        n_src = len(np.unique(graph._ii)) if args.config == "C2" else len(np.unique(ii))
+        conv_flops = (CONV_FLOPS_PER_EDGE_PIXEL * e_op + CONV_FLOPS_PER_FRAME_PIXEL * n_src) * hw
         if factored:   # the algorithm run: gate inp term per source frame, not per edge
-            conv_flops -= GATE_INP_FLOPS_PER_PIXEL * (len(ii) - n_src) * hw
-        hbm_bytes = HBM_BYTES_PER_EDGE * len(ii) + HBM_BYTES_PER_FRAME * args.frames
+            conv_flops -= GATE_INP_FLOPS_PER_PIXEL * (e_op - n_src) * hw
+        hbm_bytes = HBM_BYTES_PER_EDGE * e_op + HBM_BYTES_PER_FRAME * args.frames
         mfma_floor = conv_flops / (PEAK_F16_TFLOPS * 1e12) * 1e3 / world
         hbm_floor = hbm_bytes / (PEAK_HBM_GBS * 1e9) * 1e3 / world
         result["iteration_roofline"] = {
@@ -380,7 +452,9 @@ def main():
                 "update_op_ms": op_ms, "note": "update_op includes the fused lookup + corr_encoder[0]"}
         if breakdown:
             result["breakdown_ms"] = breakdown
-        if world == 1 and not args.no_cpu_baseline:
+        if frontend:
+            result["frontend"] = frontend
+        if world == 1 and not args.no_cpu_baseline and args.config == "C3":
             try:
                 result["cpu_baseline"] = cpu_baseline(graph, video, args)
             except Exception as ex:  # the baseline is reported, never fatal

@@ -215,3 +215,44 @@ def altcorr_backward(fmap1, fmap2, coords, corr_grad, r):
                     g1[b] += g[..., None] * f2[b, hc, wc]
                     np.add.at(g2[b], (hc[inb], wc[inb]), (g[..., None] * f1[b])[inb])
     return g1, g2, np.zeros(coords.shape)
+
+
+# --- torch CPU formulation (the "pure-PyTorch CPU path" of the baseline) ------
+def corr_pyramid_torch(fmap1, fmap2, num_levels=4):
+    """CorrBlock.__init__ (corr.py:24-38) in torch fp32: (B,N,C,H,W) float
+    tensors -> list of (B*N, H, W, H_l, W_l) levels (matmul + avg_pool2d)."""
+    import torch
+    import torch.nn.functional as F
+    B, N, C, H, W = fmap1.shape
+    f1 = fmap1.reshape(B * N, C, H * W) / 4.0
+    f2 = fmap2.reshape(B * N, C, H * W) / 4.0
+    vol = torch.matmul(f1.transpose(1, 2), f2).reshape(B * N * H * W, 1, H, W)
+    out = [vol.view(B * N, H, W, H, W)]
+    for _ in range(num_levels - 1):
+        vol = F.avg_pool2d(vol, 2, stride=2)
+        out.append(vol.view(B * N, H, W, vol.shape[-2], vol.shape[-1]))
+    return out
+
+
+def lookup_pyramid_torch(pyramid, coords, r=3):
+    """CorrBlock.__call__ (corr.py:40-50) as F.grid_sample(align_corners=True,
+    zero padding) at (x0 - r + i, y0 - r + j) - the same bilinear sample as
+    corr_index_forward (checked in tests/test_oracle_golden.py).  pyramid:
+    corr_pyramid_torch levels; coords (B,H,W,2) -> (B, L*(2r+1)^2, H, W)."""
+    import torch
+    import torch.nn.functional as F
+    B, H, W, _ = coords.shape
+    rd = 2 * r + 1
+    d = torch.arange(-r, r + 1, dtype=coords.dtype)
+    outs = []
+    for lvl, vol in enumerate(pyramid):
+        H2, W2 = vol.shape[-2:]
+        assert H2 > 1 and W2 > 1, "grid_sample's align_corners mapping needs levels of >= 2 pixels a side"
+        c = coords.reshape(B * H * W, 1, 1, 2) / 2 ** lvl
+        gx = (c[..., 0] + d.view(1, rd, 1)).expand(B * H * W, rd, rd)   # [:, i, j]: x offset i
+        gy = (c[..., 1] + d.view(1, 1, rd)).expand(B * H * W, rd, rd)   #            y offset j
+        grid = torch.stack([2 * gx / (W2 - 1) - 1, 2 * gy / (H2 - 1) - 1], -1)
+        # grid_sample indexes (N, C, H_out, W_out) with grid[..., (x, y)]: out[:, 0, i, j] samples (gx_i, gy_j)
+        s = F.grid_sample(vol.reshape(B * H * W, 1, H2, W2), grid, align_corners=True, padding_mode="zeros")
+        outs.append(s.view(B, H, W, rd * rd).permute(0, 3, 1, 2))
+    return torch.cat(outs, 1)

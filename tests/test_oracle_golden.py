@@ -165,3 +165,19 @@ def test_oracle_ba_jacobians_match_reference(golden_dir):
     np.testing.assert_allclose(ours_ji, ref_ji, atol=1e-5 * scale)
     np.testing.assert_allclose(ours_jz, ref_jz[..., 0], atol=1e-5 * scale)
     np.testing.assert_allclose(J["coords"].reshape(E, H, W, 2)[use], g["coords_shared"][use], rtol=1e-5, atol=1e-4)
+
+
+def test_torch_cpu_lookup_equals_kernel_restatement():
+    """The CPU baseline's torch formulation (matmul / avg_pool2d / grid_sample)
+    equals the loop restatement of CorrBlock + correlation_kernels.cu."""
+    import torch
+    from oracle import corr as oc
+    rng = np.random.default_rng(12)
+    f1 = rng.normal(size=(1, 2, 128, 16, 24)).astype(np.float32)
+    f2 = rng.normal(size=(1, 2, 128, 16, 24)).astype(np.float32)
+    coords = (np.stack(np.meshgrid(np.arange(24), np.arange(16)), -1)[None, None]
+              + rng.normal(0, 3, (1, 2, 16, 24, 2))).astype(np.float32)
+    ref = oc.lookup_pyramid(oc.corr_pyramid(f1, f2), coords, 3)[0]
+    pyr = oc.corr_pyramid_torch(torch.from_numpy(f1), torch.from_numpy(f2))
+    got = oc.lookup_pyramid_torch(pyr, torch.from_numpy(coords[0])).numpy()
+    np.testing.assert_allclose(got, ref, atol=2e-5 * np.abs(ref).max())
