@@ -34,6 +34,9 @@ PEAK_F16_TFLOPS = 2500.0        # MI355X_MICROARCH.md: dense fp16/bf16 MFMA peak
 LOOKUP_BYTES_PER_EDGE = 2801664  # volume-API lookup, 4 lvl x 64 taps x 2 B x HW + coords + out
 # fused lookup + corr_encoder[0] (corr_ce0_kernel): the same window reads + coords, 128-ch fp16 output
 LOOKUP_CE0_BYTES_PER_EDGE = 4 * 64 * 2 * 3072 + 2 * 4 * 3072 + 128 * 2 * 3072
+# on-demand lookup (corr_alt_ce0): SURVEY.md §8d fused feature-pyramid row (fmap1 + fmap2 pyramid + coords)
+# with the 128-channel corr_encoder[0] output instead of the 196-channel lookup
+ALT_BYTES_PER_EDGE = 786432 + 1044480 + 24576 + 128 * 2 * 3072
 # ConvGRU z|r conv (modules/gru.py:19-32, convz+convr fused): 3x3, 448 -> 256 channels
 ZR_FLOPS_PER_PIXEL = 2 * 256 * 448 * 9
 # ... with the context features factored out per source frame (droid_conv_gru_pre_f16):
@@ -105,7 +108,8 @@ def build_state(args, rank, world, device):
     if not args.reference_op:
         from droid_mi355x.fused import FusedUpdateModule
         net = FusedUpdateModule(net)
-    graph = FactorGraph(video, net, device=device, corr_impl=args.corr if not args.reference_op else "volume")
+    corr_impl = "alt" if args.lowmem else args.corr if not args.reference_op else "volume"
+    graph = FactorGraph(video, net, device=device, corr_impl=corr_impl)
     graph.comm = comm
     with torch.no_grad():
         graph.add_factors(ii_l, jj_l)
@@ -298,6 +302,9 @@ def main():
     ap.add_argument("--corr", choices=["pyramid", "volume"], default="volume",
                     help="correlation: 'volume' = CorrBlock's all-pairs volume (built in add_factors), "
                          "'pyramid' = windows computed on demand on MFMA from the feature pyramid")
+    ap.add_argument("--lowmem", action="store_true",
+                    help="time update_lowmem(steps=1) (the global-BA backend's step, factor_graph.py:245-290: "
+                         "on-demand correlation, BA over [1, t) with lm=1e-5, ep=1e-2) instead of update()")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--breakdown", action="store_true")
     ap.add_argument("--reference-op", action="store_true",
@@ -333,7 +340,7 @@ def main():
 
     import droid_backends
     LOOKUP_FN[0] = ("corr_pyramid_lookup" if args.reference_op else
-                    "corr_alt_ce0" if args.corr == "pyramid" else "corr_lookup_ce0")
+                    "corr_alt_ce0" if args.corr == "pyramid" or args.lowmem else "corr_lookup_ce0")
     lookup = KernelTimer(droid_backends, LOOKUP_FN[0])
     zr = zrp = None
     if not args.reference_op:
@@ -343,8 +350,9 @@ def main():
     with torch.no_grad():
         t_w = time.time()
         upd = dict(use_inactive=True) if args.config == "C2" else {}
+        step_fn = (lambda: graph.update_lowmem(steps=1)) if args.lowmem else (lambda: graph.update(**upd))
         for _ in range(args.warmup):
-            graph.update(**upd)
+            step_fn()
         torch.cuda.synchronize(device)
         if rank == 0:
             log("warmup %.1fs" % (time.time() - t_w))
@@ -356,7 +364,7 @@ def main():
             zr.active = zrp.active = True
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            graph.update(**upd)
+            step_fn()
         torch.cuda.synchronize(device)
         if world > 1:
             dist.barrier()
@@ -401,8 +409,15 @@ def main():
                         "launch_ms": zr_ms, "algorithmic_flops_per_launch": flops}
         else:
             roofline, lookup_roof = lookup_roof, None
+        if args.lowmem or args.corr == "pyramid":
+            lookup_roof["kernel"] = ("corr_alt_ce0_kernel (on-demand 4-level correlation windows on MFMA from the "
+                                     "feature pyramid, fused with corr_encoder[0] 1x1 196->128)")
+            lookup_roof["algorithmic_bytes_per_launch"] = ALT_BYTES_PER_EDGE * e_local
+            lookup_roof["achieved"] = ALT_BYTES_PER_EDGE * e_local / (lookup_ms * 1e-3) / 1e9 if lookup_ms else None
+            lookup_roof["frac"] = lookup_roof["achieved"] / PEAK_HBM_GBS if lookup_ms else None
+            lookup_roof["traffic"] = None
         result = {
-            "metric": ("factor_graph.update() iters/sec at 256 KF x 2k edges, 384x512" if args.config == "C3"
+            "metric": ("factor_graph.update_lowmem() steps/sec at 256 KF x 2k edges, 384x512" if args.lowmem else "factor_graph.update() iters/sec at 256 KF x 2k edges, 384x512" if args.config == "C3"
                        else "factor_graph.update() iters/sec, C4 stereo %d KF x %d edges, 384x512" % (args.frames, len(ii))
                        if args.config == "C4" else
                        "factor_graph.update(use_inactive=True) iters/sec, C2 frontend 16-KF buffer x %d edges, 384x512"
@@ -420,7 +435,8 @@ def main():
             "data": "synthetic (SURVEY.md §8d %s graph, random-init UpdateModule)" % args.config,
             "config": {"workload": {"C4": "C4 stereo graph", "C3": "C3 global graph",
                                     "C2": "C2 frontend window (use_inactive=True)"}[args.config]
-                                   + ": update(itrs=2), %s corr" % args.corr, "keyframes": args.frames,
+                                   + (": update_lowmem(steps=1, itrs=2), on-demand corr" if args.lowmem else
+                                      ": update(itrs=2), %s corr" % args.corr), "keyframes": args.frames,
                        "edges": len(ii), "image": [args.ht, args.wd], "fmap": [args.ht // 8, args.wd // 8],
                        "parallelism": "edge-sharded x%d (RCCL all-reduce of reduced camera system)" % world},
             "roofline": roofline,

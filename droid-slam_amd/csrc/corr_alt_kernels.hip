@@ -10,28 +10,34 @@
 // gathered from a 51 GB volume whose 16-B window rows make the lookup
 // DRAM-burst bound.
 //
-// corr_alt_ce0_kernel: persistent, one 8-wave workgroup per CU.  Work unit =
-// an 8x8-pixel query tile of one edge.  Per level:
-//   * the union of the 64 windows (their bounding box, clipped to the map) is
-//     DMA'd from the f2 pyramid level into LDS (NHWC rows are contiguous, one
-//     16-B piece per lane, XOR-swizzled slots);
-//   * C = F1 (64 px x 128) x box^T on MFMA (f32 accumulate), rounded to fp16 -
-//     the values the volume would hold at those taps;
-//   * each pixel's 7x7 bilinear outputs are formed from its 8x8 taps of C with
-//     the volume lookup's at::Half arithmetic (rnd16 after every op).
-// A tile whose box exceeds the LDS capacity (incoherent coordinates) is split
-// into its four 4x4 quadrants, and a quadrant still too wide into single
-// pixels (box = the pixel's own window); correctness never depends on
-// coherence, only speed does.  The 196 lookup channels of the tile then go
-// through corr_encoder[0] (1x1 196 -> 128, bias, ReLU) on MFMA with the
-// weights held in registers (wave w owns output channels 16w .. 16w+15), and
-// only the 128-channel result is written.
+// corr_alt_ce0_kernel: persistent, one 8-wave workgroup per CU, software
+// pipelined over "stages" = (8x8-pixel query tile of one edge, pyramid level):
+//   * the union of the tile's 64 windows at that level (their bounding box,
+//     clipped to the map) reaches LDS by LDS-DMA (NHWC rows are contiguous, one
+//     16-B piece per lane, XOR-swizzled slots) ONE STAGE AHEAD, into the other
+//     of two box buffers, while the current stage computes;
+//   * C = F1 (64 px x 128, in registers for the tile's four levels) x box^T on
+//     MFMA (f32 accumulate), rounded to fp16 - the values the volume would hold
+//     at those taps;
+//   * each pixel's 7x7 bilinear outputs come from its 8x8 taps of C with the
+//     volume lookup's at::Half arithmetic (rnd16 after every op);
+//   * the level's 49 lookup channels go straight through their slice of
+//     corr_encoder[0] (1x1 196 -> 128) on MFMA into fp32 accumulators (K = 49
+//     padded to 64 per level; the weights live in registers, wave w owns output
+//     channels 16w .. 16w+15), so the 196-channel lookup never exists;
+//   * after level 3: bias, ReLU, fp16, one coalesced 128-channel row per pixel.
+// The next tile's coordinates arrive by LDS-DMA and its window boxes are
+// computed during the current tile, so the pipeline never drains between
+// tiles.  A box larger than a buffer (incoherent coordinates) runs that stage
+// synchronously: its four 4x4 quadrants, a quadrant still too wide pixel by
+// pixel (box = the pixel's own window); correctness never depends on
+// coherence, only speed does.
 //
 // Numerics vs the volume path: level 0 differs only in the fp32 summation order
 // of the dot products before their fp16 rounding; levels >= 1 pool the
 // features instead of the correlations (both fp16), a difference at the fp16
-// rounding level.  The bilinear arithmetic and the corr_encoder[0] GEMM are
-// the same.
+// rounding level.  The bilinear arithmetic is the same; corr_encoder[0] sums
+// its 196 products level by level in fp32.
 #include "common.hpp"
 #include "lds_dma.hpp"
 
@@ -53,34 +59,135 @@ struct AltArgs {
   __half* out;           // (E, H, W, 128)
   int H, W;
   long ntiles;           // E * (H / 8) * (W / 8)
+  long long* prof;       // profiling builds: s_memtime per (workgroup, stage < 32, phase < 8), or null
 };
 
-constexpr int kAltCap = 240;   // box taps held in LDS
-constexpr int kAltCS = 248;    // C row stride (halves)
-constexpr int kAltAS = 232;    // lookup tile row stride (halves)
+#ifndef DROID_CONV_PROFILE
+#define DROID_CONV_PROFILE 0
+#endif
+#if DROID_CONV_PROFILE
+#define ALT_STAMP(ph, v)                                                                            \
+  do {                                                                                            \
+    if (a.prof && tid == 0 && stage < 32)                                                         \
+      a.prof[((long)blockIdx.x * 32 + stage) * 8 + (ph)] = (v);                                    \
+  } while (0)
+#else
+#define ALT_STAMP(ph, v) do { } while (0)
+#endif
+#define ALT_NOW() ((long long)__builtin_amdgcn_s_memtime())
+
+constexpr int kAltCap = 232;   // box taps per LDS buffer (a coherent tile's level-0 box is 15 x 15)
+constexpr int kAltCS = 244;    // C row stride (halves): >= 16 * ceil(kAltCap / 16), 8-B aligned rows
+constexpr int kAltAS = 72;     // per-level lookup tile row stride (halves): 49 used, 64 multiplied
 constexpr int kAltOS = 136;    // output staging row stride (halves)
-constexpr int kAltMaxGroups = 1 + 4 + 64;
+constexpr int kAltMaxGroups = 1 + 2 + 4 + 64;
+constexpr int kAltF1 = 20 * 1024;   // next tile's query features, inside box 1 past the output staging
 // LDS map (bytes)
-constexpr int kAltF1 = 0;                                  // [64 px][256 B] query features
-constexpr int kAltBox = kAltF1 + 64 * 256;                 // [kAltCap taps][256 B]  (output staging aliases it)
-constexpr int kAltC = kAltBox + kAltCap * 256;             // [64 px][kAltCS] fp16
-constexpr int kAltA = kAltC + 64 * kAltCS * 2;             // [64 px][kAltAS] fp16 lookup tile
-constexpr int kAltMeta = kAltA + 64 * kAltAS * 2;          // per px: cx, cy, box x0, y0, bw (5 x 4 B)
-constexpr int kAltGrp = kAltMeta + 64 * 5 * 4;             // groups: x0, y0, bw, bh, mmask, pix (6 x 4 B)
+constexpr int kAltBox0 = 0;                                  // [kAltCap taps][256 B]
+constexpr int kAltBox1 = kAltBox0 + kAltCap * 256;           // the other stage's box (output staging aliases it)
+constexpr int kAltC = kAltBox1 + kAltCap * 256;              // [64 px][kAltCS] fp16
+constexpr int kAltA = kAltC + 64 * kAltCS * 2;               // [64 px][kAltAS] fp16 lookup of one level
+constexpr int kAltCoord = kAltA + 64 * kAltAS * 2;           // [2 tiles][64 px] float2 (by LDS-DMA)
+constexpr int kAltLvl = kAltCoord + 2 * 64 * 8;              // [2 tiles][4 levels] box x0, y0, w, h (int)
+constexpr int kAltPix = kAltLvl + 2 * 4 * 4 * 4;             // slow path: per px group box x0, y0, w (int)
+constexpr int kAltGrp = kAltPix + 64 * 3 * 4;                // slow path: count + groups (x0, y0, w, h, mmask, pix)
 constexpr int kAltLds = kAltGrp + (kAltMaxGroups * 6 + 4) * 4;
+static_assert(kAltLds <= 160 * 1024, "corr_alt_ce0 LDS budget");
+static_assert(64 * kAltOS * 2 <= kAltF1 && kAltF1 + 64 * 256 <= kAltCap * 256, "output staging + F1 fit box 1");
 
 // tile pixel p = 16 q + r: quadrant q = (qy, qx) = (q >> 1, q & 1), r = (ry, rx)
 __device__ __forceinline__ int alt_py(int p) { return 4 * ((p >> 4) >> 1) + ((p & 15) >> 2); }
 __device__ __forceinline__ int alt_px(int p) { return 4 * ((p >> 4) & 1) + (p & 3); }
 
+__device__ __forceinline__ int alt_floor(float v) { return (int)fminf(fmaxf(floorf(v), -1e6f), 1e6f); }
+
+// a wave-uniform int32 from global memory by a SCALAR load (lgkmcnt): the
+// compiler would otherwise use a vector load + vmcnt(0), which also drains the
+// box DMA in flight (the vmcnt counter is in order)
+__device__ __forceinline__ int alt_sload(const int* p) {
+  int v;
+  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+
+// clipped box [x0,x1] x [y0,y1] of the map -> tap count (0 when empty)
+__device__ __forceinline__ int alt_clip(int& x0, int& x1, int& y0, int& y1, int Wl, int Hl) {
+  x0 = max(x0, 0); x1 = min(x1, Wl - 1); y0 = max(y0, 0); y1 = min(y1, Hl - 1);
+  return (x1 >= x0 && y1 >= y0) ? (x1 - x0 + 1) * (y1 - y0 + 1) : 0;
+}
+
+// one wave: level boxes [l0, l1) of a tile from its coordinates in LDS (lane = pixel)
+__device__ __forceinline__ void alt_tile_boxes(const AltArgs& a, const float* cxy, int* lvl, int lane, int l0 = 0,
+                                               int l1 = 4) {
+#pragma unroll
+  for (int l = l0; l < l1; ++l) {
+    const float scl = 1.0f / (float)(1 << l);
+    const int ox = alt_floor(cxy[2 * lane] * scl) - 3, oy = alt_floor(cxy[2 * lane + 1] * scl) - 3;
+    // wave reductions on DPP (ockl), not LDS-routed shuffles
+    int x0 = __ockl_wfred_min_i32(ox), x1 = __ockl_wfred_max_i32(ox) + 7;
+    int y0 = __ockl_wfred_min_i32(oy), y1 = __ockl_wfred_max_i32(oy) + 7;
+    const int tn = alt_clip(x0, x1, y0, y1, a.Wl[l], a.Hl[l]);
+    if (lane == 0) {
+      lvl[4 * l + 0] = x0;
+      lvl[4 * l + 1] = y0;
+      lvl[4 * l + 2] = tn ? x1 - x0 + 1 : 0;
+      lvl[4 * l + 3] = tn ? y1 - y0 + 1 : 0;
+    }
+  }
+}
+
+// all waves: LDS-DMA of a gbw x gbh box of level `l` of frame f2 into `box`
+__device__ __forceinline__ void alt_box_dma(const AltArgs& a, int l, int f2, int gx0, int gy0, int gbw, int gbh,
+                                            unsigned box, int wave_u, int lane) {
+  const int tn = gbw * gbh;
+  if (tn <= 0) return;
+  const int Hl = a.Hl[l], Wl = a.Wl[l];
+  const rsrc_t rs = make_rsrc(a.pyr[l] + (long)f2 * Hl * Wl * 128, (unsigned)(Hl * Wl * 256));
+  const int nins = (tn + 3) >> 2;
+  for (int ins = wave_u; ins < nins; ins += 8) {
+    const int tap = ins * 4 + (lane >> 4);
+    const int piece = (lane & 15) ^ (tap & 15);
+    const int ry = tap / gbw, rx = tap - ry * gbw;
+    const unsigned off = tap < tn ? (unsigned)((((gy0 + ry) * Wl + gx0 + rx) * 128 + piece * 8) * 2) : kOob;
+    dma16(rs, box + ins * 1024, off);
+  }
+}
+
+// C[p][tap] = <F1(p), box tap> for the taps of one box (nb blocks of 16), pixels
+// restricted to the quadrants in mmask (and to pixel `gpix` when >= 0)
+__device__ __forceinline__ void alt_box_mfma(const char* lds, int box, _Float16* Cs, const half8 (&af)[4][4], int tn,
+                                             int mmask, int gpix, int wave_u, int fr, int fq) {
+  const int nb = (tn + 15) >> 4;
+  for (int b = wave_u; b < nb; b += 8) {
+    half8 bf[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int row = b * 16 + fr, piece = ks * 4 + fq;
+      bf[ks] = *reinterpret_cast<const half8*>(lds + box + row * 256 + ((piece ^ (row & 15)) << 4));
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!((mmask >> q) & 1)) continue;
+      // taps x pixels: lane (fr, fq) gets taps b*16 + 4 fq + k (k < 4) of pixel q*16 + fr
+      floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[ks], af[q][ks], c, 0, 0, 0);
+      const int p = q * 16 + fr;
+      if (gpix < 0 || gpix == p) {
+        half4_t h = {(_Float16)c[0], (_Float16)c[1], (_Float16)c[2], (_Float16)c[3]};
+        // taps past tn land in the row's slack (kAltCS >= 16 * ceil(cap / 16)) and are never read
+        *reinterpret_cast<half4_t*>(Cs + p * kAltCS + b * 16 + 4 * fq) = h;
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  float* meta = reinterpret_cast<float*>(lds + kAltMeta);
-  int* imeta = reinterpret_cast<int*>(lds + kAltMeta);
-  int* grp = reinterpret_cast<int*>(lds + kAltGrp);
   _Float16* Cs = reinterpret_cast<_Float16*>(lds + kAltC);
   _Float16* As = reinterpret_cast<_Float16*>(lds + kAltA);
-  _Float16* Os = reinterpret_cast<_Float16*>(lds + kAltBox);
+  int* pix = reinterpret_cast<int*>(lds + kAltPix);
+  int* grp = reinterpret_cast<int*>(lds + kAltGrp);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int H = a.H, W = a.W, HW = H * W;
@@ -88,224 +195,295 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
   const unsigned lds_a = lds_addr(lds);
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
 
-  // corr_encoder[0] B fragments of this wave's 16 output channels, all 7 K-steps
-  half8 wb[7];
-#pragma unroll
-  for (int ks = 0; ks < 7; ++ks)
-    wb[ks] = *reinterpret_cast<const half8*>(a.w + (wave * 16 + fr) * 224 + ks * 32 + fq * 8);
-  const float bias = a.bias[wave * 16 + fr];
-  // lookup-tile pad columns 196..231 stay zero
-  for (int idx = tid; idx < 64 * 36; idx += 512) As[(idx / 36) * kAltAS + 196 + idx % 36] = (_Float16)0.f;
+  // XCD-aware order: the workgroups of one XCD (blockIdx % 8) walk adjacent tiles
+  const int G = gridDim.x;
+  const int b0 = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  if (b0 >= a.ntiles) return;
 
-  for (long t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
-    const long e = t / tpe;
-    const int tt = (int)(t - e * tpe);
-    const int ty0 = (tt / tcols) * 8, tx0 = (tt % tcols) * 8;
-    const int f1 = a.f1[e], f2 = a.f2[e];
-
-    // query features of the 64 pixels -> LDS (16 x 1 KB DMA, 2 per wave)
-    {
-      const rsrc_t rs = make_rsrc(a.pyr[0] + (long)f1 * HW * 128, (unsigned)HW * 256);
+  // corr_encoder[0] B fragments of this wave's 16 output channels: per level,
+  // K = 49 real columns padded to 64 (2 K-steps of 32)
+  half8 wl[4][2];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int ins = wave_u + 8 * q;
-        const int p = ins * 4 + (lane >> 4);
-        const int piece = (lane & 15) ^ (p & 15);
-        const unsigned off = (unsigned)((((ty0 + alt_py(p)) * W + tx0 + alt_px(p)) * 128 + piece * 8) * 2);
-        dma16(rs, lds_a + kAltF1 + ins * 1024, off);
+  for (int l = 0; l < 4; ++l)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      half8 v;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = 32 * s + 8 * fq + i;
+        v[i] = k < 49 ? (_Float16)a.w[(wave * 16 + fr) * 224 + 49 * l + k] : (_Float16)0.f;
       }
+      wl[l][s] = v;
     }
-    if (tid < 64) {
-      const float2 c = *reinterpret_cast<const float2*>(a.coords + ((e * H + ty0 + alt_py(tid)) * (long)W + tx0 + alt_px(tid)) * 2);
-      meta[tid * 5 + 0] = c.x;
-      meta[tid * 5 + 1] = c.y;
+  const float bias = a.bias[wave * 16 + fr];
+  // lookup-tile columns 49..71 stay zero (the bilinear writes 0..48 only)
+  for (int idx = tid; idx < 64 * (kAltAS - 49); idx += 512)
+    As[(idx / (kAltAS - 49)) * kAltAS + 49 + idx % (kAltAS - 49)] = (_Float16)0.f;
+
+  // tile geometry (32-bit: the launcher checks ntiles < 2^31).  Edge and frame
+  // indices are wave-uniform scalar loads (lgkmcnt), so no vmcnt wait - which
+  // would also drain the in-flight box DMA - is ever needed for them.
+  struct Tile { int e, ty0, tx0, f1, f2; };
+  auto tile_of = [&](int t) {
+    Tile r;
+    r.e = __builtin_amdgcn_readfirstlane(t / tpe);
+    const int tt = t - r.e * tpe;
+    r.ty0 = (tt / tcols) * 8;
+    r.tx0 = (tt - (tt / tcols) * tcols) * 8;
+    r.f1 = alt_sload(a.f1 + r.e);
+    r.f2 = alt_sload(a.f2 + r.e);
+    return r;
+  };
+  // coordinates of a tile's 64 pixels -> LDS slot by LDS-DMA (lanes 0..31 of wave 0, 16 B = 2 px each)
+  auto coords_dma = [&](const Tile& T, int slot) {
+    if (wave_u == 0) {
+      const int e = T.e, ty0 = T.ty0, tx0 = T.tx0;
+      const rsrc_t rs = make_rsrc(a.coords + (long)e * HW * 2, (unsigned)(HW * 8));
+      // slot pixel p <- image pixel (ty0 + alt_py(p), tx0 + alt_px(p)); pairs (p, p+1) share a row piece
+      const int p = 2 * (lane & 31);
+      const unsigned off = lane < 32 ? (unsigned)((((ty0 + alt_py(p)) * W + tx0 + alt_px(p)) * 2) * 4) : kOob;
+      dma16(rs, lds_a + kAltCoord + slot * 512, off);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // query A fragments stay in registers for all four levels
-    half8 af[4][4];
+  };
+  // a tile's 64 query feature rows (16 KB) -> box 1 + kAltF1 by LDS-DMA, once per
+  // workgroup (each wave then reads the fragments it needs from LDS): 2 x 1 KB per wave
+  auto f1_dma = [&](const Tile& T) {
+    const rsrc_t rs = make_rsrc(a.pyr[0] + (long)T.f1 * HW * 128, (unsigned)(HW * 256));
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int ins = wave_u + 8 * k;
+      const int p = ins * 4 + (lane >> 4);
+      const int piece = (lane & 15) ^ (p & 15);
+      const unsigned off = (unsigned)((((T.ty0 + alt_py(p)) * W + T.tx0 + alt_px(p)) * 128 + piece * 8) * 2);
+      dma16(rs, lds_a + kAltBox1 + kAltF1 + ins * 1024, off);
+    }
+  };
+  auto read_f1 = [&](half8 (&af)[4][4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int row = q * 16 + fr, piece = ks * 4 + fq;
-        af[q][ks] = *reinterpret_cast<const half8*>(lds + kAltF1 + row * 256 + ((piece ^ (row & 15)) << 4));
+        af[q][ks] = *reinterpret_cast<const half8*>(lds + kAltBox1 + kAltF1 + row * 256 + ((piece ^ (row & 15)) << 4));
       }
+  };
+  auto stage_fits = [&](int slot, int l) {
+    const int* lv = reinterpret_cast<const int*>(lds + kAltLvl) + slot * 16 + 4 * l;
+    return lv[2] * lv[3] <= kAltCap;
+  };
+  // Stages run the levels coarse to fine (3, 2, 1, 0): the largest box (level
+  // 0) is prefetched during level 1's compute, and the next tile's first box
+  // (level 3, tiny) is what competes with this tile's last level and the next
+  // query features for the vector memory pipe.  Stage s uses box buffer s & 1.
+  auto stage_dma = [&](const Tile& T, int slot, int l, int buf) {   // the whole-tile box of (T, l)
+    const int* lv = reinterpret_cast<const int*>(lds + kAltLvl) + slot * 16 + 4 * l;
+    alt_box_dma(a, l, T.f2, lv[0], lv[1], lv[2], lv[3], lds_a + (buf ? kAltBox1 : kAltBox0), wave_u, lane);
+  };
 
-    for (int lvl = 0; lvl < 4; ++lvl) {
-      const int Hl = a.Hl[lvl], Wl = a.Wl[lvl];
-      const float scl = 1.0f / (float)(1 << lvl);
-      // ---- groups: wave 0, one lane per pixel ----
-      if (wave == 0) {
-        const float x0 = meta[lane * 5 + 0] * scl, y0 = meta[lane * 5 + 1] * scl;
-        const int ox = (int)fminf(fmaxf(floorf(x0), -1e6f), 1e6f) - 3;
-        const int oy = (int)fminf(fmaxf(floorf(y0), -1e6f), 1e6f) - 3;
-        // bounding boxes of the windows (tile, quadrant), clipped to the map
-        int bx0 = ox, bx1 = ox + 7, by0 = oy, by1 = oy + 7;
-        int qx0 = bx0, qx1 = bx1, qy0 = by0, qy1 = by1;
+  // ---- prologue: tile b0's coordinates and boxes, its level-0 box in flight ----
+  int t = b0;
+  int slot = 0;
+  Tile cur = tile_of(t);
+  coords_dma(cur, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (wave_u == 0)
+    alt_tile_boxes(a, reinterpret_cast<const float*>(lds + kAltCoord), reinterpret_cast<int*>(lds + kAltLvl), lane);
+  __syncthreads();
+  if (stage_fits(0, 3)) stage_dma(cur, 0, 3, 0);
+  f1_dma(cur);
+  half8 af[4][4];
+  floatx4 acc[4];
 #pragma unroll
-        for (int m = 1; m < 64; m <<= 1) {
-          bx0 = min(bx0, __shfl_xor(bx0, m)); bx1 = max(bx1, __shfl_xor(bx1, m));
-          by0 = min(by0, __shfl_xor(by0, m)); by1 = max(by1, __shfl_xor(by1, m));
-          if (m < 16) {
+  for (int q = 0; q < 4; ++q) acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  int stage = 0;   // profiling stamps only
+  (void)stage;
+  for (;;) {
+    const int tn_ = t + G;                  // the tile after this one
+    const bool more = tn_ < a.ntiles;
+    const Tile nxt = more ? tile_of(tn_) : cur;
+    const int e = cur.e, ty0 = cur.ty0, tx0 = cur.tx0, f2 = cur.f2;
+    const float* cxy = reinterpret_cast<const float*>(lds + kAltCoord + slot * 512);
+    const int* lvb = reinterpret_cast<const int*>(lds + kAltLvl) + slot * 16;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {   // unrolled: the level's weight fragments stay static register operands
+      const int l = 3 - st;
+      const int Hl = a.Hl[l], Wl = a.Wl[l];
+      const unsigned box = (st & 1) ? kAltBox1 : kAltBox0;
+      ALT_STAMP(0, ALT_NOW());
+      // (a) this stage's box (and the next tile's coordinates) have landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      ALT_STAMP(1, ALT_NOW());
+      if (st == 0) {
+        // the query features (DMA'd during the previous tile's last stage) -> registers,
+        // and every wave is done reading them before box 1 is refilled below
+        read_f1(af);
+        __syncthreads();
+      }
+      const bool fits = lvb[4 * l + 2] * lvb[4 * l + 3] <= kAltCap;
+      ALT_STAMP(7, (long long)(lvb[4 * l + 2] * lvb[4 * l + 3]) * 2 + (fits ? 0 : 1));
+      // (b) the next stage's box -> the other buffer, in flight during this stage
+      if (st < 3) {
+        if (stage_fits(slot, l - 1)) stage_dma(cur, slot, l - 1, (st + 1) & 1);
+      } else if (more) {
+        if (stage_fits(slot ^ 1, 3)) stage_dma(nxt, slot ^ 1, 3, 0);
+      }
+      if (st == 0 && more) coords_dma(nxt, slot ^ 1);
+      // (c) C = F1 x box^T
+      if (fits) {
+        alt_box_mfma(lds, box, Cs, af, lvb[4 * l + 2] * lvb[4 * l + 3], 15, -1, wave_u, fr, fq);
+        if (tid < 64) { pix[3 * tid] = lvb[4 * l]; pix[3 * tid + 1] = lvb[4 * l + 1]; pix[3 * tid + 2] = lvb[4 * l + 2]; }
+      } else {
+        // slow path: groups = per quadrant its box if it fits, else its 16 pixels' own windows
+        // slow path: groups = per half (quadrants 2h, 2h+1) its box if it fits, else
+        // per quadrant its box if it fits, else its 16 pixels' own windows
+        if (wave_u == 0) {
+          const float scl = 1.0f / (float)(1 << l);
+          const int ox = alt_floor(cxy[2 * lane] * scl) - 3, oy = alt_floor(cxy[2 * lane + 1] * scl) - 3;
+          int qx0 = ox, qx1 = ox + 7, qy0 = oy, qy1 = oy + 7;
+#pragma unroll
+          for (int m = 1; m < 16; m <<= 1) {
             qx0 = min(qx0, __shfl_xor(qx0, m)); qx1 = max(qx1, __shfl_xor(qx1, m));
             qy0 = min(qy0, __shfl_xor(qy0, m)); qy1 = max(qy1, __shfl_xor(qy1, m));
           }
-        }
-        auto clip = [&](int& x0c, int& x1c, int& y0c, int& y1c) {
-          x0c = max(x0c, 0); x1c = min(x1c, Wl - 1); y0c = max(y0c, 0); y1c = min(y1c, Hl - 1);
-          return (x1c >= x0c && y1c >= y0c) ? (x1c - x0c + 1) * (y1c - y0c + 1) : 0;
-        };
-        const int tn = clip(bx0, bx1, by0, by1);
-        const int qn = clip(qx0, qx1, qy0, qy1);
-        int px0 = ox, px1 = ox + 7, py0 = oy, py1 = oy + 7;
-        const int pn = clip(px0, px1, py0, py1);
-        // lane's group box (its pixel's C row is indexed in it)
-        int gx0, gy0, gbw;
-        if (tn <= kAltCap) { gx0 = bx0; gy0 = by0; gbw = bx1 - bx0 + 1; }
-        else if (qn <= kAltCap) { gx0 = qx0; gy0 = qy0; gbw = qx1 - qx0 + 1; }
-        else { gx0 = px0; gy0 = py0; gbw = px1 - px0 + 1; }
-        imeta[lane * 5 + 2] = gx0;
-        imeta[lane * 5 + 3] = gy0;
-        imeta[lane * 5 + 4] = gbw;
-        // group list: the tile if its box fits; else per quadrant q (in order) the
-        // quadrant if its box fits, or its 16 pixels one by one
-        if (tn <= kAltCap) {
-          if (lane == 0) {
-            int* g = grp + 4;
-            g[0] = bx0; g[1] = by0; g[2] = tn ? bx1 - bx0 + 1 : 0; g[3] = tn ? by1 - by0 + 1 : 0;
-            g[4] = 15; g[5] = -1;
-            grp[0] = 1;
-          }
-        } else {
-          const unsigned long long narrow = __ballot(qn <= kAltCap);  // bit 16 q: quadrant q fits
-          const int q = lane >> 4;
-          int base = 0, ng = 0;
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const int cnt = ((narrow >> (16 * qq)) & 1ull) ? 1 : 16;
-            if (qq < q) base += cnt;
-            ng += cnt;
-          }
-          if (qn <= kAltCap) {
+          int hx0 = min(qx0, __shfl_xor(qx0, 16)), hx1 = max(qx1, __shfl_xor(qx1, 16));
+          int hy0 = min(qy0, __shfl_xor(qy0, 16)), hy1 = max(qy1, __shfl_xor(qy1, 16));
+          const int hn = alt_clip(hx0, hx1, hy0, hy1, Wl, Hl);
+          const int qn = alt_clip(qx0, qx1, qy0, qy1, Wl, Hl);
+          int px0 = ox, px1 = ox + 7, py0 = oy, py1 = oy + 7;
+          const int pn = alt_clip(px0, px1, py0, py1, Wl, Hl);
+          const bool hfit = hn <= kAltCap, qfit = qn <= kAltCap;
+          pix[3 * lane] = hfit ? hx0 : qfit ? qx0 : px0;
+          pix[3 * lane + 1] = hfit ? hy0 : qfit ? qy0 : py0;
+          pix[3 * lane + 2] = hfit ? hx1 - hx0 + 1 : qfit ? qx1 - qx0 + 1 : px1 - px0 + 1;
+          const unsigned long long hb = __ballot(hfit), qb = __ballot(qfit);
+          const int q = lane >> 4, h = lane >> 5;
+          auto qcnt = [&](int qq) { return ((qb >> (16 * qq)) & 1ull) ? 1 : 16; };
+          auto hcnt = [&](int hh) { return ((hb >> (32 * hh)) & 1ull) ? 1 : qcnt(2 * hh) + qcnt(2 * hh + 1); };
+          const int hbase = h ? hcnt(0) : 0;
+          const int qbase = hbase + ((q & 1) ? qcnt(q - 1) : 0);
+          if (hfit) {
+            if ((lane & 31) == 0) {
+              int* g = grp + 4 + 6 * hbase;
+              g[0] = hx0; g[1] = hy0; g[2] = hn ? hx1 - hx0 + 1 : 0; g[3] = hn ? hy1 - hy0 + 1 : 0;
+              g[4] = 3 << (2 * h); g[5] = -1;
+            }
+          } else if (qfit) {
             if ((lane & 15) == 0) {
-              int* g = grp + 4 + 6 * base;
+              int* g = grp + 4 + 6 * qbase;
               g[0] = qx0; g[1] = qy0; g[2] = qn ? qx1 - qx0 + 1 : 0; g[3] = qn ? qy1 - qy0 + 1 : 0;
               g[4] = 1 << q; g[5] = -1;
             }
           } else {
-            int* g = grp + 4 + 6 * (base + (lane & 15));
+            int* g = grp + 4 + 6 * (qbase + (lane & 15));
             g[0] = px0; g[1] = py0; g[2] = pn ? px1 - px0 + 1 : 0; g[3] = pn ? py1 - py0 + 1 : 0;
             g[4] = 1 << q; g[5] = lane;
           }
-          if (lane == 0) grp[0] = ng;
+          if (lane == 0) grp[0] = hcnt(0) + hcnt(1);
         }
-      }
-      __syncthreads();
-      const int ng = grp[0];
-      const rsrc_t rs = make_rsrc(a.pyr[lvl] + (long)f2 * Hl * Wl * 128, (unsigned)(Hl * Wl * 256));
-      // ---- per group: box -> LDS, C = F1 x box^T ----
-      for (int gi = 0; gi < ng; ++gi) {
-        const int* g = grp + 4 + 6 * gi;
-        const int gx0 = g[0], gy0 = g[1], gbw = g[2], gbh = g[3], mmask = g[4], gpix = g[5];
-        const int tn = gbw * gbh;
-        if (tn > 0) {
-          const int nins = (tn + 3) >> 2;
-          for (int ins = wave_u; ins < nins; ins += 8) {
-            const int tap = ins * 4 + (lane >> 4);
-            const int piece = (lane & 15) ^ (tap & 15);
-            const int ry = tap / gbw, rx = tap - ry * gbw;
-            const unsigned off = tap < tn ? (unsigned)((((gy0 + ry) * Wl + gx0 + rx) * 128 + piece * 8) * 2) : kOob;
-            dma16(rs, lds_a + kAltBox + ins * 1024, off);
-          }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        const int nb = (tn + 15) >> 4;
-        for (int b = wave_u; b < nb; b += 8) {
-          half8 bf[4];
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            const int row = b * 16 + fr, piece = ks * 4 + fq;
-            bf[ks] = *reinterpret_cast<const half8*>(lds + kAltBox + row * 256 + ((piece ^ (row & 15)) << 4));
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (!((mmask >> q) & 1)) continue;
-            floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[q][ks], bf[ks], c, 0, 0, 0);
-            const int tap = b * 16 + fr;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const int p = q * 16 + fq * 4 + k;
-              if (tap < tn && (gpix < 0 || gpix == p)) Cs[p * kAltCS + tap] = (_Float16)c[k];
-            }
-          }
+        const int ng = grp[0];
+        for (int gi = 0; gi < ng; ++gi) {
+          const int* g = grp + 4 + 6 * gi;
+          alt_box_dma(a, l, f2, g[0], g[1], g[2], g[3], lds_a + box, wave_u, lane);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          alt_box_mfma(lds, box, Cs, af, g[2] * g[3], g[4], g[5], wave_u, fr, fq);
+          __syncthreads();  // box free for the next group
         }
-        __syncthreads();  // box free for the next group, C complete
       }
-      // ---- bilinear windows (volume-lookup arithmetic): thread (px, a) -> 7 outputs ----
+      ALT_STAMP(2, ALT_NOW());
+      __syncthreads();
+      // box 1 (this stage's box) is free past the output staging: the next tile's
+      // query features land there during the bilinear, the encoder and the stores
+      if (st == 3 && more) f1_dma(nxt);
+      ALT_STAMP(3, ALT_NOW());
+      // (d) bilinear windows (volume-lookup arithmetic): thread (px, x offset) -> 7 outputs
+      // The reference rounds every product and sum of halves through float
+      // (at::Half); float carries >= 2*11+2 bits, so that equals the native
+      // half op (corr_kernels.hip): _Float16 arithmetic, no contraction.
       if (tid < 64 * 7) {
         const int p = tid / 7, ac = tid - p * 7;
-        const float x0 = meta[p * 5 + 0] * scl, y0 = meta[p * 5 + 1] * scl;
+        const float scl = 1.0f / (float)(1 << l);
+        const float x0 = cxy[2 * p] * scl, y0 = cxy[2 * p + 1] * scl;
         const float fx0 = floorf(x0), fy0 = floorf(y0);
         const float dx = x0 - fx0, dy = y0 - fy0;
-        const int xi0 = (int)fminf(fmaxf(fx0, -1e6f), 1e6f), yi0 = (int)fminf(fmaxf(fy0, -1e6f), 1e6f);
-        const float w11 = rnd16(dx * dy);
-        const float w10 = rnd16(dx * (1.0f - dy));
-        const float w01 = rnd16((1.0f - dx) * dy);
-        const float w00 = rnd16((1.0f - dx) * (1.0f - dy));
-        const int gx0 = imeta[p * 5 + 2], gy0 = imeta[p * 5 + 3], gbw = imeta[p * 5 + 4];
-        const _Float16* crow = Cs + p * kAltCS;
-        auto tapv = [&](int x, int y) -> float {
-          return (x >= 0 && x < Wl && y >= 0 && y < Hl) ? (float)crow[(y - gy0) * gbw + (x - gx0)] : 0.f;
-        };
+        const int xi0 = alt_floor(x0), yi0 = alt_floor(y0);
+        // float product, then half (rnd16 keeps hipcc from one-rounding v_fma_mixlo)
+        const _Float16 w11 = (_Float16)rnd16(dx * dy);
+        const _Float16 w10 = (_Float16)rnd16(dx * (1.0f - dy));
+        const _Float16 w01 = (_Float16)rnd16((1.0f - dx) * dy);
+        const _Float16 w00 = (_Float16)rnd16((1.0f - dx) * (1.0f - dy));
+        const int gx0 = pix[3 * p], gy0 = pix[3 * p + 1], gbw = pix[3 * p + 2];
         const int xa = xi0 - 3 + ac;
-        float pa = 0.f, pb = 0.f;
-        _Float16* arow = As + p * kAltAS + lvl * 49 + ac * 7;
+        const bool va = xa >= 0 && xa < Wl, vb = xa + 1 >= 0 && xa + 1 < Wl;
+        const _Float16* crow = Cs + p * kAltCS + (xa - gx0);   // + (y - gy0) * gbw per row
+        const _Float16 z = (_Float16)0.f;
+        _Float16 pa = z, pb = z;
+        _Float16* arow = As + p * kAltAS + ac * 7;
 #pragma unroll
         for (int j = 0; j <= 7; ++j) {
           const int y = yi0 - 3 + j;
-          const float ca = tapv(xa, y), cb = tapv(xa + 1, y);
+          const bool vy = y >= 0 && y < Hl;
+          const _Float16* cr = crow + (y - gy0) * gbw;
+          const _Float16 ca = (vy && va) ? cr[0] : z, cb = (vy && vb) ? cr[1] : z;
           if (j > 0) {
-            float acc = 0.f + rnd16(pa * w00);
-            acc = rnd16(acc + rnd16(ca * w01));
-            acc = rnd16(acc + rnd16(pb * w10));
-            acc = rnd16(acc + rnd16(cb * w11));
-            arow[j - 1] = (_Float16)acc;
+            _Float16 s = z + pa * w00;
+            s = s + ca * w01;
+            s = s + pb * w10;
+            s = s + cb * w11;
+            arow[j - 1] = s;
           }
           pa = ca;
           pb = cb;
         }
       }
-      __syncthreads();  // C and the per-pixel group boxes are reused by the next level
-    }
-
-    // ---- corr_encoder[0]: 64 px x 16 co per wave, K = 224 ----
-    floatx4 acc[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 7; ++ks) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const half8 x = *reinterpret_cast<const half8*>(&As[(q * 16 + fr) * kAltAS + ks * 32 + fq * 8]);
-        acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, wb[ks], acc[q], 0, 0, 0);
+      ALT_STAMP(4, ALT_NOW());
+      if ((st == 1 || st == 2) && more && wave_u == 7) {
+        // the next tile's level boxes, on the wave the bilinear leaves idle (its
+        // coordinates, DMA'd during the first stage, landed at stage 1's wait):
+        // levels 3, 2 now (level 3 is prefetched at stage 3), levels 1, 0 next stage
+        alt_tile_boxes(a, reinterpret_cast<const float*>(lds + kAltCoord + (slot ^ 1) * 512),
+                       reinterpret_cast<int*>(lds + kAltLvl) + (slot ^ 1) * 16, lane, st == 1 ? 2 : 0,
+                       st == 1 ? 4 : 2);
       }
-    }
+      __syncthreads();
+      ALT_STAMP(5, ALT_NOW());
+      // (e) this level's slice of corr_encoder[0]: 64 px x 16 co per wave, K = 64
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int s = 0; s < 2; ++s) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        Os[(q * 16 + fq * 4 + k) * kAltOS + wave * 16 + fr] = (_Float16)fmaxf(acc[q][k] + bias, 0.f);
-    __syncthreads();
-    for (int idx = tid; idx < 64 * 16; idx += 512) {
-      const int p = idx >> 4, pc = idx & 15;
-      const long m = (e * H + ty0 + alt_py(p)) * (long)W + tx0 + alt_px(p);
-      *reinterpret_cast<uint4*>(a.out + m * 128 + pc * 8) = *reinterpret_cast<const uint4*>(&Os[p * kAltOS + pc * 8]);
+        for (int q = 0; q < 4; ++q) {
+          const half8 x = *reinterpret_cast<const half8*>(&As[(q * 16 + fr) * kAltAS + s * 32 + fq * 8]);
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, wl[l][s], acc[q], 0, 0, 0);
+        }
+      }
+      if (st == 3) {
+        // (f) bias, ReLU -> staging in this stage's box buffer (box 1: its MFMA is done) -> rows
+        _Float16* Os = reinterpret_cast<_Float16*>(lds + kAltBox1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            Os[(q * 16 + fq * 4 + k) * kAltOS + wave * 16 + fr] = (_Float16)fmaxf(acc[q][k] + bias, 0.f);
+          acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        __syncthreads();
+        for (int idx = tid; idx < 64 * 16; idx += 512) {
+          const int p = idx >> 4, pc = idx & 15;
+          const long m = ((long)e * H + ty0 + alt_py(p)) * W + tx0 + alt_px(p);
+          *reinterpret_cast<uint4*>(a.out + m * 128 + pc * 8) = *reinterpret_cast<const uint4*>(&Os[p * kAltOS + pc * 8]);
+        }
+      }
+      ALT_STAMP(6, ALT_NOW());
+      ++stage;
     }
-    __syncthreads();  // output staging (box region) and meta free for the next tile
+    if (!more) break;
+    t = tn_;
+    cur = nxt;
+    slot ^= 1;
   }
 }
 
@@ -313,7 +491,22 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
 
 using namespace droid;
 
+static long long* g_alt_prof = nullptr;
+
 extern "C" {
+
+// Profiling builds (make prof): per workgroup, for its first 32 stages, 8 int64:
+// s_memtime at stage start / box landed / C done / C barrier / bilinear done /
+// lookup barrier / stage end, then (box taps * 2 + slow-path flag).
+int droid_alt_set_profile(void* buf) {
+#if DROID_CONV_PROFILE
+  g_alt_prof = static_cast<long long*>(buf);
+  return kOk;
+#else
+  (void)buf;
+  return fail(kUnsupported, "alt_set_profile: build with make prof (DROID_CONV_PROFILE=1)");
+#endif
+}
 
 // On-the-fly CorrBlock lookup fused with corr_encoder[0] (corr_alt_ce0_kernel).
 int droid_corr_alt_ce0(const void* const* pyr, const int* Hl, const int* Wl, const int* f1, const int* f2,
@@ -332,10 +525,13 @@ int droid_corr_alt_ce0(const void* const* pyr, const int* Hl, const int* Wl, con
     a.Wl[l] = Wl[l];
   }
   if (Hl[0] != H || Wl[0] != W) return fail(kInvalidArgument, "corr_alt_ce0: level 0 must be H x W");
+  if ((long)H * W * 8 > 0x7fffffffL) return fail(kUnsupported, "corr_alt_ce0: coordinate plane too large");
   a.f1 = f1; a.f2 = f2; a.coords = coords;
   a.w = (const __half*)w; a.bias = bias; a.out = (__half*)out;
   a.H = H; a.W = W;
   a.ntiles = (long)E * (H / 8) * (W / 8);
+  if (a.ntiles + device_cu_count() >= 0x7fffffffL) return fail(kUnsupported, "corr_alt_ce0: too many tiles");
+  a.prof = g_alt_prof;
   if (a.ntiles == 0) return kOk;
   static bool attr = false;
   if (!attr) {

@@ -286,11 +286,32 @@ class FactorGraph:
         return PendingAltLookup(self._alt_pyr[1], f1, f2, coords1)
 
     def update_lowmem(self, t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, steps=8):
-        """factor_graph.py:245-290: alternate (on-the-fly) correlation, chunks of 8 sources."""
+        """factor_graph.py:245-290: `steps` x [reprojection, on-the-fly (alt)
+        correlation + update operator, BA over poses [1, t) with lm=1e-5,
+        ep=1e-2] - the global-BA backend's update (droid_backend.py:31-38).
+
+        The reference walks the source frames in chunks of 8 to bound the memory
+        of its fp32 correlation; every per-edge stage and GraphAgg's per-frame
+        mean are independent across chunks, so the fused path runs all edges in
+        one pass: the lookup is corr_alt_ce0 (windows computed on demand from the
+        feature pyramid of the frames, fused with corr_encoder[0]) and the gate
+        convs take the context term per source frame (video.inps[ii])."""
         t = self.video.counter.value
         num, rig, ch, ht, wd = self.video.fmaps.shape
-        corr_op = AltCorrBlock(self.video.fmaps.view(1, num * rig, ch, ht, wd))
         E = len(self._ii)
+        if self.fused:
+            f = self.video.fmaps[:num]
+            blk = AltCorrBlock(f.reshape((1, num * rig) + tuple(f.shape[2:])))
+            pyr = [lv.view((-1,) + tuple(lv.shape[2:])) for lv in blk.pyramid]
+            f1 = self._dev("alt_f1", (rig * self._ii).astype(np.int32))
+            f2 = self._dev("alt_f2", (rig * self._jj + ((self._ii == self._jj) & (rig > 1))).astype(np.int32))
+            uniq, inverse = np.unique(self._ii, return_inverse=True)
+            dinv = self._dev("inverse", inverse.astype(np.int64))
+            ptr, idx = edge_segments(inverse, len(uniq))
+            segs = (self._dev("seg_ptr", ptr), self._dev("seg_idx", idx))
+            duniq = self._dev("uniq", uniq)
+        else:
+            corr_op = AltCorrBlock(self.video.fmaps.view(1, num * rig, ch, ht, wd))
         for _ in range(steps):
             with torch.autocast("cuda", enabled=False):
                 coords1, _, motn = droid_backends.projective_transform(
@@ -298,43 +319,48 @@ class FactorGraph:
                     target=self.target.view(E, ht, wd, 2), with_valid=False)
                 coords1 = coords1.view(1, E, ht, wd, 2)
                 motn = motn.view(1, E, 4, ht, wd)
-            s = 8
-            for i in range(0, int(self._jj.max()) + 1, s):
-                vh = (self._ii >= i) & (self._ii < i + s)
-                if not vh.any():
-                    continue
-                v = torch.as_tensor(vh, device=self.device)
-                iis_h, jjs_h = self._ii[vh], self._jj[vh]
-                iis = torch.as_tensor(iis_h, device=self.device)
-                jjs = torch.as_tensor(jjs_h, device=self.device)
-                src = torch.as_tensor(rig * iis_h, device=self.device)
-                dst = torch.as_tensor(rig * jjs_h + (iis_h == jjs_h), device=self.device)
-                corr1 = corr_op(coords1[:, v], src, dst)
-                uq, inv = np.unique(iis_h, return_inverse=True)
-                dinv = torch.as_tensor(inv, device=self.device)
-                if self.fused:
-                    ev = len(iis_h)
-                    c200 = torch.zeros((ev, ht, wd, 200), dtype=torch.float16, device=self.device)
-                    c200[..., :196] = corr1[0].permute(0, 2, 3, 1)
-                    inp = self.video.inps[iis].permute(0, 2, 3, 1).contiguous()
-                    net, delta, weight, damping = self.update_op(self.net[v].contiguous(), inp, c200,
-                                                                 motn[0, v].contiguous(), dinv, len(uq))
-                    self.net[v] = net
-                else:
-                    with torch.autocast("cuda", enabled=True):
-                        net, delta, weight, damping, _ = self.update_op(
-                            self.net[:, v], self.video.inps[None, iis], corr1, motn[:, v], iis, jjs,
-                            inverse=dinv, num_unique=len(uq))
-                    self.net[:, v] = net
-                self.target[:, v] = coords1[:, v] + delta.float()
-                self.weight[:, v] = weight.float()
-                self.damping[torch.as_tensor(uq, device=self.device)] = damping[0].float()
+            if self.fused:
+                inp_frames = self.video.inps[duniq].permute(0, 2, 3, 1).contiguous()
+                corr = PendingAltLookup(pyr, f1, f2, coords1)
+                self.net, delta, weight, damping = self.update_op(self.net, None, corr, motn[0], dinv, len(uniq),
+                                                                  segments=segs, inp_frames=inp_frames)
+                with torch.autocast("cuda", enabled=False):
+                    self.target = coords1 + delta.to(dtype=torch.float)
+                    self.weight = weight.to(dtype=torch.float)
+                    self.damping[duniq] = damping[0].to(torch.float)
+            else:
+                self._lowmem_chunks(corr_op, coords1, motn, rig)
             damping = 0.2 * self.damping[self._dev("uniq_all", np.unique(self._ii))].contiguous() + EP
             target = self.target.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
             weight = self.weight.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
             self.video.ba(target, weight, damping, self.ii, self.jj, 1, t, itrs=itrs, lm=1e-5, ep=1e-2,
-                          motion_only=False, ii_host=self._ii, jj_host=self._jj)
+                          motion_only=False, ii_host=self._ii, jj_host=self._jj, comm=self.comm)
             self.video.dirty[:t] = True
+
+    def _lowmem_chunks(self, corr_op, coords1, motn, rig):
+        """the reference-structured operator: chunks of 8 source frames (factor_graph.py:262-280)."""
+        s = 8
+        for i in range(0, int(self._jj.max()) + 1, s):
+            vh = (self._ii >= i) & (self._ii < i + s)
+            if not vh.any():
+                continue
+            v = torch.as_tensor(vh, device=self.device)
+            iis_h, jjs_h = self._ii[vh], self._jj[vh]
+            iis = torch.as_tensor(iis_h, device=self.device)
+            jjs = torch.as_tensor(jjs_h, device=self.device)
+            src = torch.as_tensor(rig * iis_h, device=self.device)
+            dst = torch.as_tensor(rig * jjs_h + (iis_h == jjs_h), device=self.device)
+            corr1 = corr_op(coords1[:, v], src, dst)
+            uq, inv = np.unique(iis_h, return_inverse=True)
+            dinv = torch.as_tensor(inv, device=self.device)
+            with torch.autocast("cuda", enabled=True):
+                net, delta, weight, damping, _ = self.update_op(
+                    self.net[:, v], self.video.inps[None, iis], corr1, motn[:, v], iis, jjs,
+                    inverse=dinv, num_unique=len(uq))
+            self.net[:, v] = net
+            self.target[:, v] = coords1[:, v] + delta.float()
+            self.weight[:, v] = weight.float()
+            self.damping[torch.as_tensor(uq, device=self.device)] = damping[0].float()
 
     # -- edge construction (factor_graph.py:292-369) --------------------------
     def add_neighborhood_factors(self, t0, t1, r=3):

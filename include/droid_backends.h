@@ -72,6 +72,11 @@ int droid_corr_pyramid_lookup_nhwc(const void* const* levels, const int* H2s, co
  * drained).  buf = null switches it off.  Not part of the reference interface
  * (scripts/conv_timeline.py). */
 int droid_conv_set_profile(void* buf);
+/* The same for corr_alt_ce0_kernel: per workgroup, its first 32 stages x 8
+ * int64 (s_memtime at stage start / box landed / C done / C barrier / bilinear
+ * done / lookup barrier / stage end, then box taps * 2 + slow-path flag)
+ * (scripts/alt_timeline.py). */
+int droid_alt_set_profile(void* buf);
 
 /* CorrBlock lookup fused with the update operator's corr_encoder[0]
  * (modules/corr.py:40-50 + droid_net.py:84-86): out (E,H,W,128) fp16 =

@@ -27,11 +27,15 @@ from . import update_module as oum
 
 
 def update(params, poses, disps, disps_sens, intrinsics, fmaps, ii, jj, net, inp, target, weight, damping,
-           t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, motion_only=False, inactive=None):
+           t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, motion_only=False, inactive=None, lm=1e-4,
+           ep=0.1):
     """params: UpdateModule state dict (numpy); poses (N,7), disps/disps_sens
     (N,H,W), intrinsics (N,4), fmaps (N,rig,128,H,W); ii/jj (E); net/inp
     (E,128,H,W); target/weight (E,H,W,2); damping (N,H,W); inactive =
     (ii, jj, target, weight) of the stored edges.  Inputs are not mutated.
+    update_lowmem (factor_graph.py:245-290) is one call per step with t0=1,
+    t1=counter, lm=1e-5, ep=1e-2 (its alt correlation equals the volume's up
+    to fp16 rounding, corr.py:91-139).
 
     Returns dict(net, target, weight, damping, coords1, ba_in=(targets, weights,
     eta, ii, jj, t0, t1), poses, disps)."""
@@ -73,7 +77,7 @@ def update(params, poses, disps, disps_sens, intrinsics, fmaps, ii, jj, net, inp
     wgt = wgt.transpose(0, 3, 1, 2)
     if t1 is None:
         t1 = int(max(ii_ba.max(), jj_ba.max())) + 1
-    out = oba.ba(poses, disps, intrinsics[0], disps_sens, tgt, wgt, eta_ba, ii_ba, jj_ba, t0, t1, itrs, 1e-4, 0.1,
+    out = oba.ba(poses, disps, intrinsics[0], disps_sens, tgt, wgt, eta_ba, ii_ba, jj_ba, t0, t1, itrs, lm, ep,
                  motion_only)
     return dict(net=net1[0].double().numpy(), target=target, weight=weight, damping=damping, coords1=coords1,
                 ba_in=(tgt, wgt, eta_ba, ii_ba, jj_ba, t0, t1), poses=out["poses"],

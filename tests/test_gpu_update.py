@@ -177,3 +177,42 @@ def test_update_unit_matches_oracle_composition():
     np.testing.assert_allclose(host(video.disps[:n]), np.maximum(ba_ref["disps"][:n], 0.001), atol=1e-4)
     # and the whole composition lands close to the oracle's own BA result
     np.testing.assert_allclose(host(video.poses[:n]), ref["poses"][:n], atol=2e-3)
+
+
+def test_update_lowmem_matches_oracle_composition():
+    """update_lowmem (factor_graph.py:245-290, the global-BA backend's step) on
+    the fused path - on-demand correlation (corr_alt_ce0) + factored gates, all
+    edges in one pass - against the oracle composition with the backend's BA
+    parameters (t0=1, t1=counter, lm=1e-5, ep=1e-2), at 48x64."""
+    from droid_mi355x import FactorGraph, UpdateModule, synthetic
+    from droid_mi355x.fused import FusedUpdateModule
+    from oracle import factor_graph as ofg
+    H, W = 48, 64
+    video = _c2_video(H, W, seed=52)
+    m = UpdateModule().to("cuda").eval()
+    det_fill(m)
+    g = FactorGraph(video, FusedUpdateModule(m), device="cuda", corr_impl="alt")
+    # the backend's graph covers every frame (unique(ii) must be unique([1, t) U ii), the eta rows)
+    ii, jj = synthetic.c3_edges(16, 96, rng=np.random.default_rng(7))
+    with torch.no_grad():
+        g.add_factors(ii, jj)
+    n = video.counter.value
+    st = dict(poses=host(video.poses[:n]), disps=host(video.disps[:n]), disps_sens=host(video.disps_sens[:n]),
+              intrinsics=host(video.intrinsics[:n]), fmaps=host(video.fmaps[:n].float()),
+              net=host(g.net.float()).transpose(0, 3, 1, 2), target=host(g.target[0]), weight=host(g.weight[0]),
+              damping=host(g.damping[:n]))
+    inp = host(video.inps[:n].float())[g._ii]
+    params = {k: host(v.float()) for k, v in m.state_dict().items()}
+    with torch.no_grad():
+        g.update_lowmem(steps=1)
+    torch.cuda.synchronize()
+    ref = ofg.update(params, st["poses"], st["disps"], st["disps_sens"], st["intrinsics"], st["fmaps"], g._ii,
+                     g._jj, st["net"], inp, st["target"], st["weight"], st["damping"], t0=1, t1=n, lm=1e-5, ep=1e-2)
+    np.testing.assert_allclose(host(g.net.float()).transpose(0, 3, 1, 2), ref["net"], atol=2e-2)
+    dmax = max(1.0, float(np.abs(ref["target"] - ref["coords1"]).max()))
+    np.testing.assert_allclose(host(g.target[0]), ref["target"], atol=3e-2 * dmax)
+    np.testing.assert_allclose(host(g.weight[0]), ref["weight"], atol=1.5e-2)
+    u = np.unique(g._ii)
+    np.testing.assert_allclose(host(g.damping[u]), ref["damping"][u], atol=1e-3 + 2e-2 * np.abs(ref["damping"][u]).max())
+    np.testing.assert_allclose(host(video.poses[:n]), ref["poses"][:n], atol=2e-3)
+    np.testing.assert_allclose(host(video.disps[:n]), ref["disps"][:n], atol=2e-2)
