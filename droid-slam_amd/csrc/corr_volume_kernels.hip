@@ -1,0 +1,342 @@
+// CorrBlock pyramid construction (modules/corr.py:24-38, 63-71) in one pass,
+// gfx950.
+//
+// The reference builds, per edge, the all-pairs volume V0 = (f1/4)^T (f2/4)
+// with an autocast fp16 GEMM (fp32 accumulation, fp16 result, HW x HW) and then
+// three F.avg_pool2d(2) levels over the target dimensions, each from the
+// previous level's fp16 values (float sum in (h, w) order / 4, rounded).  Every
+// level is written to HBM and read back by the next; at 2048 edges that is
+// 51 GB written + 70 GB re-read, plus the tile8 copy for the fused lookup.
+//
+// corr_volume_pyramid_kernel writes every level exactly once: a workgroup owns
+// 256 query pixels of one edge (8 waves x 32) and walks the target map in 8x8
+// patches (Z order, so each level-1 / level-2 tile of the 8x8-tiled layout is
+// completed by consecutive patches while its lines are in L2):
+//   * the patch's 64 target feature rows (16 KB) reach LDS by LDS-DMA, one
+//     patch ahead (double buffer), shared by the 8 waves;
+//   * a wave multiplies its 32 query rows (registers) by the patch on MFMA
+//     (v_mfma_f32_16x16x32_f16, fp32 accumulation), 4 N-blocks of 16 target
+//     pixels, each a 4x4 target sub-patch, and rounds to fp16 (V0);
+//   * the three pooling levels are formed in registers from the rounded
+//     values with the reference's arithmetic: a 2x2 window's four fp16 values
+//     summed in float in (h, w) order, times 1/4, rounded - across lanes
+//     (xor 1 / 4 for level 1, 2 / 8 for level 2) and across the 4 N-blocks
+//     (level 3);
+//   * V0 and the pooled values go through a per-wave LDS staging area to
+//     coalesced stores: 128 B per query pixel and patch for level 0 (one 8x8
+//     tile, or 8 row pieces of the reference layout), 4 x 8 B, 2 x 4 B, 2 B for
+//     levels 1..3.
+// Query features come from the frames' NHWC level-0 feature maps (the
+// AltCorrBlock pyramid level 0, i.e. fmap / 4) indexed per edge, so no
+// per-edge feature copy exists either.
+#include "common.hpp"
+#include "lds_dma.hpp"
+
+#include <algorithm>
+
+#pragma clang fp contract(off)
+
+namespace droid {
+
+struct VolArgs {
+  const __half* f;   // (NF, H, W, 128) fp16 = fmap / 4
+  const int* f1;     // (E) query frame of each edge
+  const int* f2;     // (E) target frame
+  __half* lvl[4];    // outputs
+  int H, W;          // query and target maps are H x W
+  int tiled;         // 1: (E,H,W,ceil(H_l/8),W_l/8,8,8) 8x8 tiles; 0: (E,H,W,H_l,W_l)
+  int qblocks;       // ceil(HW / 256)
+};
+
+constexpr int kVolQ = 256;                 // query pixels per workgroup
+constexpr int kVolB = 0;                   // 2 x [64 target px][256 B] patch buffers
+constexpr int kVolStage = 2 * 64 * 256;    // per wave: [32 q][64] V0 | [32][16] L1 | [32][4] L2 | [32] L3 fp16
+constexpr int kVolStageWave = 32 * 64 * 2 + 32 * 16 * 2 + 32 * 4 * 2 + 32 * 2;
+constexpr int kVolLds = kVolStage + 8 * kVolStageWave;
+
+// target pixel of N-block b, column c inside an 8x8 patch at (ty0, tx0)
+__device__ __forceinline__ int vol_ty(int b, int c) { return 4 * (b >> 1) + (c >> 2); }
+__device__ __forceinline__ int vol_tx(int b, int c) { return 4 * (b & 1) + (c & 3); }
+
+__device__ __forceinline__ float vol_pool4(float a, float b, float c, float d) {
+  // F.avg_pool2d(2) on half: float accumulation over the window in (h, w) order, / 4, rounded
+  float s = 0.0f;
+  s += a;
+  s += b;
+  s += c;
+  s += d;
+  return rnd16(s / 4.0f);
+}
+
+__global__ void __launch_bounds__(512) corr_volume_pyramid_kernel(VolArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int H = a.H, W = a.W, HW = H * W;
+  const int e = __builtin_amdgcn_readfirstlane((int)(blockIdx.x / a.qblocks));
+  const int qb = (int)(blockIdx.x % a.qblocks);
+  const int fa = __builtin_amdgcn_readfirstlane(a.f1[e]);
+  const int fb = __builtin_amdgcn_readfirstlane(a.f2[e]);
+  const unsigned lds_a = lds_addr(lds);
+  char* stage = lds + kVolStage + wave * kVolStageWave;
+  _Float16* s0 = reinterpret_cast<_Float16*>(stage);                   // [32][64]
+  _Float16* s1 = s0 + 32 * 64;                                         // [32][16]
+  _Float16* s2 = s1 + 32 * 16;                                         // [32][4]
+  _Float16* s3 = s2 + 32 * 4;                                          // [32]
+
+  // this wave's 32 query rows: A fragments for 2 row blocks x 4 K-steps
+  const int q0 = qb * kVolQ + wave * 32;
+  half8 af[2][4];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int q = min(q0 + 16 * r + fr, HW - 1);
+    const __half* row = a.f + ((long)fa * HW + q) * 128;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) af[r][ks] = *reinterpret_cast<const half8*>(row + ks * 32 + fq * 8);
+  }
+
+  const rsrc_t rsb = make_rsrc(a.f + (long)fb * HW * 128, (unsigned)(HW * 256));
+  const int pcols = W / 8, npatch = (H / 8) * pcols;
+  // Z order over 2x2 patch groups (a level-1 tile = 2x2 patches)
+  auto patch_yx = [&](int p, int& py, int& px) {
+    const int gcols = (pcols + 1) / 2;
+    const int g = p >> 2, k = p & 3;
+    int gy = g / gcols, gx = g - gy * gcols;
+    py = 2 * gy + (k >> 1);
+    px = 2 * gx + (k & 1);
+  };
+  // patches in Z order may fall off an odd edge of the grid: skip those slots
+  const int gslots = ((H / 8 + 1) / 2) * ((pcols + 1) / 2) * 4;
+  auto patch_dma = [&](int p, int buf) {
+    int py, px;
+    patch_yx(p, py, px);
+    // 16 x 1 KB: wave w issues rows 4w..4w+3 and 32+4w..; row = 16 b + c
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int ins = wave_u + 8 * k;
+      const int row = ins * 4 + (lane >> 4);
+      const int b = row >> 4, c = row & 15;
+      const int t = (8 * py + vol_ty(b, c)) * W + 8 * px + vol_tx(b, c);
+      const int piece = (lane & 15) ^ (row & 15);
+      dma16(rsb, lds_a + kVolB + buf * 16384 + ins * 1024, (unsigned)((t * 128 + piece * 8) * 2));
+    }
+  };
+  auto valid = [&](int p) {
+    int py, px;
+    patch_yx(p, py, px);
+    return py < H / 8 && px < pcols;
+  };
+  int first = 0;
+  while (first < gslots && !valid(first)) ++first;
+  if (first < gslots) patch_dma(first, 0);
+  int buf = 0;
+  // level geometry
+  int Hl[4], Wl[4], TR[4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    Hl[l] = H >> l;
+    Wl[l] = W >> l;
+    TR[l] = (Hl[l] + 7) / 8;  // tile rows (tiled layout)
+  }
+  for (int p = first; p < gslots;) {
+    int nxt = p + 1;
+    while (nxt < gslots && !valid(nxt)) ++nxt;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // patch p landed in buf; every wave done with buf ^ 1
+    if (nxt < gslots) patch_dma(nxt, buf ^ 1);
+    int py, px;
+    patch_yx(p, py, px);
+    const int ty0 = 8 * py, tx0 = 8 * px;
+
+    // V0 for 32 query rows x 64 target pixels: D[target col][query row] per N-block
+    float v[2][4][4];   // [row block][N-block][i]: query row 16 r + 4 fq + i, target col fr
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      half8 bf[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int row = b * 16 + fr, piece = ks * 4 + fq;
+        bf[ks] = *reinterpret_cast<const half8*>(lds + kVolB + buf * 16384 + row * 256 + ((piece ^ (row & 15)) << 4));
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r][ks], bf[ks], c, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[r][b][i] = rnd16(c[i]);
+      }
+    }
+    // level 0 -> staging [q][tile-row-major 8x8]
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          s0[(16 * r + 4 * fq + i) * 64 + vol_ty(b, fr) * 8 + vol_tx(b, fr)] = (_Float16)v[r][b][i];
+    // level 1: 2x2 windows of each 4x4 sub-patch (cols c, c^1, c^4, c^5 with c's row / col even)
+    float u[2][4][4];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float x00 = v[r][b][i];
+          const float x01 = __shfl_xor(x00, 1), x10 = __shfl_xor(x00, 4), x11 = __shfl_xor(x00, 5);
+          u[r][b][i] = vol_pool4(x00, x01, x10, x11);   // valid on lanes whose col has even row and col
+        }
+    const bool l1lane = (fr & 5) == 0;
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (l1lane)   // level-1 pixel (2 (b>>1) + (fr>>3), 2 (b&1) + ((fr>>1)&1)) of the 4x4 level-1 patch
+            s1[(16 * r + 4 * fq + i) * 16 + (2 * (b >> 1) + (fr >> 3)) * 4 + 2 * (b & 1) + ((fr >> 1) & 1)] =
+                (_Float16)u[r][b][i];
+    // level 2: 2x2 of the level-1 values at cols 0, 2, 8, 10 of each N-block; level 3: the 4 N-blocks
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float w2[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const float y00 = u[r][b][i];
+          w2[b] = vol_pool4(y00, __shfl_xor(y00, 2), __shfl_xor(y00, 8), __shfl_xor(y00, 10));
+        }
+        if (fr == 0) {
+          const int q = 16 * r + 4 * fq + i;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) s2[q * 4 + b] = (_Float16)w2[b];   // (b>>1, b&1) of the 2x2 level-2 patch
+          s3[q] = (_Float16)vol_pool4(w2[0], w2[1], w2[2], w2[3]);
+        }
+      }
+    // stores (the staging area is this wave's own: a wave barrier suffices)
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const long E0 = (long)e * HW;
+    // level 0: 32 q x 128 B, 8 lanes per query pixel
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = 8 * k + (lane >> 3), seg = lane & 7;   // seg = tile row
+      const int qg = q0 + q;
+      const uint4 val = *reinterpret_cast<const uint4*>(s0 + q * 64 + seg * 8);
+      if (qg < HW) {
+        long off;
+        if (a.tiled) off = ((E0 + qg) * TR[0] * (Wl[0] / 8) + py * (Wl[0] / 8) + px) * 64 + seg * 8;
+        else off = (E0 + qg) * (long)HW + (long)(ty0 + seg) * W + tx0;
+        *reinterpret_cast<uint4*>(a.lvl[0] + off) = val;
+      }
+    }
+    // level 1: 32 q x 4 rows x 8 B (the patch's 4x4 level-1 block)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = 16 * k + (lane >> 2), rr = lane & 3;
+      const int qg = q0 + q;
+      const uint2 val = *reinterpret_cast<const uint2*>(s1 + q * 16 + rr * 4);
+      const int y = ty0 / 2 + rr, x = tx0 / 2;
+      if (qg < HW) {
+        long off;
+        if (a.tiled) off = ((E0 + qg) * TR[1] * (Wl[1] / 8) + (y >> 3) * (Wl[1] / 8) + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7);
+        else off = (E0 + qg) * (long)(Hl[1] * Wl[1]) + (long)y * Wl[1] + x;
+        *reinterpret_cast<uint2*>(a.lvl[1] + off) = val;
+      }
+    }
+    // level 2: 32 q x 2 rows x 4 B; level 3: 32 q x 2 B
+    {
+      const int q = lane >> 1, rr = lane & 1;
+      const int qg = q0 + q;
+      const unsigned val = *reinterpret_cast<const unsigned*>(s2 + q * 4 + rr * 2);
+      const int y = ty0 / 4 + rr, x = tx0 / 4;
+      if (qg < HW) {
+        long off;
+        if (a.tiled) off = ((E0 + qg) * TR[2] * (Wl[2] / 8) + (y >> 3) * (Wl[2] / 8) + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7);
+        else off = (E0 + qg) * (long)(Hl[2] * Wl[2]) + (long)y * Wl[2] + x;
+        *reinterpret_cast<unsigned*>(a.lvl[2] + off) = val;
+      }
+    }
+    if (lane < 32) {
+      const int qg = q0 + lane;
+      const int y = ty0 / 8, x = tx0 / 8;
+      if (qg < HW) {
+        long off;
+        if (a.tiled) off = ((E0 + qg) * TR[3] * (Wl[3] / 8) + (y >> 3) * (Wl[3] / 8) + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7);
+        else off = (E0 + qg) * (long)(Hl[3] * Wl[3]) + (long)y * Wl[3] + x;
+        a.lvl[3][off] = *reinterpret_cast<const __half*>(s3 + lane);
+      }
+    }
+    buf ^= 1;
+    p = nxt;
+  }
+  // tiled layout: rows of the last tile row past H_l are zero (levels whose height is not a multiple of 8)
+  if (a.tiled) {
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+      const int pad = TR[l] * 8 - Hl[l];
+      if (pad == 0) continue;
+      const int tcols = Wl[l] / 8;
+      // per query pixel: tcols tiles x pad rows x 16 B
+      const int pieces = tcols * pad;
+      for (int idx = lane; idx < 32 * pieces; idx += 64) {
+        const int q = idx / pieces, k = idx - q * pieces;
+        const int tc = k / pad, rr = Hl[l] - (TR[l] - 1) * 8 + (k - tc * pad);
+        const int qg = q0 + q;
+        if (qg < HW) {
+          const long off = (((long)e * HW + qg) * TR[l] * tcols + (TR[l] - 1) * tcols + tc) * 64 + rr * 8;
+          *reinterpret_cast<uint4*>(a.lvl[l] + off) = uint4{0u, 0u, 0u, 0u};
+        }
+      }
+    }
+  }
+}
+
+}  // namespace droid
+
+using namespace droid;
+
+extern "C" {
+
+// CorrBlock pyramid (modules/corr.py:24-38,63-71) of E edges from the frames'
+// NHWC feature maps divided by 4 (fmaps (NF,H,W,128) fp16, the AltCorrBlock
+// level 0): level l of edge e = avgpool^l(<fmaps[f1[e]], fmaps[f2[e]]>) as
+// fp16, written to levels[l]: (E,H,W,ceil(H_l/8),W_l/8,8,8) when tiled (the
+// layout of droid_corr_lookup_ce0_tiled) or (E,H,W,H_l,W_l).  H, W multiples of 8.
+int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, int E, int NF, int H, int W,
+                              void* const* levels, int tiled, hipStream_t stream) {
+  if (!fmaps || !f1 || !f2 || !levels || E < 0 || NF <= 0 || H <= 0 || W <= 0)
+    return fail(kInvalidArgument, "corr_volume_pyramid: bad arguments");
+  if (H % 8 || W % 8) return fail(kUnsupported, "corr_volume_pyramid: H and W must be multiples of 8");
+  if (tiled && (W >> 3) % 8) return fail(kUnsupported, "corr_volume_pyramid: tiled levels need W / 8 % 8 == 0");
+  if ((long)H * W * 256 > 0x7fffffffL) return fail(kUnsupported, "corr_volume_pyramid: frames too large");
+  VolArgs a{};
+  a.f = (const __half*)fmaps;
+  a.f1 = f1;
+  a.f2 = f2;
+  for (int l = 0; l < 4; ++l) {
+    if (!levels[l]) return fail(kInvalidArgument, "corr_volume_pyramid: null level");
+    a.lvl[l] = (__half*)levels[l];
+  }
+  a.H = H;
+  a.W = W;
+  a.tiled = tiled ? 1 : 0;
+  a.qblocks = ceil_div(H * W, kVolQ);
+  const long grid = (long)E * a.qblocks;
+  if (grid == 0) return kOk;
+  if (grid > 0x7fffffffL) return fail(kUnsupported, "corr_volume_pyramid: too many edges");
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kVolLds));
+    attr = true;
+  }
+  corr_volume_pyramid_kernel<<<dim3((unsigned)grid), 512, kVolLds, stream>>>(a);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+}  // extern "C"

@@ -131,6 +131,38 @@ def corr_pyramid_lookup_nhwc(levels, coords, out_cstride=200, out=None):
     return out
 
 
+def corr_volume_pyramid(fmaps, f1, f2, tiled, num_levels=4):
+    """CorrBlock pyramid of E edges (include/droid_backends.h:
+    droid_corr_volume_pyramid): fmaps (NF,H,W,128) fp16 = frame features / 4,
+    NHWC; f1/f2 (E) int32 frame rows -> 4 levels, (E,H,W,H_l,W_l) or, tiled,
+    (E,H,W,ceil(H_l/8),W_l/8,8,8) fp16."""
+    _check_inputs(("fmaps", "f1", "f2"), (fmaps, f1, f2))
+    _need(fmaps, torch.float16, "fmaps")
+    _need(f1, torch.int32, "f1")
+    _need(f2, torch.int32, "f2")
+    if num_levels != 4 or fmaps.dim() != 4 or fmaps.shape[-1] != 128:
+        raise RuntimeError("corr_volume_pyramid: fmaps must be (NF,H,W,128) and 4 levels")
+    NF, H, W, _ = fmaps.shape
+    E = f1.numel()
+    if f2.numel() != E:
+        raise RuntimeError("corr_volume_pyramid: f1 and f2 must have one entry per edge")
+    levels = []
+    for l in range(4):
+        h, w = H >> l, W >> l
+        shape = (E, H, W, (h + 7) // 8, w // 8, 8, 8) if tiled else (E, H, W, h, w)
+        levels.append(torch.empty(shape, dtype=torch.float16, device=fmaps.device))
+    ptrs = (ctypes.c_void_p * 4)(*[lv.data_ptr() for lv in levels])
+    with torch.cuda.device(fmaps.device):
+        check(lib.droid_corr_volume_pyramid(_ptr(fmaps), _ptr(f1), _ptr(f2), E, NF, H, W, ptrs, int(bool(tiled)),
+                                            _stream(fmaps)), "corr_volume_pyramid")
+    return levels
+
+
+def corr_volume_pyramid_supported(H, W, tiled):
+    """Shapes droid_corr_volume_pyramid accepts."""
+    return H % 8 == 0 and W % 8 == 0 and (not tiled or W % 64 == 0)
+
+
 def corr_lookup_ce0_supported(levels, H, W):
     """Shapes droid_corr_lookup_ce0 accepts: 4 levels, H*W % 128 == 0."""
     return len(levels) == 4 and (H * W) % 128 == 0

@@ -1,11 +1,14 @@
 """Correlation blocks (mirror of modules/corr.py) on the HIP kernels.
 
-CorrBlock keeps the reference's volume pyramid layout (E, H, W, H/2^i, W/2^i)
-built by a batched GEMM (hipBLASLt) + avg-pool, exactly as corr.py:24-38,
-63-71; its lookup runs all 4 levels in ONE kernel launch and writes the
+CorrBlock builds the reference's volume pyramid (corr.py:24-38, 63-71) with ONE
+hand-written kernel (droid_corr_volume_pyramid: MFMA GEMM of the frames' NHWC
+features, the three 2x2 pooling levels formed in registers, every level
+written once, optionally straight into the 8x8-tiled layout of the fused
+lookup); its lookup runs all 4 levels in ONE kernel launch and writes the
 concatenated (B, N, 196, H, W) tensor directly (corr.py:40-50 does 4 launches
-+ cat).  Under autograd it falls back to the per-level CorrSampler so the
-backward kernel is used (training path).
++ cat).  Under autograd the volume comes from torch's GEMM + avg_pool2d and
+the lookup uses the per-level CorrSampler so the backward kernel runs
+(training path).
 """
 import torch
 import torch.nn.functional as F
@@ -75,10 +78,26 @@ class CorrBlock:
     whose lookup windows touch fewer DRAM lines; the reference layout is
     rebuilt on demand for the other lookups (reference_pyramid)."""
 
-    def __init__(self, fmap1, fmap2, num_levels=4, radius=3, tiled=False):
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=3, tiled=False, _levels=None):
         self.num_levels = num_levels
         self.radius = radius
         self.corr_pyramid = []
+        if _levels is not None:                      # from_frames
+            self.corr_pyramid, self.level_shapes, self.tiled = _levels
+            return
+        batch, num, dim, ht, wd = fmap1.shape
+        self.level_shapes = [(ht // 2 ** i, wd // 2 ** i) for i in range(num_levels)]
+        t = bool(tiled) and all(w % 8 == 0 for _, w in self.level_shapes)
+        if (num_levels == 4 and dim == 128 and fmap1.is_cuda and not torch.is_grad_enabled()
+                and droid_backends.corr_volume_pyramid_supported(ht, wd, t)):
+            # the fused kernel: the edges' feature maps as 2E frames (NHWC / 4)
+            E = batch * num
+            f = torch.cat([fmap1.reshape(E, dim, ht, wd), fmap2.reshape(E, dim, ht, wd)], 0)
+            f = (f.half() / 4.0).permute(0, 2, 3, 1).contiguous()
+            idx = torch.arange(E, dtype=torch.int32, device=f.device)
+            self.corr_pyramid = droid_backends.corr_volume_pyramid(f, idx, idx + E, t)
+            self.tiled = t
+            return
         vol = CorrBlock.corr(fmap1, fmap2)
         batch, num, h1, w1, h2, w2 = vol.shape
         self.level_shapes = [(h2 // 2 ** i, w2 // 2 ** i) for i in range(num_levels)]
@@ -90,6 +109,17 @@ class CorrBlock:
                 vol = _avg_pool2(vol)
             self.corr_pyramid.append(tile8(lv) if self.tiled else lv)
             del lv
+
+    @classmethod
+    def from_frames(cls, fmaps, f1, f2, tiled=False, num_levels=4, radius=3):
+        """The pyramid of the edges (f1[e] -> f2[e]) straight from the frames'
+        features: fmaps (NF,H,W,128) fp16 = fmap / 4 in NHWC (AltCorrBlock level
+        0), f1 / f2 (E) int32 rows - no per-edge feature copies."""
+        NF, H, W, _ = fmaps.shape
+        shapes = [(H // 2 ** i, W // 2 ** i) for i in range(num_levels)]
+        t = bool(tiled) and all(w % 8 == 0 for _, w in shapes)
+        levels = droid_backends.corr_volume_pyramid(fmaps, f1, f2, t)
+        return cls(None, None, num_levels, radius, _levels=(levels, shapes, t))
 
     def reference_pyramid(self):
         """the levels in the reference layout (E,H,W,H2,W2)."""

@@ -142,11 +142,21 @@ class FactorGraph:
         djj = torch.as_tensor(jj, device=self.device)
         net = self._edge_state(self.video.nets[dii].to(self.device))
         if self.corr_impl == "volume":
-            c = torch.as_tensor((ii == jj).astype(np.int64), device=self.device)
-            fmap1 = self.video.fmaps[dii, 0].to(self.device).unsqueeze(0)
-            fmap2 = self.video.fmaps[djj, c].to(self.device).unsqueeze(0)
-            # the fused operator reads the volume through the 8x8-tiled layout
-            corr = CorrBlock(fmap1, fmap2, tiled=self.fused and self.tiled_volume)
+            # the new edges' pyramids from the frames' NHWC features / 4 (one kernel;
+            # the stereo edge (i, i) correlates against the right image,
+            # factor_graph.py:112-114); the fused operator reads the 8x8-tiled layout
+            num, rig, ch, ht, wd = self.video.fmaps.shape
+            n = int(max(ii.max(), jj.max())) + 1
+            frames = (self.video.fmaps[:n].reshape(n * rig, ch, ht, wd).half() / 4.0).permute(0, 2, 3, 1).contiguous()
+            f1 = torch.as_tensor((rig * ii).astype(np.int32), device=self.device)
+            f2 = torch.as_tensor((rig * jj + ((ii == jj) & (rig > 1))).astype(np.int32), device=self.device)
+            tiled = self.fused and self.tiled_volume
+            if droid_backends.corr_volume_pyramid_supported(ht, wd, tiled and wd // 8 % 8 == 0):
+                corr = CorrBlock.from_frames(frames, f1, f2, tiled=tiled)
+            else:
+                c = torch.as_tensor((ii == jj).astype(np.int64), device=self.device)
+                corr = CorrBlock(self.video.fmaps[dii, 0].unsqueeze(0), self.video.fmaps[djj, c].unsqueeze(0),
+                                 tiled=tiled)
             self.corr = corr if self.corr is None else self.corr.cat(corr)
         if self.corr_impl == "pyramid":
             self._alt_pyr = None   # frames may have changed: rebuilt at the next update

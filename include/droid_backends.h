@@ -78,6 +78,16 @@ int droid_conv_set_profile(void* buf);
  * (scripts/alt_timeline.py). */
 int droid_alt_set_profile(void* buf);
 
+/* CorrBlock pyramid construction (modules/corr.py:24-38,63-71) for E edges in
+ * one pass: fmaps (NF,H,W,128) fp16 = frame features / 4 in NHWC (the
+ * AltCorrBlock level 0), f1/f2 (E) int32 query / target frames; level l =
+ * avgpool^l(<fmaps[f1[e]], fmaps[f2[e]]>) in fp16 (fp32-accumulated GEMM,
+ * float-sum/4 pooling as F.avg_pool2d) written to levels[l] as
+ * (E,H,W,ceil(H_l/8),W_l/8,8,8) 8x8 tiles when tiled (W % 64 == 0) or
+ * (E,H,W,H_l,W_l).  H, W multiples of 8. */
+int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, int E, int NF, int H, int W,
+                              void* const* levels, int tiled, hipStream_t stream);
+
 /* CorrBlock lookup fused with the update operator's corr_encoder[0]
  * (modules/corr.py:40-50 + droid_net.py:84-86): out (E,H,W,128) fp16 =
  * relu(conv1x1(lookup(coords), w) + bias), the 196-channel lookup never

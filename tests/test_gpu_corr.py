@@ -117,3 +117,48 @@ def test_altcorr_backward_vs_oracle():
     np.testing.assert_allclose(host(g1), r1, atol=1e-4, rtol=1e-4)
     np.testing.assert_allclose(host(g2), r2, atol=1e-4, rtol=1e-4)
     assert np.all(host(gc) == 0)
+
+
+# --- CorrBlock pyramid construction (droid_corr_volume_pyramid) -------------
+def test_volume_pyramid_matches_reference_golden(golden_dir):
+    """The hand-written pyramid kernel vs the reference's own CorrBlock
+    (tests/golden/corr_pyramid.npz, fp32 on the CPU): fp16 inputs and outputs,
+    so the tolerance is fp16 rounding of values of magnitude ~|level|."""
+    import os
+    from droid_mi355x.corr import CorrBlock
+    g = np.load(os.path.join(golden_dir, "corr_pyramid.npz"))
+    with torch.no_grad():
+        cb = CorrBlock(dev(g["fmap1"]).half(), dev(g["fmap2"]).half())
+    for i in range(4):
+        ref = g["level%d" % i]
+        got = host(cb.corr_pyramid[i].float()).reshape(ref.shape)
+        np.testing.assert_allclose(got, ref, atol=4e-3 * max(1.0, np.abs(ref).max()), rtol=2e-3)
+
+
+def test_volume_pyramid_levels_are_avg_pools_and_tiles():
+    """Level l+1 is exactly F.avg_pool2d(2) of level l's fp16 values (the
+    reference's pooling arithmetic), level 0 is the fp32-accumulated GEMM
+    rounded to fp16, and the 8x8-tiled output is tile8 of the plain one, bit
+    for bit; stereo-style indices (f2 = another rig slot) included."""
+    import torch.nn.functional as F
+    import droid_backends
+    from droid_mi355x.corr import tile8
+    rng = np.random.default_rng(5)
+    NF, H, W = 5, 48, 64
+    f = torch.from_numpy((rng.normal(size=(NF, H, W, 128)) / 4).astype(np.float16)).cuda()
+    f1 = torch.tensor([0, 1, 2, 3, 4, 2], dtype=torch.int32, device="cuda")
+    f2 = torch.tensor([1, 0, 3, 3, 2, 4], dtype=torch.int32, device="cuda")
+    plain = droid_backends.corr_volume_pyramid(f, f1, f2, tiled=False)
+    tiled = droid_backends.corr_volume_pyramid(f, f1, f2, tiled=True)
+    E = f1.numel()
+    a = f[f1.long()].reshape(E, H * W, 128).float()
+    b = f[f2.long()].reshape(E, H * W, 128).float()
+    v0 = torch.bmm(a, b.transpose(1, 2)).reshape(E, H, W, H, W)
+    np.testing.assert_allclose(host(plain[0].float()), host(v0), atol=1e-3, rtol=1e-3)
+    for i in range(3):
+        lv = plain[i]
+        h2, w2 = lv.shape[3:]
+        pooled = F.avg_pool2d(lv.reshape(-1, 1, h2, w2), 2, stride=2).reshape(plain[i + 1].shape)
+        assert torch.equal(pooled, plain[i + 1]), "level %d pooling" % (i + 1)
+    for i in range(4):
+        assert torch.equal(tile8(plain[i]), tiled[i]), "level %d tiling" % i
