@@ -239,10 +239,12 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
     if (wave_u == 0) {
       const int e = T.e, ty0 = T.ty0, tx0 = T.tx0;
       const rsrc_t rs = make_rsrc(a.coords + (long)e * HW * 2, (unsigned)(HW * 8));
-      // slot pixel p <- image pixel (ty0 + alt_py(p), tx0 + alt_px(p)); pairs (p, p+1) share a row piece
+      // slot pixel p <- image pixel (ty0 + alt_py(p), tx0 + alt_px(p)); pairs (p, p+1) share a row piece.
+      // Only lanes 0..31 may run the DMA: every active lane writes its 16 B at LDS base + 16 lane,
+      // and lanes 32..63 would land on the next 512 B (the other slot / the level boxes).
       const int p = 2 * (lane & 31);
-      const unsigned off = lane < 32 ? (unsigned)((((ty0 + alt_py(p)) * W + tx0 + alt_px(p)) * 2) * 4) : kOob;
-      dma16(rs, lds_a + kAltCoord + slot * 512, off);
+      if (lane < 32)
+        dma16(rs, lds_a + kAltCoord + slot * 512, (unsigned)((((ty0 + alt_py(p)) * W + tx0 + alt_px(p)) * 2) * 4));
     }
   };
   // a tile's 64 query feature rows (16 KB) -> box 1 + kAltF1 by LDS-DMA, once per

@@ -516,8 +516,12 @@ struct CorrCe0Args {
 
 constexpr int kCeTP = 128, kCeKS = 232, kCeOS = 136;
 constexpr unsigned kCeOob = 0x80000000u;  // buffer offset past any descriptor: the load returns 0
-// + coordinate staging Cs [2 slots][2 pixel halves][64 px] float2 (LDS-DMA)
-constexpr int kCeLds = (2 * 128 * kCeKS + kCeTP * kCeOS) * 2 + 2 * 2 * 64 * 8;
+// + coordinate staging Cs [2 slots][8 waves][64 px] float2 (LDS-DMA), private
+// per wave: the four waves of a pixel half would otherwise share a slot, and a
+// wave ahead could overwrite it (tile t + 4g) before a wave behind has read it
+// (tile t + 2g) - nothing orders different waves' reads and DMAs in between
+constexpr int kCeLds = (2 * 128 * kCeKS + kCeTP * kCeOS) * 2 + 2 * 8 * 64 * 8;
+static_assert(kCeLds <= 160 * 1024, "corr_ce0 LDS budget");
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
@@ -543,7 +547,7 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
   _Float16* Ws = smem_ce;                 // [128 co][kCeKS]
   _Float16* As = Ws + 128 * kCeKS;        // [128 px][kCeKS] lookup tile (cols 196.. zero)
   _Float16* Os = As + kCeTP * kCeKS;      // [128 px][kCeOS] output staging
-  float2* Cs = reinterpret_cast<float2*>(Os + kCeTP * kCeOS);  // [2 slots][2 halves][64 px]
+  float2* Cs = reinterpret_cast<float2*>(Os + kCeTP * kCeOS);  // [2 slots][8 waves][64 px]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // level is wave-uniform: keep it (and everything derived from it) in SGPRs
   const int lvl = __builtin_amdgcn_readfirstlane(wave & 3), px = (wave >> 2) * 64 + lane;
@@ -581,19 +585,19 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
       x = c.x; y = c.y;
     }
   };
-  // Coordinates of the tile a slot issues next are staged in LDS by this wave's
-  // own LDS-DMA (its 64 pixels, 2 x 4 B per lane), issued right BEFORE the slot's
+  // Coordinates of the tile a slot issues next are staged in this wave's own LDS
+  // region by its own LDS-DMA (its 64 pixels, 2 x 4 B per lane), issued right BEFORE the slot's
   // window rows: when the wave has waited for those rows (the bilinear step),
   // the coordinates have landed too (vmcnt retires in order) and no VGPR holds a
   // load across the loop - a loop-carried loaded value costs a vmcnt wait on its
   // copy at the back edge, which would drain the other slot's rows.
   const int half = wave >> 2;
-  const unsigned cs_lds = lds_addr(Cs) + (unsigned)(half * 512);
+  const unsigned cs_lds = lds_addr(Cs) + (unsigned)(wave * 512);
   auto stage_coords = [&](const int sl, long t) __attribute__((always_inline)) {
     if (t >= a.ntiles) return;
     const long p0 = (t / tpe) * (long)HW + (t % tpe) * kCeTP + half * 64;
     const rsrc_t rs = make_rsrc(a.coords + p0 * 2, 512);
-    const unsigned dst = cs_lds + (unsigned)(sl * 1024);
+    const unsigned dst = cs_lds + (unsigned)(sl * 4096);
     ce_dma4(rs, dst, (unsigned)lane * 4u);
     ce_dma4(rs, dst + 256, 256u + (unsigned)lane * 4u);
   };
@@ -727,7 +731,7 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
     }
     // (2) the tile two steps ahead goes into this slot while this one is multiplied
     // and stored; its coordinates were staged before the rows just consumed.
-    const float2 c2 = Cs[sl * 128 + half * 64 + lane];  // staged with the rows just consumed
+    const float2 c2 = Cs[sl * 512 + wave * 64 + lane];  // staged with the rows just consumed
     stage_coords(sl, t + 4L * gridDim.x);
     issue(sl, t + 2L * gridDim.x, c2.x, c2.y);
     __syncthreads();

@@ -320,19 +320,24 @@ def test_flow_encoder0(E, H, W):
     np.testing.assert_allclose(host(out.float()), host(ref), atol=2e-3 * max(1.0, float(ref.abs().max())), rtol=2e-3)
 
 
-@pytest.mark.parametrize("noise", [1.5, 40.0])   # coherent windows / incoherent (quadrant and pixel fallbacks)
-def test_corr_alt_ce0_matches_volume_path(noise):
+@pytest.mark.parametrize("noise,H,W,E", [(1.5, 16, 24, 6), (40.0, 16, 24, 6), (1.5, 48, 64, 300), (8.0, 48, 64, 300)])
+def test_corr_alt_ce0_matches_volume_path(noise, H, W, E):
     """On-demand correlation (feature pyramid, MFMA) + corr_encoder[0] == the
     volume lookup + corr_encoder[0] up to fp16 rounding of the pooled levels
-    (modules/corr.py: CorrBlock vs AltCorrBlock semantics)."""
+    (modules/corr.py: CorrBlock vs AltCorrBlock semantics).  Coherent windows /
+    incoherent (half, quadrant and pixel fallbacks); at 48x64 with 300 edges
+    every workgroup walks many tiles (the cross-tile pipeline)."""
     import droid_backends
     from droid_mi355x.corr import AltCorrBlock, CorrBlock
     rng = np.random.default_rng(31)
-    NF, H, W = 4, 16, 24
+    NF = 4 if E <= 6 else 12
     fm = torch.from_numpy(rng.normal(size=(NF, 128, H, W)).astype(np.float16)).to(DEV)
-    ii = np.array([0, 1, 2, 3, 1, 2], np.int64)
-    jj = np.array([1, 0, 3, 1, 1, 0], np.int64)
-    E = len(ii)
+    if E <= 6:
+        ii = np.array([0, 1, 2, 3, 1, 2], np.int64)
+        jj = np.array([1, 0, 3, 1, 1, 0], np.int64)
+    else:
+        ii = rng.integers(0, NF, E).astype(np.int64)
+        jj = rng.integers(0, NF, E).astype(np.int64)
     cb = CorrBlock(fm[ii][None], fm[jj][None])
     pyr = [lv.view((-1,) + tuple(lv.shape[2:])) for lv in AltCorrBlock(fm[None]).pyramid]
     grid = np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None].astype(np.float32)
