@@ -81,6 +81,8 @@ def build_state(args, rank, world, device):
         ii, jj = synthetic.c4_edges(args.frames, rng=np.random.default_rng(1004))
     elif args.config == "C2":   # frontend window: 16-KF buffer, 96 edges
         ii, jj = synthetic.c2_edges()
+    elif args.config == "C5":   # 2048 KF, 8 laps of a circuit, temporal + revisit loops (~16k edges)
+        ii, jj = synthetic.c5_edges(args.frames, rng=np.random.default_rng(1005))
     else:
         ii, jj = synthetic.c3_edges(args.frames, args.edges, rng=np.random.default_rng(1003))
     comm = None
@@ -92,7 +94,7 @@ def build_state(args, rank, world, device):
     else:
         ii_l, jj_l = ii, jj
     n = args.frames
-    gt = synthetic.trajectory(n, rng)
+    gt = synthetic.trajectory_laps(n, 256, rng) if args.config == "C5" else synthetic.trajectory(n, rng)
     poses, disps = synthetic.perturb(gt, synthetic.smooth_disps(n, H, W, rng), rng)
     video = DepthVideo(image_size=(args.ht, args.wd), buffer=n, stereo=stereo, device=device)
     video.poses[:n] = torch.from_numpy(poses.astype(np.float32)).to(device)
@@ -289,10 +291,12 @@ def load_traffic(name, e_local, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=["C2", "C3", "C4"], default="C3",
+    ap.add_argument("--config", choices=["C2", "C3", "C4", "C5"], default="C3",
                     help="C3 (default, the metric's config): 256 KF / 2048 edges mono; "
                          "C4: stereo, 128 KF, (i, i) stereo edges + temporal + loops (~1k edges); "
-                         "C2: frontend window, 16-KF buffer, 96 edges, update(use_inactive=True)")
+                         "C2: frontend window, 16-KF buffer, 96 edges, update(use_inactive=True); "
+                         "C5: 2048 KF / ~16k edges (the edge-sharded global BA), on-demand (pyramid) "
+                         "correlation - its volumes would need ~300 GB")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=256)
@@ -314,6 +318,10 @@ def main():
         args.frames = 128
     if args.config == "C2":
         args.frames = 16
+    if args.config == "C5":
+        if args.frames == 256:
+            args.frames = 2048
+        args.corr = "pyramid"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -355,7 +363,7 @@ def main():
             step_fn()
         torch.cuda.synchronize(device)
         if rank == 0:
-            log("warmup %.1fs" % (time.time() - t_w))
+            log("warmup %.1fs, peak HBM %.1f GB" % (time.time() - t_w, torch.cuda.max_memory_allocated(device) / 1e9))
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(device)
@@ -418,7 +426,8 @@ def main():
             lookup_roof["traffic"] = None
         result = {
             "metric": ("factor_graph.update_lowmem() steps/sec at 256 KF x 2k edges, 384x512" if args.lowmem else "factor_graph.update() iters/sec at 256 KF x 2k edges, 384x512" if args.config == "C3"
-                       else "factor_graph.update() iters/sec, C4 stereo %d KF x %d edges, 384x512" % (args.frames, len(ii))
+                       else "factor_graph.update() iters/sec, C5 %d KF x %d edges, 384x512" % (args.frames, len(ii))
+                       if args.config == "C5" else "factor_graph.update() iters/sec, C4 stereo %d KF x %d edges, 384x512" % (args.frames, len(ii))
                        if args.config == "C4" else
                        "factor_graph.update(use_inactive=True) iters/sec, C2 frontend 16-KF buffer x %d edges, 384x512"
                        % len(ii)),
@@ -433,7 +442,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f16 (corr volume, update-operator convs) / f32 (BA linearisation, Schur) / f64 (reduced system)",
             "data": "synthetic (SURVEY.md §8d %s graph, random-init UpdateModule)" % args.config,
-            "config": {"workload": {"C4": "C4 stereo graph", "C3": "C3 global graph",
+            "config": {"workload": {"C4": "C4 stereo graph", "C3": "C3 global graph", "C5": "C5 2048-KF global graph",
                                     "C2": "C2 frontend window (use_inactive=True)"}[args.config]
                                    + (": update_lowmem(steps=1, itrs=2), on-demand corr" if args.lowmem else
                                       ": update(itrs=2), %s corr" % args.corr), "keyframes": args.frames,
