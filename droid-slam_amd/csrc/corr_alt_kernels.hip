@@ -75,25 +75,43 @@ struct AltArgs {
 #define ALT_STAMP(ph, v) do { } while (0)
 #endif
 #define ALT_NOW() ((long long)__builtin_amdgcn_s_memtime())
+// timing ablations (scripts only; results are wrong): bit 0 skips the box MFMA,
+// bit 1 the bilinear, bit 2 the encoder MFMA, bit 3 the next-box DMA, bit 4 the
+// output stores, bit 5 the next tile's boxes, bit 6 the frame-index loads, bit 7
+// the slow path, bit 8 the lookup tile's K-padding zeroes
+#ifndef DROID_ALT_ABL
+#define DROID_ALT_ABL 0
+#endif
 
-constexpr int kAltCap = 232;   // box taps per LDS buffer (a coherent tile's level-0 box is 15 x 15)
-constexpr int kAltCS = 244;    // C row stride (halves): >= 16 * ceil(kAltCap / 16), 8-B aligned rows
+// Box buffer 0 holds the boxes of levels 3 and 1, buffer 1 those of levels 2 and
+// 0, so buffer 1 is the larger: on the C3 trajectory the level-0 box of a tile
+// is 210 taps at the median and exceeds 288 for ~7 % of the tiles, the level-1
+// box exceeds 191 for ~1.5 %.
+constexpr int kAltCap0 = 191;  // box taps in buffer 0
+constexpr int kAltCap1 = 288;  // box taps in buffer 1
+constexpr int kAltCS = 292;    // C row stride (halves): >= 16 * ceil(kAltCap1 / 16), 8-B aligned rows
 constexpr int kAltAS = 72;     // per-level lookup tile row stride (halves): 49 used, 64 multiplied
 constexpr int kAltOS = 136;    // output staging row stride (halves)
 constexpr int kAltMaxGroups = 1 + 2 + 4 + 64;
 constexpr int kAltF1 = 20 * 1024;   // next tile's query features, inside box 1 past the output staging
+constexpr int kAltA1 = kAltF1 + 64 * 256;   // the lookup tile of the stages on box 1, past the features
 // LDS map (bytes)
-constexpr int kAltBox0 = 0;                                  // [kAltCap taps][256 B]
-constexpr int kAltBox1 = kAltBox0 + kAltCap * 256;           // the other stage's box (output staging aliases it)
-constexpr int kAltC = kAltBox1 + kAltCap * 256;              // [64 px][kAltCS] fp16
-constexpr int kAltA = kAltC + 64 * kAltCS * 2;               // [64 px][kAltAS] fp16 lookup of one level
-constexpr int kAltCoord = kAltA + 64 * kAltAS * 2;           // [2 tiles][64 px] float2 (by LDS-DMA)
+// The per-level lookup tile [64 px][kAltAS] fp16 lives in the stage's own box
+// buffer (dead once C is computed): at offset 0 of box 0, at kAltA1 of box 1.
+constexpr int kAltBox0 = 0;                                  // [kAltCap0 taps][256 B]
+constexpr int kAltBox1 = kAltBox0 + kAltCap0 * 256;          // [kAltCap1 taps][256 B] (+ output staging, F1)
+constexpr int kAltC = kAltBox1 + kAltCap1 * 256;             // [64 px][kAltCS] fp16
+constexpr int kAltCoord = kAltC + 64 * kAltCS * 2;           // [2 tiles][64 px] float2 (by LDS-DMA)
 constexpr int kAltLvl = kAltCoord + 2 * 64 * 8;              // [2 tiles][4 levels] box x0, y0, w, h (int)
 constexpr int kAltPix = kAltLvl + 2 * 4 * 4 * 4;             // slow path: per px group box x0, y0, w (int)
 constexpr int kAltGrp = kAltPix + 64 * 3 * 4;                // slow path: count + groups (x0, y0, w, h, mmask, pix)
 constexpr int kAltLds = kAltGrp + (kAltMaxGroups * 6 + 4) * 4;
 static_assert(kAltLds <= 160 * 1024, "corr_alt_ce0 LDS budget");
-static_assert(64 * kAltOS * 2 <= kAltF1 && kAltF1 + 64 * 256 <= kAltCap * 256, "output staging + F1 fit box 1");
+static_assert(64 * kAltOS * 2 <= kAltF1 && kAltA1 + 64 * kAltAS * 2 <= kAltCap1 * 256,
+              "output staging + F1 + lookup tile fit box 1");
+static_assert(64 * kAltAS * 2 <= kAltCap0 * 256 && kAltBox1 % 16 == 0 && kAltAS == 72, "lookup tile fits box 0, 16-B aligned rows");
+static_assert(kAltCS >= 16 * ((kAltCap1 + 15) / 16) && kAltCap0 <= kAltCap1, "C rows hold a box's taps");
+__host__ __device__ constexpr int alt_cap(int l) { return (l & 1) ? kAltCap0 : kAltCap1; }
 
 // tile pixel p = 16 q + r: quadrant q = (qy, qx) = (q >> 1, q & 1), r = (ry, rx)
 __device__ __forceinline__ int alt_py(int p) { return 4 * ((p >> 4) >> 1) + ((p & 15) >> 2); }
@@ -175,7 +193,7 @@ __device__ __forceinline__ void alt_box_mfma(const char* lds, int box, _Float16*
       const int p = q * 16 + fr;
       if (gpix < 0 || gpix == p) {
         half4_t h = {(_Float16)c[0], (_Float16)c[1], (_Float16)c[2], (_Float16)c[3]};
-        // taps past tn land in the row's slack (kAltCS >= 16 * ceil(cap / 16)) and are never read
+        // taps past tn land in the row's slack (kAltCS >= 16 * ceil(kAltCap1 / 16)) and are never read
         *reinterpret_cast<half4_t*>(Cs + p * kAltCS + b * 16 + 4 * fq) = h;
       }
     }
@@ -185,7 +203,6 @@ __device__ __forceinline__ void alt_box_mfma(const char* lds, int box, _Float16*
 __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   _Float16* Cs = reinterpret_cast<_Float16*>(lds + kAltC);
-  _Float16* As = reinterpret_cast<_Float16*>(lds + kAltA);
   int* pix = reinterpret_cast<int*>(lds + kAltPix);
   int* grp = reinterpret_cast<int*>(lds + kAltGrp);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -216,9 +233,6 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
       wl[l][s] = v;
     }
   const float bias = a.bias[wave * 16 + fr];
-  // lookup-tile columns 49..71 stay zero (the bilinear writes 0..48 only)
-  for (int idx = tid; idx < 64 * (kAltAS - 49); idx += 512)
-    As[(idx / (kAltAS - 49)) * kAltAS + 49 + idx % (kAltAS - 49)] = (_Float16)0.f;
 
   // tile geometry (32-bit: the launcher checks ntiles < 2^31).  Edge and frame
   // indices are wave-uniform scalar loads (lgkmcnt), so no vmcnt wait - which
@@ -230,8 +244,8 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
     const int tt = t - r.e * tpe;
     r.ty0 = (tt / tcols) * 8;
     r.tx0 = (tt - (tt / tcols) * tcols) * 8;
-    r.f1 = alt_sload(a.f1 + r.e);
-    r.f2 = alt_sload(a.f2 + r.e);
+    r.f1 = (DROID_ALT_ABL & 64) ? 0 : alt_sload(a.f1 + r.e);
+    r.f2 = (DROID_ALT_ABL & 64) ? 0 : alt_sload(a.f2 + r.e);
     return r;
   };
   // coordinates of a tile's 64 pixels -> LDS slot by LDS-DMA (lanes 0..31 of wave 0, 16 B = 2 px each)
@@ -271,7 +285,7 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
   };
   auto stage_fits = [&](int slot, int l) {
     const int* lv = reinterpret_cast<const int*>(lds + kAltLvl) + slot * 16 + 4 * l;
-    return lv[2] * lv[3] <= kAltCap;
+    return lv[2] * lv[3] <= alt_cap(l);
   };
   // Stages run the levels coarse to fine (3, 2, 1, 0): the largest box (level
   // 0) is prefetched during level 1's compute, and the next tile's first box
@@ -324,10 +338,12 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
         read_f1(af);
         __syncthreads();
       }
-      const bool fits = lvb[4 * l + 2] * lvb[4 * l + 3] <= kAltCap;
+      const bool fits = (DROID_ALT_ABL & 128) || lvb[4 * l + 2] * lvb[4 * l + 3] <= alt_cap(l);
+      _Float16* As = reinterpret_cast<_Float16*>(lds + ((st & 1) ? kAltBox1 + kAltA1 : kAltBox0));
       ALT_STAMP(7, (long long)(lvb[4 * l + 2] * lvb[4 * l + 3]) * 2 + (fits ? 0 : 1));
       // (b) the next stage's box -> the other buffer, in flight during this stage
-      if (st < 3) {
+      if (DROID_ALT_ABL & 8) {
+      } else if (st < 3) {
         if (stage_fits(slot, l - 1)) stage_dma(cur, slot, l - 1, (st + 1) & 1);
       } else if (more) {
         if (stage_fits(slot ^ 1, 3)) stage_dma(nxt, slot ^ 1, 3, 0);
@@ -335,7 +351,7 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
       if (st == 0 && more) coords_dma(nxt, slot ^ 1);
       // (c) C = F1 x box^T
       if (fits) {
-        alt_box_mfma(lds, box, Cs, af, lvb[4 * l + 2] * lvb[4 * l + 3], 15, -1, wave_u, fr, fq);
+        if (!(DROID_ALT_ABL & 1)) alt_box_mfma(lds, box, Cs, af, min(lvb[4 * l + 2] * lvb[4 * l + 3], alt_cap(l)), 15, -1, wave_u, fr, fq);
         if (tid < 64) { pix[3 * tid] = lvb[4 * l]; pix[3 * tid + 1] = lvb[4 * l + 1]; pix[3 * tid + 2] = lvb[4 * l + 2]; }
       } else {
         // slow path: groups = per quadrant its box if it fits, else its 16 pixels' own windows
@@ -356,7 +372,7 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
           const int qn = alt_clip(qx0, qx1, qy0, qy1, Wl, Hl);
           int px0 = ox, px1 = ox + 7, py0 = oy, py1 = oy + 7;
           const int pn = alt_clip(px0, px1, py0, py1, Wl, Hl);
-          const bool hfit = hn <= kAltCap, qfit = qn <= kAltCap;
+          const bool hfit = hn <= alt_cap(l), qfit = qn <= alt_cap(l);
           pix[3 * lane] = hfit ? hx0 : qfit ? qx0 : px0;
           pix[3 * lane + 1] = hfit ? hy0 : qfit ? qy0 : py0;
           pix[3 * lane + 2] = hfit ? hx1 - hx0 + 1 : qfit ? qx1 - qx0 + 1 : px1 - px0 + 1;
@@ -406,7 +422,7 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
       // The reference rounds every product and sum of halves through float
       // (at::Half); float carries >= 2*11+2 bits, so that equals the native
       // half op (corr_kernels.hip): _Float16 arithmetic, no contraction.
-      if (tid < 64 * 7) {
+      if (tid < 64 * 7 && !(DROID_ALT_ABL & 2)) {
         const int p = tid / 7, ac = tid - p * 7;
         const float scl = 1.0f / (float)(1 << l);
         const float x0 = cxy[2 * p] * scl, y0 = cxy[2 * p + 1] * scl;
@@ -421,29 +437,52 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
         const int gx0 = pix[3 * p], gy0 = pix[3 * p + 1], gbw = pix[3 * p + 2];
         const int xa = xi0 - 3 + ac;
         const bool va = xa >= 0 && xa < Wl, vb = xa + 1 >= 0 && xa + 1 < Wl;
-        const _Float16* crow = Cs + p * kAltCS + (xa - gx0);   // + (y - gy0) * gbw per row
+        const _Float16* crow = Cs + p * kAltCS;
         const _Float16 z = (_Float16)0.f;
-        _Float16 pa = z, pb = z;
-        _Float16* arow = As + p * kAltAS + ac * 7;
+        // all 16 taps are read unconditionally (an invalid tap reads element 0 and
+        // is replaced by zero) so that the reads issue back to back under one wait
+        // instead of one LDS round trip per window row
+        _Float16 ca[8], cb[8];
+        int mk[8];
 #pragma unroll
         for (int j = 0; j <= 7; ++j) {
           const int y = yi0 - 3 + j;
           const bool vy = y >= 0 && y < Hl;
-          const _Float16* cr = crow + (y - gy0) * gbw;
-          const _Float16 ca = (vy && va) ? cr[0] : z, cb = (vy && vb) ? cr[1] : z;
-          if (j > 0) {
-            _Float16 s = z + pa * w00;
-            s = s + ca * w01;
-            s = s + pb * w10;
-            s = s + cb * w11;
-            arow[j - 1] = s;
-          }
-          pa = ca;
-          pb = cb;
+          const int o = (xa - gx0) + (y - gy0) * gbw;
+          mk[j] = (vy && va) | ((vy && vb) << 1);
+          ca[j] = crow[(mk[j] & 1) ? o : 0];
+          cb[j] = crow[(mk[j] & 2) ? o + 1 : 0];
+        }
+        // (the scheduler would otherwise interleave a wait after every pair of reads)
+        asm volatile("" : "+v"(ca[0]), "+v"(ca[1]), "+v"(ca[2]), "+v"(ca[3]), "+v"(ca[4]), "+v"(ca[5]),
+                     "+v"(ca[6]), "+v"(ca[7]), "+v"(cb[0]), "+v"(cb[1]), "+v"(cb[2]), "+v"(cb[3]), "+v"(cb[4]),
+                     "+v"(cb[5]), "+v"(cb[6]), "+v"(cb[7]));
+#pragma unroll
+        for (int j = 0; j <= 7; ++j) {
+          ca[j] = (mk[j] & 1) ? ca[j] : z;
+          cb[j] = (mk[j] & 2) ? cb[j] : z;
+        }
+        _Float16* arow = As + p * kAltAS + ac * 7;
+#pragma unroll
+        for (int j = 1; j <= 7; ++j) {
+          _Float16 s = z + ca[j - 1] * w00;
+          s = s + ca[j] * w01;
+          s = s + cb[j - 1] * w10;
+          s = s + cb[j] * w11;
+          arow[j - 1] = s;
         }
       }
+      if (wave_u == 7 && !(DROID_ALT_ABL & 256)) {
+        // the idle wave zeroes the lookup tile's K padding (columns 49..63): the
+        // tile shares its buffer with box data.  Row = lane; 2 + 4 + 8 + 16 B.
+        char* row = reinterpret_cast<char*>(As + lane * kAltAS);
+        *reinterpret_cast<_Float16*>(row + 98) = (_Float16)0.f;
+        *reinterpret_cast<unsigned*>(row + 100) = 0u;
+        *reinterpret_cast<uint2*>(row + 104) = make_uint2(0u, 0u);
+        *reinterpret_cast<uint4*>(row + 112) = make_uint4(0u, 0u, 0u, 0u);
+      }
       ALT_STAMP(4, ALT_NOW());
-      if ((st == 1 || st == 2) && more && wave_u == 7) {
+      if ((st == 1 || st == 2) && more && wave_u == 7 && !(DROID_ALT_ABL & 32)) {
         // the next tile's level boxes, on the wave the bilinear leaves idle (its
         // coordinates, DMA'd during the first stage, landed at stage 1's wait):
         // levels 3, 2 now (level 3 is prefetched at stage 3), levels 1, 0 next stage
@@ -455,7 +494,7 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
       ALT_STAMP(5, ALT_NOW());
       // (e) this level's slice of corr_encoder[0]: 64 px x 16 co per wave, K = 64
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < 2 * !(DROID_ALT_ABL & 4); ++s) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const half8 x = *reinterpret_cast<const half8*>(&As[(q * 16 + fr) * kAltAS + s * 32 + fq * 8]);
@@ -473,7 +512,7 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
           acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
         __syncthreads();
-        for (int idx = tid; idx < 64 * 16; idx += 512) {
+        for (int idx = tid; idx < 64 * 16 * !(DROID_ALT_ABL & 16); idx += 512) {
           const int p = idx >> 4, pc = idx & 15;
           const long m = ((long)e * H + ty0 + alt_py(p)) * W + tx0 + alt_px(p);
           *reinterpret_cast<uint4*>(a.out + m * 128 + pc * 8) = *reinterpret_cast<const uint4*>(&Os[p * kAltOS + pc * 8]);
