@@ -462,6 +462,29 @@ def frame_distance(poses, disps, intrinsics, ii, jj, beta):
     return dist
 
 
+def proximity_select(d, t0, t1, t, rad, nms, thresh, ei, ej, stereo, n_cap):
+    """add_proximity_factors' candidate walk on the device (include/droid_backends.h:
+    droid_proximity_select): d (t-t0)*(t-t1) f32 distances, ei/ej int32 existing
+    edges -> (pairs (n, 2) int32 device tensor in acceptance order)."""
+    _check_inputs(("d", "ei", "ej"), (d, ei, ej))
+    _need(d, torch.float32, "d")
+    _need(ei, torch.int32, "ei")
+    _need(ej, torch.int32, "ej")
+    n = (t - t0) * (t - t1)
+    if d.numel() != n or ei.numel() != ej.numel():
+        raise RuntimeError("proximity_select: d must hold (t-t0)*(t-t1) distances, ei/ej the same length")
+    dev = d.device
+    ws = torch.empty((int(lib.droid_proximity_workspace(t0, t1, t)),), dtype=torch.uint8, device=dev)
+    out = torch.empty((2, max(int(n_cap), 1)), dtype=torch.int32, device=dev)
+    cnt = torch.zeros((1,), dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        check(lib.droid_proximity_select(_ptr(d), t0, t1, t, int(rad), int(nms), float(thresh), _ptr(ei), _ptr(ej),
+                                         ei.numel(), int(bool(stereo)), int(n_cap), _ptr(out[0]), _ptr(out[1]),
+                                         _ptr(cnt), _ptr(ws), ws.numel(), _stream(d)), "proximity_select")
+    k = int(cnt.item())
+    return out[:, :k].t()
+
+
 def projmap(poses, disps, intrinsics, ii, jj):
     """droid_kernels.cu:1463-1488 -> [coords (E,H,W,3), valid (E,H,W,1)]."""
     _check_inputs(("poses", "disps", "intrinsics", "ii", "jj"), (poses, disps, intrinsics, ii, jj))

@@ -381,48 +381,41 @@ class FactorGraph:
         self.add_factors(ii[keep], jj[keep])
 
     def add_proximity_factors(self, t0=0, t1=0, rad=2, nms=2, beta=0.25, thresh=16.0, remove=False):
+        """factor_graph.py:305-369 on the device: the meshgrid distances
+        (droid_frame_distance, both directions), then proximity_edge_list."""
         t = self.video.counter.value
-        ix = np.arange(t0, t)
-        jx = np.arange(t1, t)
-        ii, jj = np.meshgrid(ix, jx, indexing="ij")
-        ii, jj = ii.reshape(-1), jj.reshape(-1)
-        d = self.video.distance(ii, jj, beta=beta).cpu().numpy().astype(np.float64)
-        d[ii - rad < jj] = np.inf
-        d[d > 100] = np.inf
-        ncol = t - t1
+        dev = self.video.poses.device
+        ii, jj = torch.meshgrid(torch.arange(t0, t, device=dev), torch.arange(t1, t, device=dev), indexing="ij")
+        d = self.video.distance(ii.reshape(-1), jj.reshape(-1), beta=beta)
+        es = proximity_edge_list(d, t0, t1, t, rad, nms, thresh, np.concatenate([self._ii, self._ii_bad, self._ii_inac]),
+                                 np.concatenate([self._jj, self._jj_bad, self._jj_inac]), self.video.stereo,
+                                 self.max_factors)
+        self.add_factors(es[:, 0], es[:, 1], remove)
 
-        def suppress(i, j):
-            lim = max(min(abs(i - j) - 2, nms), 0)
-            for di in range(-nms, nms + 1):
-                for dj in range(-nms, nms + 1):
-                    if abs(di) + abs(dj) <= lim:
-                        i1, j1 = i + di, j + dj
-                        if t0 <= i1 < t and t1 <= j1 < t:
-                            d[(i1 - t0) * ncol + (j1 - t1)] = np.inf
 
-        for i, j in zip(np.concatenate([self._ii, self._ii_bad, self._ii_inac]).tolist(),
-                        np.concatenate([self._jj, self._jj_bad, self._jj_inac]).tolist()):
-            suppress(i, j)
-
-        es = []
-        for i in range(t0, t):
-            if self.video.stereo:
-                es.append((i, i))
-                d[(i - t0) * ncol + (i - t1)] = np.inf
-            for j in range(max(i - rad - 1, 0), i):
-                es.append((i, j))
-                es.append((j, i))
-                d[(i - t0) * ncol + (j - t1)] = np.inf
-
-        for k in np.argsort(d, kind="stable"):
-            if d[k] > thresh:
-                continue
-            if len(es) > self.max_factors:
-                break
-            i, j = int(ii[k]), int(jj[k])
+def proximity_edge_list(d, t0, t1, t, rad, nms, thresh, ii_all, jj_all, stereo, max_factors):
+    """The edge list add_proximity_factors hands to add_factors
+    (factor_graph.py:312-369) from the device distances d ((t-t0)*(t-t1), f32):
+    the candidate mask, the NMS suppression around ii_all/jj_all (the graph's
+    ii|ii_bad|ii_inac), the sort and the greedy accept-and-suppress walk run in
+    droid_proximity_select (csrc/proximity_kernels.hip); only the accepted
+    pairs come back.  The static neighbour edges are built here, in the
+    reference's order, and lead the list.  -> (k, 2) int64 numpy."""
+    es = []
+    for i in range(t0, t):                  # :333-341
+        if stereo:
+            es.append((i, i))
+        for j in range(max(i - rad - 1, 0), i):
             es.append((i, j))
             es.append((j, i))
-            suppress(i, j)
-
-        es = np.asarray(es, dtype=np.int64).reshape(-1, 2)
-        self.add_factors(es[:, 0], es[:, 1], remove)
+    # :355-356 - a candidate is appended while len(es) <= max_factors
+    n_cap = (max_factors - len(es)) // 2 + 1 if max_factors >= len(es) else 0
+    n_cap = min(n_cap, (t - t0) * (t - t1))
+    dev = d.device
+    ei = torch.from_numpy(np.asarray(ii_all).astype(np.int32)).to(dev)
+    ej = torch.from_numpy(np.asarray(jj_all).astype(np.int32)).to(dev)
+    pairs = droid_backends.proximity_select(d.float().contiguous(), t0, t1, t, rad, nms, thresh, ei, ej, stereo,
+                                            n_cap).cpu().numpy().astype(np.int64)
+    es = np.asarray(es, dtype=np.int64).reshape(-1, 2)
+    both = np.stack([pairs, pairs[:, ::-1]], 1).reshape(-1, 2)   # (i, j), (j, i) per accepted pair
+    return np.concatenate([es, both], 0)

@@ -220,6 +220,19 @@ int droid_frame_distance(const float* poses, const float* disps, const float* in
                          const int64_t* ii, const int64_t* jj, int E, int H, int W, float beta,
                          float* dist, hipStream_t stream);
 
+/* FactorGraph.add_proximity_factors after the distances (factor_graph.py:305-369;
+ * the reference walks it in Python - no droid_backends export exists for it):
+ * d = the (t-t0) x (t-t1) distances of video.distance over the meshgrid
+ * [t0,t) x [t1,t), row-major; ei/ej (ne) int32 = ii|ii_bad|ii_inac, jj|...;
+ * n_cap = candidate pairs that may still be accepted before the edge list
+ * exceeds max_factors.  -> out_i/out_j (n_cap) int32 accepted pairs in
+ * acceptance order, *out_count (all device).  The caller adds the static
+ * neighbour edges (and their (j, i) twins) itself.  ws: droid_proximity_workspace bytes. */
+size_t droid_proximity_workspace(int t0, int t1, int t);
+int droid_proximity_select(const float* d, int t0, int t1, int t, int rad, int nms, float thresh,
+                           const int* ei, const int* ej, int ne, int stereo, int n_cap, int* out_i,
+                           int* out_j, int* out_count, void* ws, size_t ws_bytes, hipStream_t stream);
+
 /* replaces projmap (src/droid.cpp:139-154, droid_kernels.cu:1463-1488)
  * -> coords (E,H,W,3), valid (E,H,W,1) */
 int droid_projmap(const float* poses, const float* disps, const float* intrinsics,

@@ -82,3 +82,50 @@ def update(params, poses, disps, disps_sens, intrinsics, fmaps, ii, jj, net, inp
     return dict(net=net1[0].double().numpy(), target=target, weight=weight, damping=damping, coords1=coords1,
                 ba_in=(tgt, wgt, eta_ba, ii_ba, jj_ba, t0, t1), poses=out["poses"],
                 disps=np.maximum(out["disps"], 0.001))
+
+
+def proximity_edges(d, t0, t1, t, rad, nms, thresh, ii_all, jj_all, stereo, max_factors):
+    """FactorGraph.add_proximity_factors (reference factor_graph.py:305-369)
+    after video.distance, restated line by line: d = the float32 distances of
+    the meshgrid [t0, t) x [t1, t) (row-major), ii_all/jj_all = ii|ii_bad|ii_inac,
+    jj|jj_bad|jj_inac.  Returns the edge list es (k, 2) int64 in the
+    reference's order (static edges, then accepted pairs (i, j), (j, i)).
+    argsort is stable here; torch.argsort's order among equal distances is
+    unspecified (the fixtures use distinct distances)."""
+    d = np.array(d, dtype=np.float32).reshape(-1).copy()
+    ncol = t - t1
+    ii, jj = np.meshgrid(np.arange(t0, t), np.arange(t1, t), indexing="ij")
+    ii, jj = ii.reshape(-1), jj.reshape(-1)
+    d[ii - rad < jj] = np.inf                                     # :316
+    with np.errstate(invalid="ignore"):
+        d[d > 100] = np.inf                                       # :317
+
+    def suppress(i, j):                                           # :321-330, :361-366
+        for di in range(-nms, nms + 1):
+            for dj in range(-nms, nms + 1):
+                if abs(di) + abs(dj) <= max(min(abs(i - j) - 2, nms), 0):
+                    i1, j1 = i + di, j + dj
+                    if t0 <= i1 < t and t1 <= j1 < t:
+                        d[(i1 - t0) * ncol + (j1 - t1)] = np.inf
+
+    for i, j in zip(np.asarray(ii_all).tolist(), np.asarray(jj_all).tolist()):
+        suppress(i, j)
+    es = []
+    for i in range(t0, t):                                        # :333-341 (negative indices wrap)
+        if stereo:
+            es.append((i, i))
+            d[(i - t0) * ncol + (i - t1)] = np.inf
+        for j in range(max(i - rad - 1, 0), i):
+            es.append((i, j))
+            es.append((j, i))
+            d[(i - t0) * ncol + (j - t1)] = np.inf
+    for k in np.argsort(d, kind="stable"):                        # :343-366 (NaN sorts last)
+        if d[k] > thresh:
+            continue
+        if len(es) > max_factors:
+            break
+        i, j = int(ii[k]), int(jj[k])
+        es.append((i, j))
+        es.append((j, i))
+        suppress(i, j)
+    return np.asarray(es, dtype=np.int64).reshape(-1, 2)

@@ -16,6 +16,7 @@ computed in fp32 on CPU by the reference code itself:
   convgru.npz        ConvGRU.forward(...)                   (modules/gru.py:19-32)
   cvx_upsample.npz   cvx_upsample(...)                      (droid_net.py:21-35)
   projective_ops.npz projective_transform(..., jacobian=True) (geom/projective_ops.py:96-125)
+  proximity.npz      FactorGraph.add_proximity_factors(...)  (factor_graph.py:305-369)
 
 lietorch (un-vendored, v0.2) is needed by geom/projective_ops.py as a working
 group: `LieStandIn.SE3` below restates the lietorch SE3 operations that file
@@ -167,6 +168,54 @@ def projective_fixture(rng):
                         Jz_shared=Jzs[0].numpy())
 
 
+def proximity_fixture(rng):
+    """FactorGraph.add_proximity_factors (factor_graph.py:305-369) run by the
+    reference itself on stand-in graph state: video.distance returns the stored
+    distances, add_factors records the edge list it is handed.  Cases cover the
+    static edges with t0 > t1 (the negative-index wrap), stereo, the
+    max_factors cap, max_factors = -1, NaN and > 100 distances."""
+    sys.modules.setdefault("matplotlib", types.ModuleType("matplotlib"))
+    sys.modules.setdefault("matplotlib.pyplot", types.ModuleType("matplotlib.pyplot"))
+    from factor_graph import FactorGraph
+    from types import SimpleNamespace as NS
+    cases = [dict(t=48, t0=0, t1=0, rad=2, nms=2, thresh=16.0, stereo=False, max_factors=100000, ne=60, nan=0),
+             dict(t=40, t0=12, t1=6, rad=2, nms=2, thresh=16.0, stereo=True, max_factors=300, ne=40, nan=0),
+             dict(t=64, t0=0, t1=0, rad=3, nms=3, thresh=12.0, stereo=False, max_factors=-1, ne=30, nan=0),
+             dict(t=56, t0=4, t1=4, rad=2, nms=1, thresh=20.0, stereo=False, max_factors=100000, ne=50, nan=6),
+             dict(t=72, t0=0, t1=0, rad=2, nms=2, thresh=16.0, stereo=False, max_factors=500, ne=80, nan=0)]
+    out = {}
+    for c, cs in enumerate(cases):
+        t, t0, t1 = cs["t"], cs["t0"], cs["t1"]
+        gi, gj = np.meshgrid(np.arange(t0, t), np.arange(t1, t), indexing="ij")
+        # a camera lapping a 16-frame circuit: frames 16 apart see the same place
+        ph = np.pi * (gi - gj) / 16.0
+        d = (40.0 * np.abs(np.sin(ph)) + rng.uniform(0.0, 6.0, gi.shape) + 0.02 * np.abs(gi - gj)).astype(np.float32)
+        d = d.reshape(-1)
+        far = rng.choice(d.size, size=d.size // 20, replace=False)
+        d[far] = rng.uniform(100.5, 200.0, far.size).astype(np.float32)
+        if cs["nan"]:
+            d[rng.choice(d.size, size=cs["nan"], replace=False)] = np.nan
+        ne = cs["ne"]
+        ei = rng.integers(0, t, ne)
+        ej = np.clip(ei + rng.integers(-20, 21, ne), 0, t - 1)
+        k1, k2 = ne // 2, 3 * ne // 4
+        rec = {}
+        fake = NS(video=NS(counter=NS(value=t), stereo=cs["stereo"],
+                           distance=lambda ii, jj, beta=0.25, _d=d: torch.from_numpy(_d.copy())),
+                  ii=torch.from_numpy(ei[:k1]), jj=torch.from_numpy(ej[:k1]),
+                  ii_bad=torch.from_numpy(ei[k1:k2]), jj_bad=torch.from_numpy(ej[k1:k2]),
+                  ii_inac=torch.from_numpy(ei[k2:]), jj_inac=torch.from_numpy(ej[k2:]),
+                  max_factors=cs["max_factors"], device="cpu",
+                  add_factors=lambda ii, jj, remove=False: rec.update(ii=ii.numpy().copy(), jj=jj.numpy().copy()))
+        FactorGraph.add_proximity_factors(fake, t0=t0, t1=t1, rad=cs["rad"], nms=cs["nms"], beta=0.25,
+                                          thresh=cs["thresh"], remove=False)
+        out.update({"c%d_%s" % (c, k): np.asarray(v) for k, v in cs.items()})
+        out.update({"c%d_d" % c: d, "c%d_ei" % c: ei, "c%d_ej" % c: ej, "c%d_k1" % c: k1, "c%d_k2" % c: k2,
+                    "c%d_es_ii" % c: rec["ii"], "c%d_es_jj" % c: rec["jj"]})
+    out["ncases"] = len(cases)
+    np.savez_compressed(os.path.join(HERE, "proximity.npz"), **out)
+
+
 def main():
     _install_stubs()
     sys.path.insert(0, REF)
@@ -224,6 +273,9 @@ def main():
 
     # --- projective transform + Jacobians (BA linearisation) -----------------
     projective_fixture(np.random.default_rng(2025))
+
+    # --- proximity edges (global-backend edge rebuild) --------------------------
+    proximity_fixture(np.random.default_rng(2026))
     print("golden fixtures written to", HERE)
 
 

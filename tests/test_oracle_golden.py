@@ -181,3 +181,24 @@ def test_torch_cpu_lookup_equals_kernel_restatement():
     pyr = oc.corr_pyramid_torch(torch.from_numpy(f1), torch.from_numpy(f2))
     got = oc.lookup_pyramid_torch(pyr, torch.from_numpy(coords[0])).numpy()
     np.testing.assert_allclose(got, ref, atol=2e-5 * np.abs(ref).max())
+
+
+def _proximity_case(z, c):
+    g = lambda k: z["c%d_%s" % (c, k)]
+    ei, ej, k1, k2 = g("ei"), g("ej"), int(g("k1")), int(g("k2"))
+    args = dict(d=g("d"), t0=int(g("t0")), t1=int(g("t1")), t=int(g("t")), rad=int(g("rad")), nms=int(g("nms")),
+                thresh=float(g("thresh")), ii_all=np.concatenate([ei[:k1], ei[k1:k2], ei[k2:]]),
+                jj_all=np.concatenate([ej[:k1], ej[k1:k2], ej[k2:]]), stereo=bool(g("stereo")),
+                max_factors=int(g("max_factors")))
+    return args, np.stack([g("es_ii"), g("es_jj")], 1)
+
+
+def test_oracle_proximity_edges_match_reference(golden_dir):
+    """oracle.factor_graph.proximity_edges vs the reference's own
+    add_proximity_factors (tests/golden/proximity.npz): the identical edge list
+    for t0 > t1 (negative-index wrap), stereo, the max_factors cap, -1, NaN."""
+    from oracle.factor_graph import proximity_edges
+    z = np.load(os.path.join(golden_dir, "proximity.npz"))
+    for c in range(int(z["ncases"])):
+        args, ref = _proximity_case(z, c)
+        np.testing.assert_array_equal(proximity_edges(**args), ref, err_msg="case %d" % c)
