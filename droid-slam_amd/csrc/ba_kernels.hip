@@ -662,7 +662,20 @@ struct CholDev {
   double* x;    // [n] (permuted order)
   float* dx;    // [n]
   int inject;   // test hook (DROID_CHOL_FAULT_INJECT=1): raise the abort at once, as a timeout would
+  long long* prof;  // profiling builds: s_memrealtime per (task, phase < 8), or null
 };
+
+#ifndef DROID_CONV_PROFILE
+#define DROID_CONV_PROFILE 0
+#endif
+#if DROID_CONV_PROFILE
+#define CH_STAMP(ph)                                                                          \
+  do {                                                                                        \
+    if (d.prof && tid == 0) d.prof[(long)tk * 8 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define CH_STAMP(ph) do { } while (0)
+#endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mkrs(const void* p, size_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
@@ -797,27 +810,49 @@ __device__ __forceinline__ double rsqrt_f64(double x) {
 }
 
 // 16-wide panel of the diagonal factor: wave 0, lane r owns row r's panel
-// values in registers; pivots and scaled column entries are broadcast with
-// v_readlane (wave-synchronous: no LDS, no waits, no branches).  Lanes above
-// the diagonal update their (never read) upper-triangle entries too, and
-// pivot columns past the block's Bp real columns use a unit pivot, so every
-// panel is a full, branch-free 16 columns.
-// dinv[c] = 1 / L[c][c].
-__device__ __forceinline__ void panel_factor(double* T, double* dinv, int c0, int Bp, int lane, int* flag) {
+// values in registers; each pivot comes by one v_readlane pair, each scaled
+// column by one LDS store and wave-uniform (broadcast) LDS reads, and the next
+// pivot is formed ahead of the column update.  Lanes above the diagonal
+// update their (never read) upper-triangle entries too, and pivot columns past
+// the block's Bp real columns use a unit pivot, so every panel is a full,
+// branch-free 16 columns.  dinv[c] = 1 / L[c][c]; colbuf: 64 doubles of LDS.
+// (DROID_CHOL_PANEL_LDS=0: the column by v_readlane, 2.84 vs 2.0 us per panel.)
+#ifndef DROID_CHOL_PANEL_LDS
+#define DROID_CHOL_PANEL_LDS 1
+#endif
+__device__ __forceinline__ void panel_factor(double* T, double* dinv, int c0, int Bp, int lane, int* flag,
+                                             double* colbuf) {
   double v[16], invs[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) v[q] = T[lane * LT + c0 + q];
   bool bad = false;
+  // the next pivot is formed first, from the pivot lane's own entries (its
+  // update needs no broadcast), so the pivot chain never waits on the column
+  // broadcast: per column it is rsqrt -> scale -> one fma -> one v_readlane pair
+  double piv = c0 < Bp ? bcast_lane(v[0], c0) : 1.0;
 #pragma unroll
   for (int jj = 0; jj < 16; ++jj) {
-    const bool real = c0 + jj < Bp;  // wave-uniform
-    const double piv = real ? bcast_lane(v[jj], c0 + jj) : 1.0;
     bad |= !(piv > 0.0 && piv < 1e300);
     const double inv = rsqrt_f64(piv);
     invs[jj] = inv;
     v[jj] *= inv;  // the diagonal lane gets piv / sqrt(piv)
+    if (jj < 15) {
+      const double pn = fma(-v[jj], v[jj], v[jj + 1]);
+      piv = c0 + jj + 1 < Bp ? bcast_lane(pn, c0 + jj + 1) : 1.0;   // wave-uniform condition
+#if DROID_CHOL_PANEL_LDS
+      // the column's entries below the pivot reach every lane as wave-uniform LDS
+      // reads (one store, broadcast loads on the LDS pipe) instead of 2 v_readlane each
+      colbuf[lane] = v[jj];
+      double lq[16];
 #pragma unroll
-    for (int q = jj + 1; q < 16; ++q) v[q] = fma(-v[jj], bcast_lane(v[jj], c0 + q), v[q]);
+      for (int q = jj + 1; q < 16; ++q) lq[q] = colbuf[c0 + q];
+#pragma unroll
+      for (int q = jj + 1; q < 16; ++q) v[q] = fma(-v[jj], lq[q], v[q]);
+#else
+#pragma unroll
+      for (int q = jj + 1; q < 16; ++q) v[q] = fma(-v[jj], bcast_lane(v[jj], c0 + q), v[q]);
+#endif
+    }
   }
 #pragma unroll
   for (int q = 0; q < 16; ++q) T[lane * LT + c0 + q] = v[q];
@@ -865,6 +900,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
     const int type = __builtin_amdgcn_readfirstlane(tsk[0]), i = __builtin_amdgcn_readfirstlane(tsk[1]);
     const int j = __builtin_amdgcn_readfirstlane(tsk[2]), k = __builtin_amdgcn_readfirstlane(tsk[3]);
     const int ta = __builtin_amdgcn_readfirstlane(tsk[4]), tb = __builtin_amdgcn_readfirstlane(tsk[5]);
+    CH_STAMP(0);
     if (tid == 0) {
       bool ok = true;
       switch (type) {
@@ -900,6 +936,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
     }
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(shi[1])) break;
+    CH_STAMP(1);
 
     if (type == kPotrf) {
       const int R0 = 64 * k, Bp = min(64, n - R0), Br = min(64, n + 1 - R0);
@@ -922,8 +959,10 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         tile_commit(pre, T0);
       }
       __syncthreads();
+      CH_STAMP(2);
       for (int c0 = 0; c0 < Bp; c0 += 16) {  // whole 16-wide panels (unit-padded)
-        if (wave == 0) panel_factor(T0, vec + 128, c0, Bp, lane, d.flag);
+        if (wave == 0) panel_factor(T0, vec + 128, c0, Bp, lane, d.flag, scr);
+        if (c0 == 0) CH_STAMP(6);
         __syncthreads();
         const int s0 = c0 + 16;
         const int nt = (64 - s0) / 16;
@@ -941,6 +980,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         }
         __syncthreads();
       }
+      CH_STAMP(3);
       const bool below = tb != 0;  // trsm(k+1, k) runs in this task
       const int R1 = R0 + 64, nr1 = below ? min(64, n + 1 - R1) : 0;
       const int sb = below ? SL(k + 1, k) : 0;
@@ -992,6 +1032,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         }
         __syncthreads();
       }
+      CH_STAMP(4);
       tile_store(rM, skk, Br, Bp, T0);
       tile_store(rL, k, 64, 64, T1);
       const bool rhs = Br > Bp;
@@ -1006,6 +1047,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         __syncthreads();
         acc_store(T0, acc, wr, wc, lane);
         __syncthreads();
+        CH_STAMP(5);
         tile_store(rM, sb, nr1, Bp, T0);
         const bool rhs1 = (k + 1 == nbr - 1);
         if (rhs1 && tid < 32) st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[(n - R1) * LT + 2 * tid]));
@@ -1093,6 +1135,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       }
       publish(&yver[j], 2 + ta);
     }
+    CH_STAMP(7);
   }
 }
 
@@ -1256,6 +1299,7 @@ static BaDev make_dev(BaPlan& p, char* ws) {
 }
 
 static int num_cus() { return device_cu_count(); }
+static long long* g_chol_prof = nullptr;
 
 static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_t stream) {
   const int* I = reinterpret_cast<const int*>(ws + p.off_ints);
@@ -1274,6 +1318,7 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_
   c.dx = dx;
   const char* inj = getenv("DROID_CHOL_FAULT_INJECT");
   c.inject = (inj && atoi(inj) != 0) ? 1 : 0;
+  c.prof = g_chol_prof;
   static bool attr = false;
   if (!attr) {
     DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&chol_dataflow_kernel),
@@ -1292,6 +1337,19 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_
 using namespace droid;
 
 extern "C" {
+
+// Profiling builds (make prof): per Cholesky task, 8 int64 s_memrealtime
+// stamps (100 MHz): start, dependencies met, [potrf: last update applied,
+// panels factored, Linv done, trsm(k+1,k) done], end.
+int droid_chol_set_profile(void* buf) {
+#if DROID_CONV_PROFILE
+  g_chol_prof = static_cast<long long*>(buf);
+  return kOk;
+#else
+  (void)buf;
+  return fail(kUnsupported, "chol_set_profile: build with make prof (DROID_CONV_PROFILE=1)");
+#endif
+}
 
 int droid_ba_plan_upload(void* plan, void* workspace, hipStream_t stream) {
   auto* p = static_cast<BaPlan*>(plan);

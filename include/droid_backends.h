@@ -77,6 +77,8 @@ int droid_conv_set_profile(void* buf);
  * done / lookup barrier / stage end, then box taps * 2 + slow-path flag)
  * (scripts/alt_timeline.py). */
 int droid_alt_set_profile(void* buf);
+/* profiling builds only (make prof): Cholesky task timeline, 8 int64 per task */
+int droid_chol_set_profile(void* buf);
 
 /* CorrBlock pyramid construction (modules/corr.py:24-38,63-71) for E edges in
  * one pass: fmaps (NF,H,W,128) fp16 = frame features / 4 in NHWC (the
