@@ -423,7 +423,7 @@ def main():
             lookup_roof["algorithmic_bytes_per_launch"] = ALT_BYTES_PER_EDGE * e_local
             lookup_roof["achieved"] = ALT_BYTES_PER_EDGE * e_local / (lookup_ms * 1e-3) / 1e9 if lookup_ms else None
             lookup_roof["frac"] = lookup_roof["achieved"] / PEAK_HBM_GBS if lookup_ms else None
-            lookup_roof["traffic"] = None
+            lookup_roof["traffic"] = load_traffic("corr_alt", e_local, "corr_alt_ce0_kernel")
         result = {
             "metric": ("factor_graph.update_lowmem() steps/sec at 256 KF x 2k edges, 384x512" if args.lowmem else "factor_graph.update() iters/sec at 256 KF x 2k edges, 384x512" if args.config == "C3"
                        else "factor_graph.update() iters/sec, C5 %d KF x %d edges, 384x512" % (args.frames, len(ii))

@@ -530,7 +530,8 @@ __device__ __forceinline__ float hess_val(const float* H, int r, int c) {
   return H[r * (r + 1) / 2 + c];
 }
 
-__device__ __forceinline__ double gram_sum(const BaDev& d, int f, int i, int j) {
+// chunks c0, c0 + cstep, ... of the per-chunk Gram partials of element (i, j)
+__device__ __forceinline__ double gram_sum(const BaDev& d, int f, int i, int j, int c0, int cstep) {
   if (i > j) { int t = i; i = j; j = t; }
   const int nb = d.fnb[f];
   const int I = i >> 4, J = j >> 4;
@@ -538,7 +539,7 @@ __device__ __forceinline__ double gram_sum(const BaDev& d, int f, int i, int j) 
   const int Tf = nb * (nb + 1) / 2;
   const float* g = d.gram + d.fgoff[f] + (long)tf * 256 + (i & 15) * 16 + (j & 15);
   double s = 0.0;
-  for (int c = 0; c < d.nchunk; ++c) s += (double)g[(long)c * Tf * 256];
+  for (int c = c0; c < d.nchunk; c += cstep) s += (double)g[(long)c * Tf * 256];
   return s;
 }
 
@@ -548,44 +549,61 @@ __device__ __forceinline__ double& sys_at(const BaDev& d, int v, int u) {
   return d.M[(size_t)sl * kTile + (v & 63) * 64 + (u & 63)];
 }
 
-__global__ void __launch_bounds__(64) ba_assemble_kernel(BaDev d) {
+// One workgroup per 6x6 pose block (36 elements) or rhs block (6): the
+// element's partial sums (edge Hessian splits, Gram chunks) are spread over
+// 256 / elements thread groups with a fixed stride and the group sums added in
+// group order - deterministic, and a small graph's few blocks (C2: one tile)
+// no longer sum hundreds of partials per thread.
+__global__ void __launch_bounds__(256) ba_assemble_kernel(BaDev d) {
+  __shared__ double part[256];
   const int b = blockIdx.x;
   const int t = threadIdx.x;
-  if (b < d.nblk) {
-    if (t >= 36) return;
-    const int r = t / 6, c = t % 6;
-    double s = 0.0;
-    for (int k = d.blkcptr[b]; k < d.blkcptr[b + 1]; ++k) {
-      const int4 q = d.contrib[k];
-      if (q.x == kEdgeBlock) {
-        for (int sp = 0; sp < d.nsplit; ++sp)
-          s += (double)hess_val(d.hpart + ((long)q.y * d.nsplit + sp) * kHessStride, q.z + r, q.w + c);
-      } else {
-        s -= gram_sum(d, q.y, 6 * q.z + r, 6 * q.w + c);
+  const bool blk = b < d.nblk;
+  const int EL = blk ? 36 : 6, G = 256 / EL;
+  const int e = t % EL, g = t / EL;
+  double s = 0.0;
+  if (g < G) {
+    if (blk) {
+      const int r = e / 6, c = e % 6;
+      for (int k = d.blkcptr[b]; k < d.blkcptr[b + 1]; ++k) {
+        const int4 q = d.contrib[k];
+        if (q.x == kEdgeBlock) {
+          for (int sp = g; sp < d.nsplit; sp += G)
+            s += (double)hess_val(d.hpart + ((long)q.y * d.nsplit + sp) * kHessStride, q.z + r, q.w + c);
+        } else {
+          s -= gram_sum(d, q.y, 6 * q.z + r, 6 * q.w + c, g, G);
+        }
+      }
+    } else {
+      const int a = b - d.nblk;
+      for (int k = d.rhscptr[a]; k < d.rhscptr[a + 1]; ++k) {
+        const int4 q = d.rhscontrib[k];
+        if (q.x == kEdgeRhs) {
+          for (int sp = g; sp < d.nsplit; sp += G)
+            s += (double)d.hpart[((long)q.y * d.nsplit + sp) * kHessStride + 78 + q.z + e];
+        } else {
+          const int wcol = 6 * (d.frptr[q.y + 1] - d.frptr[q.y]);
+          s -= gram_sum(d, q.y, 6 * q.z + e, wcol, g, G);
+        }
       }
     }
+  }
+  part[t] = s;
+  __syncthreads();
+  if (t >= EL) return;
+  double tot = 0.0;
+  for (int gg = 0; gg < G; ++gg) tot += part[gg * EL + t];
+  if (blk) {
     // block (a, b) of the original order (a >= b) sits at permuted positions
     // (pa, pb); its (r, c) element is M'(v, u), stored as M'(u, v) when above
     // the diagonal (a diagonal block's upper half is its lower half mirrored)
+    const int r = t / 6, c = t % 6;
     const int pa = d.blka[b], pb = d.blkb[b];
     const int v = 6 * pa + r, u = 6 * pb + c;
-    if (v >= u) sys_at(d, v, u) = s;
-    else if (pa != pb) sys_at(d, u, v) = s;
+    if (v >= u) sys_at(d, v, u) = tot;
+    else if (pa != pb) sys_at(d, u, v) = tot;
   } else {
-    const int a = b - d.nblk;
-    if (t >= 6) return;
-    double s = 0.0;
-    for (int k = d.rhscptr[a]; k < d.rhscptr[a + 1]; ++k) {
-      const int4 q = d.rhscontrib[k];
-      if (q.x == kEdgeRhs) {
-        for (int sp = 0; sp < d.nsplit; ++sp)
-          s += (double)d.hpart[((long)q.y * d.nsplit + sp) * kHessStride + 78 + q.z + t];
-      } else {
-        const int wcol = 6 * (d.frptr[q.y + 1] - d.frptr[q.y]);
-        s -= gram_sum(d, q.y, 6 * q.z + t, wcol);
-      }
-    }
-    sys_at(d, d.n, 6 * d.rhspos[a] + t) = s;
+    sys_at(d, d.n, 6 * d.rhspos[b - d.nblk] + t) = tot;
   }
 }
 
@@ -1396,7 +1414,7 @@ int droid_ba_build_system(void* plan, void* workspace, float* poses, float* disp
   }
   DROID_HIP_CHECK(hipMemsetAsync(d.M, 0, (size_t)p->cs.nslots * kTile * sizeof(double), stream));
   if (d.nblk + p->P > 0) {
-    ba_assemble_kernel<<<d.nblk + p->P, 64, 0, stream>>>(d);
+    ba_assemble_kernel<<<d.nblk + p->P, 256, 0, stream>>>(d);
     DROID_LAUNCH_CHECK();
   }
   return kOk;

@@ -473,7 +473,10 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, co
   }
 
   // launch geometry
-  p.nsplit = std::max(1, std::min(std::max(1, HW / 256), (2048 + std::max(E, 1) - 1) / std::max(E, 1)));
+  // pixel splits per edge: enough (edge, split) workgroups to cover the CUs
+  // (~512), but few enough that each sums >= 256 pixels before its 90-partial
+  // reduction and the assembly does not sum many partials per element
+  p.nsplit = std::max(1, std::min(std::max(1, HW / 256), (512 + std::max(E, 1) - 1) / std::max(E, 1)));
   const int rounds = ceil_div(HW, 256);
   p.group_per_wave = std::max(1, std::min(rounds, (int)((long)p.K * rounds / 1024)));
   p.nchunk = ceil_div(rounds, p.group_per_wave);

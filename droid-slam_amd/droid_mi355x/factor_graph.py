@@ -53,6 +53,7 @@ class FactorGraph:
         # corr_impl "pyramid" (MI355X): no per-edge volume; update() computes the
         # correlation windows on demand from this feature pyramid of the frames
         self._alt_pyr = None
+        self._inp_frames = None   # (inp tensor, first-edge bytes, per-source-frame inp rows)
         self.comm = None  # set for edge-sharded multi-GPU: dict(group, own=(lo,hi), t0, t1)
         # fused (MI355X) operator: per-edge hidden state kept channels-last (E,H,W,128)
         from .fused import FusedUpdateModule
@@ -244,7 +245,14 @@ class FactorGraph:
             # segment - lets the gate convs compute their inp term once per frame
             inp_frames = None
             if self.inp is not None:
-                inp_frames = self.inp.index_select(0, self._dev("seg_first", idx[ptr[:-1]]))
+                # the per-frame rows change only with the edge set (add/rm_factors)
+                # (the cache holds self.inp itself: a new edge set is a new tensor object)
+                first = idx[ptr[:-1]]
+                c = self._inp_frames
+                if c is None or c[0] is not self.inp or c[1] != first.tobytes():
+                    c = self._inp_frames = (self.inp, first.tobytes(),
+                                            self.inp.index_select(0, self._dev("seg_first", first)))
+                inp_frames = c[2]
             self.net, delta, weight, damping = self.update_op(self.net, self.inp, corr, motn[0], dinv, len(uniq),
                                                               segments=segs, inp_frames=inp_frames)
         else:
@@ -263,11 +271,16 @@ class FactorGraph:
 
             if use_inactive:
                 m = (self._ii_inac >= t0 - 3) & (self._jj_inac >= t0 - 3)
-                dm = torch.as_tensor(m, device=self.device)
                 ii_h = np.concatenate([self._ii_inac[m], self._ii])
                 jj_h = np.concatenate([self._jj_inac[m], self._jj])
-                target = torch.cat([self.target_inac[:, dm], self.target], 1)
-                weight = torch.cat([self.weight_inac[:, dm], self.weight], 1)
+                # the selection as a cached index (a boolean mask would sync on its count)
+                if m.all():
+                    t_in, w_in = self.target_inac, self.weight_inac
+                else:
+                    sel = self._dev("inac_sel", np.nonzero(m)[0].astype(np.int64))
+                    t_in, w_in = self.target_inac.index_select(1, sel), self.weight_inac.index_select(1, sel)
+                target = torch.cat([t_in, self.target], 1)
+                weight = torch.cat([w_in, self.weight], 1)
             else:
                 ii_h, jj_h, target, weight = self._ii, self._jj, self.target, self.weight
 

@@ -9,7 +9,7 @@ import sys
 
 _LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "droid-slam_amd", "lib", "prof", "libdroid_hip.so")
 os.environ.setdefault("DROID_HIP_LIB", _LIB)
-sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."),
+sys.path[:0] = [os.path.dirname(os.path.abspath(__file__)), os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."),
                 os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "droid-slam_amd")]
 import ctypes  # noqa: E402
 
@@ -18,25 +18,10 @@ import torch  # noqa: E402
 
 import droid_backends  # noqa: E402
 from droid_backends._lib import lib  # noqa: E402
-from droid_mi355x import synthetic  # noqa: E402
-from droid_mi355x.corr import AltCorrBlock  # noqa: E402
-from oracle import geometry as og  # noqa: E402
+from c3_alt_inputs import c3_alt_inputs  # noqa: E402
 
-H, W, n = 48, 64, 256
-rng = np.random.default_rng(1003)
-ii, jj = synthetic.c3_edges(256, 2048, rng=np.random.default_rng(1003))
-gt = synthetic.trajectory(n, rng)
-poses, disps = synthetic.perturb(gt, synthetic.smooth_disps(n, H, W, rng), rng)
-coords, _ = og.projective_transform(poses, disps, np.tile(synthetic.INTRINSICS, (n, 1)), ii, jj)
 dev = torch.device("cuda:0")
-fm = torch.randn((1, n, 128, H, W), device=dev).half()
-pyr = [lv.view((-1,) + tuple(lv.shape[2:])) for lv in AltCorrBlock(fm).pyramid]
-c = torch.from_numpy(coords.astype(np.float32)).to(dev).contiguous()
-w = (torch.randn((128, 224), device=dev) / 14).half()
-w[:, 196:] = 0
-b = torch.zeros(128, device=dev)
-f1 = torch.as_tensor(ii, dtype=torch.int32, device=dev)
-f2 = torch.as_tensor(jj, dtype=torch.int32, device=dev)
+pyr, f1, f2, c, w, b = c3_alt_inputs(dev)
 G = 256
 prof = torch.zeros((G, 32, 8), dtype=torch.int64, device=dev)
 lib.droid_alt_set_profile.argtypes = [ctypes.c_void_p]

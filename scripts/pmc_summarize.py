@@ -29,7 +29,8 @@ def per_kernel(counter):
         name = r["Kernel_Name"]
         key = ("copy" if name.startswith("__amd_rocclr_copyBuffer") and len(out.get("copy", [])) < 3 else
                "zr" if "conv_band_kernel<256, 256, false, false, 6>" in name else
-               "lookup" if ("corr_ce0_kernel" in name or "corr_pyramid_f16_r3_kernel" in name) else None)
+               "lookup" if ("corr_ce0_kernel" in name or "corr_pyramid_f16_r3_kernel" in name) else
+               "alt" if "corr_alt_ce0_kernel" in name else None)
         if key:
             out.setdefault(key, []).append(float(r["Counter_Value"]))
             KNAME[key] = name
@@ -46,7 +47,10 @@ res = {"calibration": {"fetch_bytes_per_unit": kf, "write_bytes_per_unit": kw,
 # fused lookup + corr_encoder[0]: window reads + coords + 128-channel fp16 output per edge
 LOOKUP_CE0 = 4 * 64 * 2 * 3072 + 2 * 4 * 3072 + 128 * 2 * 3072
 # z|r gates with the inp term per source frame: 3x3 over net | corr | flow (320 channels)
-for key, name, algo in (("zr", "conv_zr", 2 * 256 * 320 * 9 * 3072 * E), ("lookup", "corr_lookup", LOOKUP_CE0 * E)):
+# on-demand lookup: query + target feature-pyramid rows, coords, 128-channel fp16 output per edge (bench.py)
+ALT = 786432 + 1044480 + 24576 + 128 * 2 * 3072
+for key, name, algo in (("zr", "conv_zr", 2 * 256 * 320 * 9 * 3072 * E), ("lookup", "corr_lookup", LOOKUP_CE0 * E),
+                        ("alt", "corr_alt", ALT * E)):
     fb = kf * min(fetch[key])
     wb = kw * min(write[key])
     d = {"edges": E, "kernel": KNAME.get(key), "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,

@@ -3,12 +3,14 @@ scripts/pmc_traffic.sh): a 1 GiB device copy (calibration of the FETCH/WRITE
 counters on a known byte count), then the C3 ZR gate conv as update() runs it
 (over net | corr | flow, the inp term per source frame of bench.py's C3 edge
 list: droid_conv_gru_pre_f16) and the C3 4-level
-correlation lookup fused with corr_encoder[0] (corr_lookup_ce0 on the 8x8-tiled volume), each launched
-3 times on synthetic data."""
+correlation lookup fused with corr_encoder[0] (corr_lookup_ce0 on the 8x8-tiled volume), then the
+on-demand lookup (corr_alt_ce0) on the C3 graph's reprojected coordinates, each
+launched 3 times on synthetic data."""
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "droid-slam_amd"))
+sys.path[:0] = [os.path.dirname(os.path.abspath(__file__)),
+                os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "droid-slam_amd")]
 import numpy as np
 import torch
 
@@ -59,5 +61,12 @@ c = coords.view(E, H, W, 2).contiguous()
 with torch.no_grad():
     for _ in range(3):
         droid_backends.corr_lookup_ce0(cb.corr_pyramid, c, w224, b128, tiled_shapes=cb.level_shapes)
+torch.cuda.synchronize()
+del cb, f
+
+from c3_alt_inputs import c3_alt_inputs  # noqa: E402
+pyr, f1, f2, ca, wa, ba = c3_alt_inputs(dev)
+for _ in range(3):
+    droid_backends.corr_alt_ce0(pyr, f1, f2, ca, wa, ba)
 torch.cuda.synchronize()
 print("ok")
