@@ -1500,6 +1500,9 @@ constexpr int kGloTP = 64;
 constexpr int kGloRing = 5;  // 80 KB: two workgroups fill a CU's 160 KB LDS
 constexpr int kGloLds = kGloRing * 2 * kGloTP * 128;  // the tile ring (bytes)
 
+// split: blockIdx.y of gridDim.y pixel ranges of the edge (whole 64-pixel tiles);
+// range y writes its share of the mean to glo + y * E * 128 (the caller adds
+// the ranges in order; one range = the plain mean)
 __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__ h, const __half* __restrict__ w,
                                                       const float* __restrict__ bias, float* __restrict__ glo,
                                                       int HW) {
@@ -1509,7 +1512,8 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int e = blockIdx.x;
   const int fr = lane & 15, fq = lane >> 4;
-  const int ntile = HW / kGloTP;
+  const int ntot = HW / kGloTP, S = gridDim.y, sp = blockIdx.y;
+  const int tbeg = (int)((long)ntot * sp / S), ntile = (int)((long)ntot * (sp + 1) / S) - tbeg;
   // this wave's weight fragments (B operand of K-step ks, column block j)
   half8 wf[4][2];
 #pragma unroll
@@ -1519,8 +1523,8 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
       const int co = wave * 32 + j * 16 + fr, k = (ks >> 1) * 64 + ((ks & 1) * 4 + fq) * 8;
       wf[ks][j] = *reinterpret_cast<const half8*>(w + co * 128 + k);
     }
-  const __half* he = h + (long)e * HW * 128;
-  const rsrc_t rs = make_rsrc(he, (unsigned)HW * 256);
+  const __half* he = h + ((long)e * HW + (long)tbeg * kGloTP) * 128;
+  const rsrc_t rs = make_rsrc(he, (unsigned)(ntile * kGloTP * 256));
   const unsigned Al_a = lds_addr(Al);
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   // DMA: 16 instructions of 8 pixel rows (one k-chunk) per tile, 4 per wave:
@@ -1601,7 +1605,7 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
       v += __shfl_xor(v, 2);
       v += __shfl_xor(v, 4);
       v += __shfl_xor(v, 8);
-      if (fr == 0) glo[(long)e * 128 + wave * 32 + j * 16 + fq * 4 + k] = v / (float)HW;
+      if (fr == 0) glo[((long)sp * gridDim.x + e) * 128 + wave * 32 + j * 16 + fq * 4 + k] = v / (float)HW;
     }
 }
 
@@ -1945,6 +1949,16 @@ int droid_conv_dw_head_f16(const void* const* srcs, const int* C, const int* cst
 
 // ConvGRU global context (gru_glo_kernel): h (E, HW, 128) fp16, w [128][128]
 // fp16 (the 1x1 conv weight, [co][ci]), bias [128] f32 -> glo (E, 128) f32.
+static int glo_set_attr() {
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gru_glo_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kGloLds));
+    attr = true;
+  }
+  return kOk;
+}
+
 int droid_gru_global_f16(const void* h, const void* w, const float* bias, float* glo, int E, int HW,
                          hipStream_t stream) {
   if (E < 0 || HW <= 0 || !h || !w || !bias || !glo) return fail(kInvalidArgument, "gru_global_f16: bad arguments");
@@ -1952,13 +1966,25 @@ int droid_gru_global_f16(const void* h, const void* w, const float* bias, float*
       (reinterpret_cast<uintptr_t>(w) & 15) || (reinterpret_cast<uintptr_t>(bias) & 15))
     return fail(kUnsupported, "gru_global_f16: needs H*W % 64 == 0 and 16-B aligned operands");
   if (E == 0) return kOk;
-  static bool attr = false;
-  if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gru_glo_kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, kGloLds));
-    attr = true;
-  }
-  gru_glo_kernel<<<E, 256, kGloLds, stream>>>((const __half*)h, (const __half*)w, bias, glo, HW);
+  { const int st = glo_set_attr(); if (st != kOk) return st; }
+  gru_glo_kernel<<<dim3(E, 1), 256, kGloLds, stream>>>((const __half*)h, (const __half*)w, bias, glo, HW);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+// ... split into `splits` pixel ranges per edge (few edges: more workgroups than
+// edges): part (splits, E, 128) f32, range y = its share of the mean; the caller
+// sums the ranges in order (glo = part.sum(0)).
+int droid_gru_global_split_f16(const void* h, const void* w, const float* bias, float* part, int splits, int E,
+                               int HW, hipStream_t stream) {
+  if (E < 0 || HW <= 0 || splits < 1 || !h || !w || !bias || !part)
+    return fail(kInvalidArgument, "gru_global_split_f16: bad arguments");
+  if (HW % kGloTP || splits > HW / kGloTP || (long)HW * 256 > 0x7fffffffL || (reinterpret_cast<uintptr_t>(h) & 15) ||
+      (reinterpret_cast<uintptr_t>(w) & 15) || (reinterpret_cast<uintptr_t>(bias) & 15))
+    return fail(kUnsupported, "gru_global_split_f16: needs H*W % 64 == 0, splits <= H*W/64, 16-B aligned operands");
+  if (E == 0) return kOk;
+  { const int st = glo_set_attr(); if (st != kOk) return st; }
+  gru_glo_kernel<<<dim3(E, splits), 256, kGloLds, stream>>>((const __half*)h, (const __half*)w, bias, part, HW);
   DROID_LAUNCH_CHECK();
   return kOk;
 }

@@ -352,12 +352,23 @@ def gru_global_f16(h, w, bias, out=None):
     E, H, W, C = h.shape
     if C != 128 or tuple(w.shape) != (128, 128):
         raise RuntimeError("gru_global_f16: h must have 128 channels and w be 128x128")
-    if out is None:
-        out = torch.empty((E, 128), dtype=torch.float32, device=h.device)
+    # a small graph (the frontend's ~100 edges) gets several workgroups per edge:
+    # ~512 in all, each at least 4 tiles of 64 pixels; their partial means are
+    # added in order (deterministic)
+    splits = max(1, min((H * W) // 256, -(-512 // max(E, 1))))
     with torch.cuda.device(h.device):
-        check(lib.droid_gru_global_f16(_ptr(h), _ptr(w), _ptr(bias), _ptr(out), E, H * W, _stream(h)),
-              "gru_global_f16")
-    return out
+        if splits == 1:
+            if out is None:
+                out = torch.empty((E, 128), dtype=torch.float32, device=h.device)
+            check(lib.droid_gru_global_f16(_ptr(h), _ptr(w), _ptr(bias), _ptr(out), E, H * W, _stream(h)),
+                  "gru_global_f16")
+            return out
+        part = torch.empty((splits, E, 128), dtype=torch.float32, device=h.device)
+        check(lib.droid_gru_global_split_f16(_ptr(h), _ptr(w), _ptr(bias), _ptr(part), splits, E, H * W,
+                                             _stream(h)), "gru_global_split_f16")
+    if out is None:
+        return part.sum(0)
+    return torch.sum(part, 0, out=out)
 
 
 def segment_mean_f16(src, seg_ptr, seg_idx, num_segments, out=None):

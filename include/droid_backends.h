@@ -182,6 +182,11 @@ int droid_flow_enc0_f16(const float* motn, const void* w, const float* bias, voi
  * (E,128) f32 (plain stores, deterministic).  Needs H*W % 64 == 0. */
 int droid_gru_global_f16(const void* h, const void* w, const float* bias, float* glo, int E, int HW,
                          hipStream_t stream);
+/* the same split into `splits` pixel ranges per edge (more workgroups than a
+ * small graph has edges): part (splits,E,128) f32, range y = its share of the
+ * mean; glo = part summed over the ranges in order */
+int droid_gru_global_split_f16(const void* h, const void* w, const float* bias, float* part, int splits,
+                               int E, int HW, hipStream_t stream);
 
 /* GraphAgg scatter_mean (droid_net.py:27-45, torch_scatter.scatter_mean over
  * dim 1): out[u] = mean of src rows seg_idx[seg_ptr[u] .. seg_ptr[u+1]), rows of

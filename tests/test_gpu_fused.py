@@ -291,9 +291,10 @@ def test_corr_lookup_ce0_tiled_volume_bitexact(E, H, W):
         assert torch.equal(cbt(c.view(1, E, H, W, 2)), cb(c.view(1, E, H, W, 2)))
 
 
-@pytest.mark.parametrize("E,H,W", [(3, 8, 24), (2, 48, 64)])
+@pytest.mark.parametrize("E,H,W", [(3, 8, 24), (2, 48, 64), (96, 48, 64), (600, 48, 64)])
 def test_gru_global_context(E, H, W):
-    """glo = mean_px sigmoid(conv1x1(h) + b) * h (modules/gru.py:24-26) vs torch fp32."""
+    """glo = mean_px sigmoid(conv1x1(h) + b) * h (modules/gru.py:24-26) vs torch fp32
+    (one workgroup per edge, or several pixel ranges per edge for small graphs)."""
     import droid_backends
     g = torch.Generator(device=DEV).manual_seed(23)
     h = torch.tanh(torch.randn((E, H, W, 128), generator=g, device=DEV)).half()
