@@ -496,6 +496,28 @@ def proximity_select(d, t0, t1, t, rad, nms, thresh, ei, ej, stereo, n_cap):
     return out[:, :k].t()
 
 
+NORM_RELU, NORM_RES_RELU, NORM_ADD_RELU, NORM_ONLY = 0, 1, 2, 3
+
+
+def instance_norm_act_f16(x, mode=NORM_RELU, res=None, out=None, eps=1e-5):
+    """nn.InstanceNorm2d(affine=False) + the encoder's ReLU / residual add
+    (include/droid_backends.h: droid_instance_norm_act_f16) on an NCHW fp16
+    tensor in channels_last memory format; returns a tensor of the same kind."""
+    if x.dtype != torch.float16 or x.dim() != 4 or not x.is_contiguous(memory_format=torch.channels_last):
+        raise RuntimeError("instance_norm_act_f16: x must be a channels_last fp16 (N,C,H,W) tensor")
+    N, C, H, W = x.shape
+    if res is not None and (res.shape != x.shape or res.dtype != torch.float16 or
+                            not res.is_contiguous(memory_format=torch.channels_last)):
+        raise RuntimeError("instance_norm_act_f16: res must match x (channels_last fp16)")
+    if out is None:
+        out = torch.empty_like(x, memory_format=torch.channels_last)
+    ws = torch.empty((int(lib.droid_instance_norm_workspace(N, H * W, C)),), dtype=torch.uint8, device=x.device)
+    with torch.cuda.device(x.device):
+        check(lib.droid_instance_norm_act_f16(_ptr(x), _ptr(res), _ptr(out), N, H * W, C, int(mode), float(eps),
+                                              _ptr(ws), ws.numel(), _stream(x)), "instance_norm_act_f16")
+    return out
+
+
 def projmap(poses, disps, intrinsics, ii, jj):
     """droid_kernels.cu:1463-1488 -> [coords (E,H,W,3), valid (E,H,W,1)]."""
     _check_inputs(("poses", "disps", "intrinsics", "ii", "jj"), (poses, disps, intrinsics, ii, jj))

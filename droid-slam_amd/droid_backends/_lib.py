@@ -48,6 +48,8 @@ _SIGS = {
     "droid_projective_transform": ([_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p], _i),
     "droid_frame_distance": ([_p, _p, _p, _p, _p, _i, _i, _i, _f, _p, _p], _i),
     "droid_chol_set_profile": ([_p], _i),
+    "droid_instance_norm_workspace": ([_i, _i, _i], _sz),
+    "droid_instance_norm_act_f16": ([_p, _p, _p, _i, _i, _i, _i, _f, _p, _sz, _p], _i),
     "droid_proximity_workspace": ([_i, _i, _i], _sz),
     "droid_proximity_select": ([_p, _i, _i, _i, _i, _i, _f, _p, _p, _i, _i, _i, _p, _p, _p, _p, _sz, _p], _i),
     "droid_projmap": ([_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p], _i),

@@ -17,3 +17,6 @@ from .corr import AltCorrBlock, CorrBlock  # noqa: E402,F401
 from .update import ConvGRU, GraphAgg, UpdateModule  # noqa: E402,F401
 from .depth_video import DepthVideo  # noqa: E402,F401
 from .factor_graph import FactorGraph  # noqa: E402,F401
+from .extractor import BasicEncoder  # noqa: E402,F401
+from .droid_net import DroidNet  # noqa: E402,F401
+from .motion_filter import MotionFilter  # noqa: E402,F401

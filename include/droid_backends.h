@@ -240,6 +240,15 @@ int droid_proximity_select(const float* d, int t0, int t1, int t, int rad, int n
                            const int* ei, const int* ej, int ne, int stereo, int n_cap, int* out_i,
                            int* out_j, int* out_count, void* ws, size_t ws_bytes, hipStream_t stream);
 
+/* MotionFilter feature encoder (modules/extractor.py BasicEncoder, norm_fn
+ * 'instance' = fnet): nn.InstanceNorm2d(affine=False) of an NHWC fp16 map
+ * (N, HW, C), fused with the ReLU / residual add around it.  mode 0 relu(n(x)),
+ * 1 relu(res + relu(n(x))), 2 relu(n(x) + res), 3 n(x).  C % 8 == 0, C <= 512;
+ * out may be x.  ws: droid_instance_norm_workspace bytes. */
+size_t droid_instance_norm_workspace(int N, int HW, int C);
+int droid_instance_norm_act_f16(const void* x, const void* res, void* out, int N, int HW, int C, int mode,
+                                float eps, void* ws, size_t ws_bytes, hipStream_t stream);
+
 /* replaces projmap (src/droid.cpp:139-154, droid_kernels.cu:1463-1488)
  * -> coords (E,H,W,3), valid (E,H,W,1) */
 int droid_projmap(const float* poses, const float* disps, const float* intrinsics,

@@ -17,6 +17,8 @@ computed in fp32 on CPU by the reference code itself:
   cvx_upsample.npz   cvx_upsample(...)                      (droid_net.py:21-35)
   projective_ops.npz projective_transform(..., jacobian=True) (geom/projective_ops.py:96-125)
   proximity.npz      FactorGraph.add_proximity_factors(...)  (factor_graph.py:305-369)
+  encoders.npz       BasicEncoder fnet / cnet                (modules/extractor.py, droid_net.py:149-150)
+  motion_filter.npz  MotionFilter.track keyframe decisions   (motion_filter.py:45-82)
 
 lietorch (un-vendored, v0.2) is needed by geom/projective_ops.py as a working
 group: `LieStandIn.SE3` below restates the lietorch SE3 operations that file
@@ -216,6 +218,100 @@ def proximity_fixture(rng):
     np.savez_compressed(os.path.join(HERE, "proximity.npz"), **out)
 
 
+def encoder_fixture(rng):
+    """BasicEncoder (modules/extractor.py) as DroidNet builds it - fnet
+    (128, 'instance') and cnet (256, 'none') - with the deterministic fill, on a
+    normalised 2-image batch."""
+    from modules.extractor import BasicEncoder
+    x = rng.standard_normal((1, 2, 3, 64, 96)).astype(np.float32)
+    out = {"x": x}
+    for name, dim, norm in (("fnet", 128, "instance"), ("cnet", 256, "none")):
+        enc = BasicEncoder(output_dim=dim, norm_fn=norm)
+        det_fill(enc)
+        out[name] = enc(torch.from_numpy(x)).numpy()
+    # DroidNet's parameter names and shapes: the layout droid.pth is saved in
+    import droid_net
+    sd = droid_net.DroidNet().state_dict()
+    out["droidnet_keys"] = np.array(list(sd.keys()))
+    out["droidnet_shapes"] = np.array([",".join(map(str, v.shape)) for v in sd.values()])
+    np.savez_compressed(os.path.join(HERE, "encoders.npz"), **out)
+
+
+def motion_filter_fixture(rng):
+    """MotionFilter.track (motion_filter.py:45-82) run by the reference on a
+    stand-in video: a textured scene translating a little more every frame;
+    fnet / cnet / update with the deterministic fill.  The reference's
+    droid_backends.corr_index_forward (CUDA) is served by the oracle's
+    restatement of correlation_kernels.cu (oracle/corr.py, checked against
+    grid_sample); lietorch's SE3.Identity by its data [0,0,0,0,0,0,1]."""
+    from types import SimpleNamespace as NS
+    sys.path.insert(0, os.path.join(HERE, "..", ".."))
+    from oracle import corr as ocorr
+    sys.modules.setdefault("cv2", types.ModuleType("cv2"))
+    db = sys.modules["droid_backends"]
+    db.corr_index_forward = lambda vol, coords, r: [torch.from_numpy(
+        ocorr.corr_index_forward(vol.numpy(), coords.numpy(), r))]
+    lt = sys.modules["lietorch"]
+    lt.SE3.Identity = staticmethod(lambda *a: NS(data=torch.as_tensor([[0, 0, 0, 0, 0, 0, 1.0]])))
+    import importlib
+    import motion_filter as mf
+    mf = importlib.reload(mf)
+    import droid_net
+    net = droid_net.DroidNet()
+    det_fill(net)
+    # scene: smooth random texture, frame k translated by shift[k] pixels (x) and shift[k]/2 (y)
+    H, W = 128, 192        # 16 x 24 maps: the volume's fourth pooling needs >= 16 rows
+    base = rng.uniform(0, 255, (3, H // 4 + 16, W // 4 + 16)).astype(np.float32)
+    tex = torch.nn.functional.interpolate(torch.from_numpy(base)[None], scale_factor=4, mode="bilinear",
+                                          align_corners=False)[0].numpy()
+    shifts = np.array([0, 1, 2, 4, 7, 11, 16, 22, 29, 37], dtype=np.int64)
+    frames = np.stack([tex[:, 4 + s // 2: 4 + s // 2 + H, 8 + s: 8 + s + W] for s in shifts]).clip(0, 255).astype(np.uint8)
+    intr = torch.as_tensor([50.0, 50.0, W / 2, H / 2])
+
+    def run(thresh):
+        appended, feats = [], []
+        video = NS(counter=NS(value=0))
+
+        def append(*item):
+            appended.append(float(item[0]))
+            if len(feats) < 3:
+                feats.append((item[6].numpy().copy(), item[7].numpy().copy(), item[8].numpy().copy()))
+            video.counter.value += 1
+        video.append = append
+        f = mf.MotionFilter(net, video, thresh=thresh, device="cpu")
+        for k in range(len(frames)):
+            f.track(float(k), torch.from_numpy(frames[k])[None], intrinsics=intr)   # (1, 3, H, W) uint8 BGR
+        return appended, feats
+
+    # the per-frame mean |delta| the check computes (a spy on its Tensor.norm call)
+    orig_norm = torch.Tensor.norm
+    seen = []
+
+    def spy(self, *a, **k):
+        r = orig_norm(self, *a, **k)
+        if k.get("dim") == -1 and self.dim() == 5:
+            seen.append(float(r.mean()))
+        return r
+    torch.Tensor.norm = spy
+    out = {"frames": frames, "intrinsics": intr.numpy()}
+    try:
+        # thresh 0: every frame is a keyframe (motion against the previous frame);
+        # thresh inf: none after the first (motion against frame 0).  With the
+        # deterministic, untrained weights the motion values differ by ~1 %, so
+        # the fixtures pin the values and both branches, not a borderline decision.
+        for tag, th in (("all", 0.0), ("none", float("inf"))):
+            seen.clear()
+            appended, feats = run(th)
+            out["motion_" + tag] = np.array(seen)
+            out["appended_" + tag] = np.array(appended)
+            if tag == "all":
+                for q, (g, n_, i_) in enumerate(feats):
+                    out["gmap%d" % q], out["net%d" % q], out["inp%d" % q] = g, n_, i_
+    finally:
+        torch.Tensor.norm = orig_norm
+    np.savez_compressed(os.path.join(HERE, "motion_filter.npz"), **out)
+
+
 def main():
     _install_stubs()
     sys.path.insert(0, REF)
@@ -276,6 +372,10 @@ def main():
 
     # --- proximity edges (global-backend edge rebuild) --------------------------
     proximity_fixture(np.random.default_rng(2026))
+
+    # --- MotionFilter: feature encoders and the keyframe check -----------------
+    encoder_fixture(np.random.default_rng(2027))
+    motion_filter_fixture(np.random.default_rng(2028))
     print("golden fixtures written to", HERE)
 
 
