@@ -19,6 +19,7 @@ computed in fp32 on CPU by the reference code itself:
   proximity.npz      FactorGraph.add_proximity_factors(...)  (factor_graph.py:305-369)
   encoders.npz       BasicEncoder fnet / cnet                (modules/extractor.py, droid_net.py:149-150)
   motion_filter.npz  MotionFilter.track keyframe decisions   (motion_filter.py:45-82)
+  geom_ba.npz        geom/ba.py BA / MoBA + their gradients   (geom/ba.py:31-158, geom/chol.py)
 
 lietorch (un-vendored, v0.2) is needed by geom/projective_ops.py as a working
 group: `LieStandIn.SE3` below restates the lietorch SE3 operations that file
@@ -116,6 +117,28 @@ class LieStandIn:
             at, ar = a[..., :3], a[..., 3:]
             tt = t.expand_as(at)
             return torch.cat([LieStandIn._rot(qi, at), LieStandIn._rot(qi, ar + torch.cross(at, tt, dim=-1))], -1)
+
+        manifold_dim = 6
+
+        @property
+        def shape(self):
+            return self.data.shape[:-1]
+
+        def retr(self, a):
+            """Exp(a) * self, Exp by the matrix exponential of the 4x4 twist
+            [[phi]x, rho; 0, 0] (torch.linalg.matrix_exp, differentiable) - an
+            evaluation independent of the closed form droid_mi355x.lie uses."""
+            rho, phi = a[..., :3], a[..., 3:]
+            o = torch.zeros_like(phi[..., 0])
+            px, py, pz = phi.unbind(-1)
+            hat = torch.stack([torch.stack([o, -pz, py, rho[..., 0]], -1), torch.stack([pz, o, -px, rho[..., 1]], -1),
+                               torch.stack([-py, px, o, rho[..., 2]], -1), torch.stack([o, o, o, o], -1)], -2)
+            T = torch.linalg.matrix_exp(hat)
+            R, t = T[..., :3, :3], T[..., :3, 3]
+            qw = 0.5 * torch.sqrt(torch.clamp(1.0 + R[..., 0, 0] + R[..., 1, 1] + R[..., 2, 2], min=1e-12))
+            q = torch.stack([(R[..., 2, 1] - R[..., 1, 2]) / (4 * qw), (R[..., 0, 2] - R[..., 2, 0]) / (4 * qw),
+                             (R[..., 1, 0] - R[..., 0, 1]) / (4 * qw), qw], -1)
+            return LieStandIn.SE3(torch.cat([t, q], -1)) * self
 
     class Sim3:
         pass
@@ -312,6 +335,78 @@ def motion_filter_fixture(rng):
     np.savez_compressed(os.path.join(HERE, "motion_filter.npz"), **out)
 
 
+def geom_ba_fixture(rng):
+    """geom/ba.py BA and MoBA (the differentiable training-path BA, with
+    geom/chol.py's implicit-gradient LLT) run by the reference on CPU in
+    float64 with the SE3 stand-in, plus the gradients of a fixed linear
+    functional of the result w.r.t. target, weight and eta."""
+    sys.modules["lietorch"].SE3 = LieStandIn.SE3
+    sys.modules["lietorch"].Sim3 = LieStandIn.Sim3
+
+    def scatter_sum(src, index, dim=-1, dim_size=None):
+        dim = dim % src.dim()
+        n = int(index.max()) + 1 if dim_size is None else dim_size
+        shape = list(src.shape)
+        shape[dim] = n
+        return torch.zeros(shape, dtype=src.dtype).index_add_(dim, index, src)
+    sys.modules["torch_scatter"].scatter_sum = scatter_sum
+    import importlib
+    import geom.projective_ops as pops
+    importlib.reload(pops)
+    import geom.chol as gchol
+    importlib.reload(gchol)
+    import geom.ba as gba
+    gba = importlib.reload(gba)
+
+    def as_cpu(*a, **k):   # the stereo-edge literal, on the CPU in float64
+        k.pop("device", None)
+        return torch.tensor(*a, dtype=torch.float64) if not isinstance(a[0], torch.Tensor) else a[0].clone()
+    orig = pops.torch.as_tensor
+    P, ht, wd = 5, 8, 12
+    poses = np.zeros((1, P, 7))
+    poses[..., 6] = 1.0
+    poses[0, :, 2] = 0.1 * np.arange(P)                       # forward motion
+    poses[0, :, :3] += rng.normal(0, 0.02, (P, 3))
+    q = rng.normal(0, 0.02, (P, 3))
+    poses[0, :, 3:6] = q
+    poses[0, :, 6] = np.sqrt(1 - (q ** 2).sum(-1))
+    disps = rng.uniform(0.4, 1.0, (1, P, ht, wd))
+    intr = np.tile([[10.0, 10.0, wd / 2, ht / 2]], (1, P, 1))
+    ii = np.array([0, 1, 1, 2, 2, 3, 3, 4, 0, 4, 2], dtype=np.int64)
+    jj = np.array([1, 0, 2, 1, 3, 2, 4, 3, 2, 2, 2], dtype=np.int64)   # last: a stereo (i == j) edge
+    E = len(ii)
+    tgt = rng.normal(0, 1.0, (1, E, ht, wd, 2))
+    wgt = rng.uniform(0.1, 1.0, (1, E, ht, wd, 2))
+    kx = np.unique(ii)
+    eta = rng.uniform(1e-3, 1e-2, (1, len(kx), ht, wd))
+    c_pose = rng.normal(0, 1.0, (1, P, 7))
+    c_disp = rng.normal(0, 1.0, (1, P, ht, wd))
+    out = dict(poses=poses, disps=disps, intrinsics=intr, ii=ii, jj=jj, eta=eta, c_pose=c_pose, c_disp=c_disp)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64))
+    pops.torch.as_tensor = as_cpu   # the reference's device="cuda" literal (projective_ops.py:105) -> CPU
+    try:
+        with torch.enable_grad():
+            Gs = LieStandIn.SE3(T(poses))
+            x0 = pops.projective_transform(Gs, T(disps), T(intr), torch.from_numpy(ii), torch.from_numpy(jj))[0]
+            target = (x0.detach() + 0.5 * T(tgt)).requires_grad_()   # residuals of a few pixels
+            weight = T(wgt).requires_grad_()
+            etat = T(eta).requires_grad_()
+            p1, d1 = gba.BA(target, weight, etat, Gs, T(disps), T(intr), torch.from_numpy(ii), torch.from_numpy(jj),
+                            fixedp=1)
+            loss = (p1.data * T(c_pose)).sum() + (d1 * T(c_disp)).sum()
+            gt, gw, ge = torch.autograd.grad(loss, [target, weight, etat])
+            out.update(target=target.detach().numpy(), weight=weight.detach().numpy(), ba_poses=p1.data.detach().numpy(),
+                       ba_disps=d1.detach().numpy(), grad_target=gt.numpy(), grad_weight=gw.numpy(), grad_eta=ge.numpy())
+            target2 = target.detach().clone().requires_grad_()
+            p2 = gba.MoBA(target2, weight.detach(), etat.detach(), Gs, T(disps), T(intr), torch.from_numpy(ii),
+                          torch.from_numpy(jj), fixedp=1)
+            g2, = torch.autograd.grad((p2.data * T(c_pose)).sum(), [target2])
+            out.update(moba_poses=p2.data.detach().numpy(), moba_grad_target=g2.numpy())
+    finally:
+        pops.torch.as_tensor = orig
+    np.savez_compressed(os.path.join(HERE, "geom_ba.npz"), **out)
+
+
 def main():
     _install_stubs()
     sys.path.insert(0, REF)
@@ -376,6 +471,9 @@ def main():
     # --- MotionFilter: feature encoders and the keyframe check -----------------
     encoder_fixture(np.random.default_rng(2027))
     motion_filter_fixture(np.random.default_rng(2028))
+
+    # --- differentiable BA (training path) --------------------------------------
+    geom_ba_fixture(np.random.default_rng(2029))
     print("golden fixtures written to", HERE)
 
 
