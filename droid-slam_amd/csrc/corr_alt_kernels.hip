@@ -83,6 +83,7 @@ struct AltArgs {
 #define DROID_ALT_ABL 0
 #endif
 
+
 // Box buffer 0 holds the boxes of levels 3 and 1, buffer 1 those of levels 2 and
 // 0, so buffer 1 is the larger: on the C3 trajectory the level-0 box of a tile
 // is 210 taps at the median and exceeds 288 for ~7 % of the tiles, the level-1
@@ -119,15 +120,6 @@ __device__ __forceinline__ int alt_px(int p) { return 4 * ((p >> 4) & 1) + (p & 
 
 __device__ __forceinline__ int alt_floor(float v) { return (int)fminf(fmaxf(floorf(v), -1e6f), 1e6f); }
 
-// a wave-uniform int32 from global memory by a SCALAR load (lgkmcnt): the
-// compiler would otherwise use a vector load + vmcnt(0), which also drains the
-// box DMA in flight (the vmcnt counter is in order)
-__device__ __forceinline__ int alt_sload(const int* p) {
-  int v;
-  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
-  return v;
-}
-
 // clipped box [x0,x1] x [y0,y1] of the map -> tap count (0 when empty)
 __device__ __forceinline__ int alt_clip(int& x0, int& x1, int& y0, int& y1, int Wl, int Hl) {
   x0 = max(x0, 0); x1 = min(x1, Wl - 1); y0 = max(y0, 0); y1 = min(y1, Hl - 1);
@@ -160,12 +152,16 @@ __device__ __forceinline__ void alt_box_dma(const AltArgs& a, int l, int f2, int
   const int tn = gbw * gbh;
   if (tn <= 0) return;
   const int Hl = a.Hl[l], Wl = a.Wl[l];
-  const rsrc_t rs = make_rsrc(a.pyr[l] + (long)f2 * Hl * Wl * 128, (unsigned)(Hl * Wl * 256));
+  const rsrc_t rs = make_rsrc(a.pyr[l] + (long)__builtin_amdgcn_readfirstlane(f2) * Hl * Wl * 128,
+                              (unsigned)(Hl * Wl * 256));
   const int nins = (tn + 3) >> 2;
+  // tap / gbw by a float reciprocal: (tap + 0.5) / gbw is >= 0.5 / gbw >= 2^-8 from
+  // an integer and tap < 2^12, so the v_rcp_f32 product (~2^-22 relative) floors exactly
+  const float inv = __builtin_amdgcn_rcpf((float)gbw);
   for (int ins = wave_u; ins < nins; ins += 8) {
     const int tap = ins * 4 + (lane >> 4);
     const int piece = (lane & 15) ^ (tap & 15);
-    const int ry = tap / gbw, rx = tap - ry * gbw;
+    const int ry = (int)(((float)tap + 0.5f) * inv), rx = tap - ry * gbw;
     const unsigned off = tap < tn ? (unsigned)((((gy0 + ry) * Wl + gx0 + rx) * 128 + piece * 8) * 2) : kOob;
     dma16(rs, box + ins * 1024, off);
   }
@@ -244,8 +240,10 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
     const int tt = t - r.e * tpe;
     r.ty0 = (tt / tcols) * 8;
     r.tx0 = (tt - (tt / tcols) * tcols) * 8;
-    r.f1 = (DROID_ALT_ABL & 64) ? 0 : alt_sload(a.f1 + r.e);
-    r.f2 = (DROID_ALT_ABL & 64) ? 0 : alt_sload(a.f2 + r.e);
+    // plain loads: the compiler waits for them at their first use (the next
+    // tile's box DMA, three stages later), not here as the scalar-load asm did
+    r.f1 = (DROID_ALT_ABL & 64) ? 0 : a.f1[r.e];
+    r.f2 = (DROID_ALT_ABL & 64) ? 0 : a.f2[r.e];
     return r;
   };
   // coordinates of a tile's 64 pixels -> LDS slot by LDS-DMA (lanes 0..31 of wave 0, 16 B = 2 px each)
@@ -264,7 +262,7 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
   // a tile's 64 query feature rows (16 KB) -> box 1 + kAltF1 by LDS-DMA, once per
   // workgroup (each wave then reads the fragments it needs from LDS): 2 x 1 KB per wave
   auto f1_dma = [&](const Tile& T) {
-    const rsrc_t rs = make_rsrc(a.pyr[0] + (long)T.f1 * HW * 128, (unsigned)(HW * 256));
+    const rsrc_t rs = make_rsrc(a.pyr[0] + (long)__builtin_amdgcn_readfirstlane(T.f1) * HW * 128, (unsigned)(HW * 256));
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int ins = wave_u + 8 * k;
@@ -313,6 +311,17 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  // a finished tile's 64 output rows, staged at box 1 + 0 (bias + ReLU applied)
+  auto store_out = [&](int oe, int oty0, int otx0) {
+    const _Float16* Os = reinterpret_cast<const _Float16*>(lds + kAltBox1);
+    for (int idx = tid; idx < 64 * 16 * !(DROID_ALT_ABL & 16); idx += 512) {
+      const int p = idx >> 4, pc = idx & 15;
+      const long m = ((long)oe * H + oty0 + alt_py(p)) * W + otx0 + alt_px(p);
+      *reinterpret_cast<uint4*>(a.out + m * 128 + pc * 8) = *reinterpret_cast<const uint4*>(&Os[p * kAltOS + pc * 8]);
+    }
+  };
+  bool has_out = false;          // the previous tile's rows wait in the staging area
+  int pe = 0, pty0 = 0, ptx0 = 0;
   int stage = 0;   // profiling stamps only
   (void)stage;
   for (;;) {
@@ -334,8 +343,12 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
       ALT_STAMP(1, ALT_NOW());
       if (st == 0) {
         // the query features (DMA'd during the previous tile's last stage) -> registers,
-        // and every wave is done reading them before box 1 is refilled below
+        // and the previous tile's output rows (staged in box 1) -> HBM; every wave is
+        // done reading both before box 1 is refilled below.  The stores go out here,
+        // not at the end of the previous tile, so that stage-start vmcnt(0) waits only
+        // retire them a stage later instead of waiting for their write latency.
         read_f1(af);
+        if (has_out) store_out(pe, pty0, ptx0);
         __syncthreads();
       }
       const bool fits = (DROID_ALT_ABL & 128) || lvb[4 * l + 2] * lvb[4 * l + 3] <= alt_cap(l);
@@ -512,16 +525,14 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
           acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
         __syncthreads();
-        for (int idx = tid; idx < 64 * 16 * !(DROID_ALT_ABL & 16); idx += 512) {
-          const int p = idx >> 4, pc = idx & 15;
-          const long m = ((long)e * H + ty0 + alt_py(p)) * W + tx0 + alt_px(p);
-          *reinterpret_cast<uint4*>(a.out + m * 128 + pc * 8) = *reinterpret_cast<const uint4*>(&Os[p * kAltOS + pc * 8]);
-        }
+        if (!more) store_out(e, ty0, tx0);   // the last tile: nothing follows to defer to
       }
       ALT_STAMP(6, ALT_NOW());
       ++stage;
     }
     if (!more) break;
+    has_out = true;
+    pe = e; pty0 = ty0; ptx0 = tx0;
     t = tn_;
     cur = nxt;
     slot ^= 1;

@@ -38,6 +38,15 @@ for step in "$@"; do
       cp "$ks" "$O/rocprof_kernel_stats.csv"
       python3 scripts/kstats.py "$O/bench_rocprof.json" "$O/rocprof_kernel_stats.csv" > "$O/rocprof_top.txt"
       head -30 "$O/rocprof_top.txt" ;;
+    rocprof:*)
+      c="${step#rocprof:}"
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/$O/prof_$c" \
+        -o run --output-format csv -- python3 "$R/bench.py" --config "$c" --steps 10 --warmup 3 --no-cpu-baseline \
+        > "$R/$O/bench_rocprof_$c.json" 2> "$R/$O/bench_rocprof_$c.err") || fail "$step" $? "$O/bench_rocprof_$c.err"
+      ks=$(find "$O/prof_$c" -name '*kernel_stats.csv' | head -n 1)
+      cp "$ks" "$O/rocprof_kernel_stats_$c.csv"
+      python3 scripts/kstats.py "$O/bench_rocprof_$c.json" "$O/rocprof_kernel_stats_$c.csv" > "$O/rocprof_top_$c.txt"
+      head -40 "$O/rocprof_top_$c.txt" ;;
     pmc)
       timeout -k 10 900 bash scripts/pmc_traffic.sh > "$O/pmc.log" 2>&1 || fail "$step" $? "$O/pmc.log"
       tail -3 "$O/pmc.log" ;;
