@@ -75,6 +75,13 @@ struct AltArgs {
 #define ALT_STAMP(ph, v) do { } while (0)
 #endif
 #define ALT_NOW() ((long long)__builtin_amdgcn_s_memtime())
+// DROID_ALT_CSTAMP=1 (timing builds): stamps 3/4/5 split the C phase instead
+// (next-box DMA issued / box MFMA done / pixel boxes written)
+#ifndef DROID_ALT_CSTAMP
+#define DROID_ALT_CSTAMP 0
+#endif
+#define ALT_CSTAMP(ph) do { if (DROID_ALT_CSTAMP) ALT_STAMP(ph, ALT_NOW()); } while (0)
+#define ALT_LSTAMP(ph) do { if (!DROID_ALT_CSTAMP) ALT_STAMP(ph, ALT_NOW()); } while (0)
 // timing ablations (scripts only; results are wrong): bit 0 skips the box MFMA,
 // bit 1 the bilinear, bit 2 the encoder MFMA, bit 3 the next-box DMA, bit 4 the
 // output stores, bit 5 the next tile's boxes, bit 6 the frame-index loads, bit 7
@@ -362,10 +369,13 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
         if (stage_fits(slot ^ 1, 3)) stage_dma(nxt, slot ^ 1, 3, 0);
       }
       if (st == 0 && more) coords_dma(nxt, slot ^ 1);
+      ALT_CSTAMP(3);
       // (c) C = F1 x box^T
       if (fits) {
         if (!(DROID_ALT_ABL & 1)) alt_box_mfma(lds, box, Cs, af, min(lvb[4 * l + 2] * lvb[4 * l + 3], alt_cap(l)), 15, -1, wave_u, fr, fq);
+        ALT_CSTAMP(4);
         if (tid < 64) { pix[3 * tid] = lvb[4 * l]; pix[3 * tid + 1] = lvb[4 * l + 1]; pix[3 * tid + 2] = lvb[4 * l + 2]; }
+        ALT_CSTAMP(5);
       } else {
         // slow path: groups = per quadrant its box if it fits, else its 16 pixels' own windows
         // slow path: groups = per half (quadrants 2h, 2h+1) its box if it fits, else
@@ -430,7 +440,7 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
       // box 1 (this stage's box) is free past the output staging: the next tile's
       // query features land there during the bilinear, the encoder and the stores
       if (st == 3 && more) f1_dma(nxt);
-      ALT_STAMP(3, ALT_NOW());
+      ALT_LSTAMP(3);
       // (d) bilinear windows (volume-lookup arithmetic): thread (px, x offset) -> 7 outputs
       // The reference rounds every product and sum of halves through float
       // (at::Half); float carries >= 2*11+2 bits, so that equals the native
@@ -494,7 +504,7 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
         *reinterpret_cast<uint2*>(row + 104) = make_uint2(0u, 0u);
         *reinterpret_cast<uint4*>(row + 112) = make_uint4(0u, 0u, 0u, 0u);
       }
-      ALT_STAMP(4, ALT_NOW());
+      ALT_LSTAMP(4);
       if ((st == 1 || st == 2) && more && wave_u == 7 && !(DROID_ALT_ABL & 32)) {
         // the next tile's level boxes, on the wave the bilinear leaves idle (its
         // coordinates, DMA'd during the first stage, landed at stage 1's wait):
@@ -504,7 +514,7 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
                        st == 1 ? 4 : 2);
       }
       __syncthreads();
-      ALT_STAMP(5, ALT_NOW());
+      ALT_LSTAMP(5);
       // (e) this level's slice of corr_encoder[0]: 64 px x 16 co per wave, K = 64
 #pragma unroll
       for (int s = 0; s < 2 * !(DROID_ALT_ABL & 4); ++s) {

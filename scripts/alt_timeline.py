@@ -40,7 +40,11 @@ st = p[:, 1:, :]                      # skip each workgroup's first stage (prolo
 slow = (st[..., 7] & 1) == 1
 taps = st[..., 7] >> 1
 names = ["box wait + B1", "C (MFMA)", "B2", "bilinear", "B3", "encoder/epilogue"]
-d = np.diff(st[..., :7], axis=-1)
+order = [0, 1, 2, 3, 4, 5, 6]
+if os.environ.get("ALT_CSTAMP") == "1":   # a DROID_ALT_CSTAMP=1 build: stamps 3/4/5 split the C phase
+    names = ["box wait + B1", "next-box DMA issue", "box MFMA", "pixel boxes", "C rest", "bilinear..end"]
+    order = [0, 1, 3, 4, 5, 2, 6]
+d = np.diff(st[..., order], axis=-1)
 lvl = 3 - np.arange(1, 32) % 4
 for l in range(4):
     for kind, m in (("fast", ~slow), ("slow", slow)):
