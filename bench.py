@@ -107,7 +107,10 @@ def build_state(args, rank, world, device):
     video.counter.value = n
     torch.manual_seed(1003)
     net = UpdateModule().to(device).eval()
-    if not args.reference_op:
+    if args.reference_layout:
+        from droid_mi355x.fused import ReferenceLayoutUpdateModule
+        net = ReferenceLayoutUpdateModule(net)
+    elif not args.reference_op:
         from droid_mi355x.fused import FusedUpdateModule
         net = FusedUpdateModule(net)
     corr_impl = "alt" if args.lowmem else args.corr if not args.reference_op else "volume"
@@ -313,7 +316,13 @@ def main():
     ap.add_argument("--breakdown", action="store_true")
     ap.add_argument("--reference-op", action="store_true",
                     help="run the reference-structured UpdateModule (torch/MIOpen convs, NCHW) instead of the fused MFMA operator")
+    ap.add_argument("--reference-layout", action="store_true",
+                    help="the reference's update() structure (NCHW state, materialised lookup) with the MI355X "
+                         "UpdateModule drop-in (ReferenceLayoutUpdateModule): what the reference's own "
+                         "factor_graph.py gets from swapping the module only")
     args = ap.parse_args()
+    if args.reference_layout:
+        args.reference_op = True
     if args.config == "C4" and args.frames == 256:
         args.frames = 128
     if args.config == "C2":
@@ -351,7 +360,7 @@ def main():
                     "corr_alt_ce0" if args.corr == "pyramid" or args.lowmem else "corr_lookup_ce0")
     lookup = KernelTimer(droid_backends, LOOKUP_FN[0])
     zr = zrp = None
-    if not args.reference_op:
+    if not args.reference_op or args.reference_layout:
         zr = KernelTimer(droid_backends, "conv_nhwc_f16", when=lambda *a, **k: k.get("epi") == droid_backends.EPI_GRU_ZR)
         zrp = KernelTimer(droid_backends, "conv_gru_pre_f16", when=lambda *a, **k: a[5] == droid_backends.EPI_GRU_ZR)
 
@@ -445,7 +454,10 @@ def main():
             "config": {"workload": {"C4": "C4 stereo graph", "C3": "C3 global graph", "C5": "C5 2048-KF global graph",
                                     "C2": "C2 frontend window (use_inactive=True)"}[args.config]
                                    + (": update_lowmem(steps=1, itrs=2), on-demand corr" if args.lowmem else
-                                      ": update(itrs=2), %s corr" % args.corr), "keyframes": args.frames,
+                                      ": update(itrs=2), %s corr" % args.corr)
+                                   + (", reference update() layout + MI355X UpdateModule drop-in" if args.reference_layout
+                                      else ", reference-structured torch UpdateModule" if args.reference_op else ""),
+                       "keyframes": args.frames,
                        "edges": len(ii), "image": [args.ht, args.wd], "fmap": [args.ht // 8, args.wd // 8],
                        "parallelism": "edge-sharded x%d (RCCL all-reduce of reduced camera system)" % world},
             "roofline": roofline,

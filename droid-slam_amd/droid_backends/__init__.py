@@ -230,6 +230,27 @@ def corr_alt_ce0(pyramid, f1, f2, coords, w, bias, out=None):
 EPI_ACT, EPI_GRU_ZR, EPI_GRU_Q, EPI_HEAD, EPI_GLO = 0, 1, 2, 3, 4
 
 
+def _conv_operands(fn, B, H, W, cout, dev, bias=None, bbias=None, maps16=(), out32=None):
+    """Dtype / layout / size checks of the conv entry points' side operands (the
+    kernels read them through raw pointers: an fp16 bias from an autocast region,
+    say, would be read as fp32 past its end)."""
+    def vec(t, name, n):
+        if t is None:
+            return
+        if (t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev or t.numel() < n):
+            raise RuntimeError("%s: %s must be a contiguous float32 tensor of >= %d elements on %s"
+                               % (fn, name, n, dev))
+    vec(bias, "bias", cout)
+    vec(bbias, "bbias", B * cout)
+    for name, t in maps16:
+        if t is not None and (t.dtype != torch.float16 or not t.is_contiguous() or t.device != dev
+                              or t.dim() != 4 or tuple(t.shape[:3]) != (B, H, W)):
+            raise RuntimeError("%s: %s must be a contiguous fp16 (B,H,W,C) tensor matching the sources" % (fn, name))
+    if out32 is not None and (out32.dtype != torch.float32 or not out32.is_contiguous() or out32.device != dev
+                              or out32.shape[0] != B):
+        raise RuntimeError("%s: out32 must be a contiguous float32 tensor with one row per image" % fn)
+
+
 def conv_nhwc_f16(sources, wp, cout, ks, bias=None, bbias=None, act=0, epi=EPI_ACT, out=None, out_coff=0,
                   h=None, z=None, zout=None, rnet=None, out32=None, gru_ch=128):
     """Implicit-GEMM MFMA conv (include/droid_backends.h: droid_conv_nhwc_f16).
@@ -245,6 +266,8 @@ def conv_nhwc_f16(sources, wp, cout, ks, bias=None, bbias=None, act=0, epi=EPI_A
     for t, _, _ in sources:
         if t.dtype != torch.float16 or not t.is_contiguous() or t.shape[:3] != (B, H, W):
             raise RuntimeError("conv_nhwc_f16: sources must be contiguous fp16 (B,H,W,C) tensors")
+    _conv_operands("conv_nhwc_f16", B, H, W, int(cout), t0.device, bias, bbias,
+                   (("out", out), ("h", h), ("z", z), ("zout", zout), ("rnet", rnet)), out32)
     out_cs = out.shape[-1] if out is not None else 0
     if epi == EPI_HEAD:
         out_cs = out32.shape[-1]
@@ -280,6 +303,8 @@ def conv_gru_pre_f16(sources, wp, cout, bias, bbias, epi, pre, pre_idx, pre_coff
     _need(pre_idx, torch.int64, "pre_idx")
     if pre.dim() != 4 or tuple(pre.shape[1:3]) != (H, W) or pre_idx.numel() != B:
         raise RuntimeError("conv_gru_pre_f16: pre must be (F,H,W,C) and pre_idx hold one frame per image")
+    _conv_operands("conv_gru_pre_f16", B, H, W, int(cout), t0.device, bias, bbias,
+                   (("out", out), ("h", h), ("z", z), ("zout", zout), ("rnet", rnet)))
     ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() + 2 * off for t, off, _ in sources])
     cs = (ctypes.c_int * n)(*[c for _, _, c in sources])
     strides = (ctypes.c_int * n)(*[t.shape[-1] for t, _, _ in sources])
@@ -309,6 +334,7 @@ def conv_dw_head_f16(sources, wp, bias, head_w, out32):
             raise RuntimeError("conv_dw_head_f16: sources must be contiguous fp16 (B,H,W,C) tensors")
     if out32.dtype != torch.float32 or not out32.is_contiguous() or tuple(out32.shape) != (B, H, W, 4):
         raise RuntimeError("conv_dw_head_f16: out32 must be a contiguous (B,H,W,4) float32 tensor")
+    _conv_operands("conv_dw_head_f16", B, H, W, 256, t0.device, bias)
     ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() + 2 * off for t, off, _ in sources])
     cs = (ctypes.c_int * n)(*[c for _, _, c in sources])
     strides = (ctypes.c_int * n)(*[t.shape[-1] for t, _, _ in sources])

@@ -25,7 +25,11 @@ Same parameters (state-dict names) and forward semantics as UpdateModule
     is computed once per source frame (one 128 -> 384 conv) and added in the
     gate epilogues (droid_conv_gru_pre_f16), and the per-edge gate convs run
     over 320 instead of 448 input channels;
-  * GraphAgg's upmask is not computed: update() discards it (factor_graph.py:209).
+  * GraphAgg's upmask is computed only on request (want_upmask): update()
+    discards it (factor_graph.py:209).
+ReferenceLayoutUpdateModule wraps it behind UpdateModule's own signature and
+tensor layout (NCHW state, materialised 196-channel lookup, 5 outputs), so the
+reference's factor_graph.py runs it with no edit but the module swap.
 All convs: fp16 operands, fp32 accumulation (the reference's autocast).
 """
 import numpy as np
@@ -196,7 +200,15 @@ class FusedUpdateModule(torch.nn.Module):
         self._packed = P
 
     @torch.no_grad()
-    def forward(self, net, inp, corr, motn, inverse, num_unique, segments=None, inp_frames=None):
+    def forward(self, *args, **kwargs):
+        # the kernels take explicit fp16 / fp32 operands: an enclosing autocast
+        # region (the reference's update() runs under one) must not recast the
+        # torch ops in between (addmm would hand an fp16 bias to a conv epilogue)
+        with torch.autocast("cuda", enabled=False):
+            return self._forward(*args, **kwargs)
+
+    def _forward(self, net, inp, corr, motn, inverse, num_unique, segments=None, inp_frames=None, want_upmask=False,
+                 agg=True):
         """net, inp (E,H,W,128) fp16 (inp may be None when inp_frames is given);
         inp_frames: optional (U,H,W,128) fp16 context features per source-frame
         slot (edge e's inp is inp_frames[inverse[e]]); corr (E,H,W,200) fp16 (196 used) or a
@@ -204,7 +216,8 @@ class FusedUpdateModule(torch.nn.Module):
         (E,4,H,W) fp32; inverse (E) frame slot of each edge's source, num_unique
         frames; segments = optional (seg_ptr (U+1), seg_idx (E)) int64 CSR of
         `inverse` (edge_segments) -> net' (E,H,W,128) fp16, delta (1,E,H,W,2)
-        f32, weight (1,E,H,W,2) f32, eta (1,U,H,W) f32."""
+        f32, weight (1,E,H,W,2) f32, eta (1,U,H,W) f32 (None when agg is False),
+        and with want_upmask GraphAgg's upmask (U,H,W,576) fp16 as a fifth output."""
         if self._packed is None:
             self.pack()
         P = self._packed
@@ -281,6 +294,8 @@ class FusedUpdateModule(torch.nn.Module):
             delta = head[..., 0:2].unsqueeze(0)
             weight = head[..., 2:4].unsqueeze(0)
 
+        if not agg:
+            return net_new, delta, weight, None
         a1 = e16(128)
         conv([(net_new, 0, 128)], P["a1"], 128, 3, bias=P["a1_b"], act=1, out=a1)
         if segments is None:
@@ -291,4 +306,54 @@ class FusedUpdateModule(torch.nn.Module):
         er = torch.empty((num_unique, H, W, 1), dtype=torch.float16, device=dev)
         conv([(a2, 0, 128)], P["eta"], 1, 3, bias=P["eta_b"], out=er)
         eta = 0.01 * F.softplus(er.float()).view(1, num_unique, H, W)
+        if want_upmask:   # GraphAgg.upmask (droid_net.py:57): 1x1 128 -> 576 on the aggregated map
+            up = self.m.agg.upmask[0]
+            upmask = F.linear(a2, up.weight[:, :, 0, 0].half(), up.bias.half())
+            return net_new, delta, weight, eta, upmask
         return net_new, delta, weight, eta
+
+
+class ReferenceLayoutUpdateModule(torch.nn.Module):
+    """UpdateModule's own interface (droid_net.py:111-143) on the MI355X kernels:
+    forward(net, inp, corr, flow=None, ii=None, jj=None) with net/inp
+    (1,E,128,H,W) fp16, the materialised lookup corr (1,E,196,H,W) and the
+    motion features flow (1,E,4,H,W) -> (net (1,E,128,H,W) fp16, delta,
+    weight (1,E,H,W,2), eta (1,U,H,W), upmask (1,U,576,H,W)), or the first
+    three when ii is None - so the reference's factor_graph.update()
+    (factor_graph.py:207-208) calls it unchanged.  Each call moves net/inp/corr
+    to channels-last and net/upmask back (the price of the reference layout;
+    FactorGraph here keeps the state channels-last and fuses the lookup).
+    Same parameter names as UpdateModule (state_dict passes through)."""
+
+    def __init__(self, module=None):
+        super().__init__()
+        self.fused = module if isinstance(module, FusedUpdateModule) else FusedUpdateModule(module)
+
+    def load_state_dict(self, *a, **k):
+        return self.fused.load_state_dict(*a, **k)
+
+    def state_dict(self, *a, **k):
+        return self.fused.state_dict(*a, **k)
+
+    @torch.no_grad()
+    def forward(self, net, inp, corr, flow=None, ii=None, jj=None, inverse=None, num_unique=None):
+        batch, num, ch, ht, wd = net.shape
+        if batch != 1:
+            raise RuntimeError("ReferenceLayoutUpdateModule: the factor graph's batch of 1 is supported")
+        dev = net.device
+        cl = lambda t: t[0].permute(0, 2, 3, 1).to(torch.float16).contiguous()
+        net_cl, inp_cl = cl(net), cl(inp)
+        c200 = torch.zeros((num, ht, wd, 200), dtype=torch.float16, device=dev)
+        c200[..., :corr.shape[2]] = corr[0].permute(0, 2, 3, 1)
+        motn = (torch.zeros((num, 4, ht, wd), device=dev) if flow is None
+                else flow.reshape(num, 4, ht, wd).float().contiguous())
+        if ii is None:
+            inverse = torch.zeros(num, dtype=torch.int64, device=dev)
+            n, d, w, _ = self.fused(net_cl, inp_cl, c200, motn, inverse, 1, agg=False)
+            return n.permute(0, 3, 1, 2).unsqueeze(0).contiguous(), d, w
+        if inverse is None:   # GraphAgg's torch.unique (droid_net.py:64), as the reference does
+            uniq, inverse = torch.unique(ii.to(dev), return_inverse=True)
+            num_unique = int(uniq.shape[0])
+        n, d, w, eta, upmask = self.fused(net_cl, inp_cl, c200, motn, inverse, num_unique, want_upmask=True)
+        upmask = upmask.permute(0, 3, 1, 2).unsqueeze(0).contiguous()
+        return n.permute(0, 3, 1, 2).unsqueeze(0).contiguous(), d, w, eta, upmask

@@ -112,3 +112,20 @@ def test_c4_stereo_edges_host_only():
     assert all((j, i) in pairs for i, j in pairs)
     d = np.abs(ii - jj)
     assert ((d >= 1) & (d <= 3)).sum() == 2 * (127 + 126 + 125)
+
+
+def test_conv_side_operands_are_validated_before_launch():
+    """The conv entry points read bias / bbias / the GRU maps through raw
+    pointers: a wrong dtype (e.g. an fp16 bias produced inside an autocast
+    region) is refused on the host before anything is launched."""
+    import torch
+    import droid_backends
+    x = torch.zeros((1, 8, 16, 64), dtype=torch.float16)
+    wp = torch.zeros((128, 9, 64), dtype=torch.float16)
+    out = torch.zeros((1, 8, 16, 128), dtype=torch.float16)
+    for kw in (dict(bias=torch.zeros(128, dtype=torch.float16)),          # fp16 bias
+               dict(bias=torch.zeros(64)),                                 # too short
+               dict(bias=torch.zeros(128), bbias=torch.zeros((1, 128), dtype=torch.float16)),
+               dict(bias=torch.zeros(128), h=torch.zeros((1, 8, 16, 128)))):   # fp32 hidden map
+        with pytest.raises(RuntimeError):
+            droid_backends.conv_nhwc_f16([(x, 0, 64)], wp, 128, 3, out=out, **kw)

@@ -596,3 +596,40 @@ def test_fused_update_matches_reference_module_48x64():
     np.testing.assert_allclose(host(fd), host(rd), atol=3e-2 * max(1.0, float(rd.abs().max())))
     np.testing.assert_allclose(host(fw), host(rw), atol=1.5e-2)
     np.testing.assert_allclose(host(fe), host(re), atol=1e-3 + 2e-2 * float(re.abs().max()))
+
+
+@pytest.mark.parametrize("H,W,E", [(16, 24, 6), (48, 64, 10)])   # generic kernels / band tiles + fused heads
+def test_reference_layout_module_matches_update_module(H, W, E):
+    """ReferenceLayoutUpdateModule is called exactly as the reference's
+    factor_graph.update() calls UpdateModule (factor_graph.py:207-208: NCHW
+    state, materialised 196-channel lookup, 5 outputs incl. upmask) and agrees
+    with the torch module (pinned to the reference by update_module.npz) at
+    fp16 tolerance; without ii it returns the 3-output form."""
+    from droid_mi355x.fused import ReferenceLayoutUpdateModule
+    from droid_mi355x.update import UpdateModule
+    m = UpdateModule().to(DEV).eval()
+    det_fill(m)
+    d = ReferenceLayoutUpdateModule(m)
+    g = torch.Generator(device=DEV).manual_seed(19)
+    net = torch.tanh(torch.randn((1, E, 128, H, W), generator=g, device=DEV)).half()
+    inp = torch.relu(torch.randn((1, E, 128, H, W), generator=g, device=DEV)).half()
+    corr = (2 * torch.randn((1, E, 196, H, W), generator=g, device=DEV)).half()
+    flow = (4 * torch.randn((1, E, 4, H, W), generator=g, device=DEV)).clamp(-64, 64)
+    ii = torch.tensor([0, 0, 1, 2, 2, 3, 1, 3, 0, 2][:E], device=DEV)
+    jj = torch.tensor([1, 2, 0, 1, 3, 2, 3, 0, 3, 0][:E], device=DEV)
+    with torch.no_grad():
+        rn, rd, rw, re, ru = m(net.float(), inp.float(), corr.float(), flow, ii, jj)
+        dn, dd, dw, de, du = d(net, inp, corr, flow, ii, jj)
+        n3 = d(net, inp, corr, flow)
+        with torch.autocast("cuda", enabled=True):   # the reference's update() runs under autocast
+            an, ad, aw, ae, au = d(net, inp, corr, flow, ii, jj)
+    assert dn.shape == rn.shape and dn.dtype == torch.float16
+    assert dd.shape == rd.shape and dw.shape == rw.shape and de.shape == re.shape and du.shape == ru.shape
+    np.testing.assert_allclose(host(dn.float()), host(rn), atol=1.5e-2)
+    np.testing.assert_allclose(host(dd), host(rd), atol=3e-2 * max(1.0, float(rd.abs().max())))
+    np.testing.assert_allclose(host(dw), host(rw), atol=1.5e-2)
+    np.testing.assert_allclose(host(de), host(re), atol=1e-3 + 2e-2 * float(re.abs().max()))
+    np.testing.assert_allclose(host(du.float()), host(ru), atol=3e-2 * max(1.0, float(ru.abs().max())))
+    assert len(n3) == 3 and torch.equal(n3[0], dn) and torch.equal(n3[1], dd) and torch.equal(n3[2], dw)
+    for a, b in ((an, dn), (ad, dd), (aw, dw), (ae, de), (au, du)):
+        assert torch.equal(a, b)
