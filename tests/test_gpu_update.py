@@ -216,3 +216,44 @@ def test_update_lowmem_matches_oracle_composition():
     np.testing.assert_allclose(host(g.damping[u]), ref["damping"][u], atol=1e-3 + 2e-2 * np.abs(ref["damping"][u]).max())
     np.testing.assert_allclose(host(video.poses[:n]), ref["poses"][:n], atol=2e-3)
     np.testing.assert_allclose(host(video.disps[:n]), ref["disps"][:n], atol=2e-2)
+
+
+def test_reference_update_structure_with_dropin_module():
+    """The reference's update() structure (FactorGraph's NCHW path: materialised
+    lookup, update_op(net, inp, corr, motn, ii, jj) under autocast, BA) with the
+    MI355X UpdateModule drop-in (ReferenceLayoutUpdateModule) vs the torch
+    UpdateModule on identical state at 48x64: targets, weights, damping and
+    the hidden state agree at fp16 tolerance, and the BA it drives matches the
+    oracle on the inputs it handed over."""
+    import droid_backends
+    from droid_mi355x.fused import ReferenceLayoutUpdateModule
+    va, ga = _graph(H=48, W=64, seed=41)
+    vb, gb = _graph(H=48, W=64, seed=41)
+    gb.update_op = ReferenceLayoutUpdateModule(gb.update_op)
+    assert not gb.fused
+    captured = {}
+    orig = droid_backends.ba
+
+    def spy(*a, **k):
+        captured["args"] = [x.detach().clone() if isinstance(x, torch.Tensor) else x for x in a]
+        return orig(*a, **k)
+
+    with torch.no_grad():
+        ga.update(itrs=2)
+        droid_backends.ba = spy
+        try:
+            gb.update(itrs=2)
+        finally:
+            droid_backends.ba = orig
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(host(gb.net.float()), host(ga.net.float()), atol=2e-2)
+    np.testing.assert_allclose(host(gb.target), host(ga.target), atol=5e-2 * max(1.0, float(ga.target.abs().max())))
+    np.testing.assert_allclose(host(gb.weight), host(ga.weight), atol=2e-2)
+    n = va.counter.value
+    np.testing.assert_allclose(host(gb.damping[:n]), host(ga.damping[:n]), atol=1e-4 + 3e-2 * float(ga.damping[:n].abs().max()))
+    a = captured["args"]
+    prob = dict(poses=host(a[0]), disps=host(a[1]), intrinsics=host(a[2]), disps_sens=host(a[3]), targets=host(a[4]),
+                weights=host(a[5]), eta=host(a[6]), ii=host(a[7]), jj=host(a[8]), t0=a[9], t1=a[10])
+    ref = oba.ba(**prob, iterations=a[11], lm=a[12], ep=a[13], motion_only=a[14])
+    np.testing.assert_allclose(host(vb.poses[:n]), ref["poses"][:n], atol=1e-4)
+    np.testing.assert_allclose(host(vb.disps[:n]), np.maximum(ref["disps"][:n], 0.001), atol=1e-4)
