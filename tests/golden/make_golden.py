@@ -20,6 +20,7 @@ computed in fp32 on CPU by the reference code itself:
   encoders.npz       BasicEncoder fnet / cnet                (modules/extractor.py, droid_net.py:149-150)
   motion_filter.npz  MotionFilter.track keyframe decisions   (motion_filter.py:45-82)
   geom_ba.npz        geom/ba.py BA / MoBA + their gradients   (geom/ba.py:31-158, geom/chol.py)
+  dense_ba.npz       one undamped geom/ba.py BA step          (geom/ba.py:31-106, chol.py:47-75)
 
 lietorch (un-vendored, v0.2) is needed by geom/projective_ops.py as a working
 group: `LieStandIn.SE3` below restates the lietorch SE3 operations that file
@@ -407,6 +408,69 @@ def geom_ba_fixture(rng):
     np.savez_compressed(os.path.join(HERE, "geom_ba.npz"), **out)
 
 
+def dense_ba_fixture(rng):
+    """geom/ba.py BA (one Gauss-Newton step: linearisation, assembly, Schur
+    complement, LLT, back-substitution, retraction) with geom/chol.py's
+    schur_solve called with ep = lm = 0 - the reference's own functions, only
+    the damping defaults changed, because ba_cuda damps A - S after the Schur
+    complement (droid_kernels.cu:1117-1219) while schur_solve damps H before it;
+    undamped, both compute the same step.  A mono graph with every point in
+    front of both cameras beyond both depth cut-offs (geom 0.2, CUDA 0.25), so
+    it pins droid_backends.ba / oracle/ba.py's step on the reference's Python."""
+    sys.modules["lietorch"].SE3 = LieStandIn.SE3
+
+    def scatter_sum(src, index, dim=-1, dim_size=None):   # torch_scatter.scatter_sum restated
+        dim = dim % src.dim()
+        n = int(index.max()) + 1 if dim_size is None else dim_size
+        shape = list(src.shape)
+        shape[dim] = n
+        return torch.zeros(shape, dtype=src.dtype).index_add_(dim, index, src)
+    sys.modules["torch_scatter"].scatter_sum = scatter_sum
+    import functools
+    import importlib
+    import geom.projective_ops as pops
+    importlib.reload(pops)
+    import geom.chol as gchol
+    importlib.reload(gchol)
+    import geom.ba as gba
+    gba = importlib.reload(gba)
+    gba.schur_solve = functools.partial(gchol.schur_solve, ep=0.0, lm=0.0)
+    P, ht, wd = 6, 16, 24
+    poses = np.zeros((1, P, 7))
+    poses[0, :, 2] = 0.08 * np.arange(P)
+    poses[0, :, :3] += rng.normal(0, 0.01, (P, 3))
+    q = rng.normal(0, 0.01, (P, 3))
+    poses[0, :, 3:6] = q
+    poses[0, :, 6] = np.sqrt(1 - (q ** 2).sum(-1))
+    disps = rng.uniform(0.4, 1.0, (1, P, ht, wd))
+    intr = np.tile([[20.0, 20.0, wd / 2, ht / 2]], (1, P, 1))
+    pairs = [(i, j) for i in range(P) for j in range(P) if 1 <= abs(i - j) <= 2]
+    ii = np.array([a for a, _ in pairs], dtype=np.int64)
+    jj = np.array([b for _, b in pairs], dtype=np.int64)
+    E = len(ii)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64))
+
+    def as_cpu(*a, **k):   # the stereo-edge literal (projective_ops.py:105), on the CPU in float64
+        k.pop("device", None)
+        return torch.tensor(*a, dtype=torch.float64) if not isinstance(a[0], torch.Tensor) else a[0].clone()
+    orig = pops.torch.as_tensor
+    pops.torch.as_tensor = as_cpu
+    try:
+        Gs = LieStandIn.SE3(T(poses))
+        x0, valid = pops.projective_transform(Gs, T(disps), T(intr), torch.from_numpy(ii), torch.from_numpy(jj))[:2]
+        assert bool((valid > 0).all())
+        target = x0 + T(rng.normal(0, 0.5, (1, E, ht, wd, 2)))
+        weight = T(rng.uniform(0.1, 1.0, (1, E, ht, wd, 2)))
+        eta = T(rng.uniform(1e-3, 1e-2, (1, P, ht, wd)))
+        p1, d1 = gba.BA(target, weight, eta, Gs, T(disps), T(intr), torch.from_numpy(ii), torch.from_numpy(jj),
+                        fixedp=1)
+    finally:
+        pops.torch.as_tensor = orig
+    np.savez_compressed(os.path.join(HERE, "dense_ba.npz"), poses=poses, disps=disps, intrinsics=intr, ii=ii, jj=jj,
+                        target=target.numpy(), weight=weight.numpy(), eta=eta.numpy(),
+                        ba_poses=p1.data.numpy(), ba_disps=d1.numpy())
+
+
 def main():
     _install_stubs()
     sys.path.insert(0, REF)
@@ -474,6 +538,9 @@ def main():
 
     # --- differentiable BA (training path) --------------------------------------
     geom_ba_fixture(np.random.default_rng(2029))
+
+    # --- the dense BA step, undamped, from geom/ba.py (pins droid_backends.ba) --
+    dense_ba_fixture(np.random.default_rng(2030))
     print("golden fixtures written to", HERE)
 
 

@@ -101,3 +101,19 @@ def test_ba_plan_reuse_is_deterministic():
         outs.append((host(dx), host(dz), host(poses), host(disps)))
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
+
+
+def test_ba_step_matches_reference_geom_ba(golden_dir):
+    """droid_backends.ba, one undamped step, vs the reference's own geom/ba.py
+    (tests/golden/dense_ba.npz): every pose and the depth frames whose rows do
+    not touch pose t0 within 1e-4 of the reference's Python; frames 0-3 carry
+    ba_cuda's skip of pose t0 in the back-substitution and are checked against
+    the oracle (itself equal to geom/ba.py without that skip, test_oracle_golden)."""
+    from test_oracle_golden import _dense_ba_problem
+    prob, ref_poses, ref_disps = _dense_ba_problem(golden_dir)
+    prob = {k: (v.astype(np.float32) if isinstance(v, np.ndarray) and v.dtype == np.float64 else v)
+            for k, v in prob.items()}
+    got, ref = run_both(prob, iterations=1, lm=0.0, ep=0.0)
+    np.testing.assert_allclose(got["poses"], ref_poses, atol=TOL, rtol=0)
+    np.testing.assert_allclose(got["disps"][4:], ref_disps[4:], atol=TOL, rtol=0)
+    check(got, ref)

@@ -202,3 +202,36 @@ def test_oracle_proximity_edges_match_reference(golden_dir):
     for c in range(int(z["ncases"])):
         args, ref = _proximity_case(z, c)
         np.testing.assert_array_equal(proximity_edges(**args), ref, err_msg="case %d" % c)
+
+
+def _dense_ba_problem(golden_dir):
+    """dense_ba.npz (geom/ba.py's undamped BA step, made by make_golden.py) as
+    droid_backends.ba / oracle.ba arguments: t0 = fixedp = 1, one iteration,
+    lm = ep = 0 (schur_solve damps H before the Schur complement, ba_cuda
+    damps A - S after it: undamped they are the same step), geom's C + eta +
+    1e-7 as eta + 1e-7, no sensor depth."""
+    d = np.load(os.path.join(golden_dir, "dense_ba.npz"))
+    prob = dict(poses=d["poses"][0], disps=d["disps"][0], intrinsics=d["intrinsics"][0][0],
+                disps_sens=np.zeros_like(d["disps"][0]), targets=d["target"][0].transpose(0, 3, 1, 2),
+                weights=d["weight"][0].transpose(0, 3, 1, 2), eta=d["eta"][0] + 1e-7, ii=d["ii"], jj=d["jj"],
+                t0=1, t1=d["poses"].shape[1])
+    return prob, d["ba_poses"][0], d["ba_disps"][0]
+
+
+def test_oracle_ba_step_matches_reference_geom_ba(golden_dir):
+    """The oracle's ba_cuda restatement (linearisation, block assembly, Schur
+    complement, LLT, back-substitution, retraction) equals the reference's own
+    geom/ba.py step to 1e-9 when the back-substitution keeps pose t0's rows.
+    ba_cuda drops them (EvT6x1's idx <= 0 skip, droid_kernels.cu:1095-1115), so
+    with that skip only the depth frames none of whose rows touch pose t0 (here
+    4 and 5) still agree; frames 0-3 move by ~1e-2 (documented)."""
+    from oracle import ba as oba
+    prob, ref_poses, ref_disps = _dense_ba_problem(golden_dir)
+    kw = dict(iterations=1, lm=0.0, ep=0.0, motion_only=False)
+    full = oba.ba(**prob, **kw, skip_t0_backsub=False)
+    np.testing.assert_allclose(full["poses"], ref_poses, atol=1e-9, rtol=0)
+    np.testing.assert_allclose(full["disps"], ref_disps, atol=1e-9, rtol=0)
+    cuda = oba.ba(**prob, **kw, skip_t0_backsub=True)
+    np.testing.assert_allclose(cuda["poses"], ref_poses, atol=1e-9, rtol=0)
+    np.testing.assert_allclose(cuda["disps"][4:], ref_disps[4:], atol=1e-9, rtol=0)
+    assert np.abs(cuda["disps"][:4] - ref_disps[:4]).max() > 1e-3
