@@ -129,10 +129,22 @@ __global__ void __launch_bounds__(256) ba_edge_hessian_kernel(BaDev d) {
     const float* tg = d.targets + (long)e * 2 * HW;
     const float* wt = d.weights + (long)e * 2 * HW;
     const float* dp = d.disps + (long)i * HW;
-    for (int p = p0 + threadIdx.x; p < p1; p += 256) {
+    // the next pixel's five inputs are loaded before this one is linearised, so
+    // their HBM latency hides under the ~200 FMAs of the current pixel (164 ->
+    // 145 us at C3).  Measured and dropped: summing only S = sum w Jj Jj^T and
+    // g = sum w r Jj and mapping them through Ji = -Adj(Tij)^T Jj once per edge
+    // (3.3x fewer FMAs, 27 instead of 90 accumulators): M S M^T cancels for
+    // long baselines, and even with fp64 sums it moved C3 results across the
+    // 1e-4 parity bar, where the reference's per-pixel accumulation stays inside.
+    int p = p0 + threadIdx.x;
+    float nd = 0.f, ntu = 0.f, ntv = 0.f, nwu = 0.f, nwv = 0.f;
+    if (p < p1) { nd = dp[p]; ntu = tg[p]; ntv = tg[HW + p]; nwu = wt[p]; nwv = wt[HW + p]; }
+    for (; p < p1; p += 256) {
+      const float cd = nd, ctu = ntu, ctv = ntv, cwu = nwu, cwv = nwv;
+      const int q = p + 256;
+      if (q < p1) { nd = dp[q]; ntu = tg[q]; ntv = tg[HW + q]; nwu = wt[q]; nwv = wt[HW + q]; }
       PixLin L;
-      linearize_pixel(T, false, fx, fy, cx, cy, (float)(p % d.W), (float)(p / d.W), dp[p],
-                      tg[p], tg[HW + p], wt[p], wt[HW + p], L);
+      linearize_pixel(T, false, fx, fy, cx, cy, (float)(p % d.W), (float)(p / d.W), cd, ctu, ctv, cwu, cwv, L);
       float Jx[12];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
