@@ -920,6 +920,17 @@ __device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn
 template <int TN>
 constexpr bool kBandSwap = TN != 256;
 
+// (1 - z) h + z q on packed fp16, every op rounded (no contraction into an
+// fma): the reference's autocast evaluates the GRU blend as fp16 tensor ops
+__device__ __forceinline__ half8 gru_blend_f16(half8 z, half8 h, half8 q) {
+#pragma clang fp contract(off)
+  const half8 one = {(_Float16)1.f, (_Float16)1.f, (_Float16)1.f, (_Float16)1.f,
+                     (_Float16)1.f, (_Float16)1.f, (_Float16)1.f, (_Float16)1.f};
+  const half8 a = (one - z) * h;
+  const half8 b = z * q;
+  return a + b;
+}
+
 template <int TMX, int TN, int FM, int FN, int WM = 4, bool CONTIG = false, int NT = 512, int EPI = -1>
 __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
                                               int n0, int wm, int wn, int lane, int tid, float bcol,
@@ -1036,20 +1047,21 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
   for (int q = 0; q < RND; ++q) {
     const long m = mrow + q * RQ;
     half8 v = *reinterpret_cast<const half8*>(&smem[(r0 + q * RQ) * ER + p * 8]);
+    // The gate algebra runs on packed fp16 (v_pk_add / v_pk_mul_f16, no f32
+    // round trips), each op rounded as the reference's autocast fp16 tensor ops
+    // round it (gru.py:27-32: conv + glo, r * h, (1 - z) * h + z * q); only the
+    // sigmoid / tanh go through f32 (torch evaluates them in f32 and rounds).
     if constexpr (kPre) {
+      const half8 x = v + ppre[q];   // the gate argument: per-edge conv + per-frame term
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float x = (float)v[e] + (float)ppre[q][e];
-        v[e] = (_Float16)(EB == EPI_GRU_ZR ? sigmoid_fast(x) : tanh_fast(x));
-      }
+      for (int e = 0; e < 8; ++e) v[e] = (_Float16)(EB == EPI_GRU_ZR ? sigmoid_fast((float)x[e]) : tanh_fast((float)x[e]));
     }
     if (epi == EPI_GRU_ZR) {
       if (rhalf) {
         half8 h;
         if constexpr (kPreH) h = hpre[q];
         else h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c - a.gru_ch);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (_Float16)((float)v[e] * (float)h[e]);
+        v = v * h;   // exact products rounded once: the same bits as the f32 product rounded
       }
     } else if (epi == EPI_GRU_Q) {
       half8 h, z;
@@ -1060,11 +1072,7 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
         h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c);
         z = *reinterpret_cast<const half8*>(a.z + m * a.z_cstride + c);
       }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float zv = (float)z[e];
-        v[e] = (_Float16)((1.0f - zv) * (float)h[e] + zv * (float)v[e]);
-      }
+      v = gru_blend_f16(z, h, v);
     }
     outv[q] = v;
   }
