@@ -1013,10 +1013,26 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
       const int c = wn * FN * 16 + j * 16 + fr;
       const float bv = bl[c];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i) {
+        if constexpr (kPre) {
+          // the staged pre-activation: bias added two values at a time (v_pk_add_f32)
+          // and rounded two at a time (v_cvt_pk_f16_f32); the halves go to their rows
+          typedef float f2_t __attribute__((ext_vector_type(2)));
+          typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+          const f2_t b2 = {bv, bv};
+          const f2_t lo = f2_t{acc[i][j][0], acc[i][j][1]} + b2, hi = f2_t{acc[i][j][2], acc[i][j][3]} + b2;
+          const h2_t l16 = __builtin_convertvector(lo, h2_t), h16 = __builtin_convertvector(hi, h2_t);
+          _Float16* const d = &smem[(frag_row<FM, WM, CONTIG>(wm, i) + fq * 4) * ER + c];
+          d[0] = l16[0];
+          d[ER] = l16[1];
+          d[2 * ER] = h16[0];
+          d[3 * ER] = h16[1];
+        } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          smem[(frag_row<FM, WM, CONTIG>(wm, i) + fq * 4 + k) * ER + c] = (_Float16)act(acc[i][j][k] + bv);
+          for (int k = 0; k < 4; ++k)
+            smem[(frag_row<FM, WM, CONTIG>(wm, i) + fq * 4 + k) * ER + c] = (_Float16)act(acc[i][j][k] + bv);
+        }
+      }
     }
   }
   if (prof && tid == 0) prof[6] = (long long)__builtin_amdgcn_s_memtime();  // pass 1 written
@@ -1053,8 +1069,25 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
     // sigmoid / tanh go through f32 (torch evaluates them in f32 and rounds).
     if constexpr (kPre) {
       const half8 x = v + ppre[q];   // the gate argument: per-edge conv + per-frame term
+      // sigmoid / tanh two at a time: the exp argument scaling and the "+ 1" on
+      // packed f32 (v_pk_mul_f32 / v_pk_add_f32), exp and rcp per value
+      typedef float f2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (_Float16)(EB == EPI_GRU_ZR ? sigmoid_fast((float)x[e]) : tanh_fast((float)x[e]));
+      for (int e = 0; e < 8; e += 2) {
+        const f2_t xf = {(float)x[e], (float)x[e + 1]};
+        const f2_t t = xf * (EB == EPI_GRU_ZR ? f2_t{-1.4426950408889634f, -1.4426950408889634f}
+                                              : f2_t{2.8853900817779268f, 2.8853900817779268f});
+        const f2_t den = f2_t{__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])} + f2_t{1.0f, 1.0f};
+        const f2_t r = {__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+        if constexpr (EB == EPI_GRU_ZR) {   // sigmoid(x) = 1 / (1 + 2^(-x log2 e))
+          v[e] = (_Float16)r[0];
+          v[e + 1] = (_Float16)r[1];
+        } else {                            // tanh(x) = 1 - 2 / (1 + 2^(2x log2 e))
+          const f2_t th = f2_t{1.0f, 1.0f} - f2_t{2.0f, 2.0f} * r;
+          v[e] = (_Float16)th[0];
+          v[e + 1] = (_Float16)th[1];
+        }
+      }
     }
     if (epi == EPI_GRU_ZR) {
       if (rhalf) {
