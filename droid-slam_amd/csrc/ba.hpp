@@ -73,6 +73,7 @@ struct CholStructure {
   int n = 0, nbc = 0, nbr = 0, nslots = 0, nslots_a = 0;
   std::vector<int> slot, fin, ycnt, tasks;
   int ntasks = 0;
+  double cp = 0.0, work = 0.0;  // critical path and total cost of the task graph (task-cost units)
 };
 
 // pattern: lower tile (i,j) of the input system is nonzero; slots of these come
@@ -105,7 +106,7 @@ struct BaPlan {
   long gram_floats = 0;
   // pose order: perm[a] = elimination position of pose a; outmap[v] = dx index of permuted var v
   std::vector<int> perm, outmap;
-  int order_kind = 0;                   // 0 identity, 1 reverse Cuthill-McKee, 2 minimum degree
+  int order_kind = 0;                   // 0 identity, 1 reverse Cuthill-McKee, 2 minimum degree, 3 nested dissection
   CholStructure cs;
   size_t sync_bytes = 0;                // ticket, abort, tile versions, y versions, x flags
   // device layout (byte offsets into the workspace)

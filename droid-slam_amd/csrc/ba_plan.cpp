@@ -227,11 +227,14 @@ void build_chol_structure(int n, const std::vector<char>& pattern, CholStructure
   for (size_t q = 0; q < order.size(); ++q)
     for (int s2 : t[order[q]].succ)
       if (--indeg[s2] == 0) order.push_back(s2);
+  cs.cp = cs.work = 0.0;
   for (int q = (int)order.size() - 1; q >= 0; --q) {
     Node& nd = t[order[q]];
     double m = 0.0;
     for (int s2 : nd.succ) m = std::max(m, 1.0 + t[s2].bl);
     nd.bl = nd.cost + m;
+    cs.cp = std::max(cs.cp, nd.bl);
+    cs.work += nd.cost;
   }
   // list scheduling by bottom level: tickets are a topological order, so a
   // task never waits on one that has not been handed out
@@ -331,6 +334,97 @@ static std::vector<int> order_mindeg(int P, const std::vector<std::vector<int>>&
   return perm;
 }
 
+// Nested dissection on 64-variable tile boundaries: a block of poses is ordered
+// [ND(A), ND(B), S], A = the first m poses of a breadth-first sweep from a
+// pseudo-peripheral pose (m near half, chosen so that B starts on a tile
+// boundary: 6 (base + m) = 0 mod 64), S = the poses outside A adjacent to it
+// (a vertex separator), B = the rest.  A and B then share no tile column, so
+// their factorisations are independent subtrees and the Cholesky's critical
+// path is the tree height instead of the whole band (a lapping trajectory's
+// revisit edges make the reduced system a banded cylinder whose band RCM cannot
+// narrow).
+static void nd_block(std::vector<int> nodes, int base, const std::vector<std::vector<int>>& adj,
+                     std::vector<int>& region, int& rid, std::vector<int>& out) {
+  constexpr int kLeaf = 32;  // poses per tile-aligned leaf (= 3 tiles)
+  const int sz = (int)nodes.size();
+  if (sz <= kLeaf) {
+    std::sort(nodes.begin(), nodes.end());
+    out.insert(out.end(), nodes.begin(), nodes.end());
+    return;
+  }
+  const int me = ++rid;
+  for (int v : nodes) region[v] = me;
+  std::vector<int> lvl(adj.size(), -1);
+  auto bfs = [&](int s, std::vector<int>& seq) {
+    seq.clear();
+    for (int v : nodes) lvl[v] = -1;
+    seq.push_back(s);
+    lvl[s] = 0;
+    for (size_t q = 0; q < seq.size(); ++q)
+      for (int b : adj[seq[q]])
+        if (region[b] == me && lvl[b] < 0) { lvl[b] = lvl[seq[q]] + 1; seq.push_back(b); }
+  };
+  std::vector<int> seq;
+  bfs(*std::min_element(nodes.begin(), nodes.end()), seq);
+  if ((int)seq.size() < sz) {  // disconnected: the components one after another
+    std::vector<int> rest;
+    for (int v : nodes) if (lvl[v] < 0) rest.push_back(v);
+    std::vector<int> comp = seq;
+    nd_block(comp, base, adj, region, rid, out);
+    for (int v : rest) region[v] = me;  // (the call above re-tagged its own nodes)
+    nd_block(rest, base + (int)comp.size(), adj, region, rid, out);
+    return;
+  }
+  for (int it = 0; it < 3; ++it) {  // pseudo-peripheral start
+    const int far = seq.back();
+    std::vector<int> s2;
+    bfs(far, s2);
+    if (lvl[s2.back()] <= lvl[seq.back()] && it > 0) break;
+    seq.swap(s2);
+  }
+  // m: B's first pose on a tile boundary, as close to half as possible
+  int m = -1;
+  for (int c = ((base + sz / 2) / 32) * 32 - base, d = 0; d <= sz; d += 32) {
+    for (int cand : {c + d, c - d + 32, c - d})
+      if (cand >= kLeaf / 2 && cand <= sz - kLeaf / 2 && (m < 0 || std::abs(cand - sz / 2) < std::abs(m - sz / 2)))
+        m = cand;
+    if (m >= 0) break;
+  }
+  if (m < 0) {
+    std::sort(nodes.begin(), nodes.end());
+    out.insert(out.end(), nodes.begin(), nodes.end());
+    return;
+  }
+  std::vector<char> inA(adj.size(), 0);
+  for (int q = 0; q < m; ++q) inA[seq[q]] = 1;
+  std::vector<int> A(seq.begin(), seq.begin() + m), B, S;
+  for (int q = m; q < sz; ++q) {
+    const int v = seq[q];
+    bool sep = false;
+    for (int b : adj[v]) if (region[b] == me && inA[b]) { sep = true; break; }
+    (sep ? S : B).push_back(v);
+  }
+  if (B.empty()) {
+    std::sort(nodes.begin(), nodes.end());
+    out.insert(out.end(), nodes.begin(), nodes.end());
+    return;
+  }
+  nd_block(A, base, adj, region, rid, out);
+  nd_block(B, base + m, adj, region, rid, out);
+  std::sort(S.begin(), S.end());
+  out.insert(out.end(), S.begin(), S.end());
+}
+
+static std::vector<int> order_nd(int P, const std::vector<std::vector<int>>& adj) {
+  std::vector<int> nodes(P), out, region(P, 0);
+  for (int a = 0; a < P; ++a) nodes[a] = a;
+  int rid = 0;
+  nd_block(nodes, 0, adj, region, rid, out);
+  std::vector<int> perm(P);
+  for (int q = 0; q < P; ++q) perm[out[q]] = q;
+  return perm;
+}
+
 static void tile_pattern(int n, int P, const std::vector<int>& perm, const std::vector<std::pair<int, int>>& pairs,
                          std::vector<char>& pat) {
   const int nbc = (n + 63) / 64, nbr = (n + 1 + 63) / 64;
@@ -345,18 +439,6 @@ static void tile_pattern(int n, int P, const std::vector<int>& perm, const std::
     const int pa = perm[pr.first], pb = perm[pr.second];
     mark(std::max(pa, pb), std::min(pa, pb));
   }
-}
-
-static long order_cost(int n, int P, const std::vector<int>& perm, const std::vector<std::pair<int, int>>& pairs) {
-  std::vector<char> pat;
-  tile_pattern(n, P, perm, pairs, pat);
-  TileBits tb;
-  init_bits(tb, n);
-  for (int i = 0; i < tb.nbr; ++i)
-    for (int j = 0; j <= std::min(i, tb.nbc - 1); ++j)
-      if (pat[(size_t)i * tb.nbc + j]) tb.set(i, j);
-  close_bits(tb);
-  return count_updates(tb);
 }
 
 // the reduced system's pose-pair pattern: edge blocks (i,j) and Schur blocks of
@@ -397,28 +479,74 @@ static void pose_pairs(const std::vector<int>& gi, const std::vector<int>& gj, i
   pairs.erase(std::unique(pairs.begin(), pairs.end()), pairs.end());
 }
 
+// tile updates of the factorisation under a pose order (its dominant work)
+static long order_updates(int n, int P, const std::vector<int>& perm, const std::vector<std::pair<int, int>>& pairs) {
+  std::vector<char> pat;
+  tile_pattern(n, P, perm, pairs, pat);
+  TileBits tb;
+  init_bits(tb, n);
+  for (int i = 0; i < tb.nbr; ++i)
+    for (int j = 0; j <= std::min(i, tb.nbc - 1); ++j)
+      if (pat[(size_t)i * tb.nbc + j]) tb.set(i, j);
+  close_bits(tb);
+  return count_updates(tb);
+}
+
+// The pose order: the candidate whose task graph the dataflow Cholesky (one
+// persistent workgroup per CU) is expected to finish first, i.e. the smaller of
+// max(critical path, work / workers) in task-cost units; the identity is kept
+// unless a candidate beats it by more than 5 %.
+static double chol_makespan(int n, int P, const std::vector<int>& perm, const std::vector<std::pair<int, int>>& pairs) {
+  constexpr double kWorkers = 256.0;
+  std::vector<char> pat;
+  tile_pattern(n, P, perm, pairs, pat);
+  CholStructure cs;
+  build_chol_structure(n, pat, cs);
+  return std::max(cs.cp, cs.work / kWorkers);
+}
+
 static void choose_order(BaPlan& p, const std::vector<std::pair<int, int>>& pairs) {
   const int P = p.P, n = p.n;
   std::vector<int> ident(P);
   for (int a = 0; a < P; ++a) ident[a] = a;
   p.perm = ident;
   p.order_kind = 0;
-  const char* force = getenv("DROID_BA_ORDER");  // identity | rcm | mindeg (A/B and tests)
+  const char* force = getenv("DROID_BA_ORDER");  // identity | rcm | mindeg | nd (A/B and tests)
   if (P <= 32 && !force) return;                  // a handful of tiles: nothing to gain
   std::vector<std::vector<int>> adj(P);
   for (auto& pr : pairs) { adj[pr.first].push_back(pr.second); adj[pr.second].push_back(pr.first); }
+  auto make = [&](int kind) {
+    return kind == 1 ? order_rcm(P, adj) : kind == 2 ? order_mindeg(P, adj) : order_nd(P, adj);
+  };
   if (force) {
     const std::string f(force);
-    if (f == "rcm") { p.perm = order_rcm(P, adj); p.order_kind = 1; }
-    else if (f == "mindeg") { p.perm = order_mindeg(P, adj); p.order_kind = 2; }
+    const int kind = f == "rcm" ? 1 : f == "mindeg" ? 2 : f == "nd" ? 3 : 0;
+    if (kind) { p.perm = make(kind); p.order_kind = kind; }
     return;
   }
-  long best = order_cost(n, P, ident, pairs);
-  // the identity is kept unless an ordering saves more than 5 % of the tile updates
-  for (int kind = 1; kind <= 2; ++kind) {
-    std::vector<int> perm = kind == 1 ? order_rcm(P, adj) : order_mindeg(P, adj);
-    const long c = order_cost(n, P, perm, pairs);
-    if (c * 20 < best * 19) { best = c; p.perm = perm; p.order_kind = kind; }
+  // the task graph (the critical path) is built only for orders whose tile
+  // update count is within 4x of the fewest: a fill-heavy order's graph is
+  // large (~1M tasks for the identity at C5) and never the fastest
+  const bool verbose = getenv("DROID_BA_PLAN_VERBOSE") != nullptr;
+  std::vector<std::vector<int>> perms(4);
+  std::vector<long> upd(4);
+  perms[0] = ident;
+  for (int kind = 0; kind <= 3; ++kind) {
+    if (kind) perms[kind] = make(kind);
+    upd[kind] = order_updates(n, P, perms[kind], pairs);
+  }
+  const long umin = *std::min_element(upd.begin(), upd.end());
+  double keep = -1.0, best = -1.0;
+  for (int kind = 0; kind <= 3; ++kind) {
+    if (upd[kind] > 4 * umin + 64) continue;
+    const double c = chol_makespan(n, P, perms[kind], pairs);
+    if (verbose) fprintf(stderr, "ba plan P=%d order %d: %ld tile updates, makespan %.0f\n", P, kind, upd[kind], c);
+    if (kind == 0) { keep = best = c; continue; }
+    if (best < 0 || (c < best && (keep < 0 || c * 20 < keep * 19))) {
+      best = c;
+      p.perm = perms[kind];
+      p.order_kind = kind;
+    }
   }
 }
 

@@ -624,7 +624,7 @@ class BaPlan:
         perm = np.zeros(max(self.P, 1), dtype=np.int32)
         check(lib.droid_ba_plan_order(h, ctypes.byref(kind), perm.ctypes.data_as(ctypes.c_void_p),
                                       ctypes.byref(nwide), ctypes.byref(ntasks)), "ba plan order")
-        self.order = ("identity", "rcm", "mindeg")[kind.value]
+        self.order = ("identity", "rcm", "mindeg", "nd")[kind.value]
         self.perm = perm[:self.P]
         self.num_wide, self.ntasks = nwide.value, ntasks.value
         nbytes = lib.droid_ba_plan_workspace_bytes(h)

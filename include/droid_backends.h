@@ -293,7 +293,8 @@ size_t droid_ba_plan_workspace_bytes(const void* plan);
 /* nb_max = largest Schur Gram tile count (16 variables) of any depth frame */
 int droid_ba_plan_info(const void* plan, int* K, int* P, int* nblocks, int* nb_max);
 int droid_ba_plan_kx(const void* plan, int64_t* kx_host);
-/* kind 0 identity / 1 reverse Cuthill-McKee / 2 minimum degree; perm[pose] =
+/* kind 0 identity / 1 reverse Cuthill-McKee / 2 minimum degree / 3 nested
+ * dissection (tile-aligned); perm[pose] =
  * elimination position (P ints); frames on the wide Schur path; tile tasks */
 int droid_ba_plan_order(const void* plan, int* kind, int* perm, int* num_wide, int* ntasks);
 /* the reduced system's input tiles inside the workspace: 64x64 fp64 tiles of

@@ -238,6 +238,9 @@ def _graph(name):
     if name == "C5":
         ii, jj = synthetic.c5_edges()
         return ii, jj, 2048, 1, 2048
+    if name == "laps":   # C5's lapping trajectory at 512 KF: the plan picks nested dissection
+        ii, jj = synthetic.c5_edges(num_kf=512, lap=64)
+        return ii, jj, 512, 1, 512
     if name == "band":   # +-1..+-3 only: block-tridiagonal in tiles after any sane order
         ii, jj = synthetic.c5_edges(num_kf=600, loop_pairs=0)
         return ii, jj, 600, 1, 600
@@ -253,6 +256,19 @@ def test_ba_plan_task_list_solves_reduced_system(name):
     _check_solves(st, _spd_with_blocks(P, pairs, rng), st["perm"], rng)
 
 
+def test_nested_dissection_order_solves():
+    """A lapping trajectory's reduced system is a banded cylinder: the plan
+    picks the tile-aligned nested dissection (kind 3) for its shorter Cholesky
+    critical path, and that task list solves the system."""
+    ii, jj, N, t0, t1 = _graph("laps")
+    st = ba_plan(ii, jj, N, t0, t1)
+    assert st["kind"] == 3
+    assert sorted(st["perm"].tolist()) == list(range(t1 - t0))
+    pairs, P = _pose_pairs(ii, jj, t0, t1)
+    rng = np.random.default_rng(9)
+    _check_solves(st, _spd_with_blocks(P, pairs, rng), st["perm"], rng)
+
+
 def test_c5_plan_is_tile_sparse():
     """2048 KF / ~16k edges with revisit loops: the chosen
     pose order keeps the factor far from dense, and the plan builds in well
@@ -262,18 +278,18 @@ def test_c5_plan_is_tile_sparse():
     st = ba_plan(ii, jj, N, t0, t1)
     nbc = st["nbc"]
     dense = sum(min(i + 1, nbc) for i in range(st["nbr"]))
-    assert st["kind"] != 0 and st["nslots"] < 0.15 * dense
+    assert st["kind"] != 0 and st["nslots"] < 0.2 * dense
     assert st["plan_seconds"] < 5.0
     # the all-reduced region (input tiles) of a sharded C5 BA
     assert st["nslots_input"] * 64 * 64 * 8 < 150e6
 
 
-@pytest.mark.parametrize("order", ["rcm", "mindeg"])
+@pytest.mark.parametrize("order", ["rcm", "mindeg", "nd"])
 def test_forced_orders_solve(order, monkeypatch):
     monkeypatch.setenv("DROID_BA_ORDER", order)
     ii, jj, N, t0, t1 = _graph("C2")
     st = ba_plan(ii, jj, N, t0, t1)
-    assert st["kind"] == {"rcm": 1, "mindeg": 2}[order]
+    assert st["kind"] == {"rcm": 1, "mindeg": 2, "nd": 3}[order]
     assert sorted(st["perm"].tolist()) == list(range(t1 - t0))
     pairs, P = _pose_pairs(ii, jj, t0, t1)
     rng = np.random.default_rng(8)
