@@ -912,6 +912,31 @@ __device__ __forceinline__ float tanh_fast(float x) {
 // sigmoid for fp16-rounded gates: 1 / (1 + e^-x) with the hardware reciprocal
 __device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
+// Pass-1 staging of a pixels x weights fragment: lane (fr, fq) holds 4
+// consecutive pixels (rows row0 .. row0 + 3) of one channel c as two fp16 pairs
+// (lo = pixels 0, 1; hi = pixels 2, 3).  Written as they are that is four 2-B
+// LDS stores.  Instead the two lanes of adjacent channels trade one pair (DPP
+// quad_perm [1,0,3,2]): the even lane then holds channels c, c + 1 of pixels 0
+// and 1, the odd lane those of pixels 2 and 3, and each writes two 4-B words
+// (half the LDS store instructions; conflict-free with the ER = TN + 8 row pitch).
+__device__ __forceinline__ void stage_pixel_pairs(_Float16* smem, int row0, int c, int ER, int fr, unsigned lo,
+                                                  unsigned hi) {
+  const bool odd = fr & 1;
+  const unsigned x = odd ? lo : hi;
+  const unsigned r = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+  const unsigned ca = odd ? r : lo;   // channel c & ~1
+  const unsigned cb = odd ? hi : r;   // channel (c & ~1) + 1
+  unsigned* d = reinterpret_cast<unsigned*>(&smem[(row0 + (odd ? 2 : 0)) * ER + (c & ~1)]);
+  d[0] = (ca & 0xFFFFu) | (cb << 16);
+  d[ER / 2] = (ca >> 16) | (cb & 0xFFFF0000u);
+}
+__device__ __forceinline__ unsigned pack_f16x2(float a, float b) {
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  const h2_t h = __builtin_convertvector(f2_t{a, b}, h2_t);
+  return __builtin_bit_cast(unsigned, h);
+}
+
 // kBandSwap: the main loop multiplies weights x pixels (MFMA A = weight
 // fragment), so a lane's accumulators are 4 consecutive channels of one pixel
 // and the epilogue's LDS staging writes 8 B per fragment instead of four 2-B
@@ -1022,15 +1047,12 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
           const f2_t b2 = {bv, bv};
           const f2_t lo = f2_t{acc[i][j][0], acc[i][j][1]} + b2, hi = f2_t{acc[i][j][2], acc[i][j][3]} + b2;
           const h2_t l16 = __builtin_convertvector(lo, h2_t), h16 = __builtin_convertvector(hi, h2_t);
-          _Float16* const d = &smem[(frag_row<FM, WM, CONTIG>(wm, i) + fq * 4) * ER + c];
-          d[0] = l16[0];
-          d[ER] = l16[1];
-          d[2 * ER] = h16[0];
-          d[3 * ER] = h16[1];
+          stage_pixel_pairs(smem, frag_row<FM, WM, CONTIG>(wm, i) + fq * 4, c, ER, fr,
+                            __builtin_bit_cast(unsigned, l16), __builtin_bit_cast(unsigned, h16));
         } else {
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            smem[(frag_row<FM, WM, CONTIG>(wm, i) + fq * 4 + k) * ER + c] = (_Float16)act(acc[i][j][k] + bv);
+          stage_pixel_pairs(smem, frag_row<FM, WM, CONTIG>(wm, i) + fq * 4, c, ER, fr,
+                            pack_f16x2(act(acc[i][j][0] + bv), act(acc[i][j][1] + bv)),
+                            pack_f16x2(act(acc[i][j][2] + bv), act(acc[i][j][3] + bv)));
         }
       }
     }
@@ -1158,9 +1180,9 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
     const float bv = bl[c];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        T[(frag_row<FM, WM, CONTIG>(wm, i) + fq * 4 + k) * TS + c] = (_Float16)fmaxf(acc[i][j][k] + bv, 0.f);
+      stage_pixel_pairs(T, frag_row<FM, WM, CONTIG>(wm, i) + fq * 4, c, TS, fr,
+                        pack_f16x2(fmaxf(acc[i][j][0] + bv, 0.f), fmaxf(acc[i][j][1] + bv, 0.f)),
+                        pack_f16x2(fmaxf(acc[i][j][2] + bv, 0.f), fmaxf(acc[i][j][3] + bv, 0.f)));
   }
   for (int idx = tid; idx < 48 * 32; idx += NT) {
     const int r = idx >> 5, p = idx & 31;
