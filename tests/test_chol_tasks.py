@@ -269,6 +269,25 @@ def test_nested_dissection_order_solves():
     _check_solves(st, _spd_with_blocks(P, pairs, rng), st["perm"], rng)
 
 
+def test_nested_dissection_disconnected_graph_solves(monkeypatch):
+    """Forced nested dissection on a pose graph in three pieces (two lapping
+    trajectories and a run of poses without edges): every pose is ordered once
+    and the task list still solves the reduced system."""
+    from droid_mi355x import synthetic
+    monkeypatch.setenv("DROID_BA_ORDER", "nd")
+    a_i, a_j = synthetic.c5_edges(num_kf=160, lap=40)
+    b_i, b_j = synthetic.c5_edges(num_kf=120, lap=30)
+    ii = np.concatenate([a_i, b_i + 200])
+    jj = np.concatenate([a_j, b_j + 200])
+    N, t0, t1 = 320, 1, 320   # poses 160..199 and 320.. have no edges
+    st = ba_plan(ii, jj, N, t0, t1)
+    assert st["kind"] == 3
+    assert sorted(st["perm"].tolist()) == list(range(t1 - t0))
+    pairs, P = _pose_pairs(ii, jj, t0, t1)
+    rng = np.random.default_rng(10)
+    _check_solves(st, _spd_with_blocks(P, pairs, rng), st["perm"], rng)
+
+
 def test_c5_plan_is_tile_sparse():
     """2048 KF / ~16k edges with revisit loops: the chosen
     pose order keeps the factor far from dense, and the plan builds in well
