@@ -89,6 +89,27 @@ def test_ba_global_c3():
     check(got, ref)
 
 
+@pytest.mark.parametrize("order", ["rcm", "mindeg", "nd"])
+def test_ba_forced_pose_orders(order, monkeypatch):
+    """Every pose order the plan can choose solves the same step: with a
+    forced reverse Cuthill-McKee, minimum degree or nested dissection order
+    (the factor's tile structure and Cholesky task graph change) a C3-graph BA
+    and a lapping-trajectory BA (where the plan picks nested dissection on its
+    own) stay within 1e-4 of the oracle."""
+    import droid_backends
+    monkeypatch.setenv("DROID_BA_ORDER", order)
+    droid_backends._PLAN_CACHE.clear()   # plans are cached per edge set, not per order
+    try:
+        got, ref = run_both(synthetic.ba_problem("C3", H=16, W=24), iterations=2, lm=1e-5, ep=1e-2)
+        check(got, ref)
+        laps = synthetic.c5_edges(num_kf=640, lap=256)
+        prob = synthetic.ba_problem("C5", H=16, W=24, edges=laps, num_frames=640, t0=1, t1=640)
+        got, ref = run_both(prob, iterations=2, lm=1e-5, ep=1e-2)
+        check(got, ref)
+    finally:
+        droid_backends._PLAN_CACHE.clear()
+
+
 def test_ba_plan_reuse_is_deterministic():
     import droid_backends
     prob = synthetic.ba_problem("C2", seed=82)
