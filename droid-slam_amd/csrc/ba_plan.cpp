@@ -604,7 +604,12 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, co
   // pixel splits per edge: enough (edge, split) workgroups to cover the CUs
   // (~512), but few enough that each sums >= 256 pixels before its 90-partial
   // reduction and the assembly does not sum many partials per element
-  p.nsplit = std::max(1, std::min(std::max(1, HW / 256), (512 + std::max(E, 1) - 1) / std::max(E, 1)));
+  // pixel splits per edge: ~192 (edge, split) workgroups for small graphs.  A/B
+  // on one MI355X (DROID_BA_NSPLIT, profiles/r02/ba_nsplit_r02dj.txt): C2 (96
+  // edges) BA(itrs=2) 0.209 ms at 2 splits vs 0.242 at 6 (the old 512-workgroup
+  // target) and 0.281 at 12; C3 is fastest unsplit (2.41 vs 2.52 ms at 2)
+  p.nsplit = std::max(1, std::min(std::max(1, HW / 256), (192 + std::max(E, 1) - 1) / std::max(E, 1)));
+  if (const char* f = getenv("DROID_BA_NSPLIT")) p.nsplit = std::max(1, std::min(std::max(1, HW / 64), atoi(f)));
   const int rounds = ceil_div(HW, 256);
   p.group_per_wave = std::max(1, std::min(rounds, (int)((long)p.K * rounds / 1024)));
   p.nchunk = ceil_div(rounds, p.group_per_wave);
