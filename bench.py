@@ -88,9 +88,10 @@ def build_state(args, rank, world, device):
     comm = None
     if world > 1:
         ii_l, jj_l, own = sharding.shard_edges(ii, jj, args.frames, rank, world)
-        # the global edge list: every rank derives the same reduced-system tile structure from it
+        # the BA gathers the global edge list once per edge-set version (every rank
+        # derives the same reduced-system tile structure from it)
         comm = dict(group=None, own=own, t0=max(1, int(ii.min()) + 1), t1=int(max(ii.max(), jj.max())) + 1,
-                    edges=(ii, jj))
+                    version=0)
     else:
         ii_l, jj_l = ii, jj
     n = args.frames
@@ -241,7 +242,7 @@ def cpu_baseline(graph, video, args):
     restatement (oracle/update_cpu.py) on the host cores, ms per stage."""
     from droid_mi355x import synthetic
     from oracle import update_cpu
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = update_cpu.baseline_threads()
     params = {k: v.detach().float().cpu().numpy() for k, v in graph.update_op.state_dict().items()}
     H, W = args.ht // 8, args.wd // 8
     t_all = time.time()
@@ -264,7 +265,8 @@ def cpu_baseline(graph, video, args):
                        "reprojection, 4-level lookup, UpdateModule fp32, BA itrs=2 fp64) through the oracle "
                        "restatement on %d host threads; corr volumes built per chunk and timed apart (they belong "
                        "to add_factors)" % c3["threads"]),
-            "cpu": info, "threads": c3["threads"],
+            "cpu": info, "threads": c3["threads"], "physical_cores": info.get("physical_cores"),
+            "sockets": info.get("sockets"), "cpu_model": info.get("model"),
             "C1": {"ms": round(c1["ms"], 2), "median_of": c1["repeats"],
                    "what": "2 frames / 1 edge CorrBlock 48x64 r=3 (volume + pyramid + lookup)"},
             "C2": {"iters_per_s": 1.0 / c2["seconds_per_update"], "ms_per_stage": r(c2["ms"]), "median_of": 3,
@@ -289,6 +291,33 @@ def load_traffic(name, e_local, kernel):
         except Exception:
             return None
     return None
+
+
+def launcher_command(n, port, argv):
+    """The child command `bench.py --gpus N` runs when started without
+    torch.distributed.run: N local ranks over 127.0.0.1, same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n, one_dev):
+    """Run N ranks as a child process (never an exec: nothing here has touched
+    the GPU, and the child is a separate program), relay their output, return
+    the child's exit code."""
+    import socket
+    import subprocess
+    if not one_dev:
+        have = torch.cuda.device_count()   # does not initialise the GPU on this image
+        if have < n:
+            log("error: --gpus %d but only %d visible GPU(s)" % (n, have))
+            return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    cmd = launcher_command(n, port, sys.argv[1:])
+    log("launching %d ranks: %s" % (n, " ".join(cmd)))
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -332,14 +361,19 @@ def main():
             args.frames = 2048
         args.corr = "pyramid"
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     # DROID_BENCH_ONE_DEVICE=1 / DROID_BENCH_BACKEND=gloo: rehearse the N-rank path
     # with every rank on cuda:0 (a one-GPU box); the driver's runs use RCCL, one GPU per rank
     one_dev = os.environ.get("DROID_BENCH_ONE_DEVICE") == "1"
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` on its own: start the N ranks (one process per GPU,
+        # as train.py:184-186 spawns its DDP workers) before anything touches the GPU
+        sys.exit(launch_ranks(args.gpus, one_dev))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("error: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+        sys.exit(2)
     device = torch.device("cuda", 0 if one_dev else local_rank)
     torch.cuda.set_device(device)
     import torch.distributed as dist
@@ -379,6 +413,8 @@ def main():
         lookup.active = True
         if zr:
             zr.active = zrp.active = True
+        if graph.comm is not None:
+            graph.comm["_ar_events"] = []
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step_fn()
@@ -394,6 +430,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    allreduce = None
+    if graph.comm is not None:
+        evs, graph.comm["_ar_events"] = graph.comm["_ar_events"], None
+        torch.cuda.synchronize(device)
+        if evs:
+            allreduce = {"collective": "all_reduce(SUM) of the reduced camera system's input tiles (fp64)",
+                         "backend": dist.get_backend(), "payload_bytes": int(evs[0][2]),
+                         "per_update": len(evs) // args.steps,
+                         "ms_per_gn_iteration": float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))}
     finite = bool(torch.isfinite(video.poses).all() and torch.isfinite(video.disps).all())
     lookup_ms = lookup.mean_ms()
     zr_ms = zr.mean_ms() if zr else None
@@ -465,6 +510,8 @@ def main():
         }
         if lookup_roof:
             result["roofline_lookup"] = lookup_roof
+        if allreduce:
+            result["allreduce"] = allreduce
         # whole-iteration fraction: max(HBM floor, MFMA floor) / measured update()
         hw = (args.ht // 8) * (args.wd // 8)
         # edges the update operator runs on (C2: the active window; the stored ones only join the BA)

@@ -1,6 +1,9 @@
 // Dense bundle adjustment kernels for gfx950 (see ba.hpp for the pipeline).
 // Numerics follow ba_cuda (droid_kernels.cu:176-424, 854-1434): fp32
 // linearisation and Schur products, fp64 reduced system and Cholesky.
+#include <cstring>
+#include <string>
+
 #include "ba.hpp"
 #include "common.hpp"
 
@@ -619,10 +622,18 @@ __global__ void __launch_bounds__(256) ba_assemble_kernel(BaDev d) {
   }
 }
 
-// diag += ep + lm * diag  (SparseBlock::solve :1197) and reset the failure flag
-__global__ void ba_damp_kernel(double* M, const int* slot, int nbc, int n, float lm, float ep, int* flag) {
+// diag += ep + lm * diag  (SparseBlock::solve :1197) and start a new status
+// word: flag[0] is this solve's (the kernels after it test its timeout bit),
+// flag[1] the sticky OR of every earlier solve's since the caller last cleared
+// it (first_solve: droid_ba_run's first GN iteration) - a timeout in GN
+// iteration 1 is still reported after iteration 2.
+__global__ void ba_damp_kernel(double* M, const int* slot, int nbc, int n, float lm, float ep, int* flag,
+                               int first_solve) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) *flag = 0;
+  if (i == 0) {
+    flag[1] = first_solve ? 0 : (flag[1] | flag[0]);
+    flag[0] = 0;
+  }
   if (i < n) {
     double& dg = M[(size_t)slot[(i >> 6) * nbc + (i >> 6)] * kTile + (i & 63) * 65];
     dg = dg + ((double)ep + (double)lm * dg);
@@ -1346,8 +1357,16 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_
   c.ybuf = reinterpret_cast<double*>(ws + p.off_ybuf);
   c.x = reinterpret_cast<double*>(ws + p.off_x);
   c.dx = dx;
+  // test hook: "1" aborts every solve; "once<tag>" only the first solve after
+  // the tag changes (a timeout in one GN iteration of a multi-iteration call)
   const char* inj = getenv("DROID_CHOL_FAULT_INJECT");
-  c.inject = (inj && atoi(inj) != 0) ? 1 : 0;
+  c.inject = 0;
+  if (inj && strncmp(inj, "once", 4) == 0) {
+    static std::string last_tag;
+    if (last_tag != inj) { c.inject = 1; last_tag = inj; }
+  } else if (inj && atoi(inj) != 0) {
+    c.inject = 1;
+  }
   c.prof = g_chol_prof;
   static bool attr = false;
   if (!attr) {
@@ -1436,12 +1455,9 @@ int droid_ba_build_system(void* plan, void* workspace, float* poses, float* disp
   return kOk;
 }
 
-// Damped Cholesky solve of the (possibly all-reduced) system, back
-// substitution and retraction (:1406-1428).  dz may be null for motion_only.
-int droid_ba_solve_update(void* plan, void* workspace, float* poses, float* disps,
-                          const float* intrinsics, const float* disps_sens, const float* targets,
-                          const float* weights, const float* eta, float lm, float ep,
-                          float* dx, float* dz, hipStream_t stream) {
+static int solve_update(void* plan, void* workspace, float* poses, float* disps, const float* intrinsics,
+                        const float* disps_sens, const float* targets, const float* weights, const float* eta,
+                        float lm, float ep, float* dx, float* dz, int first_solve, hipStream_t stream) {
   auto* p = static_cast<BaPlan*>(plan);
   int st = check_ready(p, workspace);
   if (st) return st;
@@ -1450,7 +1466,8 @@ int droid_ba_solve_update(void* plan, void* workspace, float* poses, float* disp
   d.targets = targets; d.weights = weights; d.eta = eta; d.dx = dx; d.dz = dz;
   d.lm = lm; d.ep = ep;
   const int n = p->n;
-  ba_damp_kernel<<<ceil_div(std::max(n, 1), 256), 256, 0, stream>>>(d.M, d.slot, d.nbc, n, lm, ep, d.flag);
+  ba_damp_kernel<<<ceil_div(std::max(n, 1), 256), 256, 0, stream>>>(d.M, d.slot, d.nbc, n, lm, ep, d.flag,
+                                                                     first_solve);
   DROID_LAUNCH_CHECK();
   if (n > 0) {
     st = launch_chol_dataflow(*p, static_cast<char*>(workspace), dx, stream);
@@ -1468,9 +1485,32 @@ int droid_ba_solve_update(void* plan, void* workspace, float* poses, float* disp
   return kOk;
 }
 
-// Byte offset of the status word in a plan's workspace: bit 0 = the last
-// factorisation was not positive definite (dx = 0, as the reference), bit 1 =
-// the dataflow solve timed out (poses / disparities left unchanged).
+// Damped Cholesky solve of the (possibly all-reduced) system, back
+// substitution and retraction (:1406-1428).  dz may be null for motion_only.
+// Earlier solves' status bits accumulate in the sticky word until
+// droid_ba_plan_clear_status.
+int droid_ba_solve_update(void* plan, void* workspace, float* poses, float* disps,
+                          const float* intrinsics, const float* disps_sens, const float* targets,
+                          const float* weights, const float* eta, float lm, float ep,
+                          float* dx, float* dz, hipStream_t stream) {
+  return solve_update(plan, workspace, poses, disps, intrinsics, disps_sens, targets, weights, eta, lm, ep, dx, dz,
+                      0, stream);
+}
+
+// Zero both status words (stream-ordered): the start of a staged BA call.
+int droid_ba_plan_clear_status(void* plan, void* workspace, hipStream_t stream) {
+  auto* p = static_cast<BaPlan*>(plan);
+  int st = check_ready(p, workspace);
+  if (st) return st;
+  DROID_HIP_CHECK(hipMemsetAsync(static_cast<char*>(workspace) + p->off_flag, 0, 8, stream));
+  return kOk;
+}
+
+// Byte offset of the status words in a plan's workspace (two int32): word 0 is
+// the last solve's, word 1 the OR of the earlier solves' since the status was
+// last cleared; bit 0 = a factorisation was not positive definite (dx = 0, as
+// the reference), bit 1 = the dataflow solve timed out (that solve left poses /
+// disparities unchanged).
 int droid_ba_plan_flag_offset(const void* plan, size_t* offset) {
   auto* p = static_cast<const BaPlan*>(plan);
   if (!p || !offset) return fail(kInvalidArgument, "ba_plan_flag_offset: null argument");
@@ -1507,7 +1547,7 @@ int droid_chol_solve(void* plan, void* workspace, float lm, float ep, float* dx,
   double* M = reinterpret_cast<double*>(ws + p->off_M);
   const int* slot = reinterpret_cast<const int*>(ws + p->off_ints) + p->o_slot;
   int* flag = reinterpret_cast<int*>(ws + p->off_flag);
-  ba_damp_kernel<<<ceil_div(std::max(p->n, 1), 256), 256, 0, stream>>>(M, slot, p->cs.nbc, p->n, lm, ep, flag);
+  ba_damp_kernel<<<ceil_div(std::max(p->n, 1), 256), 256, 0, stream>>>(M, slot, p->cs.nbc, p->n, lm, ep, flag, 1);
   DROID_LAUNCH_CHECK();
   if (p->n == 0) return kOk;
   return launch_chol_dataflow(*p, ws, dx, stream);
@@ -1522,8 +1562,8 @@ int droid_ba_run(void* plan, void* workspace, float* poses, float* disps, const 
     int st = droid_ba_build_system(plan, workspace, poses, disps, intrinsics, disps_sens, targets,
                                    weights, eta, stream);
     if (st) return st;
-    st = droid_ba_solve_update(plan, workspace, poses, disps, intrinsics, disps_sens, targets,
-                               weights, eta, lm, ep, dx, dz, stream);
+    st = solve_update(plan, workspace, poses, disps, intrinsics, disps_sens, targets, weights, eta, lm, ep, dx, dz,
+                      it == 0, stream);
     if (st) return st;
   }
   return kOk;

@@ -702,6 +702,31 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, co
       }
     }
   }
+  // Every block the assembly writes must land in an input tile of the factor's
+  // structure (the region a sharded caller all-reduces).  The structure comes
+  // from the global edge list, so a rank whose local edges are not part of it
+  // would otherwise write through slot -1 or into a fill tile.
+  {
+    const int nbc = p.cs.nbc;
+    auto covered = [&](int v, int u) {
+      const int s = p.cs.slot[(size_t)(v >> 6) * nbc + (u >> 6)];
+      return s >= 0 && s < p.cs.nslots_a;
+    };
+    for (auto& kv : blocks) {
+      const int pa = p.perm[kv.first.first], pb = p.perm[kv.first.second];
+      for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < 6; ++c) {
+          const int v = 6 * pa + r, u = 6 * pb + c;
+          if (!(v >= u ? covered(v, u) : (pa == pb || covered(u, v))))
+            return fail(kInvalidArgument, "ba: local edges not covered by the global edge list");
+        }
+    }
+    for (int a = 0; a < P; ++a)
+      if (!rhs[a].empty())
+        for (int c = 0; c < 6; ++c)
+          if (!covered(p.n, 6 * p.perm[a] + c))
+            return fail(kInvalidArgument, "ba: local edges not covered by the global edge list");
+  }
   p.blk_a.clear(); p.blk_b.clear(); p.blk_cptr.assign(1, 0); p.contrib.clear();
   for (auto& kv : blocks) {
     p.blk_a.push_back(p.perm[kv.first.first]);

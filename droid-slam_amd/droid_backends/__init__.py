@@ -636,9 +636,11 @@ class BaPlan:
         # the reduced system's input tiles (64x64 fp64, permuted lower triangle of
         # A - S, rhs as row n): the contiguous region a multi-GPU caller all-reduces
         self.system = self.workspace[off.value:off.value + sz.value].view(torch.float64).view(-1, 64, 64)
-        self._flag = self.workspace[foff.value:foff.value + 4].view(torch.int32)
-        self._status = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._flag = self.workspace[foff.value:foff.value + 8].view(torch.int32)   # [this solve, sticky]
+        self._status = torch.zeros(2, dtype=torch.int32, pin_memory=True)
         self._status_evt = None
+        self.name = "ba plan (%d edges, poses [%d, %d), %d depth frames%s)" % (
+            len(ii), self.t0, self.t1, self.K, ", motion only" if self.motion_only else "")
         with torch.cuda.device(self.device):
             check(lib.droid_ba_plan_upload(h, _ptr(self.workspace), _stream(self.workspace)), "ba plan upload")
 
@@ -648,22 +650,31 @@ class BaPlan:
             lib.droid_ba_plan_destroy(h)
             self._h = None
 
-    def _record_status(self):
-        """queue a copy of the status word of the solve just enqueued (checked lazily)."""
-        self._status.copy_(self._flag, non_blocking=True)
+    def _record_status(self, flag=None):
+        """queue a copy of the status words of the call just enqueued (checked
+        lazily); `flag` = a device copy to read instead (the sharded BA's
+        all-reduced status)."""
+        self._status.copy_(self._flag if flag is None else flag, non_blocking=True)
         self._status_evt = torch.cuda.Event()
         self._status_evt.record(torch.cuda.current_stream(self.device))
 
     def check_status(self):
-        """Raise if the last solve's dataflow Cholesky timed out (status bit 1):
-        that solve left poses and disparities unchanged.  Waits for that solve."""
+        """Raise if a solve of the last ba() call on this plan timed out (status
+        bit 1 in this solve's or the sticky word): that solve left poses and
+        disparities unchanged.  Waits for that call."""
         evt, self._status_evt = self._status_evt, None
         if evt is None:
             return
         evt.synchronize()
-        if int(self._status[0]) & 2:
-            raise RuntimeError("ba: the dataflow Cholesky timed out (dependency wait exceeded); "
-                               "poses and disparities were left unchanged")
+        if (int(self._status[0]) | int(self._status[1])) & 2:
+            raise RuntimeError("ba: the dataflow Cholesky timed out (dependency wait exceeded) in %s; that "
+                               "Gauss-Newton step left poses and disparities unchanged" % self.name)
+
+    def clear_status(self):
+        """zero both status words (stream-ordered): the start of a staged ba call."""
+        with torch.cuda.device(self.device):
+            check(lib.droid_ba_plan_clear_status(self._h, _ptr(self.workspace), _stream(self.workspace)),
+                  "ba clear_status")
 
     def build_system(self, poses, disps, intrinsics, disps_sens, targets, weights, eta):
         with torch.cuda.device(self.device):
@@ -672,13 +683,17 @@ class BaPlan:
                                             _ptr(eta), _stream(poses)), "ba build_system")
 
     def solve_update(self, poses, disps, intrinsics, disps_sens, targets, weights, eta, lm, ep, dx, dz):
-        self.check_status()
+        """one damped solve + back-substitution + retraction; the status words
+        accumulate on the device (clear_status / status_words, no host wait)."""
         with torch.cuda.device(self.device):
             check(lib.droid_ba_solve_update(self._h, _ptr(self.workspace), _ptr(poses), _ptr(disps),
                                             _ptr(intrinsics), _ptr(disps_sens), _ptr(targets), _ptr(weights),
                                             _ptr(eta), float(lm), float(ep), _ptr(dx), _ptr(dz), _stream(poses)),
                   "ba solve_update")
-            self._record_status()
+
+    def status_words(self):
+        """the device status words (int32 [this solve, sticky]), a view."""
+        return self._flag
 
     def run(self, poses, disps, intrinsics, disps_sens, targets, weights, eta, iterations, lm, ep):
         dx = torch.empty((self.P, 6), dtype=torch.float32, device=poses.device)
@@ -748,6 +763,7 @@ def get_plan(ii_host, jj_host, num_frames, ht, wd, t0, t1, eta_rows, motion_only
         plan = BaPlan(ii_host, jj_host, num_frames, ht, wd, t0, t1, eta_rows, motion_only, device, own, gedges)
         _PLAN_CACHE[key] = plan
         while len(_PLAN_CACHE) > _PLAN_CACHE_SIZE:
+            # the evicted plan's last call: its failure names that plan, not this call
             _PLAN_CACHE.popitem(last=False)[1].check_status()
     else:
         _PLAN_CACHE.move_to_end(key)

@@ -60,6 +60,7 @@ _SIGS = {
                                       ctypes.POINTER(_p)], _i),
     "droid_ba_plan_order": ([_p, ctypes.POINTER(_i), _p, ctypes.POINTER(_i), ctypes.POINTER(_i)], _i),
     "droid_ba_plan_flag_offset": ([_p, ctypes.POINTER(_sz)], _i),
+    "droid_ba_plan_clear_status": ([_p, _p, _p], _i),
     "droid_ba_plan_destroy": ([_p], None),
     "droid_ba_plan_workspace_bytes": ([_p], _sz),
     "droid_ba_plan_info": ([_p, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),

@@ -143,13 +143,15 @@ class DepthVideo:
         return d
 
     def ba(self, target, weight, eta, ii, jj, t0=1, t1=None, itrs=2, lm=1e-4, ep=0.1, motion_only=False,
-           ii_host=None, jj_host=None, comm=None):
+           ii_host=None, jj_host=None, comm=None, edge_tag=None):
         """dense bundle adjustment (depth_video.py:181-193).
 
         comm (edge-sharded multi-GPU): dict(group=process group, own=(lo, hi),
-        t1=global t1).  Each rank passes only the edges whose source frame it
-        owns; the reduced camera system is summed with one all-reduce per
-        Gauss-Newton iteration and solved identically on every rank."""
+        t1=global t1, version=edge-set version).  Each rank passes only the
+        edges whose source frame it owns; the reduced camera system is summed
+        with one all-reduce per Gauss-Newton iteration and solved identically
+        on every rank.  edge_tag names which of the caller's edge sets this
+        is (e.g. with / without the inactive edges) for the global-list cache."""
         with self.get_lock():
             if ii_host is None:
                 ii_host = ii.cpu().numpy()
@@ -165,49 +167,89 @@ class DepthVideo:
                                         t0, t1, itrs, lm, ep, motion_only, ii_host=ii_host, jj_host=jj_host)
             else:
                 out = ba_sharded(self.poses, self.disps, intr, self.disps_sens, target, weight, eta, ii_host,
-                                 jj_host, t0, t1, itrs, lm, ep, motion_only, comm)
+                                 jj_host, t0, t1, itrs, lm, ep, motion_only, comm, edge_tag)
             self.disps.clamp_(min=0.001)
             return out
 
 
 def ba_sharded(poses, disps, intrinsics, disps_sens, target, weight, eta, ii_host, jj_host, t0, t1, itrs, lm, ep,
-               motion_only, comm):
+               motion_only, comm, edge_tag=None):
     """One rank of the edge-sharded BA: local linearisation + Schur terms,
     all_reduce(SUM) of the reduced system's input tiles (RCCL over xGMI), then
     the same damped fp64 Cholesky on every rank; dz only for owned frames.
 
     The pose order and the factor's tile structure come from the GLOBAL edge
-    list (comm["edges"] = (ii, jj) when the caller has it, else gathered once
-    per edge set), so the tiles line up across ranks and only the structurally
-    nonzero 64x64 tiles of A - S and the rhs row cross the links (9.6 MB at
-    C3, 66 MB at C5 instead of the dense 603 MB)."""
+    list (global_edges), so the tiles line up across ranks and only the
+    structurally nonzero 64x64 tiles of A - S and the rhs row cross the links
+    (9.6 MB at C3, 66 MB at C5 instead of the dense 603 MB).
+
+    Failures are agreed on, not per rank: the solves' status words are
+    all-reduced (MAX) on the device after the last GN iteration, and every rank
+    raises at its next BA call (or droid_backends.check_status()) if any rank's
+    dataflow Cholesky timed out - no rank is left waiting in a collective."""
     import torch.distributed as dist
+    group = comm.get("group")
     N, H, W = disps.shape
     eta_rows = eta.numel() // (H * W)
-    gedges = global_edges(ii_host, jj_host, comm)
+    last = comm.pop("_last_plan", None)
+    if last is not None:
+        last.check_status()          # the previous call's agreed status (every rank raises alike)
+    gedges = global_edges(ii_host, jj_host, comm, (int(t0), int(t1), bool(motion_only), edge_tag))
     plan = droid_backends.get_plan(ii_host, jj_host, N, H, W, int(t0), int(t1), eta_rows, motion_only,
                                    poses.device, own=tuple(comm["own"]), gedges=gedges)
     dx = torch.empty((plan.P, 6), dtype=torch.float32, device=poses.device)
     dz = None if motion_only else torch.empty((plan.K, H * W), dtype=torch.float32, device=poses.device)
     flat = plan.system.view(-1)
+    plan.clear_status()
+    timing = comm.get("_ar_events")   # bench: HIP events around each all-reduce, or None
     for _ in range(itrs):
         plan.build_system(poses, disps, intrinsics, disps_sens, target, weight, eta)
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=comm.get("group"))
+        if timing is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+        if timing is not None:
+            ev[1].record()
+            timing.append(ev + (flat.numel() * flat.element_size(),))
         plan.solve_update(poses, disps, intrinsics, disps_sens, target, weight, eta, lm, ep, dx, dz)
+    # status values are 0..3 per word, so MAX keeps the timeout bit (value >= 2) of any rank
+    status = plan.status_words().clone()
+    dist.all_reduce(status, op=dist.ReduceOp.MAX, group=group)
+    plan._record_status(status)
+    comm["_last_plan"] = plan
     return [dx, dz]
 
 
-def global_edges(ii_host, jj_host, comm):
-    """The union of every rank's BA edges, in rank order (cached per local edge set)."""
-    if comm.get("edges") is not None:
-        return comm["edges"]
+def global_edges(ii_host, jj_host, comm, call_key):
+    """The union of every rank's BA edges, in rank order.
+
+    Whether to (re)gather must be decided identically on every rank, or one
+    rank blocks in the gather while the others enter the next all-reduce.  The
+    cache is therefore keyed by replicated values only: comm["version"] (bumped
+    by every FactorGraph edge edit, which the ranks issue in lockstep) and the
+    call's (t0, t1, motion_only, edge tag).  Without a "version" in comm the
+    list is gathered on every call.  On a cache hit the local edges must be
+    part of the cached list (a rank that edited alone is a caller bug: raise)."""
     import torch.distributed as dist
+    group = comm.get("group")
+    ii_host = np.asarray(ii_host, np.int64)
+    jj_host = np.asarray(jj_host, np.int64)
+    version = comm.get("version")
+    key = None if version is None else (version,) + tuple(call_key)
     cache = comm.setdefault("_gedges", {})
-    key = (np.asarray(ii_host, np.int64).tobytes(), np.asarray(jj_host, np.int64).tobytes())
-    if key not in cache:
-        parts = [None] * dist.get_world_size(comm.get("group"))
-        dist.all_gather_object(parts, (np.asarray(ii_host, np.int64), np.asarray(jj_host, np.int64)),
-                               group=comm.get("group"))
-        cache.clear()
-        cache[key] = (np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
-    return cache[key]
+    hit = cache.get(key) if key is not None else None
+    if hit is None:
+        parts = [None] * dist.get_world_size(group)
+        dist.all_gather_object(parts, (ii_host, jj_host), group=group)
+        hit = (np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
+        if key is not None:
+            if len(cache) >= 4:
+                cache.pop(next(iter(cache)))
+            cache[key] = hit
+    elif len(ii_host):
+        n = int(max(hit[0].max(), hit[1].max(), ii_host.max(), jj_host.max())) + 1
+        have = np.unique(hit[0] * n + hit[1])
+        if not np.isin(ii_host * n + jj_host, have).all():
+            raise RuntimeError("ba (sharded): this rank's edges are not in the global edge list of edge-set "
+                               "version %r - edge edits must be issued on every rank" % (version,))
+    return hit

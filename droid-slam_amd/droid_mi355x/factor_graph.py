@@ -54,7 +54,7 @@ class FactorGraph:
         # correlation windows on demand from this feature pyramid of the frames
         self._alt_pyr = None
         self._inp_frames = None   # (inp tensor, first-edge bytes, per-source-frame inp rows)
-        self.comm = None  # set for edge-sharded multi-GPU: dict(group, own=(lo,hi), t0, t1)
+        self.comm = None  # set for edge-sharded multi-GPU: dict(group, own=(lo,hi), t0, t1, version)
         # fused (MI355X) operator: per-edge hidden state kept channels-last (E,H,W,128)
         from .fused import FusedUpdateModule
         self.fused = isinstance(update_op, FusedUpdateModule)
@@ -104,6 +104,13 @@ class FactorGraph:
         return np.asarray(x, dtype=np.int64).reshape(-1)
 
     # -- graph edits (factor_graph.py:43-193) ---------------------------------
+    def _edited(self):
+        """edge-set version for the sharded BA's global-edge cache: every edit
+        (issued in lockstep on all ranks, even when it leaves this rank's shard
+        unchanged) bumps it, so all ranks agree on when to re-gather."""
+        if self.comm is not None:
+            self.comm["version"] = self.comm.get("version", 0) + 1
+
     def _filter_repeated(self, ii, jj):
         seen = set(zip(self._ii.tolist(), self._jj.tolist())) | set(zip(self._ii_inac.tolist(),
                                                                       self._jj_inac.tolist()))
@@ -130,6 +137,7 @@ class FactorGraph:
         self.inp = None
 
     def add_factors(self, ii, jj, remove=False):
+        self._edited()
         ii, jj = self._filter_repeated(self._host(ii), self._host(jj))
         if ii.shape[0] == 0:
             return
@@ -179,6 +187,7 @@ class FactorGraph:
         if isinstance(mask, torch.Tensor):
             mask = mask.detach().cpu().numpy()
         mask = np.asarray(mask, dtype=bool).reshape(-1)
+        self._edited()
         keep = ~mask
         dmask = torch.as_tensor(mask, device=self.device)
         dkeep = ~dmask
@@ -200,6 +209,7 @@ class FactorGraph:
         self.weight = self.weight[:, dkeep]
 
     def rm_keyframe(self, ix):
+        self._edited()
         self._alt_pyr = None   # frames shift
         v = self.video
         with v.get_lock():
@@ -290,7 +300,8 @@ class FactorGraph:
             weight = weight.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
             self.video.ba(target, weight, damping, self._dev("ii_ba", ii_h), self._dev("jj_ba", jj_h),
                           t0, t1, itrs=itrs, lm=1e-4, ep=0.1, motion_only=motion_only,
-                          ii_host=ii_h, jj_host=jj_h, comm=self.comm)
+                          ii_host=ii_h, jj_host=jj_h, comm=self.comm,
+                          edge_tag="update+inactive" if use_inactive else "update")
         self.age += 1
 
     def _pending_alt_lookup(self, coords1):
@@ -357,7 +368,7 @@ class FactorGraph:
             target = self.target.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
             weight = self.weight.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
             self.video.ba(target, weight, damping, self.ii, self.jj, 1, t, itrs=itrs, lm=1e-5, ep=1e-2,
-                          motion_only=False, ii_host=self._ii, jj_host=self._jj, comm=self.comm)
+                          motion_only=False, ii_host=self._ii, jj_host=self._jj, comm=self.comm, edge_tag="lowmem")
             self.video.dirty[:t] = True
 
     def _lowmem_chunks(self, corr_op, coords1, motn, rig):

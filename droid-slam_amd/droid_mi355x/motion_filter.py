@@ -19,7 +19,10 @@ def coords_grid(ht, wd, device):
 
 
 class MotionFilter:
-    """This class is used to filter incoming frames and extract features."""
+    """Keyframe gate in front of the frame graph: every frame gets its
+    matching features; only a frame whose predicted flow against the last
+    kept frame exceeds `thresh` pixels is appended to the DepthVideo (with its
+    context features)."""
 
     def __init__(self, net, video, thresh=2.5, device="cuda:0"):
         self.cnet = net.cnet
@@ -42,7 +45,11 @@ class MotionFilter:
 
     @torch.no_grad()
     def track(self, tstamp, image, depth=None, intrinsics=None):
-        """main update operation - run on every frame in video (motion_filter.py:47-82)"""
+        """Encode one frame and decide whether it becomes a keyframe
+        (reference control flow: motion_filter.py:47-82).  The first frame is
+        always kept with the identity pose; later frames are kept when the mean
+        |delta| of one update against the last keyframe's features is above
+        `thresh`, otherwise only `count` grows."""
         Id = torch.as_tensor([0, 0, 0, 0, 0, 0, 1.0])
         ht = image.shape[-2] // 8
         wd = image.shape[-1] // 8

@@ -301,10 +301,14 @@ int droid_ba_plan_order(const void* plan, int* kind, int* perm, int* num_wide, i
  * the permuted lower triangle of A - S with the rhs as row n; the contiguous
  * region a multi-GPU caller all-reduces (SUM) between build and solve */
 int droid_ba_plan_system_region(const void* plan, size_t* offset, size_t* bytes);
-/* byte offset of the int32 status word: bit 0 = last factorisation not SPD
- * (dx = 0, as the reference), bit 1 = dataflow solve timed out (poses and
- * disparities left unchanged; the caller must report an error) */
+/* byte offset of the two int32 status words: word 0 = the last solve's, word 1
+ * = the OR of the earlier solves' since droid_ba_run started or the caller
+ * cleared them (sticky); bit 0 = a factorisation was not SPD (dx = 0, as the
+ * reference), bit 1 = a dataflow solve timed out (that solve left poses and
+ * disparities unchanged; the caller must report an error) */
 int droid_ba_plan_flag_offset(const void* plan, size_t* offset);
+/* zero both status words, stream-ordered (start of a staged build/solve BA call) */
+int droid_ba_plan_clear_status(void* plan, void* workspace, hipStream_t stream);
 int droid_ba_plan_upload(void* plan, void* workspace, hipStream_t stream);
 
 /* one GN linearisation -> reduced system in the workspace (all-reduce it here for multi-GPU) */

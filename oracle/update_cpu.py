@@ -55,7 +55,32 @@ def cpu_info():
     except OSError:
         pass
     return dict(model=model, sockets=len(sockets) or None, physical_cores=len(cores) or None,
-                logical_cpus=logical or os.cpu_count())
+                logical_cpus=logical or os.cpu_count(), os_cpu_count=os.cpu_count(),
+                affinity_cpus=len(os.sched_getaffinity(0)), cgroup_cpu_quota=cgroup_cpu_quota())
+
+
+def cgroup_cpu_quota():
+    """CPUs the cgroup lets this process use (cpu.max quota / period), or None
+    when unlimited / unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        return None
+
+
+def baseline_threads():
+    """Threads for the CPU baseline: torch.set_num_threads(os.cpu_count()) as
+    BASELINE.md asks (not OMP_NUM_THREADS), bounded by the CPUs this process
+    may actually run on - its affinity mask and, when set, its cgroup CPU
+    quota (a shared GPU box shows the whole host in os.cpu_count())."""
+    n = os.cpu_count() or 1
+    n = min(n, len(os.sched_getaffinity(0)))
+    q = cgroup_cpu_quota()
+    if q is not None:
+        n = min(n, max(1, int(q)))
+    return max(1, n)
 
 
 def time_c1(threads, H=48, W=64, repeats=3, seed=1001):

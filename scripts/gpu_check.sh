@@ -60,8 +60,8 @@ for step in "$@"; do
       cat "$O/bench_$c.json" ;;
     rank2)
       # bench.py's 2-rank path rehearsed on a one-GPU box (both ranks on cuda:0, gloo collectives)
-      DROID_BENCH_ONE_DEVICE=1 DROID_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run \
-        --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 \
+      # through bench.py's own launcher (`--gpus 2` without torch.distributed.run starts the ranks)
+      DROID_BENCH_ONE_DEVICE=1 DROID_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 \
         --steps 3 --warmup 1 --no-cpu-baseline > "$O/bench_2rank.json" 2> "$O/bench_2rank.err" \
         || fail "$step" $? "$O/bench_2rank.err"
       cat "$O/bench_2rank.json" ;;

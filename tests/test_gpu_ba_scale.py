@@ -142,3 +142,20 @@ def test_chol_timeout_is_reported_and_state_untouched(monkeypatch):
     monkeypatch.delenv("DROID_CHOL_FAULT_INJECT")
     got = _gpu_ba(prob, 1, 1e-4, 0.1)          # and the next solve on the same plan is clean
     assert np.isfinite(got["dx"]).all()
+
+
+def test_chol_timeout_in_first_gn_iteration_is_still_reported(monkeypatch):
+    """the status word used to be cleared by every solve, so a
+    timeout in GN iteration 1 of ba(iterations=2) vanished when iteration 2
+    succeeded.  The sticky word keeps it: ba() raises."""
+    import droid_backends
+    prob = synthetic.ba_problem("C3", H=16, W=24, seed=7)
+    poses, disps = dev(prob["poses"]), dev(prob["disps"])
+    monkeypatch.setenv("DROID_CHOL_FAULT_INJECT", "once-first-iteration")
+    with pytest.raises(RuntimeError, match="timed out"):
+        droid_backends.ba(poses, disps, dev(prob["intrinsics"]), dev(prob["disps_sens"]), dev(prob["targets"]),
+                          dev(prob["weights"]), dev(prob["eta"]), dev(prob["ii"]), dev(prob["jj"]), prob["t0"],
+                          prob["t1"], 2, 1e-4, 0.1, False)
+    monkeypatch.delenv("DROID_CHOL_FAULT_INJECT")
+    got = _gpu_ba(prob, 2, 1e-4, 0.1)          # the next call on the same plan starts clean
+    assert np.isfinite(got["dx"]).all()

@@ -145,9 +145,10 @@ def _gather_worker(rank, world, port, q):
         ii, jj = synthetic.c5_edges(num_kf=512, lap=128)
         N = 512
         ii_l, jj_l, own = sharding.shard_edges(ii, jj, N, rank, world)
-        comm = dict(group=None, own=own)
-        gii, gjj = global_edges(ii_l, jj_l, comm)
-        assert global_edges(ii_l, jj_l, comm)[0] is gii          # cached per edge set
+        comm = dict(group=None, own=own, version=0)
+        key = (1, N, False, "update")
+        gii, gjj = global_edges(ii_l, jj_l, comm, key)
+        assert global_edges(ii_l, jj_l, comm, key)[0] is gii     # cached per (version, call)
         perm, slot = _plan_structure(ii_l, jj_l, gii, gjj, N, 1, N, own)
         parts = [None] * world
         dist.all_gather_object(parts, (np.sort(gii * N + gjj), perm, slot))
@@ -178,3 +179,63 @@ def test_sharded_plans_share_one_factor_structure():
         np.testing.assert_array_equal(edges, np.sort(ii * 512 + jj))
         np.testing.assert_array_equal(perm, ref_perm)
         np.testing.assert_array_equal(slot, ref_slot)
+
+
+def _version_worker(rank, world, port, q):
+    """an edit that changes ONE rank's shard must make every rank
+    re-gather (version bump in lockstep), and a rank that changed its edges
+    without a version bump must fail loudly instead of using a stale list."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from droid_mi355x.depth_video import global_edges
+        ii, jj = synthetic.c3_edges(num_kf=32, num_edges=160, rng=np.random.default_rng(3))
+        ii_l, jj_l, own = sharding.shard_edges(ii, jj, 32, rank, world)
+        comm = dict(group=None, own=own, version=0)
+        key = (1, 32, False, "update")
+        g0 = global_edges(ii_l, jj_l, comm, key)
+        # the edit adds an edge only on the last rank's shard; every rank bumps the version
+        if rank == world - 1:
+            ii_l, jj_l = np.append(ii_l, own[1] - 1), np.append(jj_l, 0)
+        comm["version"] += 1
+        g1 = global_edges(ii_l, jj_l, comm, key)            # both ranks gather again (no hang)
+        grew = len(g1[0]) == len(g0[0]) + 1
+        # a shard change without the version bump: that rank raises
+        stale_error = None
+        if rank == 0:
+            try:
+                global_edges(np.append(ii_l, own[0]), np.append(jj_l, 31), comm, key)
+            except RuntimeError as ex:
+                stale_error = str(ex)
+        dist.barrier()
+        q.put((rank, grew, stale_error))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_global_edges_regather_agreed_across_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_version_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (g, e)) for r, g, e in (q.get(timeout=240) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] and res[1][0]
+    assert res[0][1] is not None and "not in the global edge list" in res[0][1]
+
+
+def test_plan_rejects_local_edges_missing_from_global_list():
+    """ADVICE r2 (ba_plan.cpp): a local edge whose blocks have no input tile in
+    the factor structure built from the global list is an error, not a write
+    through slot -1."""
+    ii, jj = synthetic.c5_edges(num_kf=512, lap=128)
+    with pytest.raises(RuntimeError, match="not covered by the global edge list"):
+        # local edge (300, 40) pairs poses far apart; the global list is only the temporal chain
+        m = np.abs(ii - jj) <= 1
+        _plan_structure(np.array([300]), np.array([40]), ii[m], jj[m], 512, 1, 512, (256, 512))
