@@ -404,16 +404,21 @@ class FactorGraph:
         keep = (np.abs(ii - jj) > c) & (np.abs(ii - jj) <= r)
         self.add_factors(ii[keep], jj[keep])
 
-    def add_proximity_factors(self, t0=0, t1=0, rad=2, nms=2, beta=0.25, thresh=16.0, remove=False):
-        """factor_graph.py:305-369 on the device: the meshgrid distances
-        (droid_frame_distance, both directions), then proximity_edge_list."""
+    def proximity_factor_list(self, t0=0, t1=0, rad=2, nms=2, beta=0.25, thresh=16.0):
+        """the edge list add_proximity_factors adds (factor_graph.py:305-368):
+        the meshgrid distances on the device (droid_frame_distance, both
+        directions), then proximity_edge_list -> (k, 2) int64 numpy."""
         t = self.video.counter.value
         dev = self.video.poses.device
         ii, jj = torch.meshgrid(torch.arange(t0, t, device=dev), torch.arange(t1, t, device=dev), indexing="ij")
         d = self.video.distance(ii.reshape(-1), jj.reshape(-1), beta=beta)
-        es = proximity_edge_list(d, t0, t1, t, rad, nms, thresh, np.concatenate([self._ii, self._ii_bad, self._ii_inac]),
-                                 np.concatenate([self._jj, self._jj_bad, self._jj_inac]), self.video.stereo,
-                                 self.max_factors)
+        return proximity_edge_list(d, t0, t1, t, rad, nms, thresh, np.concatenate([self._ii, self._ii_bad, self._ii_inac]),
+                                   np.concatenate([self._jj, self._jj_bad, self._jj_inac]), self.video.stereo,
+                                   self.max_factors)
+
+    def add_proximity_factors(self, t0=0, t1=0, rad=2, nms=2, beta=0.25, thresh=16.0, remove=False):
+        """factor_graph.py:305-369 (proximity_factor_list, then add_factors)."""
+        es = self.proximity_factor_list(t0, t1, rad, nms, beta, thresh)
         self.add_factors(es[:, 0], es[:, 1], remove)
 
 

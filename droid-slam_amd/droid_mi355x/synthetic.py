@@ -223,6 +223,8 @@ def ba_problem(config="C2", H=48, W=64, seed=None, edges=None, num_frames=None, 
         ii, jj = c2_edges()
     elif config == "C3":
         ii, jj = c3_edges(rng=np.random.default_rng(1003))
+    elif config == "C4":
+        ii, jj = c4_edges(rng=np.random.default_rng(1004))
     elif config == "C5":
         ii, jj = c5_edges()
     else:

@@ -28,7 +28,7 @@ from . import update_module as oum
 
 def update(params, poses, disps, disps_sens, intrinsics, fmaps, ii, jj, net, inp, target, weight, damping,
            t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, motion_only=False, inactive=None, lm=1e-4,
-           ep=0.1):
+           ep=0.1, torch_corr=False, f16_outputs=False, device=None):
     """params: UpdateModule state dict (numpy); poses (N,7), disps/disps_sens
     (N,H,W), intrinsics (N,4), fmaps (N,rig,128,H,W); ii/jj (E); net/inp
     (E,128,H,W); target/weight (E,H,W,2); damping (N,H,W); inactive =
@@ -36,6 +36,16 @@ def update(params, poses, disps, disps_sens, intrinsics, fmaps, ii, jj, net, inp
     update_lowmem (factor_graph.py:245-290) is one call per step with t0=1,
     t1=counter, lm=1e-5, ep=1e-2 (its alt correlation equals the volume's up
     to fp16 rounding, corr.py:91-139).
+
+    torch_corr: the pyramid + lookup as torch fp32 matmul / avg_pool2d /
+    grid_sample (oracle/corr.py *_torch, equal to the loop restatement,
+    tests/test_oracle_golden.py) - the same values, fast enough for replays of
+    whole frontend sequences.  f16_outputs: round the update operator's
+    outputs (net, delta, weight, eta) to fp16, as the reference's autocast
+    region stores them (factor_graph.py:209-220) - for multi-update replays
+    whose state the reference carries in fp16.  device: a torch device for
+    the torch_corr lookup and the fp32 update operator (the plain-torch
+    reference of the same ops; TF32 must be off); the BA stays fp64 numpy.
 
     Returns dict(net, target, weight, damping, coords1, ba_in=(targets, weights,
     eta, ii, jj, t0, t1), poses, disps)."""
@@ -50,13 +60,24 @@ def update(params, poses, disps, disps_sens, intrinsics, fmaps, ii, jj, net, inp
     rig = fmaps.shape[1]
     f1 = fmaps[ii, 0].astype(np.float32)
     f2 = fmaps[jj, np.where((ii == jj) & (rig > 1), 1, 0)].astype(np.float32)
-    pyr = oc.corr_pyramid(f1[None], f2[None])
-    corr = oc.lookup_pyramid(pyr, coords1[None].astype(np.float32), 3)
+    dv = torch.device("cpu") if device is None else torch.device(device)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dv)
+    if dv.type != "cpu":
+        p = {k: v.to(dv) for k, v in p.items()}
+    if torch_corr:
+        pyr = oc.corr_pyramid_torch(T(f1[None]), T(f2[None]))
+        corr = oc.lookup_pyramid_torch(pyr, T(coords1.astype(np.float32)), 3)[None]
+        del pyr
+    else:
+        pyr = oc.corr_pyramid(f1[None], f2[None])
+        corr = T(oc.lookup_pyramid(pyr, coords1[None].astype(np.float32), 3))
     with torch.no_grad():
         net1, delta, weight1, eta, _ = oum.update_module(
-            p, torch.from_numpy(np.asarray(net, np.float32))[None], torch.from_numpy(np.asarray(inp, np.float32))[None],
-            torch.from_numpy(corr), torch.from_numpy(motn[None].astype(np.float32)), torch.from_numpy(ii),
-            torch.from_numpy(jj))
+            p, T(np.asarray(net, np.float32))[None], T(np.asarray(inp, np.float32))[None],
+            corr, T(motn[None].astype(np.float32)), T(ii), T(jj))
+    if f16_outputs:
+        net1, delta, weight1, eta = (x.half().float() for x in (net1, delta, weight1, eta))
+    net1, delta, weight1, eta = (x.cpu() for x in (net1, delta, weight1, eta))
     if t0 is None:
         t0 = max(1, int(ii.min()) + 1)
     target = coords1 + delta[0].double().numpy()

@@ -10,6 +10,7 @@ TAG="$1"; shift
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$R" || exit 1
 export PYTHONUNBUFFERED=1
+export DROID_REPORT_DIR="$R/gpurun_out/$TAG"
 O="gpurun_out/$TAG"
 mkdir -p "$O"
 

@@ -471,6 +471,30 @@ def dense_ba_fixture(rng):
                         ba_poses=p1.data.numpy(), ba_disps=d1.numpy())
 
 
+def ate_fixture():
+    """The reference's own ATE known-answer pair (thirdparty/tartanair_tools/
+    evaluation/pose_{gt,est}.txt, data) and ATEEvaluator.evaluate's outputs on
+    it (evaluator_base.py:33-55), with and without scale."""
+    import contextlib
+    import io
+    d = os.path.join(os.path.dirname(REF), "thirdparty", "tartanair_tools")
+    sys.path.insert(0, d)
+    try:
+        from evaluation.evaluator_base import ATEEvaluator
+    finally:
+        sys.path.remove(d)
+    gt = np.loadtxt(os.path.join(d, "evaluation", "pose_gt.txt"))
+    est = np.loadtxt(os.path.join(d, "evaluation", "pose_est.txt"))
+    out = dict(pose_gt=gt, pose_est=est)
+    for scale in (True, False):
+        with contextlib.redirect_stdout(io.StringIO()) as log:
+            err, _, _ = ATEEvaluator().evaluate(gt, est, scale)
+        s = [float(l.split(":")[1]) for l in log.getvalue().splitlines() if "ATE scale" in l][0]
+        out["ate_scale" if scale else "ate_noscale"] = np.float64(err)
+        out["s_scale" if scale else "s_noscale"] = np.float64(s)
+    np.savez_compressed(os.path.join(HERE, "tartanair_poses.npz"), **out)
+
+
 def main():
     _install_stubs()
     sys.path.insert(0, REF)
@@ -541,6 +565,9 @@ def main():
 
     # --- the dense BA step, undamped, from geom/ba.py (pins droid_backends.ba) --
     dense_ba_fixture(np.random.default_rng(2030))
+
+    # --- ATE known answer (the trajectory-level "ATE vs ref" evaluator) ---------
+    ate_fixture()
     print("golden fixtures written to", HERE)
 
 

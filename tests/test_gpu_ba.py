@@ -89,6 +89,18 @@ def test_ba_global_c3():
     check(got, ref)
 
 
+def test_ba_stereo_c4_full_graph():
+    """The C4 config's whole graph: 128 KF, one (i, i) stereo
+    edge per frame (fixed -0.1 baseline, depth terms only,
+    droid_kernels.cu:219-229, 319-323) + temporal + loop edges = 984 edges at
+    48x64, update()'s lm / ep, vs the oracle at 1e-4."""
+    prob = synthetic.ba_problem("C4")
+    assert len(prob["ii"]) == 984 and int(np.sum(prob["ii"] == prob["jj"])) == 128
+    got, ref = run_both(prob, iterations=2, lm=1e-4, ep=0.1)
+    check(got, ref)
+    assert np.abs(ref["dx"]).max() > 1e-4
+
+
 @pytest.mark.parametrize("order", ["rcm", "mindeg", "nd"])
 def test_ba_forced_pose_orders(order, monkeypatch):
     """Every pose order the plan can choose solves the same step: with a

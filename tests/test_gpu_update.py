@@ -83,18 +83,17 @@ def test_update_lowmem_runs():
     assert np.isfinite(host(video.poses)).all() and np.isfinite(host(video.disps)).all()
 
 
-def _c2_video(H=48, W=64, seed=51):
+def _c2_video(H=48, W=64, seed=51, stereo=False, n=16, buffer=None):
     """C2 frontend shape: 16-KF buffer, fmaps/net/inp ~ N / tanh / relu."""
     from droid_mi355x import DepthVideo, synthetic
-    n = 16
     rng = np.random.default_rng(seed)
-    video = DepthVideo(image_size=(8 * H, 8 * W), buffer=n, device="cuda")
+    video = DepthVideo(image_size=(8 * H, 8 * W), buffer=buffer or n, stereo=stereo, device="cuda")
     gt = synthetic.trajectory(n, rng)
     poses, disps = synthetic.perturb(gt, synthetic.smooth_disps(n, H, W, rng), rng)
     video.poses[:n] = dev(poses.astype(np.float32))
     video.disps[:n] = dev(disps.astype(np.float32))
     video.intrinsics[:n] = dev(np.tile(synthetic.INTRINSICS * np.float32(W / 64.0), (n, 1)))
-    video.fmaps[:n] = dev(rng.normal(size=(n, 1, 128, H, W)).astype(np.float16))
+    video.fmaps[:n] = dev(rng.normal(size=(n, 2 if stereo else 1, 128, H, W)).astype(np.float16))
     video.nets[:n] = dev(np.tanh(rng.normal(size=(n, 128, H, W))).astype(np.float16))
     video.inps[:n] = dev(np.maximum(rng.normal(size=(n, 128, H, W)), 0).astype(np.float16))
     video.counter.value = n
@@ -110,21 +109,42 @@ def test_update_unit_matches_oracle_composition():
     tiled volume, fused delta/weight heads) for target, weight, damping and
     net at fp16 tolerance; the BA inputs it builds (edge lists exactly); and
     the BA result on those inputs at the north star's 1e-4."""
+    from droid_mi355x import synthetic
+    ii, jj = synthetic.c2_edges()
+    _update_unit_vs_oracle(_c2_video(48, 64), ii, jj)
+
+
+def test_update_unit_stereo_matches_oracle_composition():
+    """The same unit check on a stereo graph (SURVEY.md §8d C4 shape at 48x64):
+    every frame of the window has its (i, i) edge, whose correlation volume is
+    built against the RIGHT image (factor_graph.py:112-114) and whose BA rows
+    carry depth terms only (droid_kernels.cu:219-229, 319-323), plus temporal
+    and loop edges; use_inactive=True after the older edges are stored."""
+    ii, jj = _stereo_edges(16, lo=4, loops=[(15, 5), (5, 15), (13, 6), (6, 13), (12, 4), (4, 12)])
+    _update_unit_vs_oracle(_c2_video(48, 64, seed=53, stereo=True), ii, jj)
+
+
+def _stereo_edges(n, lo, loops):
+    es = [(i, i) for i in range(lo, n)]
+    es += [(i, j) for i in range(lo, n) for j in range(lo, n) if i != j and abs(i - j) <= 3]
+    es += [e for e in loops if e not in es]
+    e = np.asarray(es, np.int64)
+    return e[:, 0], e[:, 1]
+
+
+def _update_unit_vs_oracle(video, ii, jj, store_below=7):
     import droid_backends
-    from droid_mi355x import FactorGraph, UpdateModule, synthetic
+    from droid_mi355x import FactorGraph, UpdateModule
     from droid_mi355x.fused import FusedUpdateModule
     from oracle import factor_graph as ofg
-    H, W = 48, 64
-    video = _c2_video(H, W)
     m = UpdateModule().to("cuda").eval()
     det_fill(m)
     g = FactorGraph(video, FusedUpdateModule(m), device="cuda")
-    ii, jj = synthetic.c2_edges()
     with torch.no_grad():
         g.add_factors(ii, jj)
         g.update()                                  # non-trivial targets / weights / damping
-        g.rm_factors(g.ii < 7, store=True)          # device-tensor mask, as droid_frontend.py:42 passes
-    assert len(g._ii_inac) > 0 and g._ii.min() == 7
+        g.rm_factors(g.ii < store_below, store=True)   # device-tensor mask, as droid_frontend.py:42 passes
+    assert len(g._ii_inac) > 0 and g._ii.min() == store_below
     n = video.counter.value
     st = dict(poses=host(video.poses[:n]), disps=host(video.disps[:n]), disps_sens=host(video.disps_sens[:n]),
               intrinsics=host(video.intrinsics[:n]), fmaps=host(video.fmaps[:n].float()),
@@ -177,6 +197,78 @@ def test_update_unit_matches_oracle_composition():
     np.testing.assert_allclose(host(video.disps[:n]), np.maximum(ba_ref["disps"][:n], 0.001), atol=1e-4)
     # and the whole composition lands close to the oracle's own BA result
     np.testing.assert_allclose(host(video.poses[:n]), ref["poses"][:n], atol=2e-3)
+    return g, ref
+
+
+def test_update_motion_only_unit_matches_oracle():
+    """update(N, N + M, motion_only=True) as the trajectory filler calls it
+    (trajectory_filler.py:64-72): M new frames appended after N keyframes
+    (fmaps only, poses interpolated), edges from each frame's bracketing
+    keyframes t0 / t1 to it, motion-only BA over poses [N, N+M) - no Schur
+    step, no depth update.  Update-operator outputs at fp16 tolerance vs the
+    oracle composition, BA 1e-4 on the inputs update() handed over, 6
+    iterations as the filler runs."""
+    import droid_backends
+    from droid_mi355x import FactorGraph, UpdateModule
+    from droid_mi355x.fused import FusedUpdateModule
+    from oracle import factor_graph as ofg
+    H, W = 48, 64
+    video = _c2_video(H, W, seed=54)
+    N, M = 12, 4
+    m = UpdateModule().to("cuda").eval()
+    det_fill(m)
+    # the filler's new frames: interpolated poses (here: the neighbours' plus noise), fmaps, counter += M
+    rng = np.random.default_rng(55)
+    t0 = np.array([8, 9, 10, 10])
+    t1 = np.minimum(t0 + 1, N - 1)
+    with torch.no_grad():
+        video.poses[N:N + M] = video.poses[dev(t0)] + dev(rng.normal(0, 0.01, (M, 7)).astype(np.float32)) * \
+            dev(np.array([1, 1, 1, 0, 0, 0, 0], np.float32))
+        video.fmaps[N:N + M] = dev(rng.normal(size=(M, 1, 128, H, W)).astype(np.float16))
+        video.disps[N:N + M] = 1.0
+    params = {k: host(v.float()) for k, v in m.state_dict().items()}
+    g = FactorGraph(video, FusedUpdateModule(m), device="cuda")
+    with torch.no_grad():
+        g.add_factors(t0, np.arange(N, N + M))
+        g.add_factors(t1, np.arange(N, N + M))
+    n = N + M
+    for it in range(6):
+        st = dict(poses=host(video.poses[:n]), disps=host(video.disps[:n]), disps_sens=host(video.disps_sens[:n]),
+                  intrinsics=host(video.intrinsics[:n]), fmaps=host(video.fmaps[:n].float()),
+                  net=host(g.net.float()).transpose(0, 3, 1, 2), inp=host(g.inp.float()).transpose(0, 3, 1, 2),
+                  target=host(g.target[0]), weight=host(g.weight[0]), damping=host(g.damping[:n]))
+        captured = {}
+        orig = droid_backends.ba
+
+        def spy(*a, **k):
+            captured["a"] = [x.detach().clone() if isinstance(x, torch.Tensor) else x for x in a]
+            return orig(*a, **k)
+
+        droid_backends.ba = spy
+        try:
+            with torch.no_grad():
+                g.update(N, N + M, motion_only=True)
+        finally:
+            droid_backends.ba = orig
+        torch.cuda.synchronize()
+        ref = ofg.update(params, st["poses"], st["disps"], st["disps_sens"], st["intrinsics"], st["fmaps"], g._ii,
+                         g._jj, st["net"], st["inp"], st["target"], st["weight"], st["damping"], t0=N, t1=N + M,
+                         motion_only=True)
+        np.testing.assert_allclose(host(g.net.float()).transpose(0, 3, 1, 2), ref["net"], atol=2e-2)
+        dmax = max(1.0, float(np.abs(ref["target"] - ref["coords1"]).max()))
+        np.testing.assert_allclose(host(g.target[0]), ref["target"], atol=3e-2 * dmax)
+        np.testing.assert_allclose(host(g.weight[0]), ref["weight"], atol=1.5e-2)
+        a = captured["a"]
+        assert (a[9], a[10], a[14]) == (N, N + M, True)
+        ba_ref = oba.ba(poses=host(a[0]), disps=host(a[1]), intrinsics=host(a[2]), disps_sens=host(a[3]),
+                        targets=host(a[4]), weights=host(a[5]), eta=host(a[6]), ii=host(a[7]), jj=host(a[8]),
+                        t0=a[9], t1=a[10], iterations=a[11], lm=a[12], ep=a[13], motion_only=True)
+        np.testing.assert_allclose(host(video.poses[:n]), ba_ref["poses"][:n], atol=1e-4)
+        # motion-only: keyframe poses [0, N) and every disparity stay as they were
+        np.testing.assert_array_equal(host(video.poses[:N]), st["poses"][:N])
+        np.testing.assert_array_equal(host(video.disps[:n]), np.maximum(st["disps"], 0.001))
+        np.testing.assert_allclose(host(video.poses[:n]), ref["poses"][:n], atol=2e-3)
+    assert np.abs(host(video.poses[N:n]) - host(video.poses[dev(t0)])).max() > 1e-3
 
 
 def test_update_lowmem_matches_oracle_composition():

@@ -235,3 +235,26 @@ def test_oracle_ba_step_matches_reference_geom_ba(golden_dir):
     np.testing.assert_allclose(cuda["poses"], ref_poses, atol=1e-9, rtol=0)
     np.testing.assert_allclose(cuda["disps"][4:], ref_disps[4:], atol=1e-9, rtol=0)
     assert np.abs(cuda["disps"][:4] - ref_disps[:4]).max() > 1e-3
+
+
+def test_ate_matches_reference_evaluator(golden_dir):
+    """oracle/ate.py vs the reference's ATEEvaluator (evaluator_base.py:33-55)
+    on its own fixture pair: the known answers 0.8344983411575012 (scale,
+    s = 1.0782526734172067) and 1.204507439280004 (no scale)."""
+    from oracle import ate
+    d = np.load(os.path.join(golden_dir, "tartanair_poses.npz"))
+    e, s = ate.ate(d["pose_gt"], d["pose_est"], True)
+    np.testing.assert_allclose(e, d["ate_scale"], rtol=1e-12)
+    np.testing.assert_allclose(s, d["s_scale"], rtol=1e-12)
+    np.testing.assert_allclose(e, 0.8344983411575012, rtol=1e-12)
+    np.testing.assert_allclose(s, 1.0782526734172067, rtol=1e-12)
+    e, s = ate.ate(d["pose_gt"], d["pose_est"], False)
+    np.testing.assert_allclose(e, d["ate_noscale"], rtol=1e-12)
+    np.testing.assert_allclose(e, 1.204507439280004, rtol=1e-12)
+    assert s == 1.0
+    # identical trajectories (any rigid motion + scale of the estimate) have zero ATE
+    gt = d["pose_gt"][:50]
+    R = np.array([[0.0, -1.0, 0.0], [1.0, 0.0, 0.0], [0.0, 0.0, 1.0]])
+    est = gt.copy()
+    est[:, :3] = (gt[:, :3] @ R.T + [1.0, 2.0, 3.0]) / 2.5
+    assert ate.ate(gt, est, True)[0] < 1e-9
