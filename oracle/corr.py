@@ -243,7 +243,7 @@ def lookup_pyramid_torch(pyramid, coords, r=3):
     import torch.nn.functional as F
     B, H, W, _ = coords.shape
     rd = 2 * r + 1
-    d = torch.arange(-r, r + 1, dtype=coords.dtype)
+    d = torch.arange(-r, r + 1, dtype=coords.dtype, device=coords.device)
     outs = []
     for lvl, vol in enumerate(pyramid):
         H2, W2 = vol.shape[-2:]

@@ -24,11 +24,12 @@ from frontend_replay import DeviceSide, oracle_side, replay, synthetic_stream
 pytestmark = pytest.mark.gpu
 
 H, W = 48, 64
-FRAMES = 24
+FRAMES = 28
 # demo.py's keyframe_thresh is 4.0 px; the untrained update operator moves
-# these synthetic frames less, so the test uses a threshold inside the
-# distances its sequence produces - some keyframes are kept, some dropped
-KEYFRAME_THRESH = 3.0
+# these synthetic frames less (0.1 - 3.3 px between consecutive keyframes,
+# profiles/r03/trajectory_parity_*.json), so the test uses a threshold inside
+# the distances its sequence produces - some keyframes are kept, some dropped
+KEYFRAME_THRESH = 1.0
 
 
 def _report(name, rep):
@@ -62,5 +63,7 @@ def test_frontend_sequence_matches_oracle():
     # the device made the same discrete decisions as the oracle
     assert rep["edge_mismatch"] == 0 and rep["keyframe_mismatch"] == 0, summary
     # bounded compounding of the fp16 update operator over the whole sequence
-    assert rep["max_dpose"] < 2e-2, summary
-    assert rep["ate_vs_ref"] < 1e-2 * max(rep["trajectory_extent"], 1e-3) + 1e-3, summary
+    # (measured: max |dpose| 1e-4 after 82 updates, ATE 3.6e-5 over a 0.25 m path)
+    assert rep["max_dpose"] < 1e-3, summary
+    assert rep["max_ddisp"] < 5e-2, summary
+    assert rep["ate_vs_ref"] < 1e-3, summary
