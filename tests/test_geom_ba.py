@@ -1,4 +1,4 @@
-"""The differentiable training-path BA (droid_mi355x.geom_ba: BA, MoBA, the
+"""The differentiable training-path BA (droid_mi355x.dense_ba: BA, MoBA, the
 implicit-gradient LLT) vs the reference's own geom/ba.py (tests/golden/
 geom_ba.npz, run by make_golden.py with an independent SE3 stand-in whose Exp
 is a matrix exponential): poses, disparities and the gradients of a fixed
@@ -12,7 +12,7 @@ import torch
 
 
 def _run(z, dev, dtype):
-    from droid_mi355x.geom_ba import BA, MoBA
+    from droid_mi355x.dense_ba import BA, MoBA
     from droid_mi355x.lie import SE3
     T = lambda k: torch.from_numpy(z[k]).to(device=dev, dtype=dtype)
     ii, jj = torch.from_numpy(z["ii"]).to(dev), torch.from_numpy(z["jj"]).to(dev)
