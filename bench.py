@@ -86,7 +86,7 @@ def build_state(args, rank, world, device):
     else:
         ii, jj = synthetic.c3_edges(args.frames, args.edges, rng=np.random.default_rng(1003))
     comm = None
-    if world > 1:
+    if world > 1 or args.force_dist:
         ii_l, jj_l, own = sharding.shard_edges(ii, jj, args.frames, rank, world)
         # the BA gathers the global edge list once per edge-set version (every rank
         # derives the same reduced-system tile structure from it)
@@ -185,6 +185,7 @@ def stage_breakdown(graph, video, steps=3):
         return out
 
     graph.update_op, video.ba = op, ba
+    graphs, graph.graphs = graph.graphs, "0"    # the wrappers must see every call (no graph replay)
     for t in timers.values():
         t.active = True
     with torch.no_grad():
@@ -192,6 +193,7 @@ def stage_breakdown(graph, video, steps=3):
             graph.update()
     torch.cuda.synchronize()
     graph.update_op, video.ba = orig_op, orig_ba
+    graph.graphs = graphs
     out = {k: t.mean_ms() for k, t in timers.items()}
     for t in timers.values():
         setattr(t.module, t.name, t.orig)
@@ -377,7 +379,11 @@ def main():
     device = torch.device("cuda", 0 if one_dev else local_rank)
     torch.cuda.set_device(device)
     import torch.distributed as dist
-    if world > 1:
+    # DROID_BENCH_FORCE_DIST=1: the sharded path (process group, all-reduce of the
+    # reduced system) even with one rank - exercises RCCL on a one-GPU box
+    args.force_dist = os.environ.get("DROID_BENCH_FORCE_DIST") == "1"
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
         backend = os.environ.get("DROID_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
@@ -407,7 +413,7 @@ def main():
         torch.cuda.synchronize(device)
         if rank == 0:
             log("warmup %.1fs, peak HBM %.1f GB" % (time.time() - t_w, torch.cuda.max_memory_allocated(device) / 1e9))
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize(device)
         lookup.active = True
@@ -419,13 +425,13 @@ def main():
         for _ in range(args.steps):
             step_fn()
         torch.cuda.synchronize(device)
-        if world > 1:
+        if dist_on:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         lookup.active = False
         if zr:
             zr.active = zrp.active = False
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -544,7 +550,7 @@ def main():
             except Exception as ex:  # the baseline is reported, never fatal
                 result["cpu_baseline"] = {"value": None, "error": repr(ex)}
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

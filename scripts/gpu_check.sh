@@ -66,6 +66,13 @@ for step in "$@"; do
         --steps 3 --warmup 1 --no-cpu-baseline > "$O/bench_2rank.json" 2> "$O/bench_2rank.err" \
         || fail "$step" $? "$O/bench_2rank.err"
       cat "$O/bench_2rank.json" ;;
+    rccl1)
+      # the sharded path on RCCL with one rank (nccl backend initialised, device all-reduce of the
+      # reduced system's tiles): the one-GPU box's check of what the 8-GPU node runs
+      DROID_BENCH_FORCE_DIST=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 1 --config C3 --steps 3 --warmup 1 \
+        --no-cpu-baseline > "$O/bench_rccl1.json" 2> "$O/bench_rccl1.err" || fail "$step" $? "$O/bench_rccl1.err"
+      cat "$O/bench_rccl1.json" ;;
     py:*)
       timeout -k 10 600 python -u ${step#py:} > "$O/py.txt" 2>&1 || fail "$step" $? "$O/py.txt"
       tail -30 "$O/py.txt" ;;
