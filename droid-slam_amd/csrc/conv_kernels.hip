@@ -2012,6 +2012,30 @@ int droid_conv_dw_head_f16(const void* const* srcs, const int* C, const int* cst
 
 // ConvGRU global context (gru_glo_kernel): h (E, HW, 128) fp16, w [128][128]
 // fp16 (the 1x1 conv weight, [co][ci]), bias [128] f32 -> glo (E, 128) f32.
+__global__ void __launch_bounds__(384) glo_gates_kernel(const float* __restrict__ part, int splits,
+                                                        const float* __restrict__ w, const float* __restrict__ b,
+                                                        float* __restrict__ out, int E) {
+  __shared__ float g[128];
+  const int e = blockIdx.x, t = threadIdx.x;
+  if (t < 128) {
+    float s = 0.f;
+    for (int r = 0; r < splits; ++r) s += part[((long)r * E + e) * 128 + t];
+    g[t] = s;
+  }
+  __syncthreads();
+  const float4* wr = reinterpret_cast<const float4*>(w + (long)t * 128);
+  float acc = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < 32; ++k) {
+    const float4 v = wr[k];
+    acc = fmaf(g[4 * k], v.x, acc);
+    acc = fmaf(g[4 * k + 1], v.y, acc);
+    acc = fmaf(g[4 * k + 2], v.z, acc);
+    acc = fmaf(g[4 * k + 3], v.w, acc);
+  }
+  out[(long)e * 384 + t] = acc + b[t];
+}
+
 static int glo_set_attr() {
   static bool attr = false;
   if (!attr) {
@@ -2048,6 +2072,20 @@ int droid_gru_global_split_f16(const void* h, const void* w, const float* bias, 
   if (E == 0) return kOk;
   { const int st = glo_set_attr(); if (st != kOk) return st; }
   gru_glo_kernel<<<dim3(E, splits), 256, kGloLds, stream>>>((const __half*)h, (const __half*)w, bias, part, HW);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+// The GRU's global-context gate terms (gru.py:29-32, convz_glo | convr_glo |
+// convq_glo on glo): out[e][o] = b[o] + sum_k glo[e][k] w[o][k], o < 384, with glo
+// the in-order sum of the `splits` per-range partial means (gru_global_split).
+// One workgroup per edge; a plain fp32 dot per output (no BLAS library call in
+// the update path - it keeps update() capturable as one HIP graph).
+int droid_glo_gates_f32(const float* part, int splits, const float* w, const float* b, float* out, int E,
+                        hipStream_t stream) {
+  if (E < 0 || splits < 1 || !part || !w || !b || !out) return fail(kInvalidArgument, "glo_gates_f32: bad arguments");
+  if (E == 0) return kOk;
+  glo_gates_kernel<<<dim3(E), 384, 0, stream>>>(part, splits, w, b, out, E);
   DROID_LAUNCH_CHECK();
   return kOk;
 }

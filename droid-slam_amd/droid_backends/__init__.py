@@ -368,6 +368,32 @@ def flow_enc0_f16(motn, w, bias, out=None):
     return out
 
 
+def gru_glo_gates(h, w, bias, gw, gb):
+    """The ConvGRU global-context branch end to end: glo = mean_px sigmoid(w h +
+    bias) h (droid_gru_global[_split]_f16), then its three 1x1 gate convs
+    (droid_glo_gates_f32): h (E,H,W,128) fp16, w [128][128] fp16, bias [128],
+    gw (384,128) f32, gb (384) f32 -> (E,384) f32 = [z | r | q] terms."""
+    _check_inputs(("h", "w", "bias", "gw", "gb"), (h, w, bias, gw, gb))
+    _need(gw, torch.float32, "gw")
+    _need(gb, torch.float32, "gb")
+    E, H, W, C = h.shape
+    if tuple(gw.shape) != (384, 128) or gb.numel() != 384:
+        raise RuntimeError("gru_glo_gates: gw must be (384,128) and gb (384)")
+    splits = max(1, min((H * W) // 256, -(-512 // max(E, 1))))
+    part = torch.empty((splits, E, 128), dtype=torch.float32, device=h.device)
+    out = torch.empty((E, 384), dtype=torch.float32, device=h.device)
+    with torch.cuda.device(h.device):
+        if splits == 1:
+            check(lib.droid_gru_global_f16(_ptr(h), _ptr(w), _ptr(bias), _ptr(part), E, H * W, _stream(h)),
+                  "gru_global_f16")
+        else:
+            check(lib.droid_gru_global_split_f16(_ptr(h), _ptr(w), _ptr(bias), _ptr(part), splits, E, H * W,
+                                                 _stream(h)), "gru_global_split_f16")
+        check(lib.droid_glo_gates_f32(_ptr(part), splits, _ptr(gw), _ptr(gb), _ptr(out), E, _stream(h)),
+              "glo_gates_f32")
+    return out
+
+
 def gru_global_f16(h, w, bias, out=None):
     """ConvGRU global context (include/droid_backends.h: droid_gru_global_f16):
     h (E,H,W,128) fp16, w [128][128] fp16, bias [128] f32 -> (E,128) f32."""

@@ -71,6 +71,7 @@ class FactorGraph:
         self._version = 0          # bumped by every edge edit
         self._graph = None         # captured update: dict(key, graph, net, target, weight, plan)
         self._graph_warm = None    # key of the last eager call (the capture follows it)
+        self._cap_stream = None
 
     # -- per-edge state layout ------------------------------------------------
     @property
@@ -273,17 +274,27 @@ class FactorGraph:
             g["plan"]._record_status()
             self.age += 1
             return
+        # the eager call before a capture runs on the capture stream (torch's
+        # warm-up rule: lazily created per-stream state must not be born inside
+        # the capture); both directions are ordered against the caller's stream
+        if self._cap_stream is None:
+            self._cap_stream = torch.cuda.Stream(device=self.device)
+        cs, main = self._cap_stream, torch.cuda.current_stream(self.device)
         if self._graph_warm != key:
             self._graph, self._graph_warm = None, key
-            self._update(*args)
+            cs.wait_stream(main)
+            with torch.cuda.stream(cs):
+                self._update(*args)
+            main.wait_stream(cs)
             return
         droid_backends.check_status()        # no host wait may happen inside the capture
         saved = (self.net, self.target, self.weight)
         static = dict(net=self.net, target=self.target, weight=self.weight.clone())
         self.weight = static["weight"]
         graph = torch.cuda.CUDAGraph()
+        cs.wait_stream(main)
         try:
-            with torch.cuda.graph(graph):
+            with torch.cuda.graph(graph, stream=cs):
                 self._update(*args, age=False)
                 for name in ("net", "target", "weight"):   # this update's state -> the static inputs
                     static[name].copy_(getattr(self, name))

@@ -180,8 +180,9 @@ class FusedUpdateModule(torch.nn.Module):
         P["zr_x"] = pack_conv(keep(wzr), [128, 128, 64])
         P["q_x"] = pack_conv(keep(g.convq.weight), [128, 128, 64])
         P["inp_zrq"] = pack_conv(torch.cat([wzr[:, 128:256], g.convq.weight[:, 128:256]], 0), [128])
-        P["glo_w"] = torch.cat([g.convz_glo.weight, g.convr_glo.weight, g.convq_glo.weight], 0)[:, :, 0, 0].float()
-        P["glo_b"] = torch.cat([g.convz_glo.bias, g.convr_glo.bias, g.convq_glo.bias]).float()
+        P["glo_w"] = torch.cat([g.convz_glo.weight, g.convr_glo.weight, g.convq_glo.weight],
+                               0)[:, :, 0, 0].float().contiguous()
+        P["glo_b"] = torch.cat([g.convz_glo.bias, g.convr_glo.bias, g.convq_glo.bias]).float().contiguous()
         P["dw0"] = pack_conv(torch.cat([m.delta[0].weight, m.weight[0].weight], 0), [128])
         P["dw0_b"] = torch.cat([m.delta[0].bias, m.weight[0].bias]).float().contiguous()
         head = torch.zeros(4, 256, 3, 3, device=m.delta[2].weight.device)
@@ -252,12 +253,12 @@ class FusedUpdateModule(torch.nn.Module):
         ff = e16(64)
         conv([(f1, 0, 128)], P["fe2"], 64, 3, bias=P["fe2_b"], act=1, out=ff)
 
-        if (H * W) % 64 == 0:
-            glo = droid_backends.gru_global_f16(net, P["w_128"], P["w_b"])
+        if (H * W) % 64 == 0:    # glo and its three gate convs: two kernels, no BLAS call
+            gb = droid_backends.gru_glo_gates(net, P["w_128"], P["w_b"], P["glo_w"], P["glo_b"])
         else:
             glo = torch.zeros((E, 128), dtype=torch.float32, device=dev)
             conv([(net, 0, 128)], P["w"], 128, 1, bias=P["w_b"], epi=EPI_GLO, h=net, out32=glo)
-        gb = torch.addmm(P["glo_b"], glo, P["glo_w"].t())          # (E, 384): z | r | q
+            gb = torch.addmm(P["glo_b"], glo, P["glo_w"].t())      # (E, 384): z | r | q
         z = e16(128)
         rn = e16(128)
         net_new = e16(128)

@@ -188,6 +188,14 @@ int droid_gru_global_f16(const void* h, const void* w, const float* bias, float*
 int droid_gru_global_split_f16(const void* h, const void* w, const float* bias, float* part, int splits,
                                int E, int HW, hipStream_t stream);
 
+/* the ConvGRU's global gate terms (gru.py:29-32: convz_glo | convr_glo | convq_glo
+ * on glo): out (E,384) f32 = b + glo w^T, glo = sum over `splits` of part
+ * (splits,E,128) f32 (the in-order sum of droid_gru_global_split_f16's ranges;
+ * splits = 1 for droid_gru_global_f16's output), w (384,128) f32 row-major,
+ * 16-B aligned. */
+int droid_glo_gates_f32(const float* part, int splits, const float* w, const float* b, float* out, int E,
+                        hipStream_t stream);
+
 /* GraphAgg scatter_mean (droid_net.py:27-45, torch_scatter.scatter_mean over
  * dim 1): out[u] = mean of src rows seg_idx[seg_ptr[u] .. seg_ptr[u+1]), rows of
  * `row` fp16 values (row % 8 == 0), fp32 accumulation.  seg_ptr (U+1), seg_idx
