@@ -524,8 +524,9 @@ def main():
         e_op = e_local if args.config == "C2" else len(ii)
         n_src = len(np.unique(graph._ii)) if args.config == "C2" else len(np.unique(ii))
         conv_flops = (CONV_FLOPS_PER_EDGE_PIXEL * e_op + CONV_FLOPS_PER_FRAME_PIXEL * n_src) * hw
-        if factored:   # the algorithm run: gate inp term per source frame, not per edge
-            conv_flops -= GATE_INP_FLOPS_PER_PIXEL * (e_op - n_src) * hw
+        if factored:   # the algorithm run: the gate's inp term once per edge set (per source
+            # frame, cached across updates - FusedUpdateModule._pre), not per edge and update
+            conv_flops -= GATE_INP_FLOPS_PER_PIXEL * e_op * hw
         hbm_bytes = HBM_BYTES_PER_EDGE * e_op + HBM_BYTES_PER_FRAME * args.frames
         mfma_floor = conv_flops / (PEAK_F16_TFLOPS * 1e12) * 1e3 / world
         hbm_floor = hbm_bytes / (PEAK_HBM_GBS * 1e9) * 1e3 / world

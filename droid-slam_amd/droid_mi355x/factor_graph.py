@@ -425,6 +425,9 @@ class FactorGraph:
             ptr, idx = edge_segments(inverse, len(uniq))
             segs = (self._dev("seg_ptr", ptr), self._dev("seg_idx", idx))
             duniq = self._dev("uniq", uniq)
+            # the source frames' context features: the same tensor for every step
+            # (the update operator caches its per-frame gate term on it)
+            inp_frames = self.video.inps[duniq].permute(0, 2, 3, 1).contiguous()
         else:
             corr_op = AltCorrBlock(self.video.fmaps.view(1, num * rig, ch, ht, wd))
         for _ in range(steps):
@@ -435,7 +438,6 @@ class FactorGraph:
                 coords1 = coords1.view(1, E, ht, wd, 2)
                 motn = motn.view(1, E, 4, ht, wd)
             if self.fused:
-                inp_frames = self.video.inps[duniq].permute(0, 2, 3, 1).contiguous()
                 corr = PendingAltLookup(pyr, f1, f2, coords1)
                 self.net, delta, weight, damping = self.update_op(self.net, None, corr, motn[0], dinv, len(uniq),
                                                                   segments=segs, inp_frames=inp_frames)

@@ -136,9 +136,11 @@ class FusedUpdateModule(torch.nn.Module):
         super().__init__()
         self.m = module if module is not None else UpdateModule()
         self._packed = None
+        self._pre = None   # (inp_frames, packed weights, per-frame gate term)
 
     def load_state_dict(self, *a, **k):
         self._packed = None
+        self._pre = None
         return self.m.load_state_dict(*a, **k)
 
     def state_dict(self, *a, **k):
@@ -263,9 +265,16 @@ class FusedUpdateModule(torch.nn.Module):
         rn = e16(128)
         net_new = e16(128)
         if inp_frames is not None and droid_backends.gru_pre_supported(H, W):
-            U = inp_frames.shape[0]
-            pre = torch.empty((U, H, W, 384), dtype=torch.float16, device=dev)
-            conv([(inp_frames, 0, 128)], P["inp_zrq"], 384, 3, out=pre)
+            # the per-source-frame gate term depends on the context features and
+            # the weights only: it is the same in every update() of an edge set,
+            # so it is computed once per inp_frames tensor (the graph caches that
+            # tensor per edge set) instead of once per update
+            c = self._pre
+            if c is None or c[0] is not inp_frames or c[1] is not P:
+                pre = torch.empty((inp_frames.shape[0], H, W, 384), dtype=torch.float16, device=dev)
+                conv([(inp_frames, 0, 128)], P["inp_zrq"], 384, 3, out=pre)
+                self._pre = c = (inp_frames, P, pre)
+            pre = c[2]
             pidx = inverse if inverse.dtype == torch.int64 else inverse.long()
             droid_backends.conv_gru_pre_f16([(net, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["zr_x"], 256, P["zr_b"],
                                             gb[:, :256].contiguous(), EPI_GRU_ZR, pre, pidx, 0, h=net, zout=z,
