@@ -104,13 +104,8 @@ __device__ __forceinline__ void wave_transpose_reduce128(float* v, int lane) {
     const bool upper = (lane & off) != 0;
 #pragma unroll
     for (int k = 0; k < n; ++k) {
-      // the two candidates pass through an empty asm so the lane-dependent
-      // choice stays a v_cndmask on registers: as a select of array elements
-      // the compiler turned it into a dynamic index and kept v[] in scratch
-      float a = v[k], b = v[k + n];
-      asm volatile("" : "+v"(a), "+v"(b));
-      const float send = upper ? a : b;
-      const float keep = upper ? b : a;
+      const float send = upper ? v[k] : v[k + n];
+      const float keep = upper ? v[k + n] : v[k];
       v[k] = keep + __shfl_xor(send, off);
     }
   }

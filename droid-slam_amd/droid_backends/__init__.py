@@ -727,27 +727,17 @@ class BaPlan:
                                                       dtype=torch.float32, device=poses.device)
         if iterations <= 0:
             return dx.zero_(), dz
-        capturing = torch.cuda.is_current_stream_capturing()
-        if not capturing:
-            self.check_status()
+        self.check_status()
         with torch.cuda.device(poses.device):
             check(lib.droid_ba_run(self._h, _ptr(self.workspace), _ptr(poses), _ptr(disps), _ptr(intrinsics),
                                    _ptr(disps_sens), _ptr(targets), _ptr(weights), _ptr(eta), int(iterations),
                                    float(lm), float(ep), _ptr(dx), _ptr(dz), _stream(poses)), "ba")
-            if not capturing:   # a captured run's status is recorded after each replay (last_plan)
-                self._record_status()
+            self._record_status()
         return dx, dz
 
 
 _PLAN_CACHE = OrderedDict()
 _PLAN_CACHE_SIZE = 8
-_LAST_PLAN = [None]
-
-
-def last_plan():
-    """the plan of the last ba() call (a caller replaying a captured ba records
-    its status with plan._record_status() after each replay)."""
-    return _LAST_PLAN[0]
 
 
 def check_status():
@@ -836,7 +826,6 @@ def ba(poses, disps, intrinsics, disps_sens, targets, weights, eta, ii, jj, t0, 
         jj_host = jj.cpu().numpy()
     eta_rows = eta.numel() // (H * W) if eta.numel() else 0
     plan = get_plan(ii_host, jj_host, N, H, W, int(t0), int(t1), eta_rows, motion_only, poses.device)
-    _LAST_PLAN[0] = plan
     dx, dz = plan.run(poses, disps, intrinsics, disps_sens, targets, weights, eta, int(iterations), lm, ep)
     if sync:
         plan.check_status()

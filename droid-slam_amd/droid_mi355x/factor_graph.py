@@ -60,18 +60,7 @@ class FactorGraph:
         self.fused = isinstance(update_op, FusedUpdateModule)
         # CorrBlock(tiled=...) for the fused lookup (DROID_TILED_VOLUME=0: reference row-major layout)
         self.tiled_volume = os.environ.get("DROID_TILED_VOLUME", "1") != "0"
-        # HIP-graph replay of update() per edge set (fused operator, one device):
-        # the second call with the same edge set and arguments captures the whole
-        # update - reprojection, lookup, update operator, GraphAgg, BA - and
-        # every later call replays it (no per-kernel host launch cost).  "auto":
-        # graphs for graphs of <= 512 edges (the frontend's, where host issue is
-        # the bottleneck); the 2k-edge global graph is GPU-bound either way and
-        # keeps the eager launches that bench.py's per-kernel HIP events time
-        self.graphs = os.environ.get("DROID_UPDATE_GRAPHS", "auto")
         self._version = 0          # bumped by every edge edit
-        self._graph = None         # captured update: dict(key, graph, net, target, weight, plan)
-        self._graph_warm = None    # key of the last eager call (the capture follows it)
-        self._cap_stream = None
 
     # -- per-edge state layout ------------------------------------------------
     @property
@@ -117,13 +106,10 @@ class FactorGraph:
 
     # -- graph edits (factor_graph.py:43-193) ---------------------------------
     def _edited(self):
-        """edge-set version: invalidates a captured update graph, and (sharded BA)
-        versions the global-edge cache - every edit, issued in lockstep on all
-        ranks even when it leaves this rank's shard unchanged, bumps it, so all
-        ranks agree on when to re-gather."""
+        """edge-set version (sharded BA: the global-edge cache key) - every edit,
+        issued in lockstep on all ranks even when it leaves this rank's shard
+        unchanged, bumps it, so all ranks agree on when to re-gather."""
         self._version += 1
-        self._graph = None
-        self._graph_warm = None
         if self.comm is not None:
             self.comm["version"] = self.comm.get("version", 0) + 1
 
@@ -247,70 +233,6 @@ class FactorGraph:
 
     # -- the hot path (factor_graph.py:196-242) -------------------------------
     def update(self, t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, motion_only=False):
-        args = (t0, t1, itrs, use_inactive, EP, motion_only)
-        use = self.graphs not in ("0", False, None) and (self.graphs != "auto" or 0 < len(self._ii) <= 512)
-        if use and self.fused and self.comm is None and len(self._ii) > 0:
-            return self._update_graphed(args)
-        self._update(*args)
-
-    def _update_graphed(self, args):
-        """update() through a HIP graph of this edge set: the first call is eager
-        (and warms every cache the body reads: edge-list uploads, BA plan, the
-        per-frame inp rows), the second captures the body and replays it, later
-        ones only replay.  The per-edge state (net, target, weight) lives in
-        static buffers the graph reads and refills, so replay t+1 sees replay
-        t's output; a new edge set (add / rm_factors, rm_keyframe) drops the
-        graph.  Results are bitwise those of the eager body (every kernel is
-        deterministic; tests/test_gpu_update.py)."""
-        key = (self._version, self.video.counter.value) + args
-        g = self._graph
-        if g is not None and g["key"] == key:
-            for name in ("net", "target", "weight"):      # state replaced from outside: copy it in
-                cur = getattr(self, name)
-                if cur is not g[name]:
-                    g[name].copy_(cur)
-                    setattr(self, name, g[name])
-            g["graph"].replay()
-            g["plan"]._record_status()
-            self.age += 1
-            return
-        # the eager call before a capture runs on the capture stream (torch's
-        # warm-up rule: lazily created per-stream state must not be born inside
-        # the capture); both directions are ordered against the caller's stream
-        if self._cap_stream is None:
-            self._cap_stream = torch.cuda.Stream(device=self.device)
-        cs, main = self._cap_stream, torch.cuda.current_stream(self.device)
-        if self._graph_warm != key:
-            self._graph, self._graph_warm = None, key
-            cs.wait_stream(main)
-            with torch.cuda.stream(cs):
-                self._update(*args)
-            main.wait_stream(cs)
-            return
-        droid_backends.check_status()        # no host wait may happen inside the capture
-        saved = (self.net, self.target, self.weight)
-        static = dict(net=self.net, target=self.target, weight=self.weight.clone())
-        self.weight = static["weight"]
-        graph = torch.cuda.CUDAGraph()
-        cs.wait_stream(main)
-        try:
-            with torch.cuda.graph(graph, stream=cs):
-                self._update(*args, age=False)
-                for name in ("net", "target", "weight"):   # this update's state -> the static inputs
-                    static[name].copy_(getattr(self, name))
-        except Exception:
-            # capture unsupported here (e.g. an op that syncs): stay eager
-            self.net, self.target, self.weight = saved
-            self.graphs = "0"
-            self._update(*args)
-            return
-        self.net, self.target, self.weight = static["net"], static["target"], static["weight"]
-        self._graph = dict(key=key, graph=graph, plan=droid_backends.last_plan(), **static)
-        graph.replay()
-        self._graph["plan"]._record_status()
-        self.age += 1
-
-    def _update(self, t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, motion_only=False, age=True):
         ht, wd = self.ht, self.wd
         E = len(self._ii)
         ii, jj = self.ii, self.jj
@@ -382,8 +304,7 @@ class FactorGraph:
                           t0, t1, itrs=itrs, lm=1e-4, ep=0.1, motion_only=motion_only,
                           ii_host=ii_h, jj_host=jj_h, comm=self.comm,
                           edge_tag="update+inactive" if use_inactive else "update")
-        if age:
-            self.age += 1
+        self.age += 1
 
     def _pending_alt_lookup(self, coords1):
         """corr_impl "pyramid": AltCorrBlock pyramid of the frames (built once per
