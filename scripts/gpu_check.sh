@@ -73,6 +73,9 @@ for step in "$@"; do
         --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 1 --config C3 --steps 3 --warmup 1 \
         --no-cpu-baseline > "$O/bench_rccl1.json" 2> "$O/bench_rccl1.err" || fail "$step" $? "$O/bench_rccl1.err"
       cat "$O/bench_rccl1.json" ;;
+    env:*)
+      # export K=V for the steps that follow (A/B runs: env:DROID_OVERLAP_GLO=0 bench:C3)
+      export "${step#env:}"; echo "export ${step#env:}" ;;
     py:*)
       timeout -k 10 600 python -u ${step#py:} > "$O/py.txt" 2>&1 || fail "$step" $? "$O/py.txt"
       tail -30 "$O/py.txt" ;;
