@@ -42,6 +42,8 @@
 #include "lds_dma.hpp"
 
 #include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 
 // the bilinear at::Half arithmetic needs every product and sum rounded separately
 #pragma clang fp contract(off)
@@ -549,11 +551,432 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
   }
 }
 
+
+// ===========================================================================
+// corr_alt2_kernel: the same lookup with TWO 4-wave workgroups per CU, so one
+// workgroup's DMA waits and barriers overlap the other's MFMA / VALU work (the
+// one-workgroup kernel above spends ~2 ms of its 4.4 ms at C3 in barrier-phased
+// stage skeletons).  LDS per workgroup <= 80 KB - one region of 304 tap rows x
+// 256 B, used three ways:
+//   * box: tap row t = the 128 fp16 features of box tap t (16-B pieces XOR
+//     swizzled by t & 15, as the LDS-DMA lands them);
+//   * C in place: C(p, t) = <F1(p), tap t> (fp16) overwrites the FIRST 128 B of
+//     tap row t.  The wave that reads a 16-tap block is the one that writes its
+//     C, after its reads, so no other wave is racing it; the bilinear then
+//     addresses C(p, t) = 256 t + 2 p - linear in t, one base per window row
+//     plus immediate offsets;
+//   * the lookup tile of level slot s, [64 px][64 k] (49 used), in the SECOND
+//     halves: As(s, p, k) at row 64 s + p, byte 128 + 16 ((k / 8) ^ (p & 7)) +
+//     2 (k % 8); the padding columns are zeroed in registers, not in LDS;
+//   * the finished tile's output rows staged in the first halves of rows 64..191.
+// Per tile: levels 3, 2, 1 in one stage (boxes packed at 4-aligned tap
+// offsets, 292 taps at the C3 trajectory's p95), then level 0 (296 at p95).  A
+// box set that does not fit runs one level at a time, a level box that does not
+// fit runs as halves / quadrants / single pixels, each group with its own
+// encoder pass over its M-block(s) (rows of pixels outside the group are zero,
+// so the pass adds exactly 0 to them).  Every value is computed by the same
+// operations in the same order as corr_alt_ce0_kernel: the outputs are
+// bitwise equal (tests/test_gpu_fused.py).
+// ===========================================================================
+constexpr int kB2Rows = 304;
+constexpr int kB2Coord = kB2Rows * 256;       // [2 slots][64 px] float2
+constexpr int kB2Lvl = kB2Coord + 2 * 512;    // [2 slots][4 levels] x0, y0, w, h
+constexpr int kB2Grp = kB2Lvl + 2 * 16 * 4;   // fallback groups: count, then (x0, y0, w, h, qmask, gpix)
+constexpr int kB2Lds = kB2Grp + (4 + kAltMaxGroups * 6) * 4;
+static_assert(kB2Lds <= 80 * 1024, "two workgroups per CU");
+static_assert(3 * 64 <= kB2Rows && 64 + 128 <= kB2Rows, "lookup tiles and output staging fit the region");
+constexpr unsigned kB2Zero = 0x100000u;       // past the LDS allocation: ds reads return 0
+
+__device__ __forceinline__ _Float16 b2_ldh(const char* lds, unsigned addr) {
+  return *reinterpret_cast<const _Float16*>(lds + addr);
+}
+
+// LDS-DMA of a gbw x gbh box of level l of frame f2 to tap rows [toff, toff + taps), 4 waves
+__device__ __forceinline__ void b2_box_dma(const AltArgs& a, int l, int f2, int gx0, int gy0, int gbw, int gbh,
+                                           int toff, unsigned lds_a, int wave_u, int lane) {
+  const int tn = gbw * gbh;
+  if (tn <= 0) return;
+  const int Hl = a.Hl[l], Wl = a.Wl[l];
+  const rsrc_t rs = make_rsrc(a.pyr[l] + (long)__builtin_amdgcn_readfirstlane(f2) * Hl * Wl * 128,
+                              (unsigned)(Hl * Wl * 256));
+  const int nins = (tn + 3) >> 2;
+  const float inv = __builtin_amdgcn_rcpf((float)gbw);   // exact floor: see alt_box_dma
+  for (int ins = wave_u; ins < nins; ins += 4) {
+    const int tap = ins * 4 + (lane >> 4);
+    const int piece = (lane & 15) ^ ((toff + tap) & 15);
+    const int ry = (int)(((float)tap + 0.5f) * inv), rx = tap - ry * gbw;
+    const unsigned off = tap < tn ? (unsigned)((((gy0 + ry) * Wl + gx0 + rx) * 128 + piece * 8) * 2) : kOob;
+    dma16(rs, lds_a + (unsigned)(toff + ins * 4) * 256u, off);
+  }
+}
+
+// C of tap rows [0, T) for the pixels of the M-blocks in qmask, written in place
+__device__ __forceinline__ void b2_corr(char* lds, int T, int qmask, const half8 (&af)[4][4], int wave_u, int fr,
+                                        int fq) {
+  const int nb = (T + 15) >> 4;
+  for (int b = wave_u; b < nb; b += 4) {
+    half8 bf[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      bf[ks] = *reinterpret_cast<const half8*>(lds + (b * 16 + fr) * 256 + (((ks * 4 + fq) ^ fr) << 4));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!((qmask >> q) & 1)) continue;
+      floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[ks], af[q][ks], c, 0, 0, 0);
+      // lane (fr, fq): C[tap b*16 + 4 fq + k][pixel q*16 + fr]
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        *reinterpret_cast<_Float16*>(lds + (b * 16 + 4 * fq + k) * 256 + (q * 16 + fr) * 2) = (_Float16)c[k];
+    }
+  }
+}
+
+// bilinear windows of level l for the pixels of the M-blocks in qmask (only
+// pixel gpix when >= 0; the others' rows are zeroed) -> lookup tile slot `as`.
+// Thread = (wave w, pixel lane): window rows w and w + 4 (volume-lookup
+// at::Half arithmetic, corr_alt_ce0_kernel's order).
+__device__ __forceinline__ void b2_bilinear(char* lds, const float* cxy, int l, int Hl, int Wl, int bx0, int by0,
+                                            int bw, int toff, int as, int qmask, int gpix, int wave_u, int lane) {
+  const int p = lane;
+  if (!((qmask >> (p >> 4)) & 1)) return;
+  const bool live = gpix < 0 || gpix == p;
+  const float scl = 1.0f / (float)(1 << l);
+  const float x0 = cxy[2 * p] * scl, y0 = cxy[2 * p + 1] * scl;
+  const float fx0 = floorf(x0), fy0 = floorf(y0);
+  const float dx = x0 - fx0, dy = y0 - fy0;
+  const int xi0 = alt_floor(x0), yi0 = alt_floor(y0);
+  const _Float16 w11 = (_Float16)rnd16(dx * dy);
+  const _Float16 w10 = (_Float16)rnd16(dx * (1.0f - dy));
+  const _Float16 w01 = (_Float16)rnd16((1.0f - dx) * dy);
+  const _Float16 w00 = (_Float16)rnd16((1.0f - dx) * (1.0f - dy));
+  const int xs = xi0 - 3;
+  // columns xs + i inside the map: i in [lo, hi)
+  const int lo = min(max(-xs, 0), 8), hi = max(min(Wl - xs, 8), 0);
+  const unsigned cmask = hi > lo ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
+  const bool partial = live && cmask != 0xffu;
+  const bool any_partial = __builtin_amdgcn_ballot_w64(partial) != 0;
+  char* arow = lds + (as * 64 + p) * 256 + 128;
+  const int sw = p & 7;
+  const _Float16 z = (_Float16)0.f;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int iy = wave_u + 4 * r;
+    if (iy >= 7) break;
+    _Float16 ra[8], rb[8];
+    const int ya = yi0 - 3 + iy;
+    const unsigned ba = (live && ya >= 0 && ya < Hl) ? (unsigned)((toff + (ya - by0) * bw + xs - bx0) * 256 + 2 * p)
+                                                     : kB2Zero;
+    const unsigned bb = (live && ya + 1 >= 0 && ya + 1 < Hl)
+                            ? (unsigned)((toff + (ya + 1 - by0) * bw + xs - bx0) * 256 + 2 * p)
+                            : kB2Zero;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      ra[i] = b2_ldh(lds, ba + i * 256);
+      rb[i] = b2_ldh(lds, bb + i * 256);
+    }
+    if (any_partial) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        ra[i] = ((cmask >> i) & 1) ? ra[i] : z;
+        rb[i] = ((cmask >> i) & 1) ? rb[i] : z;
+      }
+    }
+#pragma unroll
+    for (int ix = 0; ix < 7; ++ix) {
+      _Float16 s = z + ra[ix] * w00;
+      s = s + rb[ix] * w01;
+      s = s + ra[ix + 1] * w10;
+      s = s + rb[ix + 1] * w11;
+      const int k = ix * 7 + iy;
+      *reinterpret_cast<_Float16*>(arow + ((((k >> 3) ^ sw)) << 4) + (k & 7) * 2) = live ? s : z;
+    }
+  }
+}
+
+// corr_encoder[0] slice of level L for the M-blocks in qmask from lookup tile slot `as`
+template <int L>
+__device__ __forceinline__ void b2_encode(const char* lds, int as, int qmask, const half8 (&wl)[4][2][2],
+                                          floatx4 (&acc)[4][2], int fq, const int (&eoff)[2]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (!((qmask >> q) & 1)) continue;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      half8 x = *reinterpret_cast<const half8*>(lds + (as * 64 + q * 16) * 256 + eoff[s]);
+      if (s == 1) {   // columns 49..63 (lanes fq 2: k 48..55, fq 3: k 56..63) are padding
+        uint4 u = __builtin_bit_cast(uint4, x);
+        u.x &= fq == 3 ? 0u : fq == 2 ? 0xffffu : 0xffffffffu;
+        u.y = fq >= 2 ? 0u : u.y;
+        u.z = fq >= 2 ? 0u : u.z;
+        u.w = fq >= 2 ? 0u : u.w;
+        x = __builtin_bit_cast(half8, u);
+      }
+#pragma unroll
+      for (int n = 0; n < 2; ++n) acc[q][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, wl[L][n][s], acc[q][n], 0, 0, 0);
+    }
+  }
+}
+
+// wave 0: the fallback groups of level l of a tile whose level box does not fit
+// (halves, else quadrants, else the quadrant's 16 pixels' own windows) -> grp
+__device__ __forceinline__ void b2_plan_groups(const AltArgs& a, const float* cxy, int l, int* grp, int lane) {
+  const int Hl = a.Hl[l], Wl = a.Wl[l];
+  const float scl = 1.0f / (float)(1 << l);
+  const int ox = alt_floor(cxy[2 * lane] * scl) - 3, oy = alt_floor(cxy[2 * lane + 1] * scl) - 3;
+  int qx0 = ox, qx1 = ox + 7, qy0 = oy, qy1 = oy + 7;
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) {
+    qx0 = min(qx0, __shfl_xor(qx0, m)); qx1 = max(qx1, __shfl_xor(qx1, m));
+    qy0 = min(qy0, __shfl_xor(qy0, m)); qy1 = max(qy1, __shfl_xor(qy1, m));
+  }
+  int hx0 = min(qx0, __shfl_xor(qx0, 16)), hx1 = max(qx1, __shfl_xor(qx1, 16));
+  int hy0 = min(qy0, __shfl_xor(qy0, 16)), hy1 = max(qy1, __shfl_xor(qy1, 16));
+  const int hn = alt_clip(hx0, hx1, hy0, hy1, Wl, Hl);
+  const int qn = alt_clip(qx0, qx1, qy0, qy1, Wl, Hl);
+  int px0 = ox, px1 = ox + 7, py0 = oy, py1 = oy + 7;
+  const int pn = alt_clip(px0, px1, py0, py1, Wl, Hl);
+  const bool hfit = hn <= kB2Rows, qfit = qn <= kB2Rows;
+  const unsigned long long hb = __ballot(hfit), qb = __ballot(qfit);
+  const int q = lane >> 4, h = lane >> 5;
+  auto qcnt = [&](int qq) { return ((qb >> (16 * qq)) & 1ull) ? 1 : 16; };
+  auto hcnt = [&](int hh) { return ((hb >> (32 * hh)) & 1ull) ? 1 : qcnt(2 * hh) + qcnt(2 * hh + 1); };
+  const int hbase = h ? hcnt(0) : 0;
+  const int qbase = hbase + ((q & 1) ? qcnt(q - 1) : 0);
+  if (hfit) {
+    if ((lane & 31) == 0) {
+      int* g = grp + 4 + 6 * hbase;
+      g[0] = hx0; g[1] = hy0; g[2] = hn ? hx1 - hx0 + 1 : 0; g[3] = hn ? hy1 - hy0 + 1 : 0;
+      g[4] = 3 << (2 * h); g[5] = -1;
+    }
+  } else if (qfit) {
+    if ((lane & 15) == 0) {
+      int* g = grp + 4 + 6 * qbase;
+      g[0] = qx0; g[1] = qy0; g[2] = qn ? qx1 - qx0 + 1 : 0; g[3] = qn ? qy1 - qy0 + 1 : 0;
+      g[4] = 1 << q; g[5] = -1;
+    }
+  } else {
+    int* g = grp + 4 + 6 * (qbase + (lane & 15));
+    g[0] = px0; g[1] = py0; g[2] = pn ? px1 - px0 + 1 : 0; g[3] = pn ? py1 - py0 + 1 : 0;
+    g[4] = 1 << q; g[5] = lane;
+  }
+  if (lane == 0) grp[0] = hcnt(0) + hcnt(1);
+}
+
+__global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int* grp = reinterpret_cast<int*>(lds + kB2Grp);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int H = a.H, W = a.W, HW = H * W;
+  const int tcols = W / 8, tpe = (H / 8) * tcols;
+  const unsigned lds_a = lds_addr(lds);
+
+  // XCD-aware order: the workgroups of one XCD (blockIdx % 8) walk adjacent tiles
+  const int G = gridDim.x;
+  const int b0 = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  if (b0 >= a.ntiles) return;
+
+  // corr_encoder[0] B fragments of this wave's 32 output channels (2 N-blocks):
+  // per level K = 49 real columns padded to 64 (2 K-steps of 32)
+  half8 wl[4][2][2];
+#pragma unroll
+  for (int l = 0; l < 4; ++l)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        half8 v;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int k = 32 * s + 8 * fq + i;
+          v[i] = k < 49 ? (_Float16)a.w[(wave * 32 + 16 * n + fr) * 224 + 49 * l + k] : (_Float16)0.f;
+        }
+        wl[l][n][s] = v;
+      }
+  const float bias0 = a.bias[wave * 32 + fr], bias1 = a.bias[wave * 32 + 16 + fr];
+  int eoff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) eoff[s] = fr * 256 + 128 + (((s * 4 + fq) ^ (fr & 7)) << 4);
+
+  struct Tile { int e, ty0, tx0, f1, f2; };
+  auto tile_of = [&](int t) {
+    Tile r;
+    r.e = __builtin_amdgcn_readfirstlane(t / tpe);
+    const int tt = t - r.e * tpe;
+    r.ty0 = (tt / tcols) * 8;
+    r.tx0 = (tt - (tt / tcols) * tcols) * 8;
+    r.f1 = a.f1[r.e];
+    r.f2 = a.f2[r.e];
+    return r;
+  };
+  auto coords_dma = [&](const Tile& T, int slot) {
+    if (wave_u == 0) {
+      const rsrc_t rs = make_rsrc(a.coords + (long)T.e * HW * 2, (unsigned)(HW * 8));
+      const int p = 2 * (lane & 31);
+      if (lane < 32)
+        dma16(rs, lds_a + kB2Coord + slot * 512, (unsigned)((((T.ty0 + alt_py(p)) * W + T.tx0 + alt_px(p)) * 2) * 4));
+    }
+  };
+  // the tile's 64 query feature rows straight into the MFMA B fragments
+  auto load_f1 = [&](const Tile& T, half8 (&af)[4][4]) {
+    const unsigned long long pa =
+        (unsigned long long)(a.pyr[0] + (long)__builtin_amdgcn_readfirstlane(T.f1) * HW * 128);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(pa), (short)0, HW * 256, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int p = q * 16 + fr;
+      const int pix = (T.ty0 + alt_py(p)) * W + T.tx0 + alt_px(p);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        af[q][ks] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rs, (int)((pix * 128 + (ks * 4 + fq) * 8) * 2), 0, 0));
+    }
+  };
+
+  half8 af[4][4];
+  floatx4 acc[4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q][0] = acc[q][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // one group: DMA its box(es), C, bilinear, encoder; ends with a barrier (the
+  // region is free for the next DMA).  Levels are compile-time for the encoder.
+  auto wait_bar = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  auto run_level = [&](auto LC, const Tile& T, const float* cxy, const int* lv, bool side, const Tile& nxt,
+                       bool more, int nslot) {
+    constexpr int L = decltype(LC)::value;
+    const int Hl = a.Hl[L], Wl = a.Wl[L];
+    const int bx0 = __builtin_amdgcn_readfirstlane(lv[4 * L]), by0 = __builtin_amdgcn_readfirstlane(lv[4 * L + 1]);
+    const int bw = __builtin_amdgcn_readfirstlane(lv[4 * L + 2]), bh = __builtin_amdgcn_readfirstlane(lv[4 * L + 3]);
+    auto group = [&](int gx0, int gy0, int gw, int gh, int qmask, int gpix, bool last) {
+      b2_box_dma(a, L, T.f2, gx0, gy0, gw, gh, 0, lds_a, wave_u, lane);
+      wait_bar();
+      b2_corr(lds, gw * gh, qmask, af, wave_u, fr, fq);
+      __syncthreads();
+      b2_bilinear(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, 0, qmask, gpix, wave_u, lane);
+      if (side && last && wave_u == 3 && more)   // the next tile's boxes on the wave with one window row
+        alt_tile_boxes(a, reinterpret_cast<const float*>(lds + kB2Coord + nslot * 512),
+                       reinterpret_cast<int*>(lds + kB2Lvl) + nslot * 16, lane);
+      __syncthreads();
+      b2_encode<L>(lds, 0, qmask, wl, acc, fq, eoff);
+      __syncthreads();
+    };
+    if (bw * bh <= kB2Rows) {
+      group(bx0, by0, bw, bh, 15, -1, true);
+    } else {
+      if (wave_u == 0) b2_plan_groups(a, cxy, L, grp, lane);
+      __syncthreads();
+      const int ng = __builtin_amdgcn_readfirstlane(grp[0]);
+      for (int gi = 0; gi < ng; ++gi) {
+        const int* g = grp + 4 + 6 * gi;
+        group(__builtin_amdgcn_readfirstlane(g[0]), __builtin_amdgcn_readfirstlane(g[1]),
+              __builtin_amdgcn_readfirstlane(g[2]), __builtin_amdgcn_readfirstlane(g[3]),
+              __builtin_amdgcn_readfirstlane(g[4]), __builtin_amdgcn_readfirstlane(g[5]), gi == ng - 1);
+      }
+    }
+  };
+
+  // ---- prologue: tile b0's coordinates, boxes and query features ----
+  int t = b0;
+  int slot = 0;
+  Tile cur = tile_of(t);
+  coords_dma(cur, 0);
+  load_f1(cur, af);
+  wait_bar();
+  if (wave_u == 0)
+    alt_tile_boxes(a, reinterpret_cast<const float*>(lds + kB2Coord), reinterpret_cast<int*>(lds + kB2Lvl), lane);
+  __syncthreads();
+
+  for (;;) {
+    const int tn_ = t + G;
+    const bool more = tn_ < a.ntiles;
+    const Tile nxt = more ? tile_of(tn_) : cur;
+    const float* cxy = reinterpret_cast<const float*>(lds + kB2Coord + slot * 512);
+    const int* lv = reinterpret_cast<const int*>(lds + kB2Lvl) + slot * 16;
+    // ---- levels 3, 2, 1 ----
+    const int tn3 = __builtin_amdgcn_readfirstlane(lv[14] * lv[15]);
+    const int tn2 = __builtin_amdgcn_readfirstlane(lv[10] * lv[11]);
+    const int tn1 = __builtin_amdgcn_readfirstlane(lv[6] * lv[7]);
+    const int o2 = (tn3 + 3) & ~3, o1 = o2 + ((tn2 + 3) & ~3), T321 = o1 + tn1;
+    if (more) coords_dma(nxt, slot ^ 1);
+    if (T321 <= kB2Rows) {
+      const int l3x = __builtin_amdgcn_readfirstlane(lv[12]), l3y = __builtin_amdgcn_readfirstlane(lv[13]);
+      const int l3w = __builtin_amdgcn_readfirstlane(lv[14]), l3h = __builtin_amdgcn_readfirstlane(lv[15]);
+      const int l2x = __builtin_amdgcn_readfirstlane(lv[8]), l2y = __builtin_amdgcn_readfirstlane(lv[9]);
+      const int l2w = __builtin_amdgcn_readfirstlane(lv[10]), l2h = __builtin_amdgcn_readfirstlane(lv[11]);
+      const int l1x = __builtin_amdgcn_readfirstlane(lv[4]), l1y = __builtin_amdgcn_readfirstlane(lv[5]);
+      const int l1w = __builtin_amdgcn_readfirstlane(lv[6]), l1h = __builtin_amdgcn_readfirstlane(lv[7]);
+      b2_box_dma(a, 3, cur.f2, l3x, l3y, l3w, l3h, 0, lds_a, wave_u, lane);
+      b2_box_dma(a, 2, cur.f2, l2x, l2y, l2w, l2h, o2, lds_a, wave_u, lane);
+      b2_box_dma(a, 1, cur.f2, l1x, l1y, l1w, l1h, o1, lds_a, wave_u, lane);
+      wait_bar();
+      b2_corr(lds, T321, 15, af, wave_u, fr, fq);
+      __syncthreads();
+      b2_bilinear(lds, cxy, 3, a.Hl[3], a.Wl[3], l3x, l3y, l3w, 0, 0, 15, -1, wave_u, lane);
+      b2_bilinear(lds, cxy, 2, a.Hl[2], a.Wl[2], l2x, l2y, l2w, o2, 1, 15, -1, wave_u, lane);
+      b2_bilinear(lds, cxy, 1, a.Hl[1], a.Wl[1], l1x, l1y, l1w, o1, 2, 15, -1, wave_u, lane);
+      __syncthreads();
+      b2_encode<3>(lds, 0, 15, wl, acc, fq, eoff);
+      b2_encode<2>(lds, 1, 15, wl, acc, fq, eoff);
+      b2_encode<1>(lds, 2, 15, wl, acc, fq, eoff);
+      __syncthreads();
+    } else {
+      run_level(std::integral_constant<int, 3>{}, cur, cxy, lv, false, nxt, more, slot ^ 1);
+      run_level(std::integral_constant<int, 2>{}, cur, cxy, lv, false, nxt, more, slot ^ 1);
+      run_level(std::integral_constant<int, 1>{}, cur, cxy, lv, false, nxt, more, slot ^ 1);
+    }
+    // ---- level 0 (its last group computes the next tile's boxes on the side) ----
+    run_level(std::integral_constant<int, 0>{}, cur, cxy, lv, true, nxt, more, slot ^ 1);
+    if (more) load_f1(nxt, af);   // af is free: lands during the output and the next DMA wait
+    // ---- output: bias, ReLU -> rows staged in the first halves of rows 64..191 -> HBM
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int co = wave * 32 + 16 * n + fr;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int px = q * 16 + 4 * fq + k;
+          *reinterpret_cast<_Float16*>(lds + (64 + 2 * px + (co >> 6)) * 256 + (co & 63) * 2) =
+              (_Float16)fmaxf(acc[q][n][k] + (n ? bias1 : bias0), 0.f);
+        }
+        acc[q][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int idx = tid + 256 * r;
+      const int p = idx >> 4, pc = idx & 15;
+      const uint4 v = *reinterpret_cast<const uint4*>(lds + (64 + 2 * p + (pc >> 3)) * 256 + (pc & 7) * 16);
+      const long m = ((long)cur.e * H + cur.ty0 + alt_py(p)) * W + cur.tx0 + alt_px(p);
+      *reinterpret_cast<uint4*>(a.out + m * 128 + pc * 8) = v;
+    }
+    if (!more) break;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();   // staging read out before the next DMA overwrites it
+    t = tn_;
+    cur = nxt;
+    slot ^= 1;
+  }
+}
 }  // namespace droid
 
 using namespace droid;
 
 static long long* g_alt_prof = nullptr;
+static int& alt_variant() {
+  static int v = [] {
+    const char* e = getenv("DROID_ALT_VARIANT");
+    return (e && e[0] == '1') ? 1 : 2;
+  }();
+  return v;
+}
 
 extern "C" {
 
@@ -601,9 +1024,28 @@ int droid_corr_alt_ce0(const void* const* pyr, const int* Hl, const int* Wl, con
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kAltLds));
     attr = true;
   }
-  const long grid = std::min<long>(a.ntiles, device_cu_count());
-  corr_alt_ce0_kernel<<<dim3((unsigned)grid), 512, kAltLds, stream>>>(a);
+  if (alt_variant() == 1) {
+    const long grid = std::min<long>(a.ntiles, device_cu_count());
+    corr_alt_ce0_kernel<<<dim3((unsigned)grid), 512, kAltLds, stream>>>(a);
+  } else {
+    static bool attr2 = false;
+    if (!attr2) {
+      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
+      attr2 = true;
+    }
+    const long grid = std::min<long>(a.ntiles, 2L * device_cu_count());
+    corr_alt2_kernel<<<dim3((unsigned)grid), 256, kB2Lds, stream>>>(a);
+  }
   DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+// A/B hook: 1 = the one-workgroup-per-CU kernel, 2 = corr_alt2_kernel (default;
+// env DROID_ALT_VARIANT sets the initial value)
+int droid_alt_set_variant(int v) {
+  if (v != 1 && v != 2) return fail(kInvalidArgument, "alt_set_variant: 1 or 2");
+  alt_variant() = v;
   return kOk;
 }
 

@@ -227,6 +227,11 @@ def corr_alt_ce0(pyramid, f1, f2, coords, w, bias, out=None):
     return out
 
 
+def alt_set_variant(v):
+    """A/B hook (droid_alt_set_variant): 1 = corr_alt_ce0_kernel, 2 = corr_alt2_kernel."""
+    check(lib.droid_alt_set_variant(int(v)), "alt_set_variant")
+
+
 EPI_ACT, EPI_GRU_ZR, EPI_GRU_Q, EPI_HEAD, EPI_GLO = 0, 1, 2, 3, 4
 
 

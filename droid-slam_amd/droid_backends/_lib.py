@@ -32,6 +32,7 @@ _SIGS = {
     "droid_corr_lookup_ce0_tiled": ([_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_conv_set_profile": ([_p], _i),
     "droid_alt_set_profile": ([_p], _i),
+    "droid_alt_set_variant": ([_i], _i),
     "droid_corr_volume_pyramid": ([_p, _p, _p, _i, _i, _i, _i, _p, _i, _p], _i),
     "droid_corr_alt_ce0": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_conv_nhwc_f16": ([_p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _i, _i,

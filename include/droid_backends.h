@@ -77,6 +77,11 @@ int droid_conv_set_profile(void* buf);
  * done / lookup barrier / stage end, then box taps * 2 + slow-path flag)
  * (scripts/alt_timeline.py). */
 int droid_alt_set_profile(void* buf);
+/* A/B hook for the on-demand lookup: 1 = corr_alt_ce0_kernel (one 8-wave
+ * workgroup per CU), 2 = corr_alt2_kernel (two 4-wave workgroups per CU, the
+ * default; env DROID_ALT_VARIANT=1 selects 1 at load).  Outputs are bitwise
+ * equal; tests compare the two. */
+int droid_alt_set_variant(int v);
 /* profiling builds only (make prof): Cholesky task timeline, 8 int64 per task */
 int droid_chol_set_profile(void* buf);
 

@@ -362,6 +362,46 @@ def test_corr_alt_ce0_matches_volume_path(noise, H, W, E):
     assert torch.equal(out, out2)
 
 
+@pytest.mark.parametrize("noise,H,W,E,far", [(1.5, 16, 24, 6, 0.0), (40.0, 16, 24, 6, 0.0), (1.5, 48, 64, 300, 0.0),
+                                             (8.0, 48, 64, 300, 0.0), (4.0, 48, 64, 200, 0.1), (0.3, 32, 64, 64, 0.0)])
+def test_corr_alt2_bitwise_equals_alt1(noise, H, W, E, far):
+    """corr_alt2_kernel (two 4-wave workgroups per CU, C in place, merged
+    level-3/2/1 stage, group fallbacks) computes every value with the same
+    operations in the same order as corr_alt_ce0_kernel: outputs bitwise equal.
+    far: fraction of pixels thrown 30-200 px off the map (windows partly or
+    wholly outside, boxes over the region -> half / quadrant / pixel groups)."""
+    import droid_backends
+    from droid_mi355x.corr import AltCorrBlock
+    rng = np.random.default_rng(41)
+    NF = 8
+    fm = torch.from_numpy(rng.normal(size=(NF, 128, H, W)).astype(np.float16)).to(DEV)
+    ii = rng.integers(0, NF, E).astype(np.int32)
+    jj = rng.integers(0, NF, E).astype(np.int32)
+    pyr = [lv.view((-1,) + tuple(lv.shape[2:])) for lv in AltCorrBlock(fm[None]).pyramid]
+    grid = np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None].astype(np.float32)
+    coords = grid + rng.normal(0, noise, (E, H, W, 2)).astype(np.float32) + rng.uniform(-3, 3, (E, 1, 1, 2)).astype(np.float32)
+    if far:
+        m = rng.random((E, H, W)) < far
+        coords[m] += rng.uniform(30, 200, (int(m.sum()), 2)).astype(np.float32) * rng.choice([-1, 1], (int(m.sum()), 2))
+    c = torch.from_numpy(coords).to(DEV).contiguous()
+    g = torch.Generator(device=DEV).manual_seed(42)
+    w224 = torch.zeros((128, 224), device=DEV)
+    w224[:, :196] = torch.randn((128, 196), generator=g, device=DEV) / 14.0
+    w224 = w224.half().contiguous()
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    f1, f2 = torch.as_tensor(ii, device=DEV), torch.as_tensor(jj, device=DEV)
+    try:
+        droid_backends.alt_set_variant(1)
+        ref = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
+        droid_backends.alt_set_variant(2)
+        out = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
+    finally:
+        droid_backends.alt_set_variant(2)
+    torch.cuda.synchronize()
+    diff = (out.float() - ref.float()).abs()
+    assert torch.equal(out, ref), (float(diff.max()), int((diff > 0).sum()))
+
+
 def test_factor_graph_update_pyramid_corr():
     """FactorGraph(corr_impl="pyramid"): no volume; update() finite and its BA
     matches the oracle on the inputs it hands over."""
