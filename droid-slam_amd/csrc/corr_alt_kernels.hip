@@ -561,10 +561,10 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
 //   * box: tap row t = the 128 fp16 features of box tap t (16-B pieces XOR
 //     swizzled by t & 15, as the LDS-DMA lands them);
 //   * C in place: C(p, t) = <F1(p), tap t> (fp16) overwrites the FIRST 128 B of
-//     tap row t.  The wave that reads a 16-tap block is the one that writes its
-//     C, after its reads, so no other wave is racing it; the bilinear then
-//     addresses C(p, t) = 256 t + 2 p - linear in t, one base per window row
-//     plus immediate offsets;
+//     tap row t once every wave has read the box (wave w multiplies all blocks
+//     by its own 16 query pixels and keeps its C in registers until then); the
+//     bilinear then addresses C(p, t) = 256 t + 2 p - linear in t, one base per
+//     window row plus immediate offsets;
 //   * the lookup tile of level slot s, [64 px][64 k] (49 used), in the SECOND
 //     halves: As(s, p, k) at row 64 s + p, byte 128 + 16 ((k / 8) ^ (p & 7)) +
 //     2 (k % 8); the padding columns are zeroed in registers, not in LDS;
@@ -582,10 +582,20 @@ constexpr int kB2Rows = 304;
 constexpr int kB2Coord = kB2Rows * 256;       // [2 slots][64 px] float2
 constexpr int kB2Lvl = kB2Coord + 2 * 512;    // [2 slots][4 levels] x0, y0, w, h
 constexpr int kB2Grp = kB2Lvl + 2 * 16 * 4;   // fallback groups: count, then (x0, y0, w, h, qmask, gpix)
-constexpr int kB2Lds = kB2Grp + (4 + kAltMaxGroups * 6) * 4;
+constexpr int kB2Bias = kB2Grp + (4 + kAltMaxGroups * 6) * 4;   // [128] f32 corr_encoder[0] bias
+constexpr int kB2Lds = kB2Bias + 128 * 4;
 static_assert(kB2Lds <= 80 * 1024, "two workgroups per CU");
 static_assert(3 * 64 <= kB2Rows && 64 + 128 <= kB2Rows, "lookup tiles and output staging fit the region");
 constexpr unsigned kB2Zero = 0x100000u;       // past the LDS allocation: ds reads return 0
+#if DROID_CONV_PROFILE
+// profiling builds: s_memtime per (workgroup, tile < 8, phase < 16), wave 0's view
+#define B2_STAMP(k)                                                                                     \
+  do {                                                                                                \
+    if (a.prof && tid == 0 && tile_i < 8) a.prof[((long)blockIdx.x * 8 + tile_i) * 16 + (k)] = ALT_NOW(); \
+  } while (0)
+#else
+#define B2_STAMP(k) do { } while (0)
+#endif
 
 __device__ __forceinline__ _Float16 b2_ldh(const char* lds, unsigned addr) {
   return *reinterpret_cast<const _Float16*>(lds + addr);
@@ -610,38 +620,73 @@ __device__ __forceinline__ void b2_box_dma(const AltArgs& a, int l, int f2, int 
   }
 }
 
-// C of tap rows [0, T) for the pixels of the M-blocks in qmask, written in place
-__device__ __forceinline__ void b2_corr(char* lds, int T, int qmask, const half8 (&af)[4][4], int wave_u, int fr,
+// C of tap rows [0, T) for the pixels of M-block `wave` (if in qmask), written in
+// place.  Each wave multiplies every 16-tap block by its own 16 query pixels, so
+// a wave holds only its M-block's query features (4 fragments: the tile's 16 KB
+// of query rows cross L2 -> CU once, not once per wave), at 4x the LDS reads of
+// the box.  Since every wave reads every block, the C values (packed fp16, 2
+// VGPRs per block) are written only after a barrier.
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void b2_corr(char* lds, int T, int qmask, const half8 (&af)[4], int wave_u, int fr,
                                         int fq) {
+  constexpr int NB = kB2Rows / 16;
+  const bool on = (qmask >> wave_u) & 1;
   const int nb = (T + 15) >> 4;
-  for (int b = wave_u; b < nb; b += 4) {
-    half8 bf[4];
+  half2_t cv[NB][2];
+  if (on) {
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      bf[ks] = *reinterpret_cast<const half8*>(lds + (b * 16 + fr) * 256 + (((ks * 4 + fq) ^ fr) << 4));
+    for (int b = 0; b < NB; ++b) {
+      if (b < nb) {
+        half8 bf[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (!((qmask >> q) & 1)) continue;
-      floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int ks = 0; ks < 4; ++ks)
+          bf[ks] = *reinterpret_cast<const half8*>(lds + (b * 16 + fr) * 256 + (((ks * 4 + fq) ^ fr) << 4));
+        floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[ks], af[q][ks], c, 0, 0, 0);
-      // lane (fr, fq): C[tap b*16 + 4 fq + k][pixel q*16 + fr]
+        for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[ks], af[ks], c, 0, 0, 0);
+        cv[b][0] = half2_t{(_Float16)c[0], (_Float16)c[1]};
+        cv[b][1] = half2_t{(_Float16)c[2], (_Float16)c[3]};
+      }
+    }
+  }
+  __syncthreads();   // every wave is done reading the box
+  if (on) {
+    const int q = wave_u;
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        *reinterpret_cast<_Float16*>(lds + (b * 16 + 4 * fq + k) * 256 + (q * 16 + fr) * 2) = (_Float16)c[k];
+    for (int b = 0; b < NB; ++b) {
+      if (b < nb) {
+        // lane (fr, fq): C[tap b*16 + 4 fq + k][pixel q*16 + fr]
+        char* base = lds + (b * 16 + 4 * fq) * 256 + (q * 16 + fr) * 2;
+        *reinterpret_cast<_Float16*>(base) = cv[b][0][0];
+        *reinterpret_cast<_Float16*>(base + 256) = cv[b][0][1];
+        *reinterpret_cast<_Float16*>(base + 512) = cv[b][1][0];
+        *reinterpret_cast<_Float16*>(base + 768) = cv[b][1][1];
+      }
     }
   }
 }
 
 // bilinear windows of level l for the pixels of the M-blocks in qmask (only
 // pixel gpix when >= 0; the others' rows are zeroed) -> lookup tile slot `as`.
-// Thread = (wave w, pixel lane): window rows w and w + 4 (volume-lookup
-// at::Half arithmetic, corr_alt_ce0_kernel's order).
+// Thread = (wave w, pixel lane): window rows w and w + 4 (< 7) with the
+// volume-lookup at::Half arithmetic in corr_alt_ce0_kernel's order.  Both
+// rows' 32 taps are read before any arithmetic (one LDS round trip; wave 3's
+// second row is read and dropped).
 __device__ __forceinline__ void b2_bilinear(char* lds, const float* cxy, int l, int Hl, int Wl, int bx0, int by0,
                                             int bw, int toff, int as, int qmask, int gpix, int wave_u, int lane) {
   const int p = lane;
   if (!((qmask >> (p >> 4)) & 1)) return;
-  const bool live = gpix < 0 || gpix == p;
+  char* arow = lds + (as * 64 + p) * 256 + 128;
+  const int sw = p & 7;
+  const int nr = wave_u == 3 ? 1 : 2;
+  const _Float16 z = (_Float16)0.f;
+  auto put = [&](int k, _Float16 v) { *reinterpret_cast<_Float16*>(arow + (((k >> 3) ^ sw) << 4) + (k & 7) * 2) = v; };
+  if (gpix >= 0 && gpix != p) {   // a single-pixel group: the M-block's other rows are zero
+    for (int r = 0; r < nr; ++r)
+#pragma unroll
+      for (int ix = 0; ix < 7; ++ix) put(ix * 7 + wave_u + 4 * r, z);
+    return;
+  }
   const float scl = 1.0f / (float)(1 << l);
   const float x0 = cxy[2 * p] * scl, y0 = cxy[2 * p + 1] * scl;
   const float fx0 = floorf(x0), fy0 = floorf(y0);
@@ -652,50 +697,50 @@ __device__ __forceinline__ void b2_bilinear(char* lds, const float* cxy, int l, 
   const _Float16 w01 = (_Float16)rnd16((1.0f - dx) * dy);
   const _Float16 w00 = (_Float16)rnd16((1.0f - dx) * (1.0f - dy));
   const int xs = xi0 - 3;
-  // columns xs + i inside the map: i in [lo, hi)
+  // columns xs + i inside the map: i in [lo, hi); rows outside read the zero address
   const int lo = min(max(-xs, 0), 8), hi = max(min(Wl - xs, 8), 0);
   const unsigned cmask = hi > lo ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
-  const bool partial = live && cmask != 0xffu;
-  const bool any_partial = __builtin_amdgcn_ballot_w64(partial) != 0;
-  char* arow = lds + (as * 64 + p) * 256 + 128;
-  const int sw = p & 7;
-  const _Float16 z = (_Float16)0.f;
+  const bool any_partial = __builtin_amdgcn_ballot_w64(cmask != 0xffu) != 0;
+  auto rowbase = [&](int y) {
+    return (y >= 0 && y < Hl) ? (unsigned)((toff + (y - by0) * bw + xs - bx0) * 256 + 2 * p) : kB2Zero;
+  };
+  _Float16 ra[2][8], rb[2][8];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
-    const int iy = wave_u + 4 * r;
-    if (iy >= 7) break;
-    _Float16 ra[8], rb[8];
-    const int ya = yi0 - 3 + iy;
-    const unsigned ba = (live && ya >= 0 && ya < Hl) ? (unsigned)((toff + (ya - by0) * bw + xs - bx0) * 256 + 2 * p)
-                                                     : kB2Zero;
-    const unsigned bb = (live && ya + 1 >= 0 && ya + 1 < Hl)
-                            ? (unsigned)((toff + (ya + 1 - by0) * bw + xs - bx0) * 256 + 2 * p)
-                            : kB2Zero;
+    const int ya = yi0 - 3 + wave_u + 4 * r;
+    const unsigned ba = rowbase(ya), bb = rowbase(ya + 1);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      ra[i] = b2_ldh(lds, ba + i * 256);
-      rb[i] = b2_ldh(lds, bb + i * 256);
+      ra[r][i] = b2_ldh(lds, ba + i * 256);
+      rb[r][i] = b2_ldh(lds, bb + i * 256);
     }
-    if (any_partial) {
+  }
+  if (any_partial) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        ra[i] = ((cmask >> i) & 1) ? ra[i] : z;
-        rb[i] = ((cmask >> i) & 1) ? rb[i] : z;
+        ra[r][i] = ((cmask >> i) & 1) ? ra[r][i] : z;
+        rb[r][i] = ((cmask >> i) & 1) ? rb[r][i] : z;
       }
-    }
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (r >= nr) break;
+    const int iy = wave_u + 4 * r;
 #pragma unroll
     for (int ix = 0; ix < 7; ++ix) {
-      _Float16 s = z + ra[ix] * w00;
-      s = s + rb[ix] * w01;
-      s = s + ra[ix + 1] * w10;
-      s = s + rb[ix + 1] * w11;
-      const int k = ix * 7 + iy;
-      *reinterpret_cast<_Float16*>(arow + ((((k >> 3) ^ sw)) << 4) + (k & 7) * 2) = live ? s : z;
+      _Float16 v = z + ra[r][ix] * w00;
+      v = v + rb[r][ix] * w01;
+      v = v + ra[r][ix + 1] * w10;
+      v = v + rb[r][ix + 1] * w11;
+      put(ix * 7 + iy, v);
     }
   }
 }
 
-// corr_encoder[0] slice of level L for the M-blocks in qmask from lookup tile slot `as`
+// corr_encoder[0] slice of level L for the M-blocks in qmask from lookup tile slot `as`;
+// acc[q][n] = out^T: lane (fr, fq) holds out[pixel q*16 + fr][co 32 w + 16 n + 4 fq + k]
 template <int L>
 __device__ __forceinline__ void b2_encode(const char* lds, int as, int qmask, const half8 (&wl)[4][2][2],
                                           floatx4 (&acc)[4][2], int fq, const int (&eoff)[2]) {
@@ -714,7 +759,7 @@ __device__ __forceinline__ void b2_encode(const char* lds, int as, int qmask, co
         x = __builtin_bit_cast(half8, u);
       }
 #pragma unroll
-      for (int n = 0; n < 2; ++n) acc[q][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, wl[L][n][s], acc[q][n], 0, 0, 0);
+      for (int n = 0; n < 2; ++n) acc[q][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[L][n][s], x, acc[q][n], 0, 0, 0);
     }
   }
 }
@@ -796,7 +841,7 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
         }
         wl[l][n][s] = v;
       }
-  const float bias0 = a.bias[wave * 32 + fr], bias1 = a.bias[wave * 32 + 16 + fr];
+  if (tid < 128) reinterpret_cast<float*>(lds + kB2Bias)[tid] = a.bias[tid];   // read at the output staging
   int eoff[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) eoff[s] = fr * 256 + 128 + (((s * 4 + fq) ^ (fr & 7)) << 4);
@@ -820,65 +865,76 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
         dma16(rs, lds_a + kB2Coord + slot * 512, (unsigned)((((T.ty0 + alt_py(p)) * W + T.tx0 + alt_px(p)) * 2) * 4));
     }
   };
-  // the tile's 64 query feature rows straight into the MFMA B fragments
-  auto load_f1 = [&](const Tile& T, half8 (&af)[4][4]) {
+  // this wave's 16 query feature rows (M-block `wave`) straight into the MFMA B fragments
+  auto load_f1 = [&](const Tile& T, half8 (&af)[4]) {
     const unsigned long long pa =
         (unsigned long long)(a.pyr[0] + (long)__builtin_amdgcn_readfirstlane(T.f1) * HW * 128);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(pa), (short)0, HW * 256, 0x00020000);
+    const int p = wave * 16 + fr;
+    const int pix = (T.ty0 + alt_py(p)) * W + T.tx0 + alt_px(p);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int p = q * 16 + fr;
-      const int pix = (T.ty0 + alt_py(p)) * W + T.tx0 + alt_px(p);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-        af[q][ks] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  rs, (int)((pix * 128 + (ks * 4 + fq) * 8) * 2), 0, 0));
-    }
+    for (int ks = 0; ks < 4; ++ks)
+      af[ks] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rs, (int)((pix * 128 + (ks * 4 + fq) * 8) * 2), 0, 0));
   };
 
-  half8 af[4][4];
+  half8 af[4];
   floatx4 acc[4][2];
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q][0] = acc[q][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  int tile_i = 0;   // profiling stamps only
+  (void)tile_i;
 
-  // one group: DMA its box(es), C, bilinear, encoder; ends with a barrier (the
-  // region is free for the next DMA).  Levels are compile-time for the encoder.
+  // one group: DMA its box, C, bilinear, encoder; ends with a barrier (the
+  // region is free for the next DMA).  The level is a runtime value except in
+  // the encoder (static register operands): one copy of the group code.
   auto wait_bar = [&]() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
-  auto run_level = [&](auto LC, const Tile& T, const float* cxy, const int* lv, bool side, const Tile& nxt,
-                       bool more, int nslot) {
-    constexpr int L = decltype(LC)::value;
+  auto encode = [&](int L, int as, int qmask) {
+    switch (L) {
+      case 3: b2_encode<3>(lds, as, qmask, wl, acc, fq, eoff); break;
+      case 2: b2_encode<2>(lds, as, qmask, wl, acc, fq, eoff); break;
+      case 1: b2_encode<1>(lds, as, qmask, wl, acc, fq, eoff); break;
+      default: b2_encode<0>(lds, as, qmask, wl, acc, fq, eoff); break;
+    }
+  };
+  // level L of tile T: its tile box if it fits the region, else the fallback groups
+  auto run_level = [&](int L, const Tile& T, const Tile& nxt, const float* cxy, const int* lv, bool side, bool more,
+                       int nslot) {
     const int Hl = a.Hl[L], Wl = a.Wl[L];
-    const int bx0 = __builtin_amdgcn_readfirstlane(lv[4 * L]), by0 = __builtin_amdgcn_readfirstlane(lv[4 * L + 1]);
-    const int bw = __builtin_amdgcn_readfirstlane(lv[4 * L + 2]), bh = __builtin_amdgcn_readfirstlane(lv[4 * L + 3]);
-    auto group = [&](int gx0, int gy0, int gw, int gh, int qmask, int gpix, bool last) {
+    const int bw0 = __builtin_amdgcn_readfirstlane(lv[4 * L + 2]), bh0 = __builtin_amdgcn_readfirstlane(lv[4 * L + 3]);
+    const bool fits = bw0 * bh0 <= kB2Rows;
+    if (!fits) {
+      if (wave_u == 0) b2_plan_groups(a, cxy, L, grp, lane);
+      __syncthreads();
+    }
+    const int ng = fits ? 1 : __builtin_amdgcn_readfirstlane(grp[0]);
+    for (int gi = 0; gi < ng; ++gi) {
+      const int* g = fits ? lv + 4 * L : grp + 4 + 6 * gi;
+      const int gx0 = __builtin_amdgcn_readfirstlane(g[0]), gy0 = __builtin_amdgcn_readfirstlane(g[1]);
+      const int gw = __builtin_amdgcn_readfirstlane(g[2]), gh = __builtin_amdgcn_readfirstlane(g[3]);
+      const int qmask = fits ? 15 : __builtin_amdgcn_readfirstlane(g[4]);
+      const int gpix = fits ? -1 : __builtin_amdgcn_readfirstlane(g[5]);
       b2_box_dma(a, L, T.f2, gx0, gy0, gw, gh, 0, lds_a, wave_u, lane);
+      if (L == 0) B2_STAMP(8);
       wait_bar();
+      if (L == 0) B2_STAMP(9);
       b2_corr(lds, gw * gh, qmask, af, wave_u, fr, fq);
+      if (L == 0) B2_STAMP(10);
       __syncthreads();
       b2_bilinear(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, 0, qmask, gpix, wave_u, lane);
-      if (side && last && wave_u == 3 && more)   // the next tile's boxes on the wave with one window row
+      if (side && gi == ng - 1 && wave_u == 3 && more)   // the next tile's boxes, on the wave with one window row
         alt_tile_boxes(a, reinterpret_cast<const float*>(lds + kB2Coord + nslot * 512),
                        reinterpret_cast<int*>(lds + kB2Lvl) + nslot * 16, lane);
       __syncthreads();
-      b2_encode<L>(lds, 0, qmask, wl, acc, fq, eoff);
+      if (L == 0) B2_STAMP(11);
+      // af for the next C phase: this level's next group, the next level, or the next tile
+      encode(L, 0, qmask);
       __syncthreads();
-    };
-    if (bw * bh <= kB2Rows) {
-      group(bx0, by0, bw, bh, 15, -1, true);
-    } else {
-      if (wave_u == 0) b2_plan_groups(a, cxy, L, grp, lane);
-      __syncthreads();
-      const int ng = __builtin_amdgcn_readfirstlane(grp[0]);
-      for (int gi = 0; gi < ng; ++gi) {
-        const int* g = grp + 4 + 6 * gi;
-        group(__builtin_amdgcn_readfirstlane(g[0]), __builtin_amdgcn_readfirstlane(g[1]),
-              __builtin_amdgcn_readfirstlane(g[2]), __builtin_amdgcn_readfirstlane(g[3]),
-              __builtin_amdgcn_readfirstlane(g[4]), __builtin_amdgcn_readfirstlane(g[5]), gi == ng - 1);
-      }
+      if (L == 0) B2_STAMP(12);
     }
   };
 
@@ -904,62 +960,76 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
     const int tn2 = __builtin_amdgcn_readfirstlane(lv[10] * lv[11]);
     const int tn1 = __builtin_amdgcn_readfirstlane(lv[6] * lv[7]);
     const int o2 = (tn3 + 3) & ~3, o1 = o2 + ((tn2 + 3) & ~3), T321 = o1 + tn1;
+    B2_STAMP(0);
     if (more) coords_dma(nxt, slot ^ 1);
     if (T321 <= kB2Rows) {
-      const int l3x = __builtin_amdgcn_readfirstlane(lv[12]), l3y = __builtin_amdgcn_readfirstlane(lv[13]);
-      const int l3w = __builtin_amdgcn_readfirstlane(lv[14]), l3h = __builtin_amdgcn_readfirstlane(lv[15]);
-      const int l2x = __builtin_amdgcn_readfirstlane(lv[8]), l2y = __builtin_amdgcn_readfirstlane(lv[9]);
-      const int l2w = __builtin_amdgcn_readfirstlane(lv[10]), l2h = __builtin_amdgcn_readfirstlane(lv[11]);
-      const int l1x = __builtin_amdgcn_readfirstlane(lv[4]), l1y = __builtin_amdgcn_readfirstlane(lv[5]);
-      const int l1w = __builtin_amdgcn_readfirstlane(lv[6]), l1h = __builtin_amdgcn_readfirstlane(lv[7]);
-      b2_box_dma(a, 3, cur.f2, l3x, l3y, l3w, l3h, 0, lds_a, wave_u, lane);
-      b2_box_dma(a, 2, cur.f2, l2x, l2y, l2w, l2h, o2, lds_a, wave_u, lane);
-      b2_box_dma(a, 1, cur.f2, l1x, l1y, l1w, l1h, o1, lds_a, wave_u, lane);
+      const int toffs[3] = {0, o2, o1};
+      for (int i = 0; i < 3; ++i) {
+        const int L = 3 - i;
+        b2_box_dma(a, L, cur.f2, __builtin_amdgcn_readfirstlane(lv[4 * L]), __builtin_amdgcn_readfirstlane(lv[4 * L + 1]),
+                   __builtin_amdgcn_readfirstlane(lv[4 * L + 2]), __builtin_amdgcn_readfirstlane(lv[4 * L + 3]),
+                   toffs[i], lds_a, wave_u, lane);
+      }
+      B2_STAMP(1);
       wait_bar();
+      B2_STAMP(2);
       b2_corr(lds, T321, 15, af, wave_u, fr, fq);
+      B2_STAMP(3);
       __syncthreads();
-      b2_bilinear(lds, cxy, 3, a.Hl[3], a.Wl[3], l3x, l3y, l3w, 0, 0, 15, -1, wave_u, lane);
-      b2_bilinear(lds, cxy, 2, a.Hl[2], a.Wl[2], l2x, l2y, l2w, o2, 1, 15, -1, wave_u, lane);
-      b2_bilinear(lds, cxy, 1, a.Hl[1], a.Wl[1], l1x, l1y, l1w, o1, 2, 15, -1, wave_u, lane);
+      B2_STAMP(4);
+      for (int i = 0; i < 3; ++i) {
+        const int L = 3 - i;
+        b2_bilinear(lds, cxy, L, a.Hl[L], a.Wl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
+                    __builtin_amdgcn_readfirstlane(lv[4 * L + 1]), __builtin_amdgcn_readfirstlane(lv[4 * L + 2]),
+                    toffs[i], i, 15, -1, wave_u, lane);
+      }
+      B2_STAMP(5);
       __syncthreads();
+      B2_STAMP(6);
       b2_encode<3>(lds, 0, 15, wl, acc, fq, eoff);
       b2_encode<2>(lds, 1, 15, wl, acc, fq, eoff);
       b2_encode<1>(lds, 2, 15, wl, acc, fq, eoff);
       __syncthreads();
+      B2_STAMP(7);
     } else {
-      run_level(std::integral_constant<int, 3>{}, cur, cxy, lv, false, nxt, more, slot ^ 1);
-      run_level(std::integral_constant<int, 2>{}, cur, cxy, lv, false, nxt, more, slot ^ 1);
-      run_level(std::integral_constant<int, 1>{}, cur, cxy, lv, false, nxt, more, slot ^ 1);
+      for (int L = 3; L >= 1; --L) run_level(L, cur, nxt, cxy, lv, false, more, slot ^ 1);
     }
     // ---- level 0 (its last group computes the next tile's boxes on the side) ----
-    run_level(std::integral_constant<int, 0>{}, cur, cxy, lv, true, nxt, more, slot ^ 1);
-    if (more) load_f1(nxt, af);   // af is free: lands during the output and the next DMA wait
-    // ---- output: bias, ReLU -> rows staged in the first halves of rows 64..191 -> HBM
+    run_level(0, cur, nxt, cxy, lv, true, more, slot ^ 1);
+    // ---- output: bias, ReLU -> rows staged in the first halves of rows 64..191
+    // (pixel p: rows 64 + 2p, 64 + 2p + 1 = channels 0..63, 64..127; 16-B pieces
+    // XOR swizzled by p & 7) -> coalesced 16-B pieces to HBM
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
-        const int co = wave * 32 + 16 * n + fr;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int px = q * 16 + 4 * fq + k;
-          *reinterpret_cast<_Float16*>(lds + (64 + 2 * px + (co >> 6)) * 256 + (co & 63) * 2) =
-              (_Float16)fmaxf(acc[q][n][k] + (n ? bias1 : bias0), 0.f);
-        }
+        const int px = q * 16 + fr, co0 = wave * 32 + 16 * n + 4 * fq;
+        half4_t h;
+        const float4 bv = *reinterpret_cast<const float4*>(lds + kB2Bias + co0 * 4);
+        h[0] = (_Float16)fmaxf(acc[q][n][0] + bv.x, 0.f);
+        h[1] = (_Float16)fmaxf(acc[q][n][1] + bv.y, 0.f);
+        h[2] = (_Float16)fmaxf(acc[q][n][2] + bv.z, 0.f);
+        h[3] = (_Float16)fmaxf(acc[q][n][3] + bv.w, 0.f);
+        *reinterpret_cast<half4_t*>(lds + (64 + 2 * px + (co0 >> 6)) * 256 + (((co0 & 63) * 2) ^ ((px & 7) << 4))) = h;
         acc[q][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       }
     __syncthreads();
+    B2_STAMP(13);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int idx = tid + 256 * r;
       const int p = idx >> 4, pc = idx & 15;
-      const uint4 v = *reinterpret_cast<const uint4*>(lds + (64 + 2 * p + (pc >> 3)) * 256 + (pc & 7) * 16);
+      const uint4 v = *reinterpret_cast<const uint4*>(lds + (64 + 2 * p + (pc >> 3)) * 256 + (((pc & 7) ^ (p & 7)) << 4));
       const long m = ((long)cur.e * H + cur.ty0 + alt_py(p)) * W + cur.tx0 + alt_px(p);
       *reinterpret_cast<uint4*>(a.out + m * 128 + pc * 8) = v;
     }
+    if (more) load_f1(nxt, af);   // behind the stores: in flight during the next tile's DMA issue
+    B2_STAMP(14);
     if (!more) break;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();   // staging read out before the next DMA overwrites it
+    B2_STAMP(15);
+    ++tile_i;
     t = tn_;
     cur = nxt;
     slot ^= 1;
@@ -1034,7 +1104,11 @@ int droid_corr_alt_ce0(const void* const* pyr, const int* Hl, const int* Wl, con
                                           hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
       attr2 = true;
     }
-    const long grid = std::min<long>(a.ntiles, 2L * device_cu_count());
+    static const int per_cu = [] {
+      const char* e = getenv("DROID_ALT2_WG_PER_CU");   // timing experiments: 1 = one workgroup per CU
+      return (e && e[0] == '1') ? 1 : 2;
+    }();
+    const long grid = std::min<long>(a.ntiles, (long)per_cu * device_cu_count());
     corr_alt2_kernel<<<dim3((unsigned)grid), 256, kB2Lds, stream>>>(a);
   }
   DROID_LAUNCH_CHECK();

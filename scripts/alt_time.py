@@ -13,12 +13,18 @@ from c3_alt_inputs import c3_alt_inputs  # noqa: E402
 
 dev = torch.device("cuda:0")
 pyr, f1, f2, c, w, b = c3_alt_inputs(dev)
-ts = []
-for it in range(8):
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    droid_backends.corr_alt_ce0(pyr, f1, f2, c, w, b)
-    e.record()
-    torch.cuda.synchronize()
-    ts.append(s.elapsed_time(e))
-print("%s: median %.3f ms (min %.3f)" % (os.environ.get("DROID_HIP_LIB", "default"), float(np.median(ts[2:])), min(ts)))
+outs = {}
+for variant in (1, 2):   # droid_alt_set_variant: the one-workgroup kernel, corr_alt2_kernel
+    droid_backends.alt_set_variant(variant)
+    ts = []
+    for it in range(8):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        o = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w, b)
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e))
+    outs[variant] = o
+    print("%s variant %d: median %.3f ms (min %.3f)" % (os.environ.get("DROID_HIP_LIB", "default"), variant,
+                                                        float(np.median(ts[2:])), min(ts)))
+print("C3 outputs bitwise equal:", bool(torch.equal(outs[1], outs[2])))
