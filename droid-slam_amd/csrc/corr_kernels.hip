@@ -510,6 +510,7 @@ struct CorrCe0Args {
   const __half* w;      // [128][224], columns >= 196 zero
   const float* bias;    // [128]
   __half* out;          // (E, H, W, 128)
+  const int* slot;      // (E) volume row of edge e (a slot pool, droid_corr_lookup_ce0_tiled_slots), or null = e
   int HW;
   long ntiles;
 };
@@ -579,6 +580,11 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
   float wdx[2] = {0.f, 0.f}, wdy[2] = {0.f, 0.f};  // bilinear fractions
   int woff[2] = {0, 0};                             // window x offset within the first chunk
   auto tile_pixel = [&](long t) { return (t / tpe) * (long)HW + (t % tpe) * kCeTP + px; };
+  // the volume row of tile t's edge (wave-uniform scalar load when the volume is a slot pool)
+  auto vol_row = [&](long t) -> long {
+    const long e = t / tpe;
+    return a.slot ? (long)__builtin_amdgcn_readfirstlane(a.slot[e]) : e;
+  };
   auto load_coords = [&](long t, float& x, float& y) {
     if (t < a.ntiles) {
       const float2 c = *reinterpret_cast<const float2*>(a.coords + tile_pixel(t) * 2);
@@ -616,7 +622,7 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
       // a tile never crosses an edge since HW % 128 == 0): window pieces outside
       // the slice get an out-of-range offset and return zeros - no branches, so
       // all 16 loads of the lane stay in flight together
-      const long tp0 = valid ? (t / tpe) * (long)HW + (t % tpe) * kCeTP : 0;
+      const long tp0 = valid ? vol_row(t) * (long)HW + (t % tpe) * kCeTP : 0;
       const unsigned long long pa = (unsigned long long)(vol + tp0 * slice);
       const unsigned long long pu = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(pa >> 32)) << 32) |
                                     (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)pa);
@@ -637,7 +643,7 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
         raw[sl][j][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, 0));
       }
     } else if constexpr (!FAST) {
-      const __half* base = vol + tile_pixel(t) * slice;
+      const __half* base = vol + (vol_row(t) * (long)HW + (t % tpe) * kCeTP + px) * slice;
       // rows not 16-B aligned (W2 % 8 != 0): the 8 taps one by one, packed as an
       // aligned chunk (window offset 0)
       woff[sl] = 0;
@@ -801,7 +807,7 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
 // Fused CorrBlock lookup + corr_encoder[0] (see corr_ce0_kernel).
 static int corr_lookup_ce0_impl(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
                                 const void* w, const float* bias, void* out, int E, int H, int W, bool tiled,
-                                hipStream_t stream) {
+                                const int* slot, hipStream_t stream) {
   using namespace droid;
   if ((H * W) % kCeTP)
     return fail(kUnsupported, "corr_lookup_ce0: H*W must be a multiple of 128");
@@ -822,6 +828,7 @@ static int corr_lookup_ce0_impl(const void* const* levels, const int* H2s, const
   a.bias = bias;
   a.out = (__half*)out;
   a.HW = H * W;
+  a.slot = slot;
   a.ntiles = (long)E * (H * W / kCeTP);
   if (a.ntiles == 0) return kOk;
   static bool attr = false;
@@ -843,13 +850,22 @@ static int corr_lookup_ce0_impl(const void* const* levels, const int* H2s, const
 
 int droid_corr_lookup_ce0(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
                           const void* w, const float* bias, void* out, int E, int H, int W, hipStream_t stream) {
-  return corr_lookup_ce0_impl(levels, H2s, W2s, coords, w, bias, out, E, H, W, false, stream);
+  return corr_lookup_ce0_impl(levels, H2s, W2s, coords, w, bias, out, E, H, W, false, nullptr, stream);
 }
 
 int droid_corr_lookup_ce0_tiled(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
                                 const void* w, const float* bias, void* out, int E, int H, int W,
                                 hipStream_t stream) {
-  return corr_lookup_ce0_impl(levels, H2s, W2s, coords, w, bias, out, E, H, W, true, stream);
+  return corr_lookup_ce0_impl(levels, H2s, W2s, coords, w, bias, out, E, H, W, true, nullptr, stream);
+}
+
+// The same on a slot pool: edge e's volume is row slot[e] of the levels (device
+// int32 (E)); the frontend's edge edits then move no volume bytes.
+int droid_corr_lookup_ce0_tiled_slots(const void* const* levels, const int* H2s, const int* W2s, const int* slot,
+                                      const float* coords, const void* w, const float* bias, void* out, int E, int H,
+                                      int W, hipStream_t stream) {
+  if (!slot) return fail(kInvalidArgument, "corr_lookup_ce0_tiled_slots: null slot map");
+  return corr_lookup_ce0_impl(levels, H2s, W2s, coords, w, bias, out, E, H, W, true, slot, stream);
 }
 
 int droid_altcorr_forward(int dtype, const void* fmap1, const void* fmap2, const float* coords,

@@ -168,18 +168,29 @@ def corr_lookup_ce0_supported(levels, H, W):
     return len(levels) == 4 and (H * W) % 128 == 0
 
 
-def corr_lookup_ce0(levels, coords, w, bias, out=None, tiled_shapes=None):
+def corr_lookup_ce0(levels, coords, w, bias, out=None, tiled_shapes=None, slots=None):
     """Fused CorrBlock lookup + corr_encoder[0] (include/droid_backends.h:
     droid_corr_lookup_ce0): levels 4 x (E,H,W,H2,W2) fp16, coords (E,H,W,2) f32,
     w [128][224] fp16, bias [128] f32 -> (E,H,W,128) fp16 = relu(w . lookup + b).
     tiled_shapes [(H2,W2)] x 4: the levels are 8x8-tiled (corr.tile8) and go to
-    droid_corr_lookup_ce0_tiled."""
+    droid_corr_lookup_ce0_tiled.  slots (E) int32 (tiled only): the levels are a
+    pool of R >= E volumes, edge e's at row slots[e]
+    (droid_corr_lookup_ce0_tiled_slots)."""
     _check_inputs(["level%d" % i for i in range(len(levels))] + ["coords", "w", "bias"],
                   list(levels) + [coords, w, bias])
     _need(coords, torch.float32, "coords")
     _need(w, torch.float16, "w")
     _need(bias, torch.float32, "bias")
-    E, H, W = levels[0].shape[:3]
+    E, H, W = coords.shape[:3]
+    if slots is not None:
+        _need(slots, torch.int32, "slots")
+        if tiled_shapes is None:
+            raise RuntimeError("corr_lookup_ce0: a slot pool needs the tiled layout")
+        if slots.shape != (E,) or slots.device != coords.device or not slots.is_contiguous():
+            raise RuntimeError("corr_lookup_ce0: slots must be a contiguous (E,) int32 tensor on the coords' device")
+    elif tuple(levels[0].shape[:3]) != (E, H, W):
+        raise RuntimeError("corr_lookup_ce0: level 0 %s does not match coords %s"
+                           % (tuple(levels[0].shape), tuple(coords.shape)))
     if out is None:
         out = torch.empty((E, H, W, 128), dtype=torch.float16, device=coords.device)
     L = len(levels)
@@ -191,6 +202,12 @@ def corr_lookup_ce0(levels, coords, w, bias, out=None, tiled_shapes=None):
                                    % (tuple(lv.shape), h2, w2))
         h2s = (ctypes.c_int * L)(*[h for h, _ in tiled_shapes])
         w2s = (ctypes.c_int * L)(*[w_ for _, w_ in tiled_shapes])
+        if slots is not None:
+            with torch.cuda.device(coords.device):
+                check(lib.droid_corr_lookup_ce0_tiled_slots(ptrs, h2s, w2s, _ptr(slots), _ptr(coords), _ptr(w),
+                                                            _ptr(bias), _ptr(out), E, H, W, _stream(coords)),
+                      "corr_lookup_ce0_tiled_slots")
+            return out
         fn, name = lib.droid_corr_lookup_ce0_tiled, "corr_lookup_ce0_tiled"
     else:
         h2s = (ctypes.c_int * L)(*[lv.shape[3] for lv in levels])

@@ -30,6 +30,7 @@ _SIGS = {
     "droid_corr_pyramid_lookup_nhwc": ([_p, _p, _p, _i, _p, _p, _i, _i, _i, _i, _p], _i),
     "droid_corr_lookup_ce0": ([_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_corr_lookup_ce0_tiled": ([_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
+    "droid_corr_lookup_ce0_tiled_slots": ([_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_conv_set_profile": ([_p], _i),
     "droid_alt_set_profile": ([_p], _i),
     "droid_alt_set_variant": ([_i], _i),

@@ -10,6 +10,7 @@ concatenated (B, N, 196, H, W) tensor directly (corr.py:40-50 does 4 launches
 the lookup uses the per-level CorrSampler so the backward kernel runs
 (training path).
 """
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -81,7 +82,7 @@ class CorrBlock:
     def __init__(self, fmap1, fmap2, num_levels=4, radius=3, tiled=False, _levels=None):
         self.num_levels = num_levels
         self.radius = radius
-        self.corr_pyramid = []
+        self.corr_pyramid = []   # (resets the slot pool state)
         if _levels is not None:                      # from_frames
             self.corr_pyramid, self.level_shapes, self.tiled = _levels
             return
@@ -145,14 +146,91 @@ class CorrBlock:
         c = coords.reshape(batch * num, ht, wd, 2).float().contiguous()
         return droid_backends.corr_pyramid_lookup_nhwc(self.reference_pyramid(), c, 200)
 
+    # -- edge edits.  A tiled block (the fused operator's) is a SLOT POOL once
+    # edited: its levels hold R >= E volumes, edge e's at row slots[e]; appending
+    # edges fills free rows (the pool grows by half when full) and dropping edges
+    # frees their rows, so the frontend's per-keyframe edits (factor_graph.py:
+    # 85-160) move only the new edges' volumes, never the whole pyramid.  The
+    # fused lookup reads the pool in place (droid_corr_lookup_ce0_tiled_slots);
+    # corr_pyramid returns the edges' volumes in edge order (a gather).
+
+    @property
+    def corr_pyramid(self):
+        if self._slots is None:
+            return self._pyr
+        idx = self.slot_tensor().long()
+        return [lv.index_select(0, idx) for lv in self._pyr]
+
+    @corr_pyramid.setter
+    def corr_pyramid(self, levels):
+        self._pyr = levels
+        self._slots = None       # np.int32 (E): volume row of each edge; None = row e
+        self._free = []
+        self._slot_dev = None
+
+    def num_edges(self):
+        return len(self._slots) if self._slots is not None else self._pyr[0].shape[0]
+
+    def pool_levels(self):
+        return self._pyr
+
+    def slot_tensor(self):
+        """device int32 (E) slot map of a pooled block, None when row e is edge e."""
+        if self._slots is None:
+            return None
+        if self._slot_dev is None:
+            self._slot_dev = torch.as_tensor(self._slots, device=self._pyr[0].device)
+        return self._slot_dev
+
+    def _pool(self):
+        if self._slots is None:
+            self._slots = np.arange(self._pyr[0].shape[0], dtype=np.int32)
+            self._free = []
+            self._slot_dev = None
+
     def cat(self, other):
-        for i in range(self.num_levels):
-            self.corr_pyramid[i] = torch.cat([self.corr_pyramid[i], other.corr_pyramid[i]], 0)
+        """append other's edges (after this block's)."""
+        if not self.tiled:
+            for i in range(self.num_levels):
+                self._pyr[i] = torch.cat([self._pyr[i], other.corr_pyramid[i]], 0)
+            return self
+        self._pool()
+        new = other.corr_pyramid
+        n = new[0].shape[0]
+        if len(self._free) < n:
+            rows = self._pyr[0].shape[0]
+            grow = max(n - len(self._free), rows // 2)
+            self._pyr = [torch.cat([lv, lv.new_empty((grow,) + tuple(lv.shape[1:]))], 0) for lv in self._pyr]
+            self._free.extend(range(rows, rows + grow))
+        rows = np.asarray(self._free[:n], np.int32)
+        del self._free[:n]
+        ridx = torch.as_tensor(rows.astype(np.int64), device=self._pyr[0].device)
+        for lv, nv in zip(self._pyr, new):
+            lv.index_copy_(0, ridx, nv)
+        self._slots = np.concatenate([self._slots, rows])
+        self._slot_dev = None
+        return self
+
+    def select(self, keep):
+        """keep the edges where the host bool mask `keep` is set."""
+        keep = np.asarray(keep, dtype=bool).reshape(-1)
+        if not self.tiled:
+            k = torch.as_tensor(keep, device=self._pyr[0].device)
+            self._pyr = [lv[k] for lv in self._pyr]
+            return self
+        self._pool()
+        self._free.extend(self._slots[~keep].tolist())
+        self._slots = self._slots[keep]
+        self._slot_dev = None
         return self
 
     def __getitem__(self, index):
+        if isinstance(index, torch.Tensor) and index.dtype == torch.bool:
+            return self.select(index.cpu().numpy())
+        if self._slots is not None:
+            raise RuntimeError("CorrBlock: index a pooled block with a bool mask (select)")
         for i in range(self.num_levels):
-            self.corr_pyramid[i] = self.corr_pyramid[i][index]
+            self._pyr[i] = self._pyr[i][index]
         return self
 
     @staticmethod

@@ -156,11 +156,15 @@ class FactorGraph:
             # the new edges' pyramids from the frames' NHWC features / 4 (one kernel;
             # the stereo edge (i, i) correlates against the right image,
             # factor_graph.py:112-114); the fused operator reads the 8x8-tiled layout
+            # only the frames the new edges touch (one keyframe's edges touch a few)
             num, rig, ch, ht, wd = self.video.fmaps.shape
-            n = int(max(ii.max(), jj.max())) + 1
-            frames = (self.video.fmaps[:n].reshape(n * rig, ch, ht, wd).half() / 4.0).permute(0, 2, 3, 1).contiguous()
-            f1 = torch.as_tensor((rig * ii).astype(np.int32), device=self.device)
-            f2 = torch.as_tensor((rig * jj + ((ii == jj) & (rig > 1))).astype(np.int32), device=self.device)
+            rows_1 = (rig * ii).astype(np.int64)
+            rows_2 = (rig * jj + ((ii == jj) & (rig > 1))).astype(np.int64)
+            used, inv = np.unique(np.concatenate([rows_1, rows_2]), return_inverse=True)
+            fm = self.video.fmaps.reshape(num * rig, ch, ht, wd).index_select(0, torch.as_tensor(used, device=self.device))
+            frames = (fm.half() / 4.0).permute(0, 2, 3, 1).contiguous()
+            f1 = torch.as_tensor(inv[:len(ii)].astype(np.int32), device=self.device)
+            f2 = torch.as_tensor(inv[len(ii):].astype(np.int32), device=self.device)
             tiled = self.fused and self.tiled_volume
             if droid_backends.corr_volume_pyramid_supported(ht, wd, tiled and wd // 8 % 8 == 0):
                 corr = CorrBlock.from_frames(frames, f1, f2, tiled=tiled)
@@ -202,7 +206,7 @@ class FactorGraph:
         self._jj = self._jj[keep]
         self.age = self.age[dkeep]
         if self.corr_impl == "volume" and self.corr is not None:
-            self.corr = self.corr[dkeep]
+            self.corr = self.corr.select(keep)   # a slot pool: frees rows, copies nothing
         if self.net is not None:
             self.net = self.net[dkeep] if self.fused else self.net[:, dkeep]
         if self.inp is not None:

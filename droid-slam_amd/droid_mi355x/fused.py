@@ -229,7 +229,11 @@ class FusedUpdateModule(torch.nn.Module):
         conv = droid_backends.conv_nhwc_f16
         e16 = lambda c: torch.empty((E, H, W, c), dtype=torch.float16, device=dev)
 
-        levels = corr.block.corr_pyramid if isinstance(corr, PendingLookup) else None
+        # a tiled block may be a slot pool (edge e's volume at row slots[e]): the
+        # fused kernel reads it in place; every other path gets edge-ordered levels
+        pooled = isinstance(corr, PendingLookup) and corr.block.slot_tensor() is not None
+        levels = (corr.block.pool_levels() if pooled else corr.block.corr_pyramid) if isinstance(corr, PendingLookup) \
+            else None
         tiled = levels is not None and getattr(corr.block, "tiled", False)
         if isinstance(corr, PendingAltLookup):
             coords = corr.coords.reshape(E, H, W, 2).float().contiguous()
@@ -237,7 +241,8 @@ class FusedUpdateModule(torch.nn.Module):
         elif levels is not None and droid_backends.corr_lookup_ce0_supported(levels, H, W):
             coords = corr.coords.reshape(E, H, W, 2).float().contiguous()
             c1 = droid_backends.corr_lookup_ce0(levels, coords, P["ce0_224"], P["ce0_b"],
-                                                tiled_shapes=corr.block.level_shapes if tiled else None)
+                                                tiled_shapes=corr.block.level_shapes if tiled else None,
+                                                slots=corr.block.slot_tensor() if pooled else None)
         else:
             if isinstance(corr, PendingLookup):
                 corr = corr.materialise()

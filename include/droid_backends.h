@@ -115,6 +115,13 @@ int droid_corr_lookup_ce0(const void* const* levels, const int* H2s, const int* 
 int droid_corr_lookup_ce0_tiled(const void* const* levels, const int* H2s, const int* W2s, const float* coords,
                                 const void* w, const float* bias, void* out, int E, int H, int W,
                                 hipStream_t stream);
+/* droid_corr_lookup_ce0_tiled on a slot pool: the levels hold R >= E edge
+ * volumes and edge e's is row slot[e] (device int32 (E), every entry in
+ * [0, R)).  The frontend's edge edits (factor_graph.py:85-160) then append and
+ * drop volumes by slot instead of copying the whole pyramid. */
+int droid_corr_lookup_ce0_tiled_slots(const void* const* levels, const int* H2s, const int* W2s, const int* slot,
+                                      const float* coords, const void* w, const float* bias, void* out, int E,
+                                      int H, int W, hipStream_t stream);
 
 /* The same lookup + corr_encoder[0] computed WITHOUT the volume: the 4
  * correlation levels are formed on demand on MFMA from a feature pyramid

@@ -20,7 +20,7 @@ ap.add_argument("--edges", type=int, default=2048)
 ap.add_argument("--frames", type=int, default=256)
 a = ap.parse_args()
 args = argparse.Namespace(config=a.config, frames=16 if a.config == "C2" else a.frames, edges=a.edges, ht=384, wd=512,
-                          corr="volume", lowmem=False, reference_op=False)
+                          corr="volume", lowmem=False, reference_op=False, force_dist=False, reference_layout=False)
 dev = torch.device("cuda:0")
 video, graph, _, e_local = bench.build_state(args, 0, 1, dev)
 kw = dict(use_inactive=True) if a.config == "C2" else {}

@@ -402,6 +402,47 @@ def test_corr_alt2_bitwise_equals_alt1(noise, H, W, E, far):
     assert torch.equal(out, ref), (float(diff.max()), int((diff > 0).sum()))
 
 
+def test_corr_volume_slot_pool_matches_fresh_block():
+    """The tiled CorrBlock as a slot pool (frontend edge edits: append, drop,
+    append again, pool growth) looked up in place through
+    droid_corr_lookup_ce0_tiled_slots == a block built fresh from the final edge
+    list (bitwise), and corr_pyramid gathers the same volumes in edge order."""
+    import droid_backends
+    from droid_mi355x.corr import CorrBlock
+    rng = np.random.default_rng(51)
+    H, W, NF = 16, 64, 6   # every level's width a multiple of 8 (the tiled layout)
+    fm = torch.from_numpy(rng.normal(size=(NF, 128, H, W)).astype(np.float16)).to(DEV)
+    frames = (fm.half() / 4.0).permute(0, 2, 3, 1).contiguous()
+    def block(ii, jj):
+        return CorrBlock.from_frames(frames, torch.as_tensor(ii, dtype=torch.int32, device=DEV),
+                                     torch.as_tensor(jj, dtype=torch.int32, device=DEV), tiled=True)
+    e1 = (np.array([0, 1, 2, 3, 4]), np.array([1, 2, 3, 4, 5]))
+    e2 = (np.array([5, 0, 2]), np.array([0, 3, 5]))
+    e3 = (np.array([1, 4, 3, 0, 2, 5, 1]), np.array([0, 2, 1, 5, 4, 3, 5]))
+    cb = block(*e1).cat(block(*e2))                      # 8 edges (pool grows from 5)
+    keep = np.array([1, 0, 1, 1, 0, 1, 0, 1], bool)
+    cb.select(keep)                                      # 5 edges, 3 free rows
+    cb.cat(block(*e3))                                   # 12 edges: fills 3 rows, grows
+    ii = np.concatenate([e1[0], e2[0]])[keep].tolist() + e3[0].tolist()
+    jj = np.concatenate([e1[1], e2[1]])[keep].tolist() + e3[1].tolist()
+    ref = block(np.array(ii), np.array(jj))
+    assert cb.slot_tensor() is not None and cb.num_edges() == len(ii)
+    for a, b in zip(cb.corr_pyramid, ref.corr_pyramid):
+        assert torch.equal(a, b)
+    E = len(ii)
+    grid = np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None].astype(np.float32)
+    c = torch.from_numpy(grid + rng.normal(0, 2.0, (E, H, W, 2)).astype(np.float32)).to(DEV).contiguous()
+    g = torch.Generator(device=DEV).manual_seed(52)
+    w224 = torch.zeros((128, 224), device=DEV)
+    w224[:, :196] = torch.randn((128, 196), generator=g, device=DEV) / 14.0
+    w224 = w224.half().contiguous()
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    out = droid_backends.corr_lookup_ce0(cb.pool_levels(), c, w224, b, tiled_shapes=cb.level_shapes,
+                                         slots=cb.slot_tensor())
+    exp = droid_backends.corr_lookup_ce0(ref.corr_pyramid, c, w224, b, tiled_shapes=ref.level_shapes)
+    assert torch.equal(out, exp)
+
+
 def test_factor_graph_update_pyramid_corr():
     """FactorGraph(corr_impl="pyramid"): no volume; update() finite and its BA
     matches the oracle on the inputs it hands over."""
