@@ -149,8 +149,8 @@ class FactorGraph:
             order = np.argsort(self.age.cpu().numpy(), kind="stable")
             self.rm_factors(order >= self.max_factors - len(ii), store=True)
 
-        dii = torch.as_tensor(ii, device=self.device)
-        djj = torch.as_tensor(jj, device=self.device)
+        dij = torch.as_tensor(np.stack([ii, jj]).astype(np.int64), device=self.device)   # one upload
+        dii, djj = dij[0], dij[1]
         net = self._edge_state(self.video.nets[dii].to(self.device))
         if self.corr_impl == "volume":
             # the new edges' pyramids from the frames' NHWC features / 4 (one kernel;
@@ -161,10 +161,11 @@ class FactorGraph:
             rows_1 = (rig * ii).astype(np.int64)
             rows_2 = (rig * jj + ((ii == jj) & (rig > 1))).astype(np.int64)
             used, inv = np.unique(np.concatenate([rows_1, rows_2]), return_inverse=True)
-            fm = self.video.fmaps.reshape(num * rig, ch, ht, wd).index_select(0, torch.as_tensor(used, device=self.device))
-            frames = (fm.half() / 4.0).permute(0, 2, 3, 1).contiguous()
-            f1 = torch.as_tensor(inv[:len(ii)].astype(np.int32), device=self.device)
-            f2 = torch.as_tensor(inv[len(ii):].astype(np.int32), device=self.device)
+            up = torch.as_tensor(np.concatenate([used, inv]).astype(np.int32), device=self.device)   # one upload
+            fm = self.video.fmaps.reshape(num * rig, ch, ht, wd).index_select(0, up[:len(used)])
+            frames = torch.empty((len(used), ht, wd, ch), dtype=torch.float16, device=self.device)
+            torch.mul(fm.permute(0, 2, 3, 1), 0.25, out=frames)     # NHWC / 4 in one pass (exact in fp16)
+            f1, f2 = up[len(used):len(used) + len(ii)], up[len(used) + len(ii):]
             tiled = self.fused and self.tiled_volume
             if droid_backends.corr_volume_pyramid_supported(ht, wd, tiled and wd // 8 % 8 == 0):
                 corr = CorrBlock.from_frames(frames, f1, f2, tiled=tiled)
@@ -195,24 +196,26 @@ class FactorGraph:
         mask = np.asarray(mask, dtype=bool).reshape(-1)
         self._edited()
         keep = ~mask
-        dmask = torch.as_tensor(mask, device=self.device)
-        dkeep = ~dmask
+        # host index lists, one upload: a device bool mask would sync per tensor (nonzero)
+        nk = int(keep.sum())
+        both = torch.as_tensor(np.concatenate([np.flatnonzero(keep), np.flatnonzero(mask)]), device=self.device)
+        dkeep, dgone = both[:nk], both[nk:]
         if store:
             self._ii_inac = np.concatenate([self._ii_inac, self._ii[mask]])
             self._jj_inac = np.concatenate([self._jj_inac, self._jj[mask]])
-            self.target_inac = torch.cat([self.target_inac, self.target[:, dmask]], 1)
-            self.weight_inac = torch.cat([self.weight_inac, self.weight[:, dmask]], 1)
+            self.target_inac = torch.cat([self.target_inac, self.target.index_select(1, dgone)], 1)
+            self.weight_inac = torch.cat([self.weight_inac, self.weight.index_select(1, dgone)], 1)
         self._ii = self._ii[keep]
         self._jj = self._jj[keep]
-        self.age = self.age[dkeep]
+        self.age = self.age.index_select(0, dkeep)
         if self.corr_impl == "volume" and self.corr is not None:
             self.corr = self.corr.select(keep)   # a slot pool: frees rows, copies nothing
         if self.net is not None:
-            self.net = self.net[dkeep] if self.fused else self.net[:, dkeep]
+            self.net = self.net.index_select(0 if self.fused else 1, dkeep)
         if self.inp is not None:
-            self.inp = self.inp[dkeep] if self.fused else self.inp[:, dkeep]
-        self.target = self.target[:, dkeep]
-        self.weight = self.weight[:, dkeep]
+            self.inp = self.inp.index_select(0 if self.fused else 1, dkeep)
+        self.target = self.target.index_select(1, dkeep)
+        self.weight = self.weight.index_select(1, dkeep)
 
     def rm_keyframe(self, ix):
         self._edited()
@@ -225,11 +228,11 @@ class FactorGraph:
         self._ii_inac = np.where(self._ii_inac >= ix, self._ii_inac - 1, self._ii_inac)
         self._jj_inac = np.where(self._jj_inac >= ix, self._jj_inac - 1, self._jj_inac)
         if m.any():
-            dm = torch.as_tensor(~m, device=self.device)
+            dm = torch.as_tensor(np.flatnonzero(~m), device=self.device)
             self._ii_inac = self._ii_inac[~m]
             self._jj_inac = self._jj_inac[~m]
-            self.target_inac = self.target_inac[:, dm]
-            self.weight_inac = self.weight_inac[:, dm]
+            self.target_inac = self.target_inac.index_select(1, dm)
+            self.weight_inac = self.weight_inac.index_select(1, dm)
         m = (self._ii == ix) | (self._jj == ix)
         self._ii = np.where(self._ii >= ix, self._ii - 1, self._ii)
         self._jj = np.where(self._jj >= ix, self._jj - 1, self._jj)
