@@ -855,13 +855,19 @@ static int launch_halo(const ConvArgs& a0, hipStream_t stream) {
 // which the DMA fills with zeros.  One raw s_barrier per stage with counted
 // vmcnt waits: a wave waits only for its own DMA of the stage about to be
 // read, the barrier then publishes every wave's.
-template <int TMX, int TN>
+// NW = 8: 4 x 2 waves of 64 x TN/2 (the default); NW = 4: 2 x 2 waves of 128 x
+// 128 at TMX = TN = 256 (one wave per SIMD, its 256 accumulators in AGPRs; a
+// third fewer LDS read bytes per MFMA).  With WM = 2 a wave's fragments are 32
+// pixels apart, so at W = 64 consecutive fragments alternate between two image
+// columns: NPAR per-parity A base addresses.
+template <int TMX, int TN, int NW = 8>
 struct Band {
-  static constexpr int WM = 4, WN = 2, FM = TMX / (WM * 16), FN = TN / (WN * 16);
-  static constexpr int NT = 512;
-  static constexpr int NBI = TN / 64;                    // weight DMA instructions per wave per stage
-  static constexpr int MAX_NHI = 8;
-  static_assert(WM * WN == 8 && FM * 16 * WM == TMX, "band tile");
+  static constexpr int WM = NW / 2, WN = 2, FM = TMX / (WM * 16), FN = TN / (WN * 16);
+  static constexpr int NT = NW * 64;
+  static constexpr int NBI = TN / (8 * NW);              // weight DMA instructions per wave per stage
+  static constexpr int MAX_NHI = 64 / NW;
+  static constexpr int NPAR = WM == 2 ? 2 : 1;
+  static_assert(WM * WN == NW && FM * 16 * WM == TMX && (NW == 8 || NW == 4), "band tile");
 };
 constexpr int kLdsMax = 163840;
 // profiling builds: int64 slots per workgroup (hw id, entry, loop start, loop end,
@@ -989,20 +995,24 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
   const int c = n0 + p * 8;
   const long mrow = m0 + r0;
   const bool rhalf = epi == EPI_GRU_ZR && c >= a.gru_ch;
-  half8 hpre[kPreH ? RND : 1], zpre[EB == EPI_GRU_Q ? RND : 1], ppre[kPre ? RND : 1];
+  // pass (2) in batches of RB rounds (the 4-wave tile has 32 rounds per thread:
+  // all of them in flight would need 3 x 128 VGPRs)
+  constexpr int RB = RND > 16 ? 16 : RND;
+  static_assert(RND % RB == 0, "band epilogue: whole batches");
+  half8 hpre[kPreH ? RB : 1], zpre[EB == EPI_GRU_Q ? RB : 1], ppre[kPre ? RB : 1];
   // the per-frame term's pieces (pixel m of image b -> pixel of its source
   // frame): on the 384-row tiles they go out before pass 1 - the accumulators
   // leave room for them there - so their latency and L1 bandwidth overlap the
   // staging writes; the 256x256 tile (2 VGPRs short) issues them after pass 1
-  constexpr bool kEarlyPre = kPre && TN != 256;
-  auto load_pre = [&]() {
+  constexpr bool kEarlyPre = kPre && TN != 256 && RB == RND;
+  auto load_pre = [&](int q0) {
     const long pshift = ((long)a.pre_idx[b] - b) * HW;
-    const __half* const pp = a.pre + (mrow + pshift) * a.pre_cstride + a.pre_coff + c;
+    const __half* const pp = a.pre + (mrow + (long)q0 * RQ + pshift) * a.pre_cstride + a.pre_coff + c;
     const long pstep = (long)RQ * a.pre_cstride;
 #pragma unroll
-    for (int q = 0; q < RND; ++q) ppre[q] = *reinterpret_cast<const half8*>(pp + q * pstep);
+    for (int q = 0; q < RB; ++q) ppre[q] = *reinterpret_cast<const half8*>(pp + q * pstep);
   };
-  if constexpr (kEarlyPre) load_pre();
+  if constexpr (kEarlyPre) load_pre(0);
   __syncthreads();  // main-loop LDS reads are done
   if (tid < TN) bl[tid] = bcol;
   __syncthreads();
@@ -1058,91 +1068,102 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
     }
   }
   if (prof && tid == 0) prof[6] = (long long)__builtin_amdgcn_s_memtime();  // pass 1 written
-  if constexpr (kPre && !kEarlyPre) load_pre();
-  if constexpr (kPreH) {
-    const __half* const hp = a.h + mrow * a.h_cstride + c - (EB == EPI_GRU_ZR ? a.gru_ch : 0);
-    const __half* const zp = EB == EPI_GRU_Q ? a.z + mrow * a.z_cstride + c : nullptr;
-    const long hstep = (long)RQ * a.h_cstride, zstep = (long)RQ * a.z_cstride;
+  // h (and z) pieces of rounds [q0, q0 + RB)
+  auto load_h = [&](int q0) {
+    if constexpr (kPreH) {
+      const __half* const hp = a.h + (mrow + (long)q0 * RQ) * a.h_cstride + c - (EB == EPI_GRU_ZR ? a.gru_ch : 0);
+      const __half* const zp = EB == EPI_GRU_Q ? a.z + (mrow + (long)q0 * RQ) * a.z_cstride + c : nullptr;
+      const long hstep = (long)RQ * a.h_cstride, zstep = (long)RQ * a.z_cstride;
 #pragma unroll
-    for (int q = 0; q < RND; ++q) {
-      if constexpr (EB == EPI_GRU_Q) {
-        hpre[q] = *reinterpret_cast<const half8*>(hp + q * hstep);
-        zpre[q] = *reinterpret_cast<const half8*>(zp + q * zstep);
-      } else if (rhalf) {
-        hpre[q] = *reinterpret_cast<const half8*>(hp + q * hstep);
-      }
-    }
-  }
-  if (prof && tid == 0) prof[7] = (long long)__builtin_amdgcn_s_memtime();  // pass-2 loads issued
-  __syncthreads();
-  if (prof && tid == 0) prof[8] = (long long)__builtin_amdgcn_s_memtime();  // staging barrier passed
-  // (2a) every round's output piece computed first, (2b) then all stores: with
-  // a store inside each round, the in-order vmcnt wait for round q+1's h / z /
-  // pre pieces also drained round q's stores (gfx9 counts stores in vmcnt) -
-  // one store round trip per round
-  half8 outv[RND];
-#pragma unroll  // all rounds' LDS reads in flight together
-  for (int q = 0; q < RND; ++q) {
-    const long m = mrow + q * RQ;
-    half8 v = *reinterpret_cast<const half8*>(&smem[(r0 + q * RQ) * ER + p * 8]);
-    // The gate algebra runs on packed fp16 (v_pk_add / v_pk_mul_f16, no f32
-    // round trips), each op rounded as the reference's autocast fp16 tensor ops
-    // round it (gru.py:27-32: conv + glo, r * h, (1 - z) * h + z * q); only the
-    // sigmoid / tanh go through f32 (torch evaluates them in f32 and rounds).
-    if constexpr (kPre) {
-      const half8 x = v + ppre[q];   // the gate argument: per-edge conv + per-frame term
-      // sigmoid / tanh two at a time: the exp argument scaling and the "+ 1" on
-      // packed f32 (v_pk_mul_f32 / v_pk_add_f32), exp and rcp per value
-      typedef float f2_t __attribute__((ext_vector_type(2)));
-#pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        const f2_t xf = {(float)x[e], (float)x[e + 1]};
-        const f2_t t = xf * (EB == EPI_GRU_ZR ? f2_t{-1.4426950408889634f, -1.4426950408889634f}
-                                              : f2_t{2.8853900817779268f, 2.8853900817779268f});
-        const f2_t den = f2_t{__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])} + f2_t{1.0f, 1.0f};
-        const f2_t r = {__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
-        if constexpr (EB == EPI_GRU_ZR) {   // sigmoid(x) = 1 / (1 + 2^(-x log2 e))
-          v[e] = (_Float16)r[0];
-          v[e + 1] = (_Float16)r[1];
-        } else {                            // tanh(x) = 1 - 2 / (1 + 2^(2x log2 e))
-          const f2_t th = f2_t{1.0f, 1.0f} - f2_t{2.0f, 2.0f} * r;
-          v[e] = (_Float16)th[0];
-          v[e + 1] = (_Float16)th[1];
+      for (int q = 0; q < RB; ++q) {
+        if constexpr (EB == EPI_GRU_Q) {
+          hpre[q] = *reinterpret_cast<const half8*>(hp + q * hstep);
+          zpre[q] = *reinterpret_cast<const half8*>(zp + q * zstep);
+        } else if (rhalf) {
+          hpre[q] = *reinterpret_cast<const half8*>(hp + q * hstep);
         }
       }
     }
-    if (epi == EPI_GRU_ZR) {
-      if (rhalf) {
-        half8 h;
-        if constexpr (kPreH) h = hpre[q];
-        else h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c - a.gru_ch);
-        v = v * h;   // exact products rounded once: the same bits as the f32 product rounded
-      }
-    } else if (epi == EPI_GRU_Q) {
-      half8 h, z;
-      if constexpr (EB == EPI_GRU_Q) {
-        h = hpre[q];
-        z = zpre[q];
-      } else {
-        h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c);
-        z = *reinterpret_cast<const half8*>(a.z + m * a.z_cstride + c);
-      }
-      v = gru_blend_f16(z, h, v);
-    }
-    outv[q] = v;
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  __half* dst;
+  };
+  if constexpr (kPre && !kEarlyPre) load_pre(0);
+  load_h(0);
+  if (prof && tid == 0) prof[7] = (long long)__builtin_amdgcn_s_memtime();  // pass-2 loads issued
+  __syncthreads();
+  if (prof && tid == 0) prof[8] = (long long)__builtin_amdgcn_s_memtime();  // staging barrier passed
+  __half* dst0;
   long dstep;
   if (epi == EPI_GRU_ZR) {
-    dst = rhalf ? a.rnet + mrow * a.gru_ch + c - a.gru_ch : a.zout + mrow * a.gru_ch + c;
+    dst0 = rhalf ? a.rnet + mrow * a.gru_ch + c - a.gru_ch : a.zout + mrow * a.gru_ch + c;
     dstep = (long)RQ * a.gru_ch;
   } else {
-    dst = a.out + mrow * a.out_cstride + a.out_coff + c;
+    dst0 = a.out + mrow * a.out_cstride + a.out_coff + c;
     dstep = (long)RQ * a.out_cstride;
   }
 #pragma unroll
-  for (int q = 0; q < RND; ++q) *reinterpret_cast<half8*>(dst + q * dstep) = outv[q];
+  for (int q0 = 0; q0 < RND; q0 += RB) {
+    if (q0 > 0) {   // the next batch's pieces (the first batch's went out before the barrier)
+      if constexpr (kPre) load_pre(q0);
+      load_h(q0);
+    }
+    // (2a) every round's output piece computed first, (2b) then all stores: with
+    // a store inside each round, the in-order vmcnt wait for round q+1's h / z /
+    // pre pieces also drained round q's stores (gfx9 counts stores in vmcnt) -
+    // one store round trip per round
+    half8 outv[RB];
+#pragma unroll  // all rounds' LDS reads in flight together
+    for (int q = 0; q < RB; ++q) {
+      const long m = mrow + (q0 + q) * RQ;
+      half8 v = *reinterpret_cast<const half8*>(&smem[(r0 + (q0 + q) * RQ) * ER + p * 8]);
+      // The gate algebra runs on packed fp16 (v_pk_add / v_pk_mul_f16, no f32
+      // round trips), each op rounded as the reference's autocast fp16 tensor ops
+      // round it (gru.py:27-32: conv + glo, r * h, (1 - z) * h + z * q); only the
+      // sigmoid / tanh go through f32 (torch evaluates them in f32 and rounds).
+      if constexpr (kPre) {
+        const half8 x = v + ppre[q];   // the gate argument: per-edge conv + per-frame term
+        // sigmoid / tanh two at a time: the exp argument scaling and the "+ 1" on
+        // packed f32 (v_pk_mul_f32 / v_pk_add_f32), exp and rcp per value
+        typedef float f2_t __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const f2_t xf = {(float)x[e], (float)x[e + 1]};
+          const f2_t t = xf * (EB == EPI_GRU_ZR ? f2_t{-1.4426950408889634f, -1.4426950408889634f}
+                                                : f2_t{2.8853900817779268f, 2.8853900817779268f});
+          const f2_t den = f2_t{__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])} + f2_t{1.0f, 1.0f};
+          const f2_t r = {__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+          if constexpr (EB == EPI_GRU_ZR) {   // sigmoid(x) = 1 / (1 + 2^(-x log2 e))
+            v[e] = (_Float16)r[0];
+            v[e + 1] = (_Float16)r[1];
+          } else {                            // tanh(x) = 1 - 2 / (1 + 2^(2x log2 e))
+            const f2_t th = f2_t{1.0f, 1.0f} - f2_t{2.0f, 2.0f} * r;
+            v[e] = (_Float16)th[0];
+            v[e + 1] = (_Float16)th[1];
+          }
+        }
+      }
+      if (epi == EPI_GRU_ZR) {
+        if (rhalf) {
+          half8 h;
+          if constexpr (kPreH) h = hpre[q];
+          else h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c - a.gru_ch);
+          v = v * h;   // exact products rounded once: the same bits as the f32 product rounded
+        }
+      } else if (epi == EPI_GRU_Q) {
+        half8 h, z;
+        if constexpr (EB == EPI_GRU_Q) {
+          h = hpre[q];
+          z = zpre[q];
+        } else {
+          h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c);
+          z = *reinterpret_cast<const half8*>(a.z + m * a.z_cstride + c);
+        }
+        v = gru_blend_f16(z, h, v);
+      }
+      outv[q] = v;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < RB; ++q) *reinterpret_cast<half8*>(dst0 + (q0 + q) * dstep) = outv[q];
+  }
 }
 
 // EPI_DWHEAD (band <256,256> only): the delta/weight heads (droid_net.py:
@@ -1257,10 +1278,11 @@ struct MfmaReadPairs<0> {
   static __device__ __forceinline__ void emit() {}
 };
 
-template <int TMX, int TN, bool DWHEAD, bool ILV, int EPI>
-__global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
-  using BP = Band<TMX, TN>;
-  constexpr int FM = BP::FM, FN = BP::FN, WN = BP::WN, NBI = BP::NBI;
+template <int TMX, int TN, bool DWHEAD, bool ILV, int EPI, int NW = 8>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 ? 1 : 2, NW == 4 ? 1 : 2)))
+conv_band_kernel(ConvArgs a) {
+  using BP = Band<TMX, TN, NW>;
+  constexpr int FM = BP::FM, FN = BP::FN, WN = BP::WN, NBI = BP::NBI, NPAR = BP::NPAR;
   extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
   char* lds = reinterpret_cast<char*>(smem);
 
@@ -1276,7 +1298,7 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   const int y0 = (int)((m0 % HW) / W);
   const long band0 = m0 - W;  // pixel index of the band's first (halo) row
   const int nslot = a.nslot, nhi = a.nhi;
-  const int hbytes = nhi * 8 * 1024;  // one band buffer
+  const int hbytes = nhi * NW * 1024;  // one band buffer
   char* Bl = lds;                     // [2][TN][128 B]
   char* Hl = lds + 2 * TN * 128;      // [2][nhi * 64 slots][128 B]
 
@@ -1289,7 +1311,7 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   int hpix[BP::MAX_NHI];
 #pragma unroll
   for (int q = 0; q < BP::MAX_NHI; ++q) {
-    const int slot = (wave + 8 * q) * 8 + lrow;
+    const int slot = (wave + NW * q) * 8 + lrow;
     const int ry = slot / W;
     const int y = y0 - 1 + ry;
     hpix[q] = (q < nhi && slot < nslot && y >= 0 && y < H) ? slot : -1;
@@ -1299,12 +1321,12 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   unsigned boff[NBI];
 #pragma unroll
-  for (int q = 0; q < NBI; ++q) boff[q] = (unsigned)((((wave + 8 * q) * 8 + lrow) * a.nstage * BK + lpiece * 8) * 2);
+  for (int q = 0; q < NBI; ++q) boff[q] = (unsigned)((((wave + NW * q) * 8 + lrow) * a.nstage * BK + lpiece * 8) * 2);
 
   auto issue_b = [&](int st) {
     const unsigned dst = Bl_a + (st & 1) * TN * 128;
 #pragma unroll
-    for (int q = 0; q < NBI; ++q) dma16(rsb, dst + (wave_u + 8 * q) * 1024, boff[q] + st * BK * 2);
+    for (int q = 0; q < NBI; ++q) dma16(rsb, dst + (wave_u + NW * q) * 1024, boff[q] + st * BK * 2);
   };
   auto issue_halo = [&](int chunk) {
     int s = 0;
@@ -1321,7 +1343,7 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
     for (int q = 0; q < BP::MAX_NHI; ++q) {
       if (q < nhi) {
         const unsigned off = (okc && hpix[q] >= 0) ? (unsigned)((hpix[q] * src.cstride + c) * 2) : kOob;
-        dma16(rs, dst + (wave_u + 8 * q) * 1024, off);
+        dma16(rs, dst + (wave_u + NW * q) * 1024, off);
       }
     }
   };
@@ -1332,17 +1354,24 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   // per-lane base (by tx, K half) plus compile-time i*8192 and a uniform ty*W*128.
   // Column of the lane's pixels: (16 wm + fr) % W for every i (W | 64).
   const int fr = lane & 15;
-  const int xcol = (16 * wm + fr) % W;
   constexpr int kLdsZero = 0x100000;  // base past the LDS allocation: reads return 0
-  int abase[3][2], bbase[2];
+  // fragment i of the wave: tile pixels 16 (wm + WM i) + fr = the parity-(i % NPAR)
+  // base plus (i / NPAR) x 64 pixels (8192 B): the same image column for every i
+  // of one parity (W | 64)
+  int abase[NPAR][3][2], bbase[2];
 #pragma unroll
   for (int hk = 0; hk < 2; ++hk) {
     const int kq = (lane >> 4) + hk * 4;
 #pragma unroll
-    for (int tx = -1; tx <= 1; ++tx) {
-      const int sl = W + 16 * wm + fr + tx;
-      const bool off_image = (tx < 0 && xcol == 0) || (tx > 0 && xcol == W - 1);
-      abase[tx + 1][hk] = off_image ? kLdsZero : sl * 128 + ((kq ^ ((fr + tx) & 7)) << 4);
+    for (int par = 0; par < NPAR; ++par) {
+      const int px0 = 16 * wm + 16 * BP::WM * par + fr;
+      const int xcol = px0 % W;
+#pragma unroll
+      for (int tx = -1; tx <= 1; ++tx) {
+        const int sl = W + px0 + tx;
+        const bool off_image = (tx < 0 && xcol == 0) || (tx > 0 && xcol == W - 1);
+        abase[par][tx + 1][hk] = off_image ? kLdsZero : sl * 128 + ((kq ^ ((fr + tx) & 7)) << 4);
+      }
     }
     bbase[hk] = (wn * (TN / 2) + fr) * 128 + ((kq ^ (fr & 7)) << 4);
   }
@@ -1409,17 +1438,19 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
         // one per MFMA with the K-half-0 multiplies (sched_group_barrier), so
         // they land long before their use and the MFMA pipe is not paced by
         // the LDS latency
-        static_assert(kBandSwap<TN>, "the interleaved body runs on the swapped (384-row) tiles");
+        static_assert(kBandSwap<TN> || NW == 4, "the interleaved body: the swapped 384-row tiles, the 4-wave tile");
         __builtin_amdgcn_sched_barrier(0);
         half8 af[2][FM], bf[2][FN];
 #pragma unroll
         for (int hk = 0; hk < 2; ++hk) {
-          const char* ap = Hb + abase[tx + 1][hk] + ty * rowb;
-          af[hk][0] = *reinterpret_cast<const half8*>(ap);
+          auto aptr = [&](int i) {
+            return Hb + abase[i % NPAR][tx + 1][hk] + ty * rowb + (i / NPAR) * 8192;
+          };
+          af[hk][0] = *reinterpret_cast<const half8*>(aptr(0));
 #pragma unroll
           for (int j = 0; j < FN; ++j) bf[hk][j] = *reinterpret_cast<const half8*>(Bb + bbase[hk] + j * 2048);
 #pragma unroll
-          for (int i = 1; i < FM; ++i) af[hk][i] = *reinterpret_cast<const half8*>(ap + i * 8192);
+          for (int i = 1; i < FM; ++i) af[hk][i] = *reinterpret_cast<const half8*>(aptr(i));
         }
 #pragma unroll
         for (int hk = 0; hk < 2; ++hk)
@@ -1427,7 +1458,8 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
           for (int i = 0; i < FM; ++i)
 #pragma unroll
             for (int j = 0; j < FN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[hk][j], af[hk][i], acc[i][j], 0, 0, 0);
+              acc[i][j] = kBandSwap<TN> ? __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[hk][j], af[hk][i], acc[i][j], 0, 0, 0)
+                                        : __builtin_amdgcn_mfma_f32_16x16x32_f16(af[hk][i], bf[hk][j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, FM + FN, 0);
         MfmaReadPairs<FM + FN>::emit();
         __builtin_amdgcn_sched_group_barrier(0x008, 2 * FM * FN - (FM + FN), 0);
@@ -1435,10 +1467,10 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
       } else {
 #pragma unroll
         for (int hk = 0; hk < 2; ++hk) {
-          const char* ap = Hb + abase[tx + 1][hk] + ty * rowb;
           half8 af[FM], bf[FN];
 #pragma unroll
-          for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const half8*>(ap + i * 8192);
+          for (int i = 0; i < FM; ++i)
+            af[i] = *reinterpret_cast<const half8*>(Hb + abase[i % NPAR][tx + 1][hk] + ty * rowb + (i / NPAR) * 8192);
 #pragma unroll
           for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const half8*>(Bb + bbase[hk] + j * 2048);
 #pragma unroll
@@ -1453,10 +1485,10 @@ __global__ void __launch_bounds__(512) conv_band_kernel(ConvArgs a) {
   }
   if (prof && tid == 0) prof[3] = (long long)__builtin_amdgcn_s_memtime();
   if constexpr (DWHEAD) {
-    static_assert(TMX == 256 && TN == 256, "dw/head fusion runs on the 256x256 tile");
+    static_assert(TMX == 256 && TN == 256 && NW == 8, "dw/head fusion runs on the 8-wave 256x256 tile");
     dwhead_epilogue<FM, FN>(a, acc, smem, m0, wm, wn, lane, tid, bcol);
   } else {
-    band_epilogue<TMX, TN, FM, FN, 4, false, 512, EPI>(a, acc, smem, m0, n0, wm, wn, lane, tid, bcol, prof);
+    band_epilogue<TMX, TN, FM, FN, BP::WM, false, BP::NT, EPI>(a, acc, smem, m0, n0, wm, wn, lane, tid, bcol, prof);
   }
   if (prof) {
     if (tid == 0) prof[4] = (long long)__builtin_amdgcn_s_memtime();  // stores issued
@@ -1477,12 +1509,12 @@ static bool band_interleaved() {
   return on;
 }
 
-template <int TMX, int TN>
+template <int TMX, int TN, int NW = 8>
 static bool band_fits(int W, int* nslot, int* nhi) {
   const int ns = (TMX / W + 2) * W;
-  const int nh = ceil_div(ns, 64);
-  if (nh > Band<TMX, TN>::MAX_NHI) return false;
-  const int lds = 2 * TN * 128 + 2 * nh * 8 * 1024;
+  const int nh = ceil_div(ns, 8 * NW);
+  if (nh > Band<TMX, TN, NW>::MAX_NHI) return false;
+  const int lds = 2 * TN * 128 + 2 * nh * NW * 1024;
   const int epi = TMX * (TN + 8) * 2 + TN * 4;  // staging tile + column biases
   if (lds > kLdsMax || epi > kLdsMax) return false;
   *nslot = ns;
@@ -1490,15 +1522,44 @@ static bool band_fits(int W, int* nslot, int* nhi) {
   return true;
 }
 
-template <int TMX, int TN, bool DWHEAD, bool ILV, int EPI>
+template <int TMX, int TN, bool DWHEAD, bool ILV, int EPI, int NW = 8>
 static int launch_band_kernel(const ConvArgs& a, long nwg, int lds, hipStream_t stream) {
   static bool attr = false;  // one per instantiation
   if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN, DWHEAD, ILV, EPI>),
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN, DWHEAD, ILV, EPI, NW>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     attr = true;
   }
-  conv_band_kernel<TMX, TN, DWHEAD, ILV, EPI><<<dim3((unsigned)nwg), 512, lds, stream>>>(a);
+  conv_band_kernel<TMX, TN, DWHEAD, ILV, EPI, NW><<<dim3((unsigned)nwg), NW * 64, lds, stream>>>(a);
+  return kOk;
+}
+
+// DROID_CONV_NW4=1: the z|r gates (256x256, per-frame term) on the 4-wave tile
+// (A/B; measured 8.41 ms vs 7.4 for the 8-wave tile: one wave per SIMD leaves
+// the compiler-scheduled loop's LDS waits unhidden - it needs a hand schedule)
+static bool band_nw4() {
+  static const bool on = [] {
+    const char* e = getenv("DROID_CONV_NW4");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+template <int TMX, int TN>
+static int launch_band_nw4(const ConvArgs& a0, hipStream_t stream) {
+  ConvArgs a = a0;
+  if (!band_fits<TMX, TN, 4>(a.W, &a.nslot, &a.nhi)) return fail(kUnsupported, "conv band: shape");
+  a.n_tiles = a.Cout / TN;
+  a.m_tiles = (long)a.B * a.H * a.W / TMX;
+  const int main_b = 2 * TN * 128 + 2 * a.nhi * 4 * 1024;
+  const int epi_b = TMX * (TN + 8) * 2 + TN * 4;
+  const int lds = main_b > epi_b ? main_b : epi_b;
+  if (lds > kLdsMax) return fail(kUnsupported, "conv band: LDS");
+  const long nwg = a.m_tiles * a.n_tiles;
+  // (the interleaved stage body spills on this tile: 61 VGPRs, AGPRs used as spill space in the loop)
+  const int st = launch_band_kernel<TMX, TN, false, false, EPI_GRU_ZRP, 4>(a, nwg, lds, stream);
+  if (st != kOk) return st;
+  DROID_LAUNCH_CHECK();
   return kOk;
 }
 
@@ -1915,6 +1976,9 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
                        (epi != EPI_GRU_ZR || gru_ch % 128 == 0);
   int ns_, nh_;
   if (pre) {  // the per-source term exists on the band tiles only
+    if (band_ok && epi == EPI_GRU_ZR && Cout == 256 && 256 % W == 0 && (H * W) % 256 == 0 && band_nw4() &&
+        band_fits<256, 256, 4>(W, &ns_, &nh_))
+      return launch_band_nw4<256, 256>(a, stream);
     if (band_ok && epi == EPI_GRU_ZR && Cout == 256 && 256 % W == 0 && (H * W) % 256 == 0 &&
         band_fits<256, 256>(W, &ns_, &nh_))
       return launch_band<256, 256>(a, stream);
