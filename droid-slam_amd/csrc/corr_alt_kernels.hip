@@ -704,37 +704,51 @@ __device__ __forceinline__ void b2_bilinear(char* lds, const float* cxy, int l, 
   auto rowbase = [&](int y) {
     return (y >= 0 && y < Hl) ? (unsigned)((toff + (y - by0) * bw + xs - bx0) * 256 + 2 * p) : kB2Zero;
   };
-  _Float16 ra[2][8], rb[2][8];
+  // window rows (ya, ya + 1) of both output rows as packed tap pairs (2j, 2j + 1):
+  // the arithmetic below runs two outputs per instruction (v_pk_mul / v_pk_add
+  // _f16, each op rounded exactly as the scalar half op)
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  unsigned pe[2][2][4];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int ya = yi0 - 3 + wave_u + 4 * r;
-    const unsigned ba = rowbase(ya), bb = rowbase(ya + 1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      ra[r][i] = b2_ldh(lds, ba + i * 256);
-      rb[r][i] = b2_ldh(lds, bb + i * 256);
+    for (int ab = 0; ab < 2; ++ab) {
+      const unsigned base = rowbase(ya + ab);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        pe[r][ab][q] = __builtin_bit_cast(unsigned, h2_t{b2_ldh(lds, base + (2 * q) * 256),
+                                                         b2_ldh(lds, base + (2 * q + 1) * 256)});
     }
   }
-  if (any_partial) {
+  if (any_partial) {   // columns outside the map read zeros
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
+    for (int q = 0; q < 4; ++q) {
+      const unsigned m = (((cmask >> (2 * q)) & 1) ? 0xffffu : 0u) | (((cmask >> (2 * q + 1)) & 1) ? 0xffff0000u : 0u);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        ra[r][i] = ((cmask >> i) & 1) ? ra[r][i] : z;
-        rb[r][i] = ((cmask >> i) & 1) ? rb[r][i] : z;
+      for (int r = 0; r < 2; ++r) {
+        pe[r][0][q] &= m;
+        pe[r][1][q] &= m;
       }
+    }
   }
+  const h2_t W00 = {w00, w00}, W01 = {w01, w01}, W10 = {w10, w10}, W11 = {w11, w11}, Z2 = {z, z};
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     if (r >= nr) break;
     const int iy = wave_u + 4 * r;
 #pragma unroll
-    for (int ix = 0; ix < 7; ++ix) {
-      _Float16 v = z + ra[r][ix] * w00;
-      v = v + rb[r][ix] * w01;
-      v = v + ra[r][ix + 1] * w10;
-      v = v + rb[r][ix + 1] * w11;
-      put(ix * 7 + iy, v);
+    for (int q = 0; q < 4; ++q) {   // outputs 2q, 2q + 1 (output 7 does not exist)
+      const h2_t ae = __builtin_bit_cast(h2_t, pe[r][0][q]), be = __builtin_bit_cast(h2_t, pe[r][1][q]);
+      const unsigned an = q < 3 ? pe[r][0][q + 1] : 0u, bn = q < 3 ? pe[r][1][q + 1] : 0u;
+      const h2_t ao = __builtin_bit_cast(h2_t, __builtin_amdgcn_alignbit(an, pe[r][0][q], 16));
+      const h2_t bo = __builtin_bit_cast(h2_t, __builtin_amdgcn_alignbit(bn, pe[r][1][q], 16));
+      h2_t v = Z2 + ae * W00;
+      v = v + be * W01;
+      v = v + ao * W10;
+      v = v + bo * W11;
+      put(2 * q * 7 + iy, v[0]);
+      if (q < 3) put((2 * q + 1) * 7 + iy, v[1]);
     }
   }
 }
