@@ -1862,6 +1862,40 @@ __global__ void __launch_bounds__(512) flow_enc0_kernel(const float* __restrict_
   }
 }
 
+// The delta / weight heads' finish (droid_net.py:128-132 + factor_graph.py:
+// 209-211) in one pass over the fused head output: head (E,HW,4) f32 = the raw
+// 3x3 head sums [du, dv, wu, wv] (droid_conv_dw_head_f16), b [4]:
+//   target (E,HW,2) = base + (head[0:2] + b[0:2])     (coords1 + delta)
+//   weight (E,HW,2) = sigmoid(head[2:4] + b[2:4])
+// and, when target_ba is given, the same two maps in the BA's (rows,2,HW)
+// layout at row row0 + e (the bundle adjustment's input, so no transposing
+// copies and no concatenation with the stored inactive edges per update).
+__global__ void __launch_bounds__(256) head_finish_kernel(const float4* __restrict__ head, const float* __restrict__ b,
+                                                          const float2* __restrict__ base, float2* __restrict__ target,
+                                                          float2* __restrict__ weight, float* __restrict__ target_ba,
+                                                          float* __restrict__ weight_ba, int row0, long n, int HW) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float4 h = head[i];
+  float du = h.x + b[0], dv = h.y + b[1];
+  const float wu = 1.0f / (1.0f + expf(-(h.z + b[2]))), wv = 1.0f / (1.0f + expf(-(h.w + b[3])));
+  if (base) {
+    const float2 c = base[i];
+    du = c.x + du;
+    dv = c.y + dv;
+  }
+  target[i] = make_float2(du, dv);
+  weight[i] = make_float2(wu, wv);
+  if (target_ba) {
+    const long e = i / HW, p = i - e * HW;
+    const long o = ((long)(row0 + e) * 2) * HW + p;
+    target_ba[o] = du;
+    target_ba[o + HW] = dv;
+    weight_ba[o] = wu;
+    weight_ba[o + HW] = wv;
+  }
+}
+
 }  // namespace droid
 
 using namespace droid;
@@ -2078,7 +2112,7 @@ int droid_conv_dw_head_f16(const void* const* srcs, const int* C, const int* cst
 // fp16 (the 1x1 conv weight, [co][ci]), bias [128] f32 -> glo (E, 128) f32.
 __global__ void __launch_bounds__(384) glo_gates_kernel(const float* __restrict__ part, int splits,
                                                         const float* __restrict__ w, const float* __restrict__ b,
-                                                        float* __restrict__ out, int E) {
+                                                        float* __restrict__ out_zr, float* __restrict__ out_q, int E) {
   __shared__ float g[128];
   const int e = blockIdx.x, t = threadIdx.x;
   if (t < 128) {
@@ -2097,7 +2131,9 @@ __global__ void __launch_bounds__(384) glo_gates_kernel(const float* __restrict_
     acc = fmaf(g[4 * k + 2], v.z, acc);
     acc = fmaf(g[4 * k + 3], v.w, acc);
   }
-  out[(long)e * 384 + t] = acc + b[t];
+  // z | r terms and q terms as the two gate convs' per-image biases (contiguous rows)
+  if (t < 256) out_zr[(long)e * 256 + t] = acc + b[t];
+  else out_q[(long)e * 128 + t - 256] = acc + b[t];
 }
 
 static int glo_set_attr() {
@@ -2145,11 +2181,25 @@ int droid_gru_global_split_f16(const void* h, const void* w, const float* bias, 
 // the in-order sum of the `splits` per-range partial means (gru_global_split).
 // One workgroup per edge; a plain fp32 dot per output (no BLAS library call in
 // the update path - it keeps update() capturable as one HIP graph).
-int droid_glo_gates_f32(const float* part, int splits, const float* w, const float* b, float* out, int E,
-                        hipStream_t stream) {
-  if (E < 0 || splits < 1 || !part || !w || !b || !out) return fail(kInvalidArgument, "glo_gates_f32: bad arguments");
+int droid_head_finish_f32(const float* head, const float* b, const float* base, float* target, float* weight,
+                          float* target_ba, float* weight_ba, int row0, int E, int HW, hipStream_t stream) {
+  if (E < 0 || HW <= 0 || row0 < 0 || !head || !b || !target || !weight || (!target_ba != !weight_ba))
+    return fail(kInvalidArgument, "head_finish_f32: bad arguments");
+  const long n = (long)E * HW;
+  if (n == 0) return kOk;
+  droid::head_finish_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, stream>>>(
+      reinterpret_cast<const float4*>(head), b, reinterpret_cast<const float2*>(base),
+      reinterpret_cast<float2*>(target), reinterpret_cast<float2*>(weight), target_ba, weight_ba, row0, n, HW);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+int droid_glo_gates_f32(const float* part, int splits, const float* w, const float* b, float* out_zr, float* out_q,
+                        int E, hipStream_t stream) {
+  if (E < 0 || splits < 1 || !part || !w || !b || !out_zr || !out_q)
+    return fail(kInvalidArgument, "glo_gates_f32: bad arguments");
   if (E == 0) return kOk;
-  glo_gates_kernel<<<dim3(E), 384, 0, stream>>>(part, splits, w, b, out, E);
+  glo_gates_kernel<<<dim3(E), 384, 0, stream>>>(part, splits, w, b, out_zr, out_q, E);
   DROID_LAUNCH_CHECK();
   return kOk;
 }

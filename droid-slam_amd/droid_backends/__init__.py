@@ -366,6 +366,38 @@ def conv_dw_head_f16(sources, wp, bias, head_w, out32):
     return out32
 
 
+def head_finish(head, b, base=None, target_ba=None, weight_ba=None, row0=0):
+    """The heads' finish (include/droid_backends.h: droid_head_finish_f32):
+    head (E,H,W,4) f32 raw head sums, b (4) f32, base (E,H,W,2) f32 or None ->
+    (target, weight) (E,H,W,2) f32 = (base + delta, sigmoid(w)); target_ba /
+    weight_ba (R,2,H,W) f32: also written at rows row0 .. row0 + E - 1."""
+    E, H, W, _ = head.shape
+    _check_inputs(("head", "b"), (head, b))
+    for t, nm in ((head, "head"), (b, "b")):
+        _need(t, torch.float32, nm)
+    if base is not None:
+        _check_inputs(("base",), (base,))
+        _need(base, torch.float32, "base")
+        if tuple(base.shape) != (E, H, W, 2):
+            raise RuntimeError("head_finish: base must be (E,H,W,2)")
+    if (target_ba is None) != (weight_ba is None):
+        raise RuntimeError("head_finish: target_ba and weight_ba go together")
+    if target_ba is not None:
+        for t, nm in ((target_ba, "target_ba"), (weight_ba, "weight_ba")):
+            _check_inputs((nm,), (t,))
+            _need(t, torch.float32, nm)
+            if t.dim() != 4 or tuple(t.shape[1:]) != (2, H, W) or row0 < 0 or row0 + E > t.shape[0]:
+                raise RuntimeError("head_finish: %s must be (R,2,H,W) with rows %d..%d" % (nm, row0, row0 + E - 1))
+    target = torch.empty((E, H, W, 2), dtype=torch.float32, device=head.device)
+    weight = torch.empty((E, H, W, 2), dtype=torch.float32, device=head.device)
+    with torch.cuda.device(head.device):
+        check(lib.droid_head_finish_f32(_ptr(head), _ptr(b), _ptr(base) if base is not None else None, _ptr(target),
+                                        _ptr(weight), _ptr(target_ba) if target_ba is not None else None,
+                                        _ptr(weight_ba) if weight_ba is not None else None, int(row0), E, H * W,
+                                        _stream(head)), "head_finish_f32")
+    return target, weight
+
+
 def flow_enc0_supported(H, W):
     """Shapes droid_flow_enc0_f16 accepts."""
     return W in (16, 32, 64, 128) and (H * W) % 128 == 0
@@ -394,7 +426,7 @@ def gru_glo_gates(h, w, bias, gw, gb):
     """The ConvGRU global-context branch end to end: glo = mean_px sigmoid(w h +
     bias) h (droid_gru_global[_split]_f16), then its three 1x1 gate convs
     (droid_glo_gates_f32): h (E,H,W,128) fp16, w [128][128] fp16, bias [128],
-    gw (384,128) f32, gb (384) f32 -> (E,384) f32 = [z | r | q] terms."""
+    gw (384,128) f32, gb (384) f32 -> ((E,256) f32 z | r terms, (E,128) f32 q terms)."""
     _check_inputs(("h", "w", "bias", "gw", "gb"), (h, w, bias, gw, gb))
     _need(gw, torch.float32, "gw")
     _need(gb, torch.float32, "gb")
@@ -403,7 +435,8 @@ def gru_glo_gates(h, w, bias, gw, gb):
         raise RuntimeError("gru_glo_gates: gw must be (384,128) and gb (384)")
     splits = max(1, min((H * W) // 256, -(-512 // max(E, 1))))
     part = torch.empty((splits, E, 128), dtype=torch.float32, device=h.device)
-    out = torch.empty((E, 384), dtype=torch.float32, device=h.device)
+    out_zr = torch.empty((E, 256), dtype=torch.float32, device=h.device)
+    out_q = torch.empty((E, 128), dtype=torch.float32, device=h.device)
     with torch.cuda.device(h.device):
         if splits == 1:
             check(lib.droid_gru_global_f16(_ptr(h), _ptr(w), _ptr(bias), _ptr(part), E, H * W, _stream(h)),
@@ -411,9 +444,9 @@ def gru_glo_gates(h, w, bias, gw, gb):
         else:
             check(lib.droid_gru_global_split_f16(_ptr(h), _ptr(w), _ptr(bias), _ptr(part), splits, E, H * W,
                                                  _stream(h)), "gru_global_split_f16")
-        check(lib.droid_glo_gates_f32(_ptr(part), splits, _ptr(gw), _ptr(gb), _ptr(out), E, _stream(h)),
-              "glo_gates_f32")
-    return out
+        check(lib.droid_glo_gates_f32(_ptr(part), splits, _ptr(gw), _ptr(gb), _ptr(out_zr), _ptr(out_q), E,
+                                      _stream(h)), "glo_gates_f32")
+    return out_zr, out_q
 
 
 def gru_global_f16(h, w, bias, out=None):

@@ -61,6 +61,7 @@ class FactorGraph:
         # CorrBlock(tiled=...) for the fused lookup (DROID_TILED_VOLUME=0: reference row-major layout)
         self.tiled_volume = os.environ.get("DROID_TILED_VOLUME", "1") != "0"
         self._version = 0          # bumped by every edge edit
+        self._ba_tw = None         # (key, BA target rows, BA weight rows), see _ba_inputs
 
     # -- per-edge state layout ------------------------------------------------
     @property
@@ -272,8 +273,9 @@ class FactorGraph:
                     c = self._inp_frames = (self.inp, first.tobytes(),
                                             self.inp.index_select(0, self._dev("seg_first", first)))
                 inp_frames = c[2]
+            raw = hasattr(self.update_op, "head_bias")
             self.net, delta, weight, damping = self.update_op(self.net, self.inp, corr, motn[0], dinv, len(uniq),
-                                                              segments=segs, inp_frames=inp_frames)
+                                                              segments=segs, inp_frames=inp_frames, raw_head=raw)
         else:
             corr = self.corr(coords1)
             with torch.autocast("cuda", enabled=True):
@@ -284,34 +286,68 @@ class FactorGraph:
             t0 = self.comm["t0"] if self.comm is not None else max(1, int(self._ii.min()) + 1)
 
         with torch.autocast("cuda", enabled=False):
-            self.target = coords1 + delta.to(dtype=torch.float)
-            self.weight = weight.to(dtype=torch.float)
-            self.damping[self._dev("uniq", uniq)] = damping[0].to(torch.float)
-
             if use_inactive:
                 m = (self._ii_inac >= t0 - 3) & (self._jj_inac >= t0 - 3)
                 ii_h = np.concatenate([self._ii_inac[m], self._ii])
                 jj_h = np.concatenate([self._jj_inac[m], self._jj])
-                # the selection as a cached index (a boolean mask would sync on its count)
-                if m.all():
-                    t_in, w_in = self.target_inac, self.weight_inac
-                else:
-                    sel = self._dev("inac_sel", np.nonzero(m)[0].astype(np.int64))
-                    t_in, w_in = self.target_inac.index_select(1, sel), self.weight_inac.index_select(1, sel)
-                target = torch.cat([t_in, self.target], 1)
-                weight = torch.cat([w_in, self.weight], 1)
             else:
-                ii_h, jj_h, target, weight = self._ii, self._jj, self.target, self.weight
+                m = None
+                ii_h, jj_h = self._ii, self._jj
+            if self.fused and weight is None:
+                # fused heads: one kernel adds the bias, takes the sigmoid, forms
+                # target = coords1 + delta and writes both maps straight into the
+                # BA's (rows,2,H,W) inputs, whose inactive rows are filled once
+                # per edge set (no per-update transposes or concatenation)
+                target, weight = self._ba_inputs(m, E)
+                n_in = target.shape[0] - E
+                t_act, w_act = droid_backends.head_finish(delta, self.update_op.head_bias(), coords1[0], target,
+                                                          weight, n_in)
+                self.target, self.weight = t_act.unsqueeze(0), w_act.unsqueeze(0)
+            else:
+                self.target = coords1 + delta.to(dtype=torch.float)
+                self.weight = weight.to(dtype=torch.float)
+                if use_inactive:
+                    # the selection as a cached index (a boolean mask would sync on its count)
+                    if m.all():
+                        t_in, w_in = self.target_inac, self.weight_inac
+                    else:
+                        sel = self._dev("inac_sel", np.nonzero(m)[0].astype(np.int64))
+                        t_in, w_in = self.target_inac.index_select(1, sel), self.weight_inac.index_select(1, sel)
+                    target = torch.cat([t_in, self.target], 1)
+                    weight = torch.cat([w_in, self.weight], 1)
+                else:
+                    target, weight = self.target, self.weight
+                target = target.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
+                weight = weight.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
+            self.damping[self._dev("uniq", uniq)] = damping[0].to(torch.float)
 
             uniq_ba = np.unique(ii_h)
             damping = 0.2 * self.damping[self._dev("uniq_ba", uniq_ba)].contiguous() + EP
-            target = target.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
-            weight = weight.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
             self.video.ba(target, weight, damping, self._dev("ii_ba", ii_h), self._dev("jj_ba", jj_h),
                           t0, t1, itrs=itrs, lm=1e-4, ep=0.1, motion_only=motion_only,
                           ii_host=ii_h, jj_host=jj_h, comm=self.comm,
                           edge_tag="update+inactive" if use_inactive else "update")
         self.age += 1
+
+    def _ba_inputs(self, m, E):
+        """The BA's target / weight inputs (rows,2,H,W) f32 for update(): the
+        selected inactive edges' rows first (mask m over the inactive store, or
+        None), filled once per edge set and selection, then E rows the heads'
+        finish writes every update."""
+        key = (self._version, E, None if m is None else m.tobytes())
+        c = self._ba_tw
+        if c is None or c[0] != key:
+            ht, wd = self.ht, self.wd
+            sel = np.zeros(0, np.int64) if m is None else np.nonzero(m)[0]
+            n_in = len(sel)
+            tb = torch.empty((n_in + E, 2, ht, wd), dtype=torch.float32, device=self.device)
+            wb = torch.empty_like(tb)
+            if n_in:
+                idx = torch.as_tensor(sel, device=self.device)
+                tb[:n_in] = self.target_inac[0].index_select(0, idx).permute(0, 3, 1, 2)
+                wb[:n_in] = self.weight_inac[0].index_select(0, idx).permute(0, 3, 1, 2)
+            c = self._ba_tw = (key, tb, wb)
+        return c[1], c[2]
 
     def _pending_alt_lookup(self, coords1):
         """corr_impl "pyramid": AltCorrBlock pyramid of the frames (built once per

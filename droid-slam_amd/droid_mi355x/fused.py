@@ -210,8 +210,15 @@ class FusedUpdateModule(torch.nn.Module):
         with torch.autocast("cuda", enabled=False):
             return self._forward(*args, **kwargs)
 
+    def head_bias(self):
+        """[delta.2 bias | weight.2 bias] f32 (4): what droid_head_finish adds to
+        the raw head sums that _forward(raw_head=True) returns."""
+        if self._packed is None:
+            self.pack()
+        return self._packed["head_b"]
+
     def _forward(self, net, inp, corr, motn, inverse, num_unique, segments=None, inp_frames=None, want_upmask=False,
-                 agg=True):
+                 agg=True, raw_head=False):
         """net, inp (E,H,W,128) fp16 (inp may be None when inp_frames is given);
         inp_frames: optional (U,H,W,128) fp16 context features per source-frame
         slot (edge e's inp is inp_frames[inverse[e]]); corr (E,H,W,200) fp16 (196 used) or a
@@ -261,11 +268,12 @@ class FusedUpdateModule(torch.nn.Module):
         conv([(f1, 0, 128)], P["fe2"], 64, 3, bias=P["fe2_b"], act=1, out=ff)
 
         if (H * W) % 64 == 0:    # glo and its three gate convs: two kernels, no BLAS call
-            gb = droid_backends.gru_glo_gates(net, P["w_128"], P["w_b"], P["glo_w"], P["glo_b"])
+            gb_zr, gb_q = droid_backends.gru_glo_gates(net, P["w_128"], P["w_b"], P["glo_w"], P["glo_b"])
         else:
             glo = torch.zeros((E, 128), dtype=torch.float32, device=dev)
             conv([(net, 0, 128)], P["w"], 128, 1, bias=P["w_b"], epi=EPI_GLO, h=net, out32=glo)
             gb = torch.addmm(P["glo_b"], glo, P["glo_w"].t())      # (E, 384): z | r | q
+            gb_zr, gb_q = gb[:, :256].contiguous(), gb[:, 256:].contiguous()
         z = e16(128)
         rn = e16(128)
         net_new = e16(128)
@@ -282,25 +290,28 @@ class FusedUpdateModule(torch.nn.Module):
             pre = c[2]
             pidx = inverse if inverse.dtype == torch.int64 else inverse.long()
             droid_backends.conv_gru_pre_f16([(net, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["zr_x"], 256, P["zr_b"],
-                                            gb[:, :256].contiguous(), EPI_GRU_ZR, pre, pidx, 0, h=net, zout=z,
+                                            gb_zr, EPI_GRU_ZR, pre, pidx, 0, h=net, zout=z,
                                             rnet=rn)
             droid_backends.conv_gru_pre_f16([(rn, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["q_x"], 128, P["q_b"],
-                                            gb[:, 256:].contiguous(), EPI_GRU_Q, pre, pidx, 256, h=net, z=z,
+                                            gb_q, EPI_GRU_Q, pre, pidx, 256, h=net, z=z,
                                             out=net_new)
         else:
             if inp is None:
                 inp = inp_frames[inverse]
             conv([(net, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["zr"], 256, 3, bias=P["zr_b"],
-                 bbias=gb[:, :256].contiguous(), epi=EPI_GRU_ZR, h=net, zout=z, rnet=rn)
+                 bbias=gb_zr, epi=EPI_GRU_ZR, h=net, zout=z, rnet=rn)
             conv([(rn, 0, 128), (inp, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["q"], 128, 3, bias=P["q_b"],
-                 bbias=gb[:, 256:].contiguous(), epi=EPI_GRU_Q, h=net, z=z, out=net_new)
+                 bbias=gb_q, epi=EPI_GRU_Q, h=net, z=z, out=net_new)
 
         if droid_backends.dw_head_supported(H, W):
             head = torch.zeros((E, H, W, 4), dtype=torch.float32, device=dev)
             droid_backends.conv_dw_head_f16([(net_new, 0, 128)], P["dw0"], P["dw0_b"], P["head_taps"], head)
-            head += P["head_b"]
-            delta = head[..., 0:2].unsqueeze(0)
-            weight = torch.sigmoid(head[..., 2:4]).unsqueeze(0)
+            if raw_head:   # the caller finishes it (droid_backends.head_finish: bias, sigmoid, target)
+                delta, weight = head, None
+            else:
+                head += P["head_b"]
+                delta = head[..., 0:2].unsqueeze(0)
+                weight = torch.sigmoid(head[..., 2:4]).unsqueeze(0)
         else:
             dw = e16(256)
             conv([(net_new, 0, 128)], P["dw0"], 256, 3, bias=P["dw0_b"], act=1, out=dw)

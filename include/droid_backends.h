@@ -200,13 +200,23 @@ int droid_gru_global_f16(const void* h, const void* w, const float* bias, float*
 int droid_gru_global_split_f16(const void* h, const void* w, const float* bias, float* part, int splits,
                                int E, int HW, hipStream_t stream);
 
+/* The heads' finish (droid_net.py:128-132, factor_graph.py:209-211): head
+ * (E,HW,4) f32 raw head sums [du, dv, wu, wv] of droid_conv_dw_head_f16, b [4]
+ * f32 -> target (E,HW,2) = base + head[0:2] + b[0:2] (base (E,HW,2) f32 or
+ * null: delta), weight (E,HW,2) = sigmoid(head[2:4] + b[2:4]); when target_ba
+ * and weight_ba are given, also both maps in the BA's (rows,2,HW) layout at
+ * rows row0 + e (droid_ba's targets / weights). */
+int droid_head_finish_f32(const float* head, const float* b, const float* base, float* target, float* weight,
+                          float* target_ba, float* weight_ba, int row0, int E, int HW, hipStream_t stream);
+
 /* the ConvGRU's global gate terms (gru.py:29-32: convz_glo | convr_glo | convq_glo
- * on glo): out (E,384) f32 = b + glo w^T, glo = sum over `splits` of part
- * (splits,E,128) f32 (the in-order sum of droid_gru_global_split_f16's ranges;
- * splits = 1 for droid_gru_global_f16's output), w (384,128) f32 row-major,
- * 16-B aligned. */
-int droid_glo_gates_f32(const float* part, int splits, const float* w, const float* b, float* out, int E,
-                        hipStream_t stream);
+ * on glo): b + glo w^T, written as out_zr (E,256) f32 = the z | r terms and
+ * out_q (E,128) f32 = the q terms (the two gate convs' per-image biases);
+ * glo = sum over `splits` of part (splits,E,128) f32 (the in-order sum of
+ * droid_gru_global_split_f16's ranges; splits = 1 for droid_gru_global_f16's
+ * output), w (384,128) f32 row-major, 16-B aligned. */
+int droid_glo_gates_f32(const float* part, int splits, const float* w, const float* b, float* out_zr, float* out_q,
+                        int E, hipStream_t stream);
 
 /* GraphAgg scatter_mean (droid_net.py:27-45, torch_scatter.scatter_mean over
  * dim 1): out[u] = mean of src rows seg_idx[seg_ptr[u] .. seg_ptr[u+1]), rows of

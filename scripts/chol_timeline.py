@@ -58,5 +58,11 @@ print("first panel_factor (wave 0, 16 columns) median %.2f us" % np.median(pf))
 other = np.setdiff1d(np.nonzero(p[:, 7] > 0)[0], pot)
 dur = p[other, 7] - p[other, 1]
 print("other tasks (%d): median work %.2f us, median wait %.2f us" % (len(other), np.median(dur), np.median(p[other, 1] - p[other, 0])))
+# where the chain waits: potrf(k+1)'s other updates done (its stamp 1) vs potrf(k)'s publish (stamp 7)
+late = np.array([p[pot[a + 1], 1] - p[pot[a], 7] for a in range(len(pot) - 1)])
+print("other updates of A(k+1,k+1) done after potrf(k) published: %d of %d steps, median %.2f us (p90 %.2f); "
+      "last-update phase when not late: median %.2f us" % ((late > 0).sum(), len(late), np.median(late),
+                                                            np.percentile(late, 90),
+                                                            np.median(rows[1:, 1][late <= 0]) if (late <= 0).any() else np.nan))
 for a in range(min(6, len(pot))):
     print("  potrf #%d: " % a + " ".join("%.2f" % v for v in rows[a]))
