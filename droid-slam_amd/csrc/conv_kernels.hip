@@ -1896,6 +1896,31 @@ __global__ void __launch_bounds__(256) head_finish_kernel(const float4* __restri
   }
 }
 
+// GraphAgg's damping (droid_net.py:73: eta = 0.01 softplus(eta conv), factor_graph.py:
+// 211 / 221): for the BA's frames frames[k] (k < nba), map[k] = the frame's row of
+// er (U,HW) fp16 (the raw eta conv output) or -1 (a frame only the stored
+// inactive edges touch): state[frame] = 0.01 softplus(er[map]) where map >= 0,
+// and out[k] = 0.2 state[frame] + ep (the BA's eta) - fp32, each op rounded as
+// the torch ops it replaces (softplus: log1p(exp(x)), x itself above 20).
+__global__ void __launch_bounds__(256) eta_damping_kernel(const __half* __restrict__ er, const int* __restrict__ map,
+                                                          const int* __restrict__ frames, float* __restrict__ state,
+                                                          float* __restrict__ out, long n, int HW, float ep) {
+#pragma clang fp contract(off)
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long k = i / HW, p = i - k * HW;
+  const int f = frames[k], u = map[k];
+  float v;
+  if (u >= 0) {
+    const float x = __half2float(er[(long)u * HW + p]);
+    v = 0.01f * (x > 20.0f ? x : log1pf(expf(x)));
+    state[(long)f * HW + p] = v;
+  } else {
+    v = state[(long)f * HW + p];
+  }
+  out[i] = 0.2f * v + ep;
+}
+
 }  // namespace droid
 
 using namespace droid;
@@ -2190,6 +2215,18 @@ int droid_head_finish_f32(const float* head, const float* b, const float* base, 
   droid::head_finish_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, stream>>>(
       reinterpret_cast<const float4*>(head), b, reinterpret_cast<const float2*>(base),
       reinterpret_cast<float2*>(target), reinterpret_cast<float2*>(weight), target_ba, weight_ba, row0, n, HW);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+int droid_eta_damping_f32(const void* er, const int* map, const int* frames, float* state, float* out, int nba,
+                          int HW, float ep, hipStream_t stream) {
+  if (nba < 0 || HW <= 0 || !er || !map || !frames || !state || !out)
+    return fail(kInvalidArgument, "eta_damping_f32: bad arguments");
+  const long n = (long)nba * HW;
+  if (n == 0) return kOk;
+  droid::eta_damping_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, stream>>>(
+      static_cast<const __half*>(er), map, frames, state, out, n, HW, ep);
   DROID_LAUNCH_CHECK();
   return kOk;
 }

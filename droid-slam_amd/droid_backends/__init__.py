@@ -398,6 +398,26 @@ def head_finish(head, b, base=None, target_ba=None, weight_ba=None, row0=0):
     return target, weight
 
 
+def eta_damping(er, map_, frames, state, ep):
+    """GraphAgg's damping into the BA (include/droid_backends.h:
+    droid_eta_damping_f32): er (U,H,W,1) fp16 raw eta conv, map_ / frames (K)
+    int32 (row of er or -1, frame id), state (N,H,W) f32 (updated in place) ->
+    (K,H,W) f32 = 0.2 state[frames] + ep."""
+    U, H, W = er.shape[:3]
+    _check_inputs(("er", "map", "frames", "state"), (er, map_, frames, state))
+    _need(er, torch.float16, "er")
+    _need(map_, torch.int32, "map")
+    _need(frames, torch.int32, "frames")
+    _need(state, torch.float32, "state")
+    if tuple(state.shape[1:]) != (H, W) or map_.shape != frames.shape:
+        raise RuntimeError("eta_damping: state must be (N,H,W) and map / frames the same (K) shape")
+    out = torch.empty((frames.shape[0], H, W), dtype=torch.float32, device=er.device)
+    with torch.cuda.device(er.device):
+        check(lib.droid_eta_damping_f32(_ptr(er), _ptr(map_), _ptr(frames), _ptr(state), _ptr(out), frames.shape[0],
+                                        H * W, float(ep), _stream(er)), "eta_damping_f32")
+    return out
+
+
 def flow_enc0_supported(H, W):
     """Shapes droid_flow_enc0_f16 accepts."""
     return W in (16, 32, 64, 128) and (H * W) % 128 == 0

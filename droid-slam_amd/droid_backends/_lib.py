@@ -46,6 +46,7 @@ _SIGS = {
     "droid_gru_global_split_f16": ([_p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_glo_gates_f32": ([_p, _i, _p, _p, _p, _p, _i, _p], _i),
     "droid_head_finish_f32": ([_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
+    "droid_eta_damping_f32": ([_p, _p, _p, _p, _p, _i, _i, ctypes.c_float, _p], _i),
     "droid_segment_mean_f16": ([_p, _p, _p, _p, _i, ctypes.c_long, _p], _i),
     "droid_altcorr_forward": ([_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p], _i),
     "droid_altcorr_backward": ([_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p], _i),

@@ -319,10 +319,18 @@ class FactorGraph:
                     target, weight = self.target, self.weight
                 target = target.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
                 weight = weight.view(-1, ht, wd, 2).permute(0, 3, 1, 2).contiguous()
-            self.damping[self._dev("uniq", uniq)] = damping[0].to(torch.float)
-
             uniq_ba = np.unique(ii_h)
-            damping = 0.2 * self.damping[self._dev("uniq_ba", uniq_ba)].contiguous() + EP
+            if damping.dtype == torch.float16:
+                # the fused module's raw eta conv: one kernel applies 0.01 softplus, stores
+                # the frames' damping and gathers 0.2 damping + EP for the BA's frames
+                rows = np.searchsorted(uniq, uniq_ba)
+                hit = (rows < len(uniq)) & (uniq[np.minimum(rows, len(uniq) - 1)] == uniq_ba)
+                K = len(uniq_ba)
+                mf = self._dev("eta_map", np.concatenate([np.where(hit, rows, -1), uniq_ba]).astype(np.int32))
+                damping = droid_backends.eta_damping(damping, mf[:K], mf[K:], self.damping, EP)
+            else:
+                self.damping[self._dev("uniq", uniq)] = damping[0].to(torch.float)
+                damping = 0.2 * self.damping[self._dev("uniq_ba", uniq_ba)].contiguous() + EP
             self.video.ba(target, weight, damping, self._dev("ii_ba", ii_h), self._dev("jj_ba", jj_h),
                           t0, t1, itrs=itrs, lm=1e-4, ep=0.1, motion_only=motion_only,
                           ii_host=ii_h, jj_host=jj_h, comm=self.comm,

@@ -307,7 +307,7 @@ class FusedUpdateModule(torch.nn.Module):
             head = torch.zeros((E, H, W, 4), dtype=torch.float32, device=dev)
             droid_backends.conv_dw_head_f16([(net_new, 0, 128)], P["dw0"], P["dw0_b"], P["head_taps"], head)
             if raw_head:   # the caller finishes it (droid_backends.head_finish: bias, sigmoid, target)
-                delta, weight = head, None
+                delta, weight = head, None   # (and eta: the raw conv output er, see below)
             else:
                 head += P["head_b"]
                 delta = head[..., 0:2].unsqueeze(0)
@@ -331,6 +331,8 @@ class FusedUpdateModule(torch.nn.Module):
         conv([(agg, 0, 128)], P["a2"], 128, 3, bias=P["a2_b"], act=1, out=a2)
         er = torch.empty((num_unique, H, W, 1), dtype=torch.float16, device=dev)
         conv([(a2, 0, 128)], P["eta"], 1, 3, bias=P["eta_b"], out=er)
+        if raw_head:   # the caller applies 0.01 softplus with its damping update (droid_backends.eta_damping)
+            return net_new, delta, weight, er
         eta = 0.01 * F.softplus(er.float()).view(1, num_unique, H, W)
         if want_upmask:   # GraphAgg.upmask (droid_net.py:57): 1x1 128 -> 576 on the aggregated map
             up = self.m.agg.upmask[0]

@@ -209,6 +209,13 @@ int droid_gru_global_split_f16(const void* h, const void* w, const float* bias, 
 int droid_head_finish_f32(const float* head, const float* b, const float* base, float* target, float* weight,
                           float* target_ba, float* weight_ba, int row0, int E, int HW, hipStream_t stream);
 
+/* GraphAgg's damping into the BA (droid_net.py:73, factor_graph.py:211,221):
+ * for k < nba, frame frames[k], map[k] = its row of er (U,HW) fp16 (the raw
+ * eta conv output) or -1: state (N,HW) f32 [frame] = 0.01 softplus(er[map])
+ * where map >= 0, out (nba,HW) f32 [k] = 0.2 state[frame] + ep. */
+int droid_eta_damping_f32(const void* er, const int* map, const int* frames, float* state, float* out, int nba,
+                          int HW, float ep, hipStream_t stream);
+
 /* the ConvGRU's global gate terms (gru.py:29-32: convz_glo | convr_glo | convq_glo
  * on glo): b + glo w^T, written as out_zr (E,256) f32 = the z | r terms and
  * out_q (E,128) f32 = the q terms (the two gate convs' per-image biases);

@@ -443,6 +443,44 @@ def test_corr_volume_slot_pool_matches_fresh_block():
     assert torch.equal(out, exp)
 
 
+def test_head_finish_and_eta_damping_match_torch():
+    """droid_head_finish_f32 (bias, sigmoid, coords1 + delta, BA-layout rows)
+    and droid_eta_damping_f32 (0.01 softplus, the damping store, 0.2 d + EP
+    gather) against the torch ops they replace (factor_graph.py:209-221)."""
+    import droid_backends
+    g = torch.Generator(device=DEV).manual_seed(61)
+    E, H, W = 5, 8, 16
+    head = torch.randn((E, H, W, 4), generator=g, device=DEV) * 3
+    b = torch.randn(4, generator=g, device=DEV)
+    base = torch.randn((E, H, W, 2), generator=g, device=DEV) * 20
+    tba = torch.full((E + 3, 2, H, W), 7.0, device=DEV)
+    wba = torch.full((E + 3, 2, H, W), 7.0, device=DEV)
+    t, w = droid_backends.head_finish(head, b, base, tba, wba, 3)
+    hb = head + b
+    t_ref = base + hb[..., 0:2]
+    w_ref = torch.sigmoid(hb[..., 2:4])
+    assert torch.equal(t, t_ref)
+    np.testing.assert_allclose(host(w), host(w_ref), rtol=0, atol=1e-7)
+    assert torch.equal(tba[3:], t.permute(0, 3, 1, 2)) and torch.equal(wba[3:], w.permute(0, 3, 1, 2))
+    assert bool((tba[:3] == 7.0).all()) and bool((wba[:3] == 7.0).all())
+    d0, _ = droid_backends.head_finish(head, b)
+    assert torch.equal(d0, hb[..., 0:2].contiguous())
+    # eta / damping: frames 2, 5, 6 have eta rows 1, 0, -, frame 9 has row 2
+    U, N = 3, 12
+    er = (torch.randn((U, H, W, 1), generator=g, device=DEV) * 8).half()
+    er[0, 0, 0, 0] = 30.0   # softplus' linear branch
+    state = torch.rand((N, H, W), generator=g, device=DEV)
+    frames = torch.tensor([2, 5, 6, 9], dtype=torch.int32, device=DEV)
+    rows = torch.tensor([1, 0, -1, 2], dtype=torch.int32, device=DEV)
+    ref_state = state.clone()
+    eta = 0.01 * torch.nn.functional.softplus(er.float()).view(U, H, W)
+    ref_state[torch.tensor([2, 5, 9], device=DEV)] = eta[torch.tensor([1, 0, 2], device=DEV)]
+    ref_out = 0.2 * ref_state[frames.long()] + 1e-7
+    out = droid_backends.eta_damping(er, rows, frames, state, 1e-7)
+    np.testing.assert_allclose(host(state), host(ref_state), rtol=2e-7, atol=0)
+    np.testing.assert_allclose(host(out), host(ref_out), rtol=2e-7, atol=0)
+
+
 def test_factor_graph_update_pyramid_corr():
     """FactorGraph(corr_impl="pyramid"): no volume; update() finite and its BA
     matches the oracle on the inputs it hands over."""
