@@ -71,6 +71,17 @@ def untile8(level, H2, W2):
     return x[:, :, :, :H2].contiguous()
 
 
+def upload(arr, device):
+    """host array -> device tensor without draining the stream: a copy from
+    pageable host memory waits for the stream's queued work first (the frontend's
+    edge edits would stall the host on the previous update); this one is staged in
+    pinned memory and copied asynchronously."""
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    if torch.device(device).type == "cuda":
+        t = t.pin_memory()
+    return t.to(device, non_blocking=True)
+
+
 class CorrBlock:
     """corr.py:23-71 (volume correlation pyramid).
 
@@ -179,7 +190,7 @@ class CorrBlock:
         if self._slots is None:
             return None
         if self._slot_dev is None:
-            self._slot_dev = torch.as_tensor(self._slots, device=self._pyr[0].device)
+            self._slot_dev = upload(self._slots, self._pyr[0].device)
         return self._slot_dev
 
     def _pool(self):
@@ -204,7 +215,7 @@ class CorrBlock:
             self._free.extend(range(rows, rows + grow))
         rows = np.asarray(self._free[:n], np.int32)
         del self._free[:n]
-        ridx = torch.as_tensor(rows.astype(np.int64), device=self._pyr[0].device)
+        ridx = upload(rows.astype(np.int64), self._pyr[0].device)
         for lv, nv in zip(self._pyr, new):
             lv.index_copy_(0, ridx, nv)
         self._slots = np.concatenate([self._slots, rows])
@@ -215,7 +226,7 @@ class CorrBlock:
         """keep the edges where the host bool mask `keep` is set."""
         keep = np.asarray(keep, dtype=bool).reshape(-1)
         if not self.tiled:
-            k = torch.as_tensor(keep, device=self._pyr[0].device)
+            k = upload(keep, self._pyr[0].device)
             self._pyr = [lv[k] for lv in self._pyr]
             return self
         self._pool()

@@ -16,7 +16,7 @@ import torch
 
 import droid_backends
 
-from .corr import AltCorrBlock, CorrBlock
+from .corr import AltCorrBlock, CorrBlock, upload
 from .fused import PendingAltLookup, PendingLookup, edge_segments
 
 
@@ -75,11 +75,16 @@ class FactorGraph:
         return x.unsqueeze(0)
 
     # -- edge-list views ------------------------------------------------------
+    def _up(self, arr):
+        """host array -> device tensor without waiting for the stream (a copy from
+        pageable memory first drains the stream; this one goes through pinned memory)."""
+        return upload(arr, self.device)
+
     def _dev(self, name, arr):
         key = (name, arr.tobytes())
         t = self._dev_cache.get(name)
         if t is None or t[0] != key:
-            t = (key, torch.from_numpy(np.ascontiguousarray(arr)).to(self.device, non_blocking=True))
+            t = (key, self._up(arr))
             self._dev_cache[name] = t
         return t[1]
 
@@ -150,7 +155,7 @@ class FactorGraph:
             order = np.argsort(self.age.cpu().numpy(), kind="stable")
             self.rm_factors(order >= self.max_factors - len(ii), store=True)
 
-        dij = torch.as_tensor(np.stack([ii, jj]).astype(np.int64), device=self.device)   # one upload
+        dij = self._up(np.stack([ii, jj]).astype(np.int64))   # one upload
         dii, djj = dij[0], dij[1]
         net = self._edge_state(self.video.nets[dii].to(self.device))
         if self.corr_impl == "volume":
@@ -162,7 +167,7 @@ class FactorGraph:
             rows_1 = (rig * ii).astype(np.int64)
             rows_2 = (rig * jj + ((ii == jj) & (rig > 1))).astype(np.int64)
             used, inv = np.unique(np.concatenate([rows_1, rows_2]), return_inverse=True)
-            up = torch.as_tensor(np.concatenate([used, inv]).astype(np.int32), device=self.device)   # one upload
+            up = self._up(np.concatenate([used, inv]).astype(np.int32))   # one upload
             fm = self.video.fmaps.reshape(num * rig, ch, ht, wd).index_select(0, up[:len(used)])
             frames = torch.empty((len(used), ht, wd, ch), dtype=torch.float16, device=self.device)
             torch.mul(fm.permute(0, 2, 3, 1), 0.25, out=frames)     # NHWC / 4 in one pass (exact in fp16)
@@ -171,7 +176,7 @@ class FactorGraph:
             if droid_backends.corr_volume_pyramid_supported(ht, wd, tiled and wd // 8 % 8 == 0):
                 corr = CorrBlock.from_frames(frames, f1, f2, tiled=tiled)
             else:
-                c = torch.as_tensor((ii == jj).astype(np.int64), device=self.device)
+                c = self._up((ii == jj).astype(np.int64))
                 corr = CorrBlock(self.video.fmaps[dii, 0].unsqueeze(0), self.video.fmaps[djj, c].unsqueeze(0),
                                  tiled=tiled)
             self.corr = corr if self.corr is None else self.corr.cat(corr)
@@ -199,7 +204,7 @@ class FactorGraph:
         keep = ~mask
         # host index lists, one upload: a device bool mask would sync per tensor (nonzero)
         nk = int(keep.sum())
-        both = torch.as_tensor(np.concatenate([np.flatnonzero(keep), np.flatnonzero(mask)]), device=self.device)
+        both = self._up(np.concatenate([np.flatnonzero(keep), np.flatnonzero(mask)]))
         dkeep, dgone = both[:nk], both[nk:]
         if store:
             self._ii_inac = np.concatenate([self._ii_inac, self._ii[mask]])
@@ -229,7 +234,7 @@ class FactorGraph:
         self._ii_inac = np.where(self._ii_inac >= ix, self._ii_inac - 1, self._ii_inac)
         self._jj_inac = np.where(self._jj_inac >= ix, self._jj_inac - 1, self._jj_inac)
         if m.any():
-            dm = torch.as_tensor(np.flatnonzero(~m), device=self.device)
+            dm = self._up(np.flatnonzero(~m))
             self._ii_inac = self._ii_inac[~m]
             self._jj_inac = self._jj_inac[~m]
             self.target_inac = self.target_inac.index_select(1, dm)
@@ -348,13 +353,21 @@ class FactorGraph:
             ht, wd = self.ht, self.wd
             sel = np.zeros(0, np.int64) if m is None else np.nonzero(m)[0]
             n_in = len(sel)
-            tb = torch.empty((n_in + E, 2, ht, wd), dtype=torch.float32, device=self.device)
-            wb = torch.empty_like(tb)
+            rows = n_in + E
+            # storage reused across edge sets while it is large enough (rows rounded
+            # up to 32): an edit then costs the inactive rows' refill, not an allocation
+            if c is None or c[3].shape[0] < rows:
+                cap = (rows + 31) // 32 * 32
+                st = torch.empty((cap, 2, ht, wd), dtype=torch.float32, device=self.device)
+                sw = torch.empty_like(st)
+            else:
+                st, sw = c[3], c[4]
+            tb, wb = st[:rows], sw[:rows]
             if n_in:
-                idx = torch.as_tensor(sel, device=self.device)
+                idx = self._dev("inac_sel", sel)
                 tb[:n_in] = self.target_inac[0].index_select(0, idx).permute(0, 3, 1, 2)
                 wb[:n_in] = self.weight_inac[0].index_select(0, idx).permute(0, 3, 1, 2)
-            c = self._ba_tw = (key, tb, wb)
+            c = self._ba_tw = (key, tb, wb, st, sw)
         return c[1], c[2]
 
     def _pending_alt_lookup(self, coords1):
@@ -433,15 +446,15 @@ class FactorGraph:
             vh = (self._ii >= i) & (self._ii < i + s)
             if not vh.any():
                 continue
-            v = torch.as_tensor(vh, device=self.device)
+            v = self._up(vh)
             iis_h, jjs_h = self._ii[vh], self._jj[vh]
-            iis = torch.as_tensor(iis_h, device=self.device)
-            jjs = torch.as_tensor(jjs_h, device=self.device)
-            src = torch.as_tensor(rig * iis_h, device=self.device)
-            dst = torch.as_tensor(rig * jjs_h + (iis_h == jjs_h), device=self.device)
+            iis = self._up(iis_h)
+            jjs = self._up(jjs_h)
+            src = self._up(rig * iis_h)
+            dst = self._up(rig * jjs_h + (iis_h == jjs_h))
             corr1 = corr_op(coords1[:, v], src, dst)
             uq, inv = np.unique(iis_h, return_inverse=True)
-            dinv = torch.as_tensor(inv, device=self.device)
+            dinv = self._up(inv)
             with torch.autocast("cuda", enabled=True):
                 net, delta, weight, damping, _ = self.update_op(
                     self.net[:, v], self.video.inps[None, iis], corr1, motn[:, v], iis, jjs,
@@ -449,7 +462,7 @@ class FactorGraph:
             self.net[:, v] = net
             self.target[:, v] = coords1[:, v] + delta.float()
             self.weight[:, v] = weight.float()
-            self.damping[torch.as_tensor(uq, device=self.device)] = damping[0].float()
+            self.damping[self._up(uq)] = damping[0].float()
 
     # -- edge construction (factor_graph.py:292-369) --------------------------
     def add_neighborhood_factors(self, t0, t1, r=3):
