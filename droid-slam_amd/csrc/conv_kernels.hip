@@ -962,69 +962,23 @@ __device__ __forceinline__ half8 gru_blend_f16(half8 z, half8 h, half8 q) {
   return a + b;
 }
 
+// The band epilogue around a caller-supplied pass 1: stage1(bl, act) writes
+// act(acc + column bias) of the caller's accumulators into the fp16 staging
+// tile smem[TMX][TN + 8] (bl = the tile's column biases in LDS, act = the
+// epilogue's pass-1 activation); pass 2 below is shared by the band tile and
+// the Winograd tile.  EARLY: the per-frame term may be loaded before pass 1.
+template <int TMX, int TN, int NT, int EPI, bool EARLY, class Stage1>
+__device__ __forceinline__ void band_epilogue_core(const ConvArgs& a, _Float16* smem, long m0, int n0, int tid,
+                                                   float bcol, long long* prof, Stage1 stage1);
+
 template <int TMX, int TN, int FM, int FN, int WM = 4, bool CONTIG = false, int NT = 512, int EPI = -1>
 __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
                                               int n0, int wm, int wn, int lane, int tid, float bcol,
                                               long long* prof = nullptr) {
-  constexpr int ER = TN + 8, PPR = TN / 8;
-  const int HW = a.H * a.W;
-  const int b = (int)(m0 / HW);  // a tile never straddles two images
-  const int fr = lane & 15, fq = lane >> 4;
-  // kPre: the gate's argument gets the per-source term in pass (2), so pass (1)
-  // stages the pre-activation acc + bias (fp16, as the reference's autocast
-  // conv output is) and the gate is applied after the sum
+  constexpr int ER = TN + 8;
   constexpr bool kPre = EPI == EPI_GRU_ZRP || EPI == EPI_GRU_QP;
-  constexpr int EB = kPre ? EPI - kEpiPreShift : EPI;
-  const int epi = EB >= 0 ? EB : a.epi;
-  const bool relu = a.act == 1;
-  // the tile's column biases (bias + per-image bias, loaded by thread t < TN
-  // before the main loop) go through LDS: with kBandSwap a lane's accumulators
-  // are 4 consecutive channels of one pixel, so each lane needs 4 x FN of them
-  float* const bl = reinterpret_cast<float*>(smem + TMX * ER);
-  static_assert((TMX * PPR) % NT == 0, "band epilogue: whole store rounds");
-  constexpr int RND = TMX * PPR / NT;
-  // GRU epilogues: every round's h (and z) pieces are loaded after pass 1, all
-  // in flight together while the staging barrier waits (issued inside the store
-  // loop they were serialised behind the previous round's store)
-  constexpr bool kPreH = EB == EPI_GRU_ZR || EB == EPI_GRU_Q;
-  // round q of thread tid: tile row r0 + q*RQ, 16-B piece p (NT % PPR == 0), so
-  // every global address is a per-thread base plus q times a uniform row step
-  static_assert(NT % PPR == 0, "band epilogue: rounds are whole rows");
-  constexpr int RQ = NT / PPR;
-  const int r0 = tid / PPR, p = tid % PPR;
-  const int c = n0 + p * 8;
-  const long mrow = m0 + r0;
-  const bool rhalf = epi == EPI_GRU_ZR && c >= a.gru_ch;
-  // pass (2) in batches of RB rounds (the 4-wave tile has 32 rounds per thread:
-  // all of them in flight would need 3 x 128 VGPRs)
-  constexpr int RB = RND > 16 ? 16 : RND;
-  static_assert(RND % RB == 0, "band epilogue: whole batches");
-  half8 hpre[kPreH ? RB : 1], zpre[EB == EPI_GRU_Q ? RB : 1], ppre[kPre ? RB : 1];
-  // the per-frame term's pieces (pixel m of image b -> pixel of its source
-  // frame): on the 384-row tiles they go out before pass 1 - the accumulators
-  // leave room for them there - so their latency and L1 bandwidth overlap the
-  // staging writes; the 256x256 tile (2 VGPRs short) issues them after pass 1
-  constexpr bool kEarlyPre = kPre && TN != 256 && RB == RND;
-  auto load_pre = [&](int q0) {
-    const long pshift = ((long)a.pre_idx[b] - b) * HW;
-    const __half* const pp = a.pre + (mrow + (long)q0 * RQ + pshift) * a.pre_cstride + a.pre_coff + c;
-    const long pstep = (long)RQ * a.pre_cstride;
-#pragma unroll
-    for (int q = 0; q < RB; ++q) ppre[q] = *reinterpret_cast<const half8*>(pp + q * pstep);
-  };
-  if constexpr (kEarlyPre) load_pre(0);
-  __syncthreads();  // main-loop LDS reads are done
-  if (tid < TN) bl[tid] = bcol;
-  __syncthreads();
-  auto act = [&](float v) -> float {
-    if constexpr (kPre) return v;
-    else if constexpr (EPI == EPI_GRU_ZR) return sigmoid_fast(v);
-    else if constexpr (EPI == EPI_GRU_Q) return tanh_fast(v);
-    else if constexpr (EPI == EPI_ACT) return relu ? fmaxf(v, 0.f) : v;
-    else if (epi == EPI_GRU_ZR) return sigmoidf_(v);
-    else if (epi == EPI_GRU_Q) return tanhf(v);
-    else return (a.act == 1) ? fmaxf(v, 0.f) : v;
-  };
+  const int fr = lane & 15, fq = lane >> 4;
+  band_epilogue_core<TMX, TN, NT, EPI, true>(a, smem, m0, n0, tid, bcol, prof, [&](const float* bl, auto act) {
   if constexpr (kBandSwap<TN>) {
     // (1) lane (fr, fq) of fragment (i, j) holds channels 16 j + 4 fq .. + 3 of
     // pixel row frag_row(i) + fr: one 8-B LDS write per fragment
@@ -1067,6 +1021,71 @@ __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[
       }
     }
   }
+  });
+}
+
+template <int TMX, int TN, int NT, int EPI, bool EARLY, class Stage1>
+__device__ __forceinline__ void band_epilogue_core(const ConvArgs& a, _Float16* smem, long m0, int n0, int tid,
+                                                   float bcol, long long* prof, Stage1 stage1) {
+  constexpr int ER = TN + 8, PPR = TN / 8;
+  const int HW = a.H * a.W;
+  const int b = (int)(m0 / HW);  // a tile never straddles two images
+  // kPre: the gate's argument gets the per-source term in pass (2), so pass (1)
+  // stages the pre-activation acc + bias (fp16, as the reference's autocast
+  // conv output is) and the gate is applied after the sum
+  constexpr bool kPre = EPI == EPI_GRU_ZRP || EPI == EPI_GRU_QP;
+  constexpr int EB = kPre ? EPI - kEpiPreShift : EPI;
+  const int epi = EB >= 0 ? EB : a.epi;
+  const bool relu = a.act == 1;
+  // the tile's column biases (bias + per-image bias, loaded by thread t < TN
+  // before the main loop) go through LDS: with kBandSwap a lane's accumulators
+  // are 4 consecutive channels of one pixel, so each lane needs 4 x FN of them
+  float* const bl = reinterpret_cast<float*>(smem + TMX * ER);
+  static_assert((TMX * PPR) % NT == 0, "band epilogue: whole store rounds");
+  constexpr int RND = TMX * PPR / NT;
+  // GRU epilogues: every round's h (and z) pieces are loaded after pass 1, all
+  // in flight together while the staging barrier waits (issued inside the store
+  // loop they were serialised behind the previous round's store)
+  constexpr bool kPreH = EB == EPI_GRU_ZR || EB == EPI_GRU_Q;
+  // round q of thread tid: tile row r0 + q*RQ, 16-B piece p (NT % PPR == 0), so
+  // every global address is a per-thread base plus q times a uniform row step
+  static_assert(NT % PPR == 0, "band epilogue: rounds are whole rows");
+  constexpr int RQ = NT / PPR;
+  const int r0 = tid / PPR, p = tid % PPR;
+  const int c = n0 + p * 8;
+  const long mrow = m0 + r0;
+  const bool rhalf = epi == EPI_GRU_ZR && c >= a.gru_ch;
+  // pass (2) in batches of RB rounds (the 4-wave tile has 32 rounds per thread:
+  // all of them in flight would need 3 x 128 VGPRs)
+  constexpr int RB = RND > 16 ? 16 : RND;
+  static_assert(RND % RB == 0, "band epilogue: whole batches");
+  half8 hpre[kPreH ? RB : 1], zpre[EB == EPI_GRU_Q ? RB : 1], ppre[kPre ? RB : 1];
+  // the per-frame term's pieces (pixel m of image b -> pixel of its source
+  // frame): on the 384-row tiles they go out before pass 1 - the accumulators
+  // leave room for them there - so their latency and L1 bandwidth overlap the
+  // staging writes; the 256x256 tile (2 VGPRs short) issues them after pass 1
+  constexpr bool kEarlyPre = kPre && TN != 256 && RB == RND && EARLY;
+  auto load_pre = [&](int q0) {
+    const long pshift = ((long)a.pre_idx[b] - b) * HW;
+    const __half* const pp = a.pre + (mrow + (long)q0 * RQ + pshift) * a.pre_cstride + a.pre_coff + c;
+    const long pstep = (long)RQ * a.pre_cstride;
+#pragma unroll
+    for (int q = 0; q < RB; ++q) ppre[q] = *reinterpret_cast<const half8*>(pp + q * pstep);
+  };
+  if constexpr (kEarlyPre) load_pre(0);
+  __syncthreads();  // main-loop LDS reads are done
+  if (tid < TN) bl[tid] = bcol;
+  __syncthreads();
+  auto act = [&](float v) -> float {
+    if constexpr (kPre) return v;
+    else if constexpr (EPI == EPI_GRU_ZR) return sigmoid_fast(v);
+    else if constexpr (EPI == EPI_GRU_Q) return tanh_fast(v);
+    else if constexpr (EPI == EPI_ACT) return relu ? fmaxf(v, 0.f) : v;
+    else if (epi == EPI_GRU_ZR) return sigmoidf_(v);
+    else if (epi == EPI_GRU_Q) return tanhf(v);
+    else return (a.act == 1) ? fmaxf(v, 0.f) : v;
+  };
+  stage1(static_cast<const float*>(bl), act);
   if (prof && tid == 0) prof[6] = (long long)__builtin_amdgcn_s_memtime();  // pass 1 written
   // h (and z) pieces of rounds [q0, q0 + RB)
   auto load_h = [&](int q0) {
@@ -1611,6 +1630,280 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------------------
+// Winograd band kernel (3x3, CHUNKED, W == 64): the 3x3 conv as F(2,3) along x.
+// For an output pixel pair (x, x+1) = (2P, 2P+1) of image row y and kernel row
+// ky, with d_t = in[y + ky - 1][2P + t] (t = -1..2) and g_t = w[ky][t + 1]:
+//   u0 = d_-1 - d_1   u1 = d_0 + d_1   u2 = d_1 - d_0   u3 = d_0 - d_2
+//   v0 = g_-1         v1 = (g_-1 + g_0 + g_1) / 2   v2 = (g_-1 - g_0 + g_1) / 2   v3 = g_1
+//   M_k = sum over (ky, ci) of u_k v_k (four GEMMs, M = pairs, N = Cout, K = 3 Cin)
+//   out(2P) = M0 + M1 + M2,   out(2P+1) = M1 - M2 - M3
+// 12 multiplies per pixel pair and input channel where the direct conv does
+// 18: two thirds of the MFMA work.  u_k is formed on packed fp16 (one rounding
+// of the exact sum, v_pk_add_f16), v_k is pre-transformed on the host
+// (pack_conv_wino) from the fp16 weights and rounded once; the accumulation
+// and the output transform are fp32.  Extra error: one fp16 rounding of u_k
+// and v_k, i.e. one more fp16 ulp of each operand, the class of error the
+// reference's autocast (cuDNN picks Winograd kernels for fp16 3x3 convs too)
+// already carries; parity tests bound it against the fp32 conv.
+//
+// Tile: 256 pixels (4 image rows) x 128 output channels on 8 waves; wave (wm,
+// wn) owns image row wm and channels wn*64 .. +63: 32 pixel pairs x 64 channels
+// for each of the four M_k (128 accumulators).  Pairs are interleaved so that
+// lane fr of pair fragment f holds pair 2 fr + f = pixels 4 fr + 2f, +1: the
+// band is stored in LDS by x mod 4 ("e0" x = 4fr, "o0" 4fr+1, "e1" 4fr+2, "o1"
+// 4fr+3 - four contiguous 16-row blocks per image row, conflict-free
+// ds_read_b128 as in the band kernel) and the two shifted inputs of the
+// transform are one DPP lane shift each: d_-1 of fragment 0 is o1 of lane fr-1
+// (row_shr:1, zero at x = -1), d_2 of fragment 1 is e0 of lane fr+1 (row_shl:1,
+// zero at x = 64); every other d_t is an unshifted read.  Per K-step of 32
+// channels a wave issues 4 + 16 ds_read_b128 (band, transformed weights), 8
+// DPP moves and 32 v_pk_add_f16 for 32 MFMAs.
+// LDS (144 KB): the 6-row band of one (64-channel chunk, 32-channel K half),
+// double buffered (2 x 24 KB, LDS-DMA as in the band kernel, issued three
+// stages ahead), and the transformed weights of one stage = (chunk, K half,
+// ky): [4 comps][128 channels][32] fp16 = 32 KB, triple buffered (issued two
+// stages ahead: a stage is half the band kernel's MFMA time, one stage of lead
+// left the DMA latency exposed - 7.9 vs 7.45 ms for z|r); all rows are 64 B
+// with the 16-B slot XOR-ed by kWinoG[(row & 15) >> 2] (conflict-free for the
+// ds_read_b128 lane groups of a 16-row fragment).
+// Global transformed weights: wt[stage][comp][Cout][32], stage = (chunk*2 + hk)*3 + ky.
+// Measured (C3, 2048 edges of 48x64, scripts/wino_bench.py): z|r 8.1-8.2 ms vs
+// 7.5-7.6 for the direct 256x256 band tile, q 4.35 vs 4.14, 128->128 1.78 vs
+// 1.65 - slower despite a third less MFMA work.  The loop is bound by the SIMD's
+// issue slots, not the MFMA pipe: a 16x16x32 MFMA holds 8 of its 16 issue
+// cycles and an LDS-DMA instruction costs ~60-185 (MI355X_MICROARCH.md), and
+// this tile moves the same 40 KB per stage for half the MFMAs (its tile, bound
+// by 4 accumulator sets in 128 VGPRs, is 256 x 128 against the direct tile's
+// 256 x 256 - twice the weight bytes per MFMA; 5 DMA instructions per 32
+// MFMAs vs 4.7 per 64).  Issuing the DMAs after the stage's first MFMAs, and
+// prefetching the weights two stages ahead instead of one, measured the same.
+// Opt-in (DROID_CONV_WINO=1 in droid_mi355x.fused); parity: tests/test_gpu_wino.py.
+constexpr int kWinoTM = 256, kWinoTN = 128;
+constexpr int kWinoBand = 6 * 64 * 64;         // one band buffer: 6 rows x 64 px x 32 channels (bytes)
+constexpr int kWinoWst = 4 * kWinoTN * 64;     // one weight stage buffer (bytes)
+constexpr int kWinoNW = 3;                     // weight stage buffers (two stages in flight)
+constexpr int kWinoLds = 2 * kWinoBand + kWinoNW * kWinoWst;
+static_assert(kWinoLds <= kLdsMax, "wino LDS");
+
+__device__ __forceinline__ int wino_g(int q) { return (0x1E >> (2 * q)) & 3; }   // {0, 2, 3, 1}[q]
+
+typedef int int4v_t __attribute__((ext_vector_type(4)));
+// lane shift within each 16-lane row; lanes whose source leaves the row keep `old`
+template <int CTRL>
+__device__ __forceinline__ half8 dpp_half8(half8 old, half8 src) {
+  const int4v_t o = __builtin_bit_cast(int4v_t, old), s = __builtin_bit_cast(int4v_t, src);
+  int4v_t r;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r[k] = __builtin_amdgcn_update_dpp(o[k], s[k], CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(half8, r);
+}
+constexpr int kDppRowShl1 = 0x101, kDppRowShr1 = 0x111;
+
+__device__ __forceinline__ void wait_vmcnt_wino(int n) {
+  switch (n) {   // wave-uniform; the counts the stage pipeline produces
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_wino_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int HW = a.H * 64;
+  const long wgid = xcd_work_id(a.m_tiles * a.n_tiles);
+  const long mt = wgid / a.n_tiles;
+  const int nt = (int)(wgid - mt * a.n_tiles);
+  const long m0 = mt * kWinoTM;
+  const int n0 = nt * kWinoTN;
+  const int y0 = (int)((m0 % HW) >> 6);
+  const long band0 = m0 - 64;
+  char* Hl = lds;                      // [2][6 rows][64 px][64 B]
+  char* Bl = lds + 2 * kWinoBand;      // [3][4 comps][128 ch][64 B]
+  const unsigned Hl_a = lds_addr(Hl), Bl_a = lds_addr(Bl);
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  // column tid's bias (+ per-image bias), loaded before any DMA (the counted
+  // vmcnt waits below count DMAs only)
+  float bcol = 0.f;
+  if (tid < kWinoTN) {
+    const int co = n0 + tid;
+    if (a.bias) bcol = a.bias[co];
+    if (a.bbias) bcol += a.bbias[(long)(m0 / HW) * a.Cout + co];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // 64-B LDS rows (band and weights alike): 16-B slot kq of a row whose index
+  // within its 16-row fragment is r16 is stored at kq ^ kWinoG[r16 >> 2]
+  // ---- band DMA, stage group b = (chunk b >> 1, K half b & 1): instruction q
+  // of this wave fills LDS rows 16 (wave + 8q) .. + 15; lane l writes row
+  // r = 16 (wave + 8q) + (l >> 2), slot l & 3 = channel piece (l & 3) ^ kWinoG[l >> 4]
+  // of pixel (ry, x): r = 64 ry + 16 (x & 3) + (x >> 2)
+  const int lpiece = (lane & 3) ^ wino_g(lane >> 4);
+  int hpix[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int r = (wave + 8 * q) * 16 + (lane >> 2);
+    const int ry = r >> 6, rem = r & 63;
+    const int x = ((rem & 15) << 2) | (rem >> 4);
+    const int y = y0 - 1 + ry;
+    hpix[q] = (y >= 0 && y < a.H) ? ry * 64 + x : -1;
+  }
+  auto issue_band = [&](int bg) {
+    const int chunk = bg >> 1;
+    int s = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (q + 1 < a.nsrc && chunk >= a.chunk_end[q]) s = q + 1;
+    const int cstart = s ? a.chunk_end[s - 1] : 0;
+    const ConvSrc src = a.src[s];
+    const int c = (chunk - cstart) * BK + (bg & 1) * 32 + lpiece * 8;
+    const bool okc = c < src.C;
+    const rsrc_t rs = make_rsrc(src.ptr + band0 * src.cstride, 6 * 64 * src.cstride * 2);
+    const unsigned dst = Hl_a + (bg & 1) * kWinoBand;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const unsigned off = (okc && hpix[q] >= 0) ? (unsigned)((hpix[q] * src.cstride + c) * 2) : kOob;
+      dma16(rs, dst + (wave_u + 8 * q) * 1024, off);
+    }
+  };
+  // ---- weight DMA: instruction q fills 1-KB block wb = wave + 8q = rows 16 wb ..
+  // + 15 (comp wb >> 3, channels 16 (wb & 7) ..); lane l: channel row l >> 2,
+  // slot l & 3 = logical K piece lpiece
+  const long wst_bytes = (long)4 * a.Cout * 64;   // one global stage
+  const rsrc_t rsw = make_rsrc(a.wp, (unsigned)(wst_bytes * a.nstage));
+  unsigned woff[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int wb = wave + 8 * q;
+    const int comp = wb >> 3, ch = (wb & 7) * 16 + (lane >> 2);
+    woff[q] = (unsigned)((((long)comp * a.Cout + n0 + ch) * 32 + lpiece * 8) * 2);
+  }
+  auto issue_w = [&](int st) {
+    const unsigned dst = Bl_a + (st % kWinoNW) * kWinoWst;
+    const unsigned sb = (unsigned)(st * wst_bytes);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dma16(rsw, dst + (wave_u + 8 * q) * 1024, woff[q] + sb);
+  };
+
+  // ---- fragment addresses (lane fr reads row fr of a 16-row fragment, slot kq4)
+  const int fr = lane & 15, kq4 = lane >> 4;
+  const int rsl = fr * 64 + ((kq4 ^ wino_g(fr >> 2)) << 4);
+  const int abase = wm * 4096 + rsl;
+  const int bbase = wn * 4096 + rsl;
+
+  floatx4 acc[4][2][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[k][f][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // stage s = (band group bg = s / 3 = (chunk, K half), kernel row ty = s % 3)
+  // = weight stage s of the global layout
+  const int nb = 2 * a.cpt;
+  const int nst = a.nstage;   // 3 * nb
+  issue_band(0);
+  issue_w(0);
+  if (nst > 1) issue_w(1);
+  const half8 zero8 = {};
+  int s = 0;
+  int wbuf = 0;   // s % kWinoNW
+  for (int bg = 0; bg < nb; ++bg) {
+    const char* Hb = Hl + (bg & 1) * kWinoBand;
+#pragma unroll
+    for (int ty = 0; ty < 3; ++ty, ++s) {
+      // DMA instructions of this wave issued after W(s): W(s+1) (4, issued one
+      // stage ago or in the prologue) and the bands issued at stages s-1 and
+      // s-2 (3 each, at stages 3b' issuing band b'+1)
+      const int nafter = (s + 1 < nst ? 4 : 0) + ((s >= 1 && (s - 1) % 3 == 0 && (s - 1) / 3 + 1 < nb) ? 3 : 0) +
+                         ((s >= 2 && (s - 2) % 3 == 0 && (s - 2) / 3 + 1 < nb) ? 3 : 0);
+      wait_vmcnt_wino(nafter);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // W(s+2) into the buffer stage s-1 used; band bg+1 into the buffer band bg-1
+      // used (issuing them after this stage's first MFMAs instead measured the same)
+      if (s + 2 < nst) {
+        const unsigned dst = Bl_a + (wbuf == 0 ? 2 : wbuf - 1) * kWinoWst;
+        const unsigned sb = (unsigned)((s + 2) * wst_bytes);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dma16(rsw, dst + (wave_u + 8 * q) * 1024, woff[q] + sb);
+      }
+      if (ty == 0 && bg + 1 < nb) issue_band(bg + 1);
+      const char* Ar = Hb + abase + ty * 4096;
+      const half8 e0 = *reinterpret_cast<const half8*>(Ar);
+      const half8 o0 = *reinterpret_cast<const half8*>(Ar + 1024);
+      const half8 e1 = *reinterpret_cast<const half8*>(Ar + 2048);
+      const half8 o1 = *reinterpret_cast<const half8*>(Ar + 3072);
+      const char* Bb = Bl + wbuf * kWinoWst + bbase;
+      // fragment 0: (d_-1, d_0, d_1, d_2) = (o1[fr-1], e0, o0, e1); fragment 1: (o0, e1, o1, e0[fr+1])
+      const half8 dm = dpp_half8<kDppRowShr1>(zero8, o1);
+      const half8 dp = dpp_half8<kDppRowShl1>(zero8, e0);
+      half8 u[4][2];
+      u[0][0] = dm - o0;  u[0][1] = o0 - o1;
+      u[1][0] = e0 + o0;  u[1][1] = e1 + o1;
+      u[2][0] = o0 - e0;  u[2][1] = o1 - e1;
+      u[3][0] = e0 - e1;  u[3][1] = e1 - dp;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        half8 bf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8*>(Bb + k * 8192 + j * 1024);
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[k][f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], u[k][f], acc[k][f][j], 0, 0, 0);
+      }
+      wbuf = wbuf == 2 ? 0 : wbuf + 1;
+    }
+  }
+  (void)issue_w;
+  // output transform + pass 1: lane (fr, fq) of (f, j) holds channels wn*64 + 16 j
+  // + 4 fq .. + 3 of pair 2 fr + f = tile pixels 64 wm + 4 fr + 2 f, + 1
+  constexpr int ER = kWinoTN + 8;
+  const int fq = lane >> 4;
+  band_epilogue_core<kWinoTM, kWinoTN, 512, EPI, false>(
+      a, smem, m0, n0, tid, bcol, nullptr, [&](const float* bl, auto act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = wn * 64 + j * 16 + fq * 4;
+          const floatx4 bv = *reinterpret_cast<const floatx4*>(bl + c);
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            half4_t o0, o1;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float m0v = acc[0][f][j][k], m1v = acc[1][f][j][k], m2v = acc[2][f][j][k], m3v = acc[3][f][j][k];
+              o0[k] = (_Float16)act(((m0v + m1v) + m2v) + bv[k]);
+              o1[k] = (_Float16)act(((m1v - m2v) - m3v) + bv[k]);
+            }
+            const int px = wm * 64 + 4 * fr + 2 * f;
+            *reinterpret_cast<half4_t*>(&smem[px * ER + c]) = o0;
+            *reinterpret_cast<half4_t*>(&smem[(px + 1) * ER + c]) = o1;
+          }
+        }
+      });
+}
+
+template <int EPI>
+static int launch_wino_kernel(const ConvArgs& a, long nwg, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wino_kernel<EPI>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    attr = true;
+  }
+  conv_wino_kernel<EPI><<<dim3((unsigned)nwg), 512, kWinoLds, stream>>>(a);
+  return kOk;
+}
+
+// ---------------------------------------------------------------------------
 // ConvGRU global context (modules/gru.py:19-32, the glo branch):
 //   glo[e][co] = mean over the edge's pixels of sigmoid(w . h + b)[co] * h[co]
 // for a 1x1 128 -> 128 conv w on the hidden state h itself.  One workgroup per
@@ -1971,7 +2264,7 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
                           int Cout, int ks, int act, int epi, void* out, int out_cstride, int out_coff,
                           const void* h, int h_cstride, const void* z, int z_cstride, void* zout,
                           void* rnet, int gru_ch, void* out32, const void* pre, const long long* pre_idx,
-                          int pre_cstride, int pre_coff, hipStream_t stream) {
+                          int pre_cstride, int pre_coff, hipStream_t stream, const void* wt = nullptr) {
   if (nsrc < 1 || nsrc > 4 || B < 0 || H <= 0 || W <= 0 || Cout <= 0 || ks < 1 || ks > 7 || !(ks & 1) ||
       epi < EPI_ACT || epi > EPI_GLO)
     return fail(kInvalidArgument, "conv_nhwc_f16: bad arguments");
@@ -2034,6 +2327,26 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
                        (epi == EPI_GRU_ZR || epi == EPI_GRU_Q || (epi == EPI_ACT && a.stage_out)) &&
                        (epi != EPI_GRU_ZR || gru_ch % 128 == 0);
   int ns_, nh_;
+  if (wt) {  // Winograd tile (droid_conv_wino_f16): W == 64, whole 4-row tiles, 128-channel N tiles
+    if (a.im2col || ks != 3 || W != 64 || H % 4 || Cout % kWinoTN ||
+        !(epi == EPI_ACT ? a.stage_out != 0 : (pre && (epi == EPI_GRU_ZR || epi == EPI_GRU_Q))) ||
+        (epi == EPI_GRU_ZR && gru_ch % kWinoTN))
+      return fail(kUnsupported, "conv_wino_f16: needs a 3x3 conv, W == 64, H % 4 == 0, Cout % 128 == 0");
+    a.wp = (const __half*)wt;
+    a.nstage = 6 * chunks;
+    a.n_tiles = Cout / kWinoTN;
+    a.m_tiles = (long)B * H * W / kWinoTM;
+    const long nwg = a.m_tiles * a.n_tiles;
+    if (nwg > 0x7fffffffL || (long)4 * Cout * 64 * a.nstage > 0x7fffffffL)
+      return fail(kUnsupported, "conv_wino_f16: problem too large");
+    int st;
+    if (epi == EPI_GRU_ZR) st = launch_wino_kernel<EPI_GRU_ZRP>(a, nwg, stream);
+    else if (epi == EPI_GRU_Q) st = launch_wino_kernel<EPI_GRU_QP>(a, nwg, stream);
+    else st = launch_wino_kernel<EPI_ACT>(a, nwg, stream);
+    if (st != kOk) return st;
+    DROID_LAUNCH_CHECK();
+    return kOk;
+  }
   if (pre) {  // the per-source term exists on the band tiles only
     if (band_ok && epi == EPI_GRU_ZR && Cout == 256 && 256 % W == 0 && (H * W) % 256 == 0 && band_nw4() &&
         band_fits<256, 256, 4>(W, &ns_, &nh_))
@@ -2094,6 +2407,27 @@ int droid_conv_gru_pre_f16(const void* const* srcs, const int* C, const int* cst
                         pre_cstride, pre_coff, stream);
 }
 
+// 3x3 conv as Winograd F(2,3) along x (conv_wino_kernel): same operands as
+// droid_conv_nhwc_f16 / droid_conv_gru_pre_f16 with the weights pre-transformed
+// (wt: droid_mi355x.fused.pack_conv_wino); epi EPI_ACT (act 0 / 1) or, with a
+// per-source-frame term pre (else null), EPI_GRU_ZR / EPI_GRU_Q.  W == 64,
+// H % 4 == 0, Cout % 128 == 0; DROID_UNSUPPORTED otherwise (the caller then runs
+// the direct conv).
+int droid_conv_wino_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc, const void* wt,
+                        const float* bias, const float* bbias, int B, int H, int W, int Cout, int act, int epi,
+                        void* out, int out_cstride, int out_coff, const void* h, int h_cstride, const void* z,
+                        int z_cstride, void* zout, void* rnet, int gru_ch, const void* pre,
+                        const long long* pre_idx, int pre_cstride, int pre_coff, hipStream_t stream) {
+  if (!wt || (epi != EPI_ACT && epi != EPI_GRU_ZR && epi != EPI_GRU_Q) ||
+      (epi != EPI_ACT && (!pre || !pre_idx || pre_cstride % 8 || pre_coff % 8 || pre_coff + Cout > pre_cstride ||
+                          (reinterpret_cast<uintptr_t>(pre) & 15))) ||
+      (reinterpret_cast<uintptr_t>(wt) & 15))
+    return fail(kInvalidArgument, "conv_wino_f16: bad arguments");
+  return conv_nhwc_impl(srcs, C, cstride, nsrc, nullptr, bias, bbias, B, H, W, Cout, 3, act, epi, out, out_cstride,
+                        out_coff, h, h_cstride, z, z_cstride, zout, rnet, gru_ch, nullptr,
+                        epi == EPI_ACT ? nullptr : pre, epi == EPI_ACT ? nullptr : pre_idx, pre_cstride, pre_coff,
+                        stream, wt);
+}
 
 // Fused delta/weight heads (EPI_DWHEAD): conv3x3 (srcs -> 256, bias, ReLU) feeding
 // conv3x3 256 -> 4 (hw: [48][256] fp16, row tap*4 + c, rows 36..47 zero); raw head

@@ -13,6 +13,7 @@ mirror in `droid_mi355x`): `corr_pyramid_lookup`, `projective_transform`,
 `BaPlan`, and optional host copies of ii/jj for `ba` (avoids the D2H sync).
 """
 import ctypes
+import os
 from collections import OrderedDict
 
 import numpy as np
@@ -336,6 +337,48 @@ def conv_gru_pre_f16(sources, wp, cout, bias, bbias, epi, pre, pre_idx, pre_coff
                                          h.shape[-1], _ptr(z), z.shape[-1] if z is not None else 0, _ptr(zout),
                                          _ptr(rnet), int(gru_ch), _ptr(pre), _ptr(pre_idx), pre.shape[-1],
                                          int(pre_coff), _stream(t0)), "conv_gru_pre_f16")
+    return out
+
+
+def wino_supported(H, W, cout):
+    """Whether the update operator takes the Winograd tile: opted in with
+    DROID_CONV_WINO=1 (it measures slower than the direct band tile on MI355X,
+    csrc/conv_kernels.hip: conv_wino_kernel) and a shape droid_conv_wino_f16
+    accepts (W == 64, whole 4-row tiles, 128-channel output tiles)."""
+    return W == 64 and H % 4 == 0 and cout % 128 == 0 and os.environ.get("DROID_CONV_WINO", "0") == "1"
+
+
+def conv_wino_f16(sources, wt, cout, bias=None, bbias=None, act=0, epi=EPI_ACT, out=None, out_coff=0,
+                  pre=None, pre_idx=None, pre_coff=0, h=None, z=None, zout=None, rnet=None, gru_ch=128):
+    """3x3 conv as Winograd F(2,3) along x (include/droid_backends.h:
+    droid_conv_wino_f16).  wt: transformed weights (droid_mi355x.fused.pack_conv_wino);
+    epi EPI_ACT (act 0 / 1 -> out) or EPI_GRU_ZR / EPI_GRU_Q with the per-source-frame
+    term pre / pre_idx / pre_coff as in conv_gru_pre_f16."""
+    t0 = sources[0][0]
+    B, H, W = t0.shape[:3]
+    n = len(sources)
+    for t, _, _ in sources:
+        if t.dtype != torch.float16 or not t.is_contiguous() or t.shape[:3] != (B, H, W):
+            raise RuntimeError("conv_wino_f16: sources must be contiguous fp16 (B,H,W,C) tensors")
+    _need(wt, torch.float16, "wt")
+    if epi != EPI_ACT:
+        _check_inputs(("pre", "pre_idx"), (pre, pre_idx))
+        _need(pre, torch.float16, "pre")
+        _need(pre_idx, torch.int64, "pre_idx")
+        if pre.dim() != 4 or tuple(pre.shape[1:3]) != (H, W) or pre_idx.numel() != B:
+            raise RuntimeError("conv_wino_f16: pre must be (F,H,W,C) and pre_idx hold one frame per image")
+    _conv_operands("conv_wino_f16", B, H, W, int(cout), t0.device, bias, bbias,
+                   (("out", out), ("h", h), ("z", z), ("zout", zout), ("rnet", rnet)))
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() + 2 * off for t, off, _ in sources])
+    cs = (ctypes.c_int * n)(*[c for _, _, c in sources])
+    strides = (ctypes.c_int * n)(*[t.shape[-1] for t, _, _ in sources])
+    with torch.cuda.device(t0.device):
+        check(lib.droid_conv_wino_f16(ptrs, cs, strides, n, _ptr(wt), _ptr(bias), _ptr(bbias), B, H, W, int(cout),
+                                      int(act), int(epi), _ptr(out), out.shape[-1] if out is not None else 0,
+                                      int(out_coff), _ptr(h), h.shape[-1] if h is not None else 0, _ptr(z),
+                                      z.shape[-1] if z is not None else 0, _ptr(zout), _ptr(rnet), int(gru_ch),
+                                      _ptr(pre), _ptr(pre_idx), pre.shape[-1] if pre is not None else 0,
+                                      int(pre_coff), _stream(t0)), "conv_wino_f16")
     return out
 
 

@@ -73,6 +73,33 @@ def pack_conv(weight, splits):
     return wp.permute(0, 1, 3, 2).reshape(cout, -1, BK).to(torch.float16).contiguous()
 
 
+def pack_conv_wino(weight, splits):
+    """(Cout, Cin, 3, 3) conv weight -> the Winograd F(2,3) weights of
+    droid_conv_wino_f16: [stage][4][Cout][32] fp16, stage = (chunk*2 + K half)*3 +
+    ky, chunks as pack_conv's (64 channels per source chunk, zero padded).
+    Component k of kernel row ky over (g_-1, g_0, g_1) = w[:, :, ky, 0:3]:
+    v0 = g_-1, v1 = (g_-1 + g_0 + g_1) / 2, v2 = (g_-1 - g_0 + g_1) / 2, v3 = g_1,
+    from the fp16-rounded weights (the reference's autocast operands), each
+    rounded to fp16 once (csrc/conv_kernels.hip: conv_wino_kernel)."""
+    cout, cin, k, _ = weight.shape
+    assert k == 3 and sum(splits) == cin, (splits, cin, k)
+    w = weight.detach().half().float()
+    blocks = []
+    off = 0
+    for c in splits:
+        nch = (c + BK - 1) // BK
+        ws = torch.zeros(cout, nch * BK, 3, 3, device=w.device)
+        ws[:, :c] = w[:, off:off + c]
+        blocks.append(ws)
+        off += c
+    w = torch.cat(blocks, 1)                                   # (cout, chunks*64, ky, kx)
+    g0, g1, g2 = w[..., 0], w[..., 1], w[..., 2]
+    v = torch.stack([g0, (g0 + g1 + g2) * 0.5, (g0 - g1 + g2) * 0.5, g2], -1)   # (cout, C, ky, comp)
+    nch = v.shape[1] // BK
+    v = v.view(cout, nch, 2, 32, 3, 4)                         # (cout, chunk, hk, 32, ky, comp)
+    return v.permute(1, 2, 4, 5, 0, 3).to(torch.float16).contiguous()   # (chunk, hk, ky, comp, cout, 32)
+
+
 def pack_flow_enc0(weight):
     """(128, 4, 7, 7) flow_encoder[0] weight -> [128][416] fp16 for
     droid_flow_enc0_f16: column t*8 + c = weight[co, c, t // 7, t % 7]."""
@@ -199,6 +226,13 @@ class FusedUpdateModule(torch.nn.Module):
         P["a2"] = pack_conv(a.conv2.weight, [128])
         P["a2_b"] = a.conv2.bias.float().contiguous()
         P["eta"] = pack_conv(a.eta[0].weight, [128])
+        # Winograd F(2,3) weights of the 3x3 convs with 128-channel output tiles
+        P["ce2_w"] = pack_conv_wino(m.corr_encoder[2].weight, [128])
+        P["zr_xw"] = pack_conv_wino(keep(wzr), [128, 128, 64])
+        P["q_xw"] = pack_conv_wino(keep(g.convq.weight), [128, 128, 64])
+        P["inp_zrq_w"] = pack_conv_wino(torch.cat([wzr[:, 128:256], g.convq.weight[:, 128:256]], 0), [128])
+        P["a1_w"] = pack_conv_wino(a.conv1.weight, [128])
+        P["a2_w"] = pack_conv_wino(a.conv2.weight, [128])
         P["eta_b"] = a.eta[0].bias.float().contiguous()
         self._packed = P
 
@@ -255,8 +289,19 @@ class FusedUpdateModule(torch.nn.Module):
                 corr = corr.materialise()
             c1 = e16(128)
             conv([(corr, 0, 200)], P["ce0"], 128, 1, bias=P["ce0_b"], act=1, out=c1)
-        cf = e16(128)
-        conv([(c1, 0, 128)], P["ce2"], 128, 3, bias=P["ce2_b"], act=1, out=cf)
+        # DROID_CONV_WINO=1: the 3x3 convs with 128-channel output tiles as Winograd
+        # F(2,3) (droid_conv_wino_f16: 2/3 of the MFMA work, but issue-bound and
+        # slower than the direct band tiles on MI355X - an A/B, not the default)
+        wino = droid_backends.wino_supported(H, W, 128)
+
+        def conv3(srcs, key, cout, bias, out, act=1):
+            if wino:
+                droid_backends.conv_wino_f16(srcs, P[key + "_w"], cout, bias=bias, act=act, out=out)
+            else:
+                conv(srcs, P[key], cout, 3, bias=bias, act=act, out=out)
+            return out
+
+        cf = conv3([(c1, 0, 128)], "ce2", 128, P["ce2_b"], e16(128))
         if droid_backends.flow_enc0_supported(H, W):
             f1 = droid_backends.flow_enc0_f16(motn.contiguous(), P["fe0_416"], P["fe0_b"])
         else:
@@ -285,16 +330,22 @@ class FusedUpdateModule(torch.nn.Module):
             c = self._pre
             if c is None or c[0] is not inp_frames or c[1] is not P:
                 pre = torch.empty((inp_frames.shape[0], H, W, 384), dtype=torch.float16, device=dev)
-                conv([(inp_frames, 0, 128)], P["inp_zrq"], 384, 3, out=pre)
+                conv3([(inp_frames, 0, 128)], "inp_zrq", 384, None, pre, act=0)
                 self._pre = c = (inp_frames, P, pre)
             pre = c[2]
             pidx = inverse if inverse.dtype == torch.int64 else inverse.long()
-            droid_backends.conv_gru_pre_f16([(net, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["zr_x"], 256, P["zr_b"],
-                                            gb_zr, EPI_GRU_ZR, pre, pidx, 0, h=net, zout=z,
-                                            rnet=rn)
-            droid_backends.conv_gru_pre_f16([(rn, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["q_x"], 128, P["q_b"],
-                                            gb_q, EPI_GRU_Q, pre, pidx, 256, h=net, z=z,
-                                            out=net_new)
+            if wino:
+                droid_backends.conv_wino_f16([(net, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["zr_xw"], 256, P["zr_b"],
+                                             gb_zr, epi=EPI_GRU_ZR, pre=pre, pre_idx=pidx, pre_coff=0, h=net, zout=z,
+                                             rnet=rn)
+                droid_backends.conv_wino_f16([(rn, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["q_xw"], 128, P["q_b"],
+                                             gb_q, epi=EPI_GRU_Q, pre=pre, pre_idx=pidx, pre_coff=256, h=net, z=z,
+                                             out=net_new)
+            else:
+                droid_backends.conv_gru_pre_f16([(net, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["zr_x"], 256,
+                                                P["zr_b"], gb_zr, EPI_GRU_ZR, pre, pidx, 0, h=net, zout=z, rnet=rn)
+                droid_backends.conv_gru_pre_f16([(rn, 0, 128), (cf, 0, 128), (ff, 0, 64)], P["q_x"], 128,
+                                                P["q_b"], gb_q, EPI_GRU_Q, pre, pidx, 256, h=net, z=z, out=net_new)
         else:
             if inp is None:
                 inp = inp_frames[inverse]
@@ -322,13 +373,12 @@ class FusedUpdateModule(torch.nn.Module):
 
         if not agg:
             return net_new, delta, weight, None
-        a1 = e16(128)
-        conv([(net_new, 0, 128)], P["a1"], 128, 3, bias=P["a1_b"], act=1, out=a1)
+        a1 = conv3([(net_new, 0, 128)], "a1", 128, P["a1_b"], e16(128))
         if segments is None:
             segments = edge_segments(inverse, num_unique)
         agg = droid_backends.segment_mean_f16(a1, segments[0], segments[1], num_unique)
-        a2 = torch.empty((num_unique, H, W, 128), dtype=torch.float16, device=dev)
-        conv([(agg, 0, 128)], P["a2"], 128, 3, bias=P["a2_b"], act=1, out=a2)
+        a2 = conv3([(agg, 0, 128)], "a2", 128, P["a2_b"],
+                   torch.empty((num_unique, H, W, 128), dtype=torch.float16, device=dev))
         er = torch.empty((num_unique, H, W, 1), dtype=torch.float16, device=dev)
         conv([(a2, 0, 128)], P["eta"], 1, 3, bias=P["eta_b"], out=er)
         if raw_head:   # the caller applies 0.01 softplus with its damping update (droid_backends.eta_damping)

@@ -169,6 +169,22 @@ int droid_conv_gru_pre_f16(const void* const* srcs, const int* C, const int* cst
                            const void* pre, const long long* pre_idx, int pre_cstride, int pre_coff,
                            hipStream_t stream);
 
+/* The same 3x3 convs as Winograd F(2,3) along x (2/3 of the direct conv's
+ * multiplies; the reference runs them through cuDNN under autocast,
+ * droid_net.py:84-103, modules/gru.py:19-32).  wt = weights transformed by
+ * droid_mi355x.fused.pack_conv_wino ([6*chunks][4][Cout][32] fp16); epi 0 (act
+ * 0 / 1 -> out) or, with pre / pre_idx / pre_cstride / pre_coff as in
+ * droid_conv_gru_pre_f16, 1 (z|r gates) / 2 (GRU update).  Needs W == 64,
+ * H % 4 == 0, Cout % 128 == 0, else returns DROID_UNSUPPORTED so the caller
+ * runs the direct conv.  Measured slower than droid_conv_nhwc_f16 /
+ * droid_conv_gru_pre_f16 on MI355X (issue-bound; see conv_wino_kernel): the
+ * update operator uses it only when DROID_CONV_WINO=1. */
+int droid_conv_wino_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc, const void* wt,
+                        const float* bias, const float* bbias, int B, int H, int W, int Cout, int act, int epi,
+                        void* out, int out_cstride, int out_coff, const void* h, int h_cstride, const void* z,
+                        int z_cstride, void* zout, void* rnet, int gru_ch, const void* pre,
+                        const long long* pre_idx, int pre_cstride, int pre_coff, hipStream_t stream);
+
 /* UpdateModule delta/weight heads fused (droid_net.py:95-103, 132-133): conv3x3
  * srcs -> 256 (wp, bias, ReLU; the delta.0 || weight.0 hidden map) feeding the
  * block-diagonal conv3x3 256 -> 4 (hw [48][256] fp16, row = tap*4 + c, tap =

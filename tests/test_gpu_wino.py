@@ -1,0 +1,125 @@
+"""Winograd F(2,3) band conv (droid_conv_wino_f16, csrc/conv_kernels.hip:
+conv_wino_kernel) against the fp32 conv of the same fp16 operands (the
+reference runs these convs through cuDNN under autocast: droid_net.py:84-103,
+modules/gru.py:19-32) and against the direct band conv."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from gpu_util import host
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _ref(xs, w, bias=None, bb=None):
+    xin = torch.cat([x.float() for x in xs], -1).permute(0, 3, 1, 2)
+    y = F.conv2d(xin, w.half().float(), bias, padding=1)
+    if bb is not None:
+        y = y + bb[:, :, None, None]
+    return y.permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("B,H,splits,cout,act", [(3, 8, [128], 128, 1), (2, 4, [128, 96, 64], 256, 0),
+                                                  (1, 48, [128], 384, 0), (2, 12, [64, 8], 128, 1)])
+def test_wino_act_matches_fp32_conv(B, H, splits, cout, act):
+    """EPI_ACT (bias, optional ReLU) at W = 64: partial channel chunks (96, 8),
+    several sources, one-tile images (H = 4), several output tiles; the error
+    bound is the fp16 class (an fp16 ulp of each transformed operand + the fp16
+    output rounding) and within 3x of the direct conv's own error."""
+    import droid_backends
+    from droid_mi355x.fused import pack_conv, pack_conv_wino
+    W = 64
+    g = torch.Generator(device=DEV).manual_seed(31 + H)
+    xs = [torch.randn((B, H, W, c), generator=g, device=DEV).half() for c in splits]
+    cin = sum(splits)
+    w = torch.randn((cout, cin, 3, 3), generator=g, device=DEV) / (cin * 9) ** 0.5
+    bias = torch.randn(cout, generator=g, device=DEV)
+    srcs = [(x, 0, c) for x, c in zip(xs, splits)]
+    out = torch.full((B, H, W, cout), float("nan"), dtype=torch.float16, device=DEV)
+    droid_backends.conv_wino_f16(srcs, pack_conv_wino(w, splits), cout, bias=bias, act=act, out=out)
+    ref = _ref(xs, w, bias)
+    if act:
+        ref = torch.relu(ref)
+    err = (out.float() - ref).abs().max().item()
+    assert np.isfinite(err) and err < 6e-3, err
+    direct = torch.empty_like(out)
+    droid_backends.conv_nhwc_f16(srcs, pack_conv(w, splits), cout, 3, bias=bias, act=act, out=direct)
+    derr = (direct.float() - ref).abs().max().item()
+    assert err < 3 * derr + 1e-3, (err, derr)
+    # bias-free mean error: no systematic offset from the transform
+    assert abs((out.float() - ref).mean().item()) < 1e-4
+
+
+def test_wino_image_edges_and_zero_rows():
+    """x = -1 / x = 64 neighbours and the rows above / below each image are zero:
+    a delta input at every edge position reproduces the clipped kernel exactly."""
+    import droid_backends
+    from droid_mi355x.fused import pack_conv_wino
+    B, H, W, C = 2, 8, 64, 64
+    x = torch.zeros((B, H, W, C), dtype=torch.float16, device=DEV)
+    for (b, y, xx) in [(0, 0, 0), (0, 0, 63), (0, 7, 0), (1, 7, 63), (1, 3, 31), (1, 4, 32), (0, 3, 1), (1, 0, 62)]:
+        x[b, y, xx, 5] = 1.0
+    w = torch.zeros((128, C, 3, 3), device=DEV)
+    w[:, 5] = torch.arange(1, 10, device=DEV, dtype=torch.float32).view(3, 3) / 16   # exact in fp16
+    w[:, 5] *= torch.linspace(0.5, 1.0, 128, device=DEV).view(128, 1, 1)
+    out = torch.empty((B, H, W, 128), dtype=torch.float16, device=DEV)
+    droid_backends.conv_wino_f16([(x, 0, C)], pack_conv_wino(w, [C]), 128, act=0, out=out)
+    ref = _ref([x], w)
+    np.testing.assert_allclose(host(out.float()), host(ref), atol=2e-3, rtol=2e-3)
+    # nothing leaks across images or tile rows: pixels with no input in their 3x3 window are exactly 0
+    mask = F.max_pool2d(x[..., 5].float().unsqueeze(1), 3, 1, 1).squeeze(1) == 0
+    assert (out.float()[mask] == 0).all()
+
+
+@pytest.mark.parametrize("B,H", [(3, 8), (2, 48)])
+def test_wino_gru_pre_epilogues(B, H):
+    """z|r and q gates with the per-source-frame term (EPI_GRU_ZR / EPI_GRU_Q on
+    the Winograd tile) vs torch fp32 over the full 448-channel input, at the
+    bounds of the direct band kernel's own test (test_gpu_fused.py::test_conv_gru_pre_epilogues)."""
+    import droid_backends
+    from droid_backends import EPI_GRU_Q, EPI_GRU_ZR
+    from droid_mi355x.fused import pack_conv_wino
+    W = 64
+    g = torch.Generator(device=DEV).manual_seed(17)
+    mk = lambda n, c: torch.randn((n, H, W, c), generator=g, device=DEV).half()
+    F_ = 2
+    idx = torch.tensor([1, 0, 1, 0][:B], dtype=torch.int64, device=DEV)
+    inp_f = mk(F_, 128)
+    h = torch.tanh(mk(B, 128).float()).half()
+    cf, ff = mk(B, 128), mk(B, 64)
+    xs = [h, inp_f[idx].contiguous(), cf, ff]
+    wzr = torch.randn((256, 448, 3, 3), generator=g, device=DEV) / (448 * 9) ** 0.5
+    wq = torch.randn((128, 448, 3, 3), generator=g, device=DEV) / (448 * 9) ** 0.5
+    bzr, bq = torch.randn(256, generator=g, device=DEV), torch.randn(128, generator=g, device=DEV)
+    bbzr, bbq = torch.randn((B, 256), generator=g, device=DEV), torch.randn((B, 128), generator=g, device=DEV)
+    keep = lambda w: torch.cat([w[:, :128], w[:, 256:]], 1)
+    pre = torch.empty((F_, H, W, 384), dtype=torch.float16, device=DEV)
+    droid_backends.conv_wino_f16([(inp_f, 0, 128)], pack_conv_wino(torch.cat([wzr[:, 128:256], wq[:, 128:256]]),
+                                                                   [128]), 384, act=0, out=pre)
+    z = torch.empty((B, H, W, 128), dtype=torch.float16, device=DEV)
+    rn = torch.empty_like(z)
+    droid_backends.conv_wino_f16([(h, 0, 128), (cf, 0, 128), (ff, 0, 64)], pack_conv_wino(keep(wzr), [128, 128, 64]),
+                                 256, bzr, bbzr, epi=EPI_GRU_ZR, pre=pre, pre_idx=idx, pre_coff=0, h=h, zout=z,
+                                 rnet=rn)
+    gates = torch.sigmoid(_ref(xs, wzr, bzr, bbzr))
+    np.testing.assert_allclose(host(z.float()), host(gates[..., :128]), atol=3e-3)
+    np.testing.assert_allclose(host(rn.float()), host(gates[..., 128:] * h.float()), atol=3e-3)
+    hn = torch.empty_like(z)
+    droid_backends.conv_wino_f16([(rn, 0, 128), (cf, 0, 128), (ff, 0, 64)], pack_conv_wino(keep(wq), [128, 128, 64]),
+                                 128, bq, bbq, epi=EPI_GRU_Q, pre=pre, pre_idx=idx, pre_coff=256, h=h, z=z, out=hn)
+    q = torch.tanh(_ref([rn] + xs[1:], wq, bq, bbq))
+    ref = (1 - z.float()) * h.float() + z.float() * q
+    np.testing.assert_allclose(host(hn.float()), host(ref), atol=4e-3)
+
+
+def test_wino_rejects_unsupported_shape():
+    """W != 64 -> DROID_UNSUPPORTED raised (the caller runs the direct conv)."""
+    import droid_backends
+    from droid_mi355x.fused import pack_conv_wino
+    x = torch.zeros((1, 8, 32, 128), dtype=torch.float16, device=DEV)
+    out = torch.empty_like(x)
+    with pytest.raises(RuntimeError):
+        droid_backends.conv_wino_f16([(x, 0, 128)], pack_conv_wino(torch.zeros((128, 128, 3, 3), device=DEV), [128]),
+                                     128, act=1, out=out)
