@@ -1667,16 +1667,18 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
 // with the 16-B slot XOR-ed by kWinoG[(row & 15) >> 2] (conflict-free for the
 // ds_read_b128 lane groups of a 16-row fragment).
 // Global transformed weights: wt[stage][comp][Cout][32], stage = (chunk*2 + hk)*3 + ky.
-// Measured (C3, 2048 edges of 48x64, scripts/wino_bench.py): z|r 8.1-8.2 ms vs
-// 7.5-7.6 for the direct 256x256 band tile, q 4.35 vs 4.14, 128->128 1.78 vs
-// 1.65 - slower despite a third less MFMA work.  The loop is bound by the SIMD's
-// issue slots, not the MFMA pipe: a 16x16x32 MFMA holds 8 of its 16 issue
-// cycles and an LDS-DMA instruction costs ~60-185 (MI355X_MICROARCH.md), and
-// this tile moves the same 40 KB per stage for half the MFMAs (its tile, bound
-// by 4 accumulator sets in 128 VGPRs, is 256 x 128 against the direct tile's
-// 256 x 256 - twice the weight bytes per MFMA; 5 DMA instructions per 32
-// MFMAs vs 4.7 per 64).  Issuing the DMAs after the stage's first MFMAs, and
-// prefetching the weights two stages ahead instead of one, measured the same.
+// Measured (C3, 2048 edges of 48x64, scripts/wino_bench.py, profiles/r03/
+// wino_r03bg.txt): z|r 7.90 ms vs 7.41 for the direct 256x256 band tile, q 4.28
+// vs 4.12, 128->128 1.75 vs 1.64 - slower despite a third less MFMA work
+// (SQ_VALU_MFMA_BUSY 6.04e9 vs 9.06e9).  The loop is bound by the SIMD's issue
+// slots, not the MFMA pipe: SQ_ACTIVE_INST_ANY 3.02e9 vs 1.65e9 - per 32 MFMAs
+// a wave issues 20 ds_read_b128, 40 VALU (the transform) and 5 LDS-DMAs (~60-185
+// issue cycles each, MI355X_MICROARCH.md), against 24 reads, ~6 VALU and 4.7
+// DMAs per 64 MFMAs in the direct tile (its 256 x 128 tile, bound by 4
+// accumulator sets in 128 VGPRs, moves twice the weight bytes per MFMA).
+// Issuing the DMAs after the stage's first MFMAs, and prefetching the weights
+// two stages ahead instead of one, measured the same; the first build's slot
+// swizzle (a wrong kWinoG constant: 1.13e9 bank-conflict cycles) cost 0.3 ms.
 // Opt-in (DROID_CONV_WINO=1 in droid_mi355x.fused); parity: tests/test_gpu_wino.py.
 constexpr int kWinoTM = 256, kWinoTN = 128;
 constexpr int kWinoBand = 6 * 64 * 64;         // one band buffer: 6 rows x 64 px x 32 channels (bytes)
@@ -1685,7 +1687,7 @@ constexpr int kWinoNW = 3;                     // weight stage buffers (two stag
 constexpr int kWinoLds = 2 * kWinoBand + kWinoNW * kWinoWst;
 static_assert(kWinoLds <= kLdsMax, "wino LDS");
 
-__device__ __forceinline__ int wino_g(int q) { return (0x1E >> (2 * q)) & 3; }   // {0, 2, 3, 1}[q]
+__device__ __forceinline__ int wino_g(int q) { return (0x78 >> (2 * q)) & 3; }   // {0, 2, 3, 1}[q]
 
 typedef int int4v_t __attribute__((ext_vector_type(4)));
 // lane shift within each 16-lane row; lanes whose source leaves the row keep `old`
