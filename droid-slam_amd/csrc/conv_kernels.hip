@@ -971,15 +971,16 @@ template <int TMX, int TN, int NT, int EPI, bool EARLY, class Stage1>
 __device__ __forceinline__ void band_epilogue_core(const ConvArgs& a, _Float16* smem, long m0, int n0, int tid,
                                                    float bcol, long long* prof, Stage1 stage1);
 
-template <int TMX, int TN, int FM, int FN, int WM = 4, bool CONTIG = false, int NT = 512, int EPI = -1>
+template <int TMX, int TN, int FM, int FN, int WM = 4, bool CONTIG = false, int NT = 512, int EPI = -1,
+          bool EARLY = true, bool SWAP = kBandSwap<TN>>
 __device__ __forceinline__ void band_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
                                               int n0, int wm, int wn, int lane, int tid, float bcol,
                                               long long* prof = nullptr) {
   constexpr int ER = TN + 8;
   constexpr bool kPre = EPI == EPI_GRU_ZRP || EPI == EPI_GRU_QP;
   const int fr = lane & 15, fq = lane >> 4;
-  band_epilogue_core<TMX, TN, NT, EPI, true>(a, smem, m0, n0, tid, bcol, prof, [&](const float* bl, auto act) {
-  if constexpr (kBandSwap<TN>) {
+  band_epilogue_core<TMX, TN, NT, EPI, EARLY>(a, smem, m0, n0, tid, bcol, prof, [&](const float* bl, auto act) {
+  if constexpr (SWAP) {
     // (1) lane (fr, fq) of fragment (i, j) holds channels 16 j + 4 fq .. + 3 of
     // pixel row frag_row(i) + fr: one 8-B LDS write per fragment
 #pragma unroll
@@ -1057,7 +1058,7 @@ __device__ __forceinline__ void band_epilogue_core(const ConvArgs& a, _Float16* 
   const bool rhalf = epi == EPI_GRU_ZR && c >= a.gru_ch;
   // pass (2) in batches of RB rounds (the 4-wave tile has 32 rounds per thread:
   // all of them in flight would need 3 x 128 VGPRs)
-  constexpr int RB = RND > 16 ? 16 : RND;
+  constexpr int RB = RND > (NT >= 512 ? 16 : 8) ? (NT >= 512 ? 16 : 8) : RND;
   static_assert(RND % RB == 0, "band epilogue: whole batches");
   half8 hpre[kPreH ? RB : 1], zpre[EB == EPI_GRU_Q ? RB : 1], ppre[kPre ? RB : 1];
   // the per-frame term's pieces (pixel m of image b -> pixel of its source
@@ -1625,6 +1626,201 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
     }
   }
   if (st != kOk) return st;
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+// ---------------------------------------------------------------------------
+// Two-workgroups-per-CU band kernel (3x3, CHUNKED, W == 64): the direct conv
+// of conv_band_kernel on a 4-wave 256-pixel x 128-channel tile in 72 KB of
+// LDS, so two workgroups share a CU and one's epilogue, barriers and DMA
+// waits run under the other's MFMAs (with one 8-wave workgroup per CU the
+// SQ counters put 28 % of the z|r wave time in s_waitcnt / s_barrier and the
+// MFMA pipe idles through every tile's epilogue; profiles/r03/wino_r03bg.txt).
+// Wave (wm, wn): image rows 2 wm, 2 wm + 1 of the tile (8 pixel fragments of
+// 16, contiguous) x channels wn*64 .. +63, pixels x weights on MFMA (a lane's
+// accumulators are 4 pixels of one channel; swapped, the allocation spills, as
+// on the 256x256 band tile), 128 accumulators.
+// Stage = (32-channel half chunk, tap): one K-step, 32 MFMAs, 8 + 4
+// ds_read_b128 per wave.  LDS: the 6-row band of one half chunk (6 x 64 px x
+// 64 B = 24 KB, double buffered, issued 9 stages ahead) and the weights of one
+// stage (128 rows x 64 B = 8 KB, triple buffered, issued 2 stages ahead).
+// 64-B rows: 16-B slot kq of row r stored at kq ^ (2 * ((r >> 2) & 1)) - no
+// bank conflict for a 16-row ds_read_b128 fragment at any row offset, so the
+// taps' +-1 pixel shifts stay conflict-free (searched exhaustively over the
+// four ds_read_b128 lane groups).  Weights: the direct conv's packed layout
+// [Cout][chunks*9][64] (pack_conv), read half a stage row at a time.
+constexpr int kB2TM = 256, kB2TN = 128;
+constexpr int kB2Band = 6 * 64 * 64;     // one half-chunk band buffer (bytes)
+constexpr int kB2Wst = kB2TN * 64;       // one weight stage buffer (bytes)
+constexpr int kB2Lds = 2 * kB2Band + 3 * kB2Wst;
+static_assert(kB2Lds >= kB2TM * (kB2TN + 8) * 2 + kB2TN * 4, "band2: epilogue staging fits the loop's LDS");
+__device__ __forceinline__ int b2_slot(int r, int kq) { return kq ^ (((r >> 2) & 1) << 1); }
+// pixels x weights on MFMA; weights x pixels (DROID_B2_SWAP=1) measured the same
+#ifndef DROID_B2_SWAP
+#define DROID_B2_SWAP 0
+#endif
+constexpr bool kB2Swap = DROID_B2_SWAP != 0;
+
+template <int EPI>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_band2_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int HW = a.H * 64;
+  const long wgid = xcd_work_id(a.m_tiles * a.n_tiles);
+  const long mt = wgid / a.n_tiles;
+  const int nt = (int)(wgid - mt * a.n_tiles);
+  const long m0 = mt * kB2TM;
+  const int n0 = nt * kB2TN;
+  const int y0 = (int)((m0 % HW) >> 6);
+  const long band0 = m0 - 64;
+  char* Hl = lds;                     // [2][6 rows][64 px][64 B]
+  char* Bl = lds + 2 * kB2Band;       // [3][128 ch][64 B]
+  const unsigned Hl_a = lds_addr(Hl), Bl_a = lds_addr(Bl);
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  float bcol = 0.f;   // column tid's bias (+ per-image bias), loaded before any DMA
+  if (tid < kB2TN) {
+    const int co = n0 + tid;
+    if (a.bias) bcol = a.bias[co];
+    if (a.bbias) bcol += a.bbias[(long)(m0 / HW) * a.Cout + co];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // DMA lane geometry (band and weights): instruction block b fills LDS rows
+  // 16 b .. + 15; lane l writes row 16 b + (l >> 2), physical slot l & 3 =
+  // logical K piece (l & 3) ^ (2 * ((l >> 4) & 1))
+  const int lpiece = b2_slot(lane >> 2, lane & 3);
+  // band instruction q of wave w covers band row q, pixels 16 w + (l >> 2): the
+  // row's validity is wave-uniform
+  const int bpix = wave * 16 + (lane >> 2);
+  auto issue_band = [&](int bg) {
+    const int chunk = bg >> 1;
+    int s = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (q + 1 < a.nsrc && chunk >= a.chunk_end[q]) s = q + 1;
+    const int cstart = s ? a.chunk_end[s - 1] : 0;
+    const ConvSrc src = a.src[s];
+    const int c = (chunk - cstart) * BK + (bg & 1) * 32 + lpiece * 8;
+    const bool okc = c < src.C;
+    const rsrc_t rs = make_rsrc(src.ptr + band0 * src.cstride, 6 * 64 * src.cstride * 2);
+    const unsigned dst = Hl_a + (bg & 1) * kB2Band;
+    const unsigned off0 = okc ? (unsigned)((bpix * src.cstride + c) * 2) : kOob;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int y = y0 - 1 + q;
+      const unsigned off = (y >= 0 && y < a.H && okc) ? off0 + (unsigned)(q * 64 * src.cstride * 2) : kOob;
+      dma16(rs, dst + (wave_u + 4 * q) * 1024, off);
+    }
+  };
+  const int nst9 = a.nstage;   // chunks * 9 (the packed layout's stages)
+  const rsrc_t rsw = make_rsrc(a.wp + (long)n0 * nst9 * BK, kB2TN * nst9 * BK * 2);
+  unsigned woff[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) woff[q] = (unsigned)((((wave + 4 * q) * 16 + (lane >> 2)) * nst9 * BK + lpiece * 8) * 2);
+  // loop stage s = (half chunk bg = s / 9, tap t = s % 9): packed stage (bg >> 1) * 9 + t, K half bg & 1
+  auto issue_w = [&](int s, int buf) {
+    const int bg = s / 9, t = s - 9 * bg;
+    const unsigned sb = (unsigned)((((bg >> 1) * 9 + t) * BK + (bg & 1) * 32) * 2);
+    const unsigned dst = Bl_a + buf * kB2Wst;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) dma16(rsw, dst + (wave_u + 4 * q) * 1024, woff[q] + sb);
+  };
+
+  // fragment addresses: A fragment i = tile pixels 128 wm + 16 i + fr = image
+  // row 2 wm + (i >> 2), column x = 16 (i & 3) + fr; tap (ty, tx) reads band row
+  // 2 wm + (i >> 2) + ty + 1, column x + tx (a base past the LDS allocation,
+  // which reads as zeros, where x + tx leaves the image)
+  const int fr = lane & 15, kq = lane >> 4;
+  constexpr int kLdsZero = 0x100000;
+  // column x = 16 c4 + fr + tx: bit 2 of x (the slot swizzle) does not depend on
+  // c4, so a tap's base is one per-lane value plus c4 * 1024; only (c4 = 0, tx =
+  // -1, fr = 0) and (c4 = 3, tx = 1, fr = 15) leave the image
+  int abase[3];
+#pragma unroll
+  for (int tx = -1; tx <= 1; ++tx) abase[tx + 1] = (fr + tx) * 64 + (b2_slot(fr + tx + 16, kq) << 4);
+  const int aedge_l = fr == 0 ? kLdsZero : abase[0];
+  const int aedge_r = fr == 15 ? kLdsZero : abase[2] + 3 * 1024;
+  auto aoff = [&](int c4, int tx) {
+    return (c4 == 0 && tx < 0) ? aedge_l : (c4 == 3 && tx > 0) ? aedge_r : abase[tx + 1] + c4 * 1024;
+  };
+  const int bbase = (wn * 64 + fr) * 64 + (b2_slot(fr, kq) << 4);
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nb = 2 * a.cpt;
+  const int nst = 9 * nb;
+  issue_band(0);
+  issue_w(0, 0);
+  issue_w(1, 1);
+  int s = 0, wbuf = 0;
+  for (int bg = 0; bg < nb; ++bg) {
+    const char* Hb = Hl + (bg & 1) * kB2Band + wm * 2 * 4096;
+#pragma unroll
+    for (int t = 0; t < 9; ++t, ++s) {
+      const int ty = t / 3 - 1, tx = t % 3 - 1;
+      // this wave's DMAs issued after W(s): W(s+1) (2, one stage ago) and the
+      // bands issued at stages s-1 / s-2 (6 each, at the first stage of a group)
+      const int nafter = (s + 1 < nst ? 2 : 0) + ((t == 1 && bg + 1 < nb) ? 6 : 0) + ((t == 2 && bg + 1 < nb) ? 6 : 0);
+      wait_vmcnt(nafter);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (s + 2 < nst) issue_w(s + 2, wbuf == 0 ? 2 : wbuf - 1);
+      if (t == 0 && bg + 1 < nb) issue_band(bg + 1);
+      const char* Ab = Hb + (ty + 1) * 4096;
+      const char* Bb = Bl + wbuf * kB2Wst + bbase;
+      half8 af[8], bf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8*>(Bb + j * 1024);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const half8*>(Ab + aoff(i & 3, tx) + (i >> 2) * 4096);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = kB2Swap ? __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0)
+                              : __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      wbuf = wbuf == 2 ? 0 : wbuf + 1;
+    }
+  }
+  band_epilogue<kB2TM, kB2TN, 8, 4, 2, true, 256, EPI, false, kB2Swap>(a, acc, smem, m0, n0, wm, wn, lane, tid, bcol);
+}
+
+// Which convs take the two-workgroups-per-CU tile (C3, scripts/wino_bench.py,
+// profiles/r03/band2_r03bh.txt): the plain 128-channel-tile convs (EPI_ACT:
+// corr_encoder[2], GraphAgg conv1 / conv2, the per-frame gate term) 1.59 vs
+// 1.66 ms; the gate convs are slower on it (z|r 7.66 vs 7.41, q 4.12 = 4.12) and
+// stay on the 8-wave tiles.  DROID_CONV_BAND2=0 / 1: none / every shape it
+// takes (A/B runs).
+static bool band2_for(int epi) {
+  static const int mode = [] {
+    const char* e = getenv("DROID_CONV_BAND2");
+    return e ? atoi(e) : -1;
+  }();
+  return mode == 1 || (mode < 0 && epi == EPI_ACT);
+}
+
+template <int EPI>
+static int launch_band2_kernel(const ConvArgs& a0, hipStream_t stream) {
+  ConvArgs a = a0;
+  a.n_tiles = a.Cout / kB2TN;
+  a.m_tiles = (long)a.B * a.H * a.W / kB2TM;
+  const long nwg = a.m_tiles * a.n_tiles;
+  if (nwg > 0x7fffffffL) return fail(kUnsupported, "conv band2: problem too large");
+  static bool attr = false;
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band2_kernel<EPI>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
+    attr = true;
+  }
+  conv_band2_kernel<EPI><<<dim3((unsigned)nwg), 256, kB2Lds, stream>>>(a);
   DROID_LAUNCH_CHECK();
   return kOk;
 }
@@ -2348,6 +2544,13 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
     if (st != kOk) return st;
     DROID_LAUNCH_CHECK();
     return kOk;
+  }
+  // two-workgroups-per-CU tile: W == 64, 128-channel N tiles
+  if (band2_for(epi) && band_ok && W == 64 && H % 4 == 0 && Cout % kB2TN == 0 &&
+      (epi != EPI_GRU_ZR || gru_ch % kB2TN == 0)) {
+    if (epi == EPI_GRU_ZR) return pre ? launch_band2_kernel<EPI_GRU_ZRP>(a, stream) : launch_band2_kernel<EPI_GRU_ZR>(a, stream);
+    if (epi == EPI_GRU_Q) return pre ? launch_band2_kernel<EPI_GRU_QP>(a, stream) : launch_band2_kernel<EPI_GRU_Q>(a, stream);
+    return launch_band2_kernel<EPI_ACT>(a, stream);
   }
   if (pre) {  // the per-source term exists on the band tiles only
     if (band_ok && epi == EPI_GRU_ZR && Cout == 256 && 256 % W == 0 && (H * W) % 256 == 0 && band_nw4() &&
