@@ -1793,18 +1793,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   band_epilogue<kB2TM, kB2TN, 8, 4, 2, true, 256, EPI, false, kB2Swap>(a, acc, smem, m0, n0, wm, wn, lane, tid, bcol);
 }
 
-// Which convs take the two-workgroups-per-CU tile (C3, scripts/wino_bench.py,
-// profiles/r03/band2_r03bh.txt): the plain 128-channel-tile convs (EPI_ACT:
-// corr_encoder[2], GraphAgg conv1 / conv2, the per-frame gate term) 1.59 vs
-// 1.66 ms; the gate convs are slower on it (z|r 7.66 vs 7.41, q 4.12 = 4.12) and
-// stay on the 8-wave tiles.  DROID_CONV_BAND2=0 / 1: none / every shape it
-// takes (A/B runs).
-static bool band2_for(int epi) {
+// Which convs take the two-workgroups-per-CU tile (profiles/r03/band2_r03bh.txt,
+// band2_c2_r03bl.txt): the plain 128-channel-tile convs (EPI_ACT:
+// corr_encoder[2], GraphAgg conv1 / conv2, the per-frame gate term) always
+// (C3: 1.59 vs 1.66 ms); the gate convs only on small grids - at C3 they are
+// slower on it (z|r 7.66 vs 7.41 ms, q 4.12 = 4.12), but on the frontend window
+// (C2, 96 edges: 1152 z|r tiles = 4.5 rounds of the 8-wave tile over 256 CUs)
+// its finer tiles fill the last round: update() 1.252 vs 1.308 ms.
+// DROID_CONV_BAND2=0 / 1: none / every shape it takes (A/B runs).
+static bool band2_for(int epi, long px) {
   static const int mode = [] {
     const char* e = getenv("DROID_CONV_BAND2");
     return e ? atoi(e) : -1;
   }();
-  return mode == 1 || (mode < 0 && epi == EPI_ACT);
+  return mode == 1 || (mode < 0 && (epi == EPI_ACT || px / 256 <= 8L * device_cu_count()));
 }
 
 template <int EPI>
@@ -2546,7 +2548,7 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
     return kOk;
   }
   // two-workgroups-per-CU tile: W == 64, 128-channel N tiles
-  if (band2_for(epi) && band_ok && W == 64 && H % 4 == 0 && Cout % kB2TN == 0 &&
+  if (band2_for(epi, (long)B * H * W) && band_ok && W == 64 && H % 4 == 0 && Cout % kB2TN == 0 &&
       (epi != EPI_GRU_ZR || gru_ch % kB2TN == 0)) {
     if (epi == EPI_GRU_ZR) return pre ? launch_band2_kernel<EPI_GRU_ZRP>(a, stream) : launch_band2_kernel<EPI_GRU_ZR>(a, stream);
     if (epi == EPI_GRU_Q) return pre ? launch_band2_kernel<EPI_GRU_QP>(a, stream) : launch_band2_kernel<EPI_GRU_Q>(a, stream);
