@@ -542,6 +542,19 @@ __device__ __forceinline__ void ce_dma4(rsrc_t rs, unsigned lds, unsigned voff) 
 // FAST: every level's rows are 16-B aligned (W2 % 8 == 0) - the gather is
 // branch-free buffer loads only, which keeps the compiler's vmcnt accounting
 // exact across the loop (a CFG join with the generic path makes it wait for 0)
+#ifndef DROID_CE0_ABLATE_TA
+#define DROID_CE0_ABLATE_TA 0
+#endif
+// Cooperative gather (FAST path): lane (pixel pp = lane >> 3, window row j =
+// lane & 7) loads one window row of eight pixels per instruction instead of
+// one pixel's row per lane: an instruction then touches ~16 128-B lines
+// instead of 64 - the texture-address path was full for ~53 % of the kernel's
+// cycles (SQ_VMEM_TA_ADDR_FIFO_FULL, profiles/r03/pmc_sq_r03bj.txt); the row
+// below comes from the next lane by one DPP shift.  DROID_CE0_COOP=0: one
+// pixel per lane (A/B builds).  Outputs are bitwise the same.
+#ifndef DROID_CE0_COOP
+#define DROID_CE0_COOP 1
+#endif
 template <bool FAST>
 __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
   extern __shared__ __attribute__((aligned(16))) _Float16 smem_ce[];
@@ -628,7 +641,11 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
                                     (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)pa);
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           reinterpret_cast<void*>(pu), (short)0, __builtin_amdgcn_readfirstlane((int)(kCeTP * slice * 2)), 0x00020000);
+#if DROID_CE0_ABLATE_TA   // timing ablation only (results invalid): 8 lanes share one pixel's slice
+      const unsigned pbase = (unsigned)((px & ~7) * slice) * 2u;
+#else
       const unsigned pbase = (unsigned)(px * slice) * 2u;
+#endif
       const bool ok0 = valid && c0 >= 0 && c0 < nch, ok1 = valid && c0 + 1 >= 0 && c0 + 1 < nch;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -689,6 +706,95 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
     }
   };
 
+  // ---- cooperative gather (FAST, DROID_CE0_COOP): lane = (pixel pp, row jr);
+  // pixel group g of the wave's 64 = pixel 64 half + 8 g + pp.  The per-pixel
+  // window state of an in-flight tile is not held in registers (8 pixels per
+  // lane): the pixel's coordinates are parked in columns 224..231 of its As row
+  // (never read by the K <= 224 MFMA; float2 per slot) and the state is
+  // recomputed at the bilinear step.
+  constexpr bool kCoop = FAST && DROID_CE0_COOP;
+  const int pp = lane >> 3, jr = lane & 7;
+  // cg: this wave's staged coordinates of tile t (64 px, LDS), read one pixel
+  // group at a time
+  auto issue_co = [&](const int sl, long t, const float2* cg) __attribute__((always_inline)) {
+    const bool valid = t < a.ntiles;
+    const long tp0 = valid ? vol_row(t) * (long)HW + (t % tpe) * kCeTP : 0;
+    const unsigned long long pa = (unsigned long long)(vol + tp0 * slice);
+    const unsigned long long pu = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(pa >> 32)) << 32) |
+                                  (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)pa);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(pu), (short)0, __builtin_amdgcn_readfirstlane((int)(kCeTP * slice * 2)), 0x00020000);
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const float2 cc = cg[8 * g + pp];
+      const float x0 = cc.x * scl, y0 = cc.y * scl;
+      const int xi0 = (int)floorf(x0), yi0 = (int)floorf(y0);
+      const int xs = xi0 - 3;
+      const int c0 = (xs >= 0) ? (xs >> 3) : -((-xs + 7) >> 3);
+      const unsigned pbase = (unsigned)((half * 64 + 8 * g + pp) * slice) * 2u;
+      const bool ok0 = valid && c0 >= 0 && c0 < nch, ok1 = valid && c0 + 1 >= 0 && c0 + 1 < nch;
+      const int y1 = yi0 - 3 + jr;
+      const bool yok = y1 >= 0 && y1 < H2;
+      const int re = tiled ? (y1 >> 3) * nch * 64 + (y1 & 7) * 8 : y1 * W2;
+      const int cs = tiled ? 64 : 8;
+      const unsigned o0 = (yok && ok0) ? pbase + (unsigned)(re + cs * c0) * 2u : kCeOob;
+      const unsigned o1 = (yok && ok1) ? pbase + (unsigned)(re + cs * (c0 + 1)) * 2u : kCeOob;
+      raw[sl][g][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o0, 0, 0));
+      raw[sl][g][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, 0));
+    }
+  };
+  // bilinear windows of slot sl's tile -> As: lane (pp, jr) forms output row jr
+  // (jr < 7) of pixel group g from its row (jr) and the next lane's (jr + 1),
+  // the same products and sums, in the same order, as the per-pixel path
+  auto bilinear_co = [&](const int sl) __attribute__((always_inline)) {
+#pragma clang fp contract(off)
+    const h2_t Z = {(_Float16)0.f, (_Float16)0.f};
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const int pxg = half * 64 + 8 * g + pp;
+      const float2 c = *reinterpret_cast<const float2*>(&As[pxg * kCeKS + 224 + 4 * sl]);
+      const float x0 = c.x * scl, y0 = c.y * scl;
+      const float fx0 = floorf(x0), fy0 = floorf(y0);
+      const float dx = x0 - fx0, dy = y0 - fy0;
+      const int xs = (int)fx0 - 3;
+      const int c0 = (xs >= 0) ? (xs >> 3) : -((-xs + 7) >> 3);
+      const int wo = xs - 8 * c0;
+      const _Float16 h11 = (_Float16)rnd16(dx * dy);
+      const _Float16 h10 = (_Float16)rnd16(dx * (1.0f - dy));
+      const _Float16 h01 = (_Float16)rnd16((1.0f - dx) * dy);
+      const _Float16 h00 = (_Float16)rnd16((1.0f - dx) * (1.0f - dy));
+      const h2_t W00 = {h00, h00}, W01 = {h01, h01}, W10 = {h10, h10}, W11 = {h11, h11};
+      // this row's tap pairs (dword m + wo/2 of the two pieces, funnel-shifted)
+      const uint4 p0 = raw[sl][g][0], p1 = raw[sl][g][1];
+      const int k = wo >> 1;
+      const bool k2 = k & 2, k1 = k & 1;
+      const unsigned v0 = k2 ? p0.z : p0.x, v1 = k2 ? p0.w : p0.y, v2 = k2 ? p1.x : p0.z;
+      const unsigned v3 = k2 ? p1.y : p0.w, v4 = k2 ? p1.z : p1.x, v5 = k2 ? p1.w : p1.y;
+      const unsigned w[5] = {k1 ? v1 : v0, k1 ? v2 : v1, k1 ? v3 : v2, k1 ? v4 : v3, k1 ? v5 : v4};
+      const unsigned sh = (wo & 1) ? 16u : 0u;
+      unsigned o[4], q[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) o[m] = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) q[m] = __builtin_amdgcn_alignbit(m < 3 ? o[m + 1] : 0u, o[m], 16);
+      _Float16* arow = As + pxg * kCeKS + lvl * 49;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        // the row below: the next lane's pairs (row_shl:1; lane jr = 7 outputs nothing)
+        const unsigned oc = (unsigned)__builtin_amdgcn_update_dpp(0, (int)o[m], 0x101, 0xF, 0xF, false);
+        const unsigned qc = (unsigned)__builtin_amdgcn_update_dpp(0, (int)q[m], 0x101, 0xF, 0xF, false);
+        h2_t acc = Z + __builtin_bit_cast(h2_t, o[m]) * W00;
+        acc = acc + __builtin_bit_cast(h2_t, oc) * W01;
+        acc = acc + __builtin_bit_cast(h2_t, q[m]) * W10;
+        acc = acc + __builtin_bit_cast(h2_t, qc) * W11;
+        if (jr < 7) {
+          arow[(2 * m) * 7 + jr] = acc.x;
+          if (m < 3) arow[(2 * m + 1) * 7 + jr] = acc.y;
+        }
+      }
+    }
+  };
+
   // GEMM geometry: waves 4 (32 px) x 2 (64 co)
   const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fq = lane >> 4;
   float bias[4];
@@ -698,6 +804,9 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
   // one tile: windows of slot sl -> As, then (with the tile two steps ahead
   // issued into the same slot) the 1x1 conv on MFMA and the coalesced store
   auto process = [&](const int sl, long t) __attribute__((always_inline)) {
+   if constexpr (kCoop) {
+    bilinear_co(sl);
+   } else {
     // (1) bilinear windows of tile t -> As (corr_pyramid_f16_r3_kernel arithmetic)
     //     on packed fp16 pairs of x offsets (q, q+1).  The reference rounds every
     //     product and sum of two halves to half through float (at::Half ops);
@@ -735,12 +844,24 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
         }
       }
     }
+   }
     // (2) the tile two steps ahead goes into this slot while this one is multiplied
     // and stored; its coordinates were staged before the rows just consumed.
     const float2 c2 = Cs[sl * 512 + wave * 64 + lane];  // staged with the rows just consumed
-    stage_coords(sl, t + 4L * gridDim.x);
-    issue(sl, t + 2L * gridDim.x, c2.x, c2.y);
+    if constexpr (kCoop) {
+      // the rows first, then the coordinates' DMA over the staging slot they
+      // were read from (ce_dma4 waits for this wave's LDS reads; the rows'
+      // vmcnt wait at the bilinear step covers the later DMA: in-order retirement)
+      issue_co(sl, t + 2L * gridDim.x, Cs + sl * 512 + wave * 64);
+      stage_coords(sl, t + 4L * gridDim.x);
+    } else {
+      stage_coords(sl, t + 4L * gridDim.x);
+      issue(sl, t + 2L * gridDim.x, c2.x, c2.y);
+    }
     __syncthreads();
+    // coop: park the coordinates of the tile just issued (read by its bilinear
+    // step two steps on; every wave of this one's bilinear step is past the barrier)
+    if (kCoop && lvl == 0) *reinterpret_cast<float2*>(&As[(half * 64 + lane) * kCeKS + 224 + 4 * sl]) = c2;
     // (3) 128 px x 128 co x 224 on MFMA
     floatx4_t acc[2][4];
 #pragma unroll
@@ -781,7 +902,27 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
 
   const long g = gridDim.x;
   long t = blockIdx.x;
-  {
+  if constexpr (kCoop) {
+    // the first two tiles' coordinates straight from memory: eight pixels per
+    // lane for the gather, the lane's own pixel for the As parking slot
+    // (the gather reads 64 coordinates per wave straight from memory here; a
+    // tile past the last one reads tile 0's, which are finite, and loads nothing)
+    const float2* cg0 = reinterpret_cast<const float2*>(a.coords) + ((t < a.ntiles ? t : 0) / tpe) * (long)HW +
+                        ((t < a.ntiles ? t : 0) % tpe) * kCeTP + half * 64;
+    const float2* cg1 = reinterpret_cast<const float2*>(a.coords) + ((t + g < a.ntiles ? t + g : 0) / tpe) * (long)HW +
+                        ((t + g < a.ntiles ? t + g : 0) % tpe) * kCeTP + half * 64;
+    float cx0 = 0.f, cy0 = 0.f, cx1 = 0.f, cy1 = 0.f;
+    load_coords(t, cx0, cy0);
+    load_coords(t + g, cx1, cy1);
+    if (lvl == 0) {
+      *reinterpret_cast<float2*>(&As[px * kCeKS + 224]) = make_float2(cx0, cy0);
+      *reinterpret_cast<float2*>(&As[px * kCeKS + 228]) = make_float2(cx1, cy1);
+    }
+    stage_coords(0, t + 2 * g);
+    issue_co(0, t, cg0);
+    stage_coords(1, t + 3 * g);
+    issue_co(1, t + g, cg1);
+  } else {
     float cx0 = 0.f, cy0 = 0.f, cx1 = 0.f, cy1 = 0.f;
     load_coords(t, cx0, cy0);
     load_coords(t + g, cx1, cy1);
