@@ -28,9 +28,10 @@ def per_kernel(counter):
             continue
         name = r["Kernel_Name"]
         key = ("copy" if name.startswith("__amd_rocclr_copyBuffer") and len(out.get("copy", [])) < 3 else
-               "zr" if "conv_band_kernel<256, 256, false, false, 6>" in name else
+               "zr" if ("conv_band_kernel<256, 256, false, false, 6>" in name or
+                        "conv_band_kernel<256, 256, false, false, 6, 8>" in name) else
                "lookup" if ("corr_ce0_kernel" in name or "corr_pyramid_f16_r3_kernel" in name) else
-               "alt" if "corr_alt_ce0_kernel" in name else None)
+               "alt" if ("corr_alt_ce0_kernel" in name or "corr_alt2_kernel" in name) else None)
         if key:
             out.setdefault(key, []).append(float(r["Counter_Value"]))
             KNAME[key] = name
