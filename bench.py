@@ -43,8 +43,8 @@ ZR_FLOPS_PER_PIXEL = 2 * 256 * 448 * 9
 # the per-edge z|r conv runs over net | corr | flow = 320 channels
 ZR_PRE_FLOPS_PER_PIXEL = 2 * 256 * 320 * 9
 ZR_KERNEL = "conv_band_kernel<256,256>"   # csrc/conv_kernels.hip, chosen for 48x64 maps
-ZR_KERNEL_MATCH = "conv_band_kernel<256, 256, false, false, 1>"   # its symbol in rocprof / PMC summaries
-ZRP_KERNEL_MATCH = "conv_band_kernel<256, 256, false, false, 6>"  # ... the factored-gate instantiation
+ZR_KERNEL_MATCH = "conv_band_kernel<256, 256, false, false, 1"   # its symbol in rocprof / PMC summaries
+ZRP_KERNEL_MATCH = "conv_band_kernel<256, 256, false, false, 6"  # ... the factored-gate instantiation
 LOOKUP_KERNEL = "corr_pyramid_f16_r3_kernel"
 # SURVEY.md §8d whole-iteration floors.  Update-operator convs per edge-pixel:
 # corr_encoder 1x1 196->128 + 3x3 128->128, flow_encoder 7x7 4->128 + 3x3 128->64,
