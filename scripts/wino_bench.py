@@ -42,7 +42,15 @@ cases = {
     "128 direct": lambda: droid_backends.conv_nhwc_f16([(net, 0, 128)], P["a"], 128, 3, bias=b1, act=1, out=o1),
     "128 wino": lambda: droid_backends.conv_wino_f16([(net, 0, 128)], P["aw"], 128, bias=b1, act=1, out=o1),
 }
-flops = {"zr": 2.0 * E * H * W * 256 * 320 * 9, "q": 2.0 * E * H * W * 128 * 320 * 9,
+from droid_mi355x.fused import pack_head_taps  # noqa: E402
+wdw = torch.randn((256, 128, 3, 3), generator=g, device=dev) * 0.02
+P["dw"] = pack_conv(wdw, [128])
+hwt = pack_head_taps(torch.randn((4, 256, 3, 3), generator=g, device=dev) * 0.02)
+bdw = torch.zeros(256, device=dev)
+head = torch.zeros((E, H, W, 4), device=dev)
+cases["dwhead direct"] = lambda: droid_backends.conv_dw_head_f16([(net, 0, 128)], P["dw"], bdw, hwt, head)
+flops = {"dwhead": 2.0 * E * H * W * 256 * 128 * 9,
+         "zr": 2.0 * E * H * W * 256 * 320 * 9, "q": 2.0 * E * H * W * 128 * 320 * 9,
          "128": 2.0 * E * H * W * 128 * 128 * 9}
 only = sys.argv[2] if len(sys.argv) > 2 else None
 for name, fn in cases.items():
