@@ -48,8 +48,12 @@ P["dw"] = pack_conv(wdw, [128])
 hwt = pack_head_taps(torch.randn((4, 256, 3, 3), generator=g, device=dev) * 0.02)
 bdw = torch.zeros(256, device=dev)
 head = torch.zeros((E, H, W, 4), device=dev)
+w64 = torch.randn((64, 128, 3, 3), generator=g, device=dev) * 0.02
+P["w64"] = pack_conv(w64, [128])
+o64, b64 = t(64), torch.zeros(64, device=dev)
+cases["64 direct"] = lambda: droid_backends.conv_nhwc_f16([(net, 0, 128)], P["w64"], 64, 3, bias=b64, act=1, out=o64)
 cases["dwhead direct"] = lambda: droid_backends.conv_dw_head_f16([(net, 0, 128)], P["dw"], bdw, hwt, head)
-flops = {"dwhead": 2.0 * E * H * W * 256 * 128 * 9,
+flops = {"dwhead": 2.0 * E * H * W * 256 * 128 * 9, "64": 2.0 * E * H * W * 64 * 128 * 9,
          "zr": 2.0 * E * H * W * 256 * 320 * 9, "q": 2.0 * E * H * W * 128 * 320 * 9,
          "128": 2.0 * E * H * W * 128 * 128 * 9}
 only = sys.argv[2] if len(sys.argv) > 2 else None

@@ -127,3 +127,24 @@ def test_wino_rejects_unsupported_shape():
     with pytest.raises(RuntimeError):
         droid_backends.conv_wino_f16([(x, 0, 128)], pack_conv_wino(torch.zeros((128, 128, 3, 3), device=DEV), [128]),
                                      128, act=1, out=out)
+
+
+@pytest.mark.parametrize("B,H,splits", [(3, 8, [128]), (2, 12, [96, 64])])
+def test_conv64_matches_fp32_conv(B, H, splits):
+    """flow_encoder[2]'s shape (64 output channels, the 384x64 band tile at W = 64)
+    vs the fp32 conv of the same fp16 operands: the fp16 output rounding is its
+    only error.  (A 64-channel two-workgroups-per-CU tile measured 1.116 vs
+    1.104 ms at C3 and was left out.)"""
+    import droid_backends
+    from droid_mi355x.fused import pack_conv
+    W, cout = 64, 64
+    g = torch.Generator(device=DEV).manual_seed(5 + H)
+    xs = [torch.randn((B, H, W, c), generator=g, device=DEV).half() for c in splits]
+    cin = sum(splits)
+    w = torch.randn((cout, cin, 3, 3), generator=g, device=DEV) / (cin * 9) ** 0.5
+    bias = torch.randn(cout, generator=g, device=DEV)
+    out = torch.full((B, H, W, cout), float("nan"), dtype=torch.float16, device=DEV)
+    droid_backends.conv_nhwc_f16([(x, 0, c) for x, c in zip(xs, splits)], pack_conv(w, splits), cout, 3, bias=bias,
+                                 act=1, out=out)
+    ref = torch.relu(_ref(xs, w, bias))
+    np.testing.assert_allclose(host(out.float()), host(ref), atol=4e-3, rtol=1e-3)
