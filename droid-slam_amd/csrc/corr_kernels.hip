@@ -573,8 +573,11 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
     if (q < 28) v = *reinterpret_cast<const uint4*>(a.w + r * 224 + q * 8);
     *reinterpret_cast<uint4*>(&Ws[r * kCeKS + q * 8]) = v;
   }
-  for (int idx = tid; idx < kCeTP * 36; idx += 512) {
-    const int r = idx / 36, c = idx - r * 36;
+  // the K padding 196..223 the MFMA reads; columns 224..231 (never read by it)
+  // are the cooperative gather's coordinate parking slots, written below
+  // without a barrier in between - zeroing them here would race with those writes
+  for (int idx = tid; idx < kCeTP * 28; idx += 512) {
+    const int r = idx / 28, c = idx - r * 28;
     As[r * kCeKS + 196 + c] = (_Float16)0.f;
   }
 
