@@ -148,3 +148,34 @@ def test_conv64_matches_fp32_conv(B, H, splits):
                                  act=1, out=out)
     ref = torch.relu(_ref(xs, w, bias))
     np.testing.assert_allclose(host(out.float()), host(ref), atol=4e-3, rtol=1e-3)
+
+
+def test_corr_lookup_ce0_cooperative_gather_deterministic():
+    """The fused lookup's cooperative gather (csrc/corr_kernels.hip, DROID_CE0_COOP)
+    parks each pixel's coordinates in LDS between its issue and bilinear steps:
+    at E = 300 edges of 48x64 (4,608 tiles, each CU walking ~18 of them through
+    both in-flight slots) three launches are bitwise equal and equal to the
+    bit-exact oracle-pinned lookup followed by the 1x1 conv in fp32."""
+    import droid_backends
+    from droid_mi355x.corr import CorrBlock
+    E, H, W = 300, 48, 64
+    rng = np.random.default_rng(31)
+    f1 = torch.from_numpy(rng.normal(size=(1, E, 128, H, W)).astype(np.float16)).to(DEV)
+    f2 = torch.from_numpy(rng.normal(size=(1, E, 128, H, W)).astype(np.float16)).to(DEV)
+    cbt = CorrBlock(f1, f2, tiled=True)
+    coords = (np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None, None]
+              + rng.normal(0, 6, (1, E, H, W, 2))).astype(np.float32)
+    c = torch.from_numpy(coords).to(DEV).view(E, H, W, 2).contiguous()
+    g = torch.Generator(device=DEV).manual_seed(32)
+    w224 = torch.zeros((128, 224), device=DEV)
+    w224[:, :196] = torch.randn((128, 196), generator=g, device=DEV) / 14.0
+    w224 = w224.half().contiguous()
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    with torch.no_grad():
+        outs = [droid_backends.corr_lookup_ce0(cbt.corr_pyramid, c, w224, b, tiled_shapes=cbt.level_shapes)
+                for _ in range(3)]
+        for o in outs[1:]:
+            assert torch.equal(o, outs[0])
+        look = cbt(c.view(1, E, H, W, 2))[0].permute(0, 2, 3, 1).float()   # (E,H,W,196), bit-exact lookup
+        ref = torch.relu(look @ w224[:, :196].float().t() + b)
+    np.testing.assert_allclose(host(outs[0].float()), host(ref), atol=2e-3, rtol=2e-3)
