@@ -382,6 +382,26 @@ def conv_wino_f16(sources, wt, cout, bias=None, bbias=None, act=0, epi=EPI_ACT, 
     return out
 
 
+def transpose_f16(src, R, C, ldd=None, out=None):
+    """dst[b][c][r] = src[b][r][c] (r < R), zero for R <= r < ldd
+    (include/droid_backends.h: droid_transpose_f16): src viewed as (B, R, C) fp16
+    contiguous -> out (B, C, ldd) fp16."""
+    _check_inputs(("src",), (src,))
+    _need(src, torch.float16, "src")
+    ldd = R if ldd is None else int(ldd)
+    if R * C == 0 or src.numel() % (R * C):
+        raise RuntimeError("transpose_f16: src is not a whole number of (R, C) blocks")
+    B = src.numel() // (R * C)
+    if out is None:
+        out = torch.empty((B, C, ldd), dtype=torch.float16, device=src.device)
+    elif out.dtype != torch.float16 or not out.is_contiguous() or out.numel() != B * C * ldd:
+        raise RuntimeError("transpose_f16: out must be a contiguous fp16 tensor of B*C*ldd elements")
+    with torch.cuda.device(src.device):
+        check(lib.droid_transpose_f16(_ptr(src), _ptr(out), int(B), int(R), int(C), int(ldd), _stream(src)),
+              "transpose_f16")
+    return out
+
+
 def dw_head_supported(H, W):
     """Shapes droid_conv_dw_head_f16 accepts (the band tile: W in {16,32,64}, H*W % 256 == 0)."""
     return W in (16, 32, 64) and (H * W) % 256 == 0

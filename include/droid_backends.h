@@ -185,6 +185,13 @@ int droid_conv_wino_f16(const void* const* srcs, const int* C, const int* cstrid
                         int z_cstride, void* zout, void* rnet, int gru_ch, const void* pre,
                         const long long* pre_idx, int pre_cstride, int pre_coff, hipStream_t stream);
 
+/* Batched fp16 transpose (the reference-layout drop-in's NCHW <-> NHWC state
+ * conversions, droid_net.py:111-143 hands the operator NCHW tensors):
+ * dst[b][c][r] = src[b][r][c] for r < R, 0 for R <= r < ldd; src (B,R,C) and
+ * dst (B,C,ldd) fp16 contiguous.  NCHW -> NHWC: R = channels, C = H*W (ldd > R
+ * zero-pads the channels); NHWC -> NCHW: R = H*W, C = channels. */
+int droid_transpose_f16(const void* src, void* dst, int B, int R, int C, int ldd, hipStream_t stream);
+
 /* UpdateModule delta/weight heads fused (droid_net.py:95-103, 132-133): conv3x3
  * srcs -> 256 (wp, bias, ReLU; the delta.0 || weight.0 hidden map) feeding the
  * block-diagonal conv3x3 256 -> 4 (hw [48][256] fp16, row = tap*4 + c, tap =

@@ -179,3 +179,19 @@ def test_corr_lookup_ce0_cooperative_gather_deterministic():
         look = cbt(c.view(1, E, H, W, 2))[0].permute(0, 2, 3, 1).float()   # (E,H,W,196), bit-exact lookup
         ref = torch.relu(look @ w224[:, :196].float().t() + b)
     np.testing.assert_allclose(host(outs[0].float()), host(ref), atol=2e-3, rtol=2e-3)
+
+
+@pytest.mark.parametrize("B,R,C,ldd", [(3, 196, 3072, 200), (2, 128, 3072, None), (2, 3072, 576, None),
+                                       (1, 5, 7, 9), (4, 70, 130, 72)])
+def test_transpose_f16(B, R, C, ldd):
+    """droid_transpose_f16 (the reference-layout drop-in's NCHW <-> NHWC copies):
+    bitwise the torch transpose, channels past R zero-padded up to ldd, ragged
+    tile edges included."""
+    import droid_backends
+    g = torch.Generator(device=DEV).manual_seed(R + C)
+    src = torch.randn((B, R, C), generator=g, device=DEV).half()
+    out = droid_backends.transpose_f16(src, R, C, ldd)
+    L = ldd or R
+    ref = torch.zeros((B, C, L), dtype=torch.float16, device=DEV)
+    ref[..., :R] = src.transpose(1, 2)
+    assert torch.equal(out, ref)
