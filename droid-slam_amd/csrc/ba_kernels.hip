@@ -1455,24 +1455,25 @@ int droid_ba_build_system(void* plan, void* workspace, float* poses, float* disp
   return kOk;
 }
 
-static int solve_update(void* plan, void* workspace, float* poses, float* disps, const float* intrinsics,
-                        const float* disps_sens, const float* targets, const float* weights, const float* eta,
-                        float lm, float ep, float* dx, float* dz, int first_solve, hipStream_t stream) {
-  auto* p = static_cast<BaPlan*>(plan);
-  int st = check_ready(p, workspace);
-  if (st) return st;
+// damping + Cholesky + forward/back solve of the reduced system -> dx
+static int solve_system(BaPlan* p, void* workspace, float lm, float ep, float* dx, int first_solve,
+                        hipStream_t stream) {
   BaDev d = make_dev(*p, static_cast<char*>(workspace));
-  d.poses = poses; d.disps = disps; d.intr = intrinsics; d.disps_sens = disps_sens;
-  d.targets = targets; d.weights = weights; d.eta = eta; d.dx = dx; d.dz = dz;
-  d.lm = lm; d.ep = ep;
   const int n = p->n;
   ba_damp_kernel<<<ceil_div(std::max(n, 1), 256), 256, 0, stream>>>(d.M, d.slot, d.nbc, n, lm, ep, d.flag,
                                                                      first_solve);
   DROID_LAUNCH_CHECK();
-  if (n > 0) {
-    st = launch_chol_dataflow(*p, static_cast<char*>(workspace), dx, stream);
-    if (st) return st;
-  }
+  if (n > 0) return launch_chol_dataflow(*p, static_cast<char*>(workspace), dx, stream);
+  return kOk;
+}
+
+// back-substitution of dz + retraction (both skip on flag bit 1)
+static int apply_update(BaPlan* p, void* workspace, float* poses, float* disps, const float* intrinsics,
+                        const float* disps_sens, const float* targets, const float* weights, const float* eta,
+                        float* dx, float* dz, hipStream_t stream) {
+  BaDev d = make_dev(*p, static_cast<char*>(workspace));
+  d.poses = poses; d.disps = disps; d.intr = intrinsics; d.disps_sens = disps_sens;
+  d.targets = targets; d.weights = weights; d.eta = eta; d.dx = dx; d.dz = dz;
   if (!p->motion_only && p->K > 0) {
     if (!dz) return fail(kInvalidArgument, "ba: dz output required unless motion_only");
     ba_backsub_kernel<<<dim3(ceil_div(p->HW, 256), p->K), 256, 0, stream>>>(d);
@@ -1483,6 +1484,38 @@ static int solve_update(void* plan, void* workspace, float* poses, float* disps,
     DROID_LAUNCH_CHECK();
   }
   return kOk;
+}
+
+static int solve_update(void* plan, void* workspace, float* poses, float* disps, const float* intrinsics,
+                        const float* disps_sens, const float* targets, const float* weights, const float* eta,
+                        float lm, float ep, float* dx, float* dz, int first_solve, hipStream_t stream) {
+  auto* p = static_cast<BaPlan*>(plan);
+  int st = check_ready(p, workspace);
+  if (st) return st;
+  if (!p->motion_only && p->K > 0 && !dz) return fail(kInvalidArgument, "ba: dz output required unless motion_only");
+  st = solve_system(p, workspace, lm, ep, dx, first_solve, stream);
+  if (st) return st;
+  return apply_update(p, workspace, poses, disps, intrinsics, disps_sens, targets, weights, eta, dx, dz, stream);
+}
+
+// The two halves of droid_ba_solve_update, for a multi-GPU caller that agrees
+// on the status between them (all-reduce MAX of the status words): every rank
+// then skips the back-substitution and retraction together when any rank's
+// dataflow solve timed out, instead of only the rank that timed out.
+int droid_ba_solve_system(void* plan, void* workspace, float lm, float ep, float* dx, hipStream_t stream) {
+  auto* p = static_cast<BaPlan*>(plan);
+  int st = check_ready(p, workspace);
+  if (st) return st;
+  return solve_system(p, workspace, lm, ep, dx, 0, stream);
+}
+
+int droid_ba_apply_update(void* plan, void* workspace, float* poses, float* disps, const float* intrinsics,
+                          const float* disps_sens, const float* targets, const float* weights, const float* eta,
+                          float* dx, float* dz, hipStream_t stream) {
+  auto* p = static_cast<BaPlan*>(plan);
+  int st = check_ready(p, workspace);
+  if (st) return st;
+  return apply_update(p, workspace, poses, disps, intrinsics, disps_sens, targets, weights, eta, dx, dz, stream);
 }
 
 // Damped Cholesky solve of the (possibly all-reduced) system, back

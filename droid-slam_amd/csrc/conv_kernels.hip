@@ -1800,13 +1800,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 // slower on it (z|r 7.66 vs 7.41 ms, q 4.12 = 4.12), but on the frontend window
 // (C2, 96 edges: 1152 z|r tiles = 4.5 rounds of the 8-wave tile over 256 CUs)
 // its finer tiles fill the last round: update() 1.252 vs 1.308 ms.
-// DROID_CONV_BAND2=0 / 1: none / every shape it takes (A/B runs).
-static bool band2_for(int epi, long px) {
-  static const int mode = [] {
+// DROID_CONV_BAND2=0 / 1: none / every shape it takes (A/B runs), read at load;
+// droid_conv_set_tile changes it per call (tests compare both tiles in one process).
+static int& band2_mode() {
+  static int mode = [] {
     const char* e = getenv("DROID_CONV_BAND2");
     return e ? atoi(e) : -1;
   }();
+  return mode;
+}
+static bool band2_for(int epi, long px) {
+  const int mode = band2_mode();
   return mode == 1 || (mode < 0 && (epi == EPI_ACT || px / 256 <= 8L * device_cu_count()));
+}
+// a band-eligible 3x3 conv of this shape runs on the two-workgroup tile
+static bool band2_shape(int epi, int B, int H, int W, int Cout, int gru_ch) {
+  return band2_for(epi, (long)B * H * W) && W == 64 && H % 4 == 0 && Cout % kB2TN == 0 &&
+         (epi != EPI_GRU_ZR || gru_ch % kB2TN == 0);
 }
 
 template <int EPI>
@@ -2548,8 +2558,7 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
     return kOk;
   }
   // two-workgroups-per-CU tile: W == 64, 128-channel N tiles
-  if (band2_for(epi, (long)B * H * W) && band_ok && W == 64 && H % 4 == 0 && Cout % kB2TN == 0 &&
-      (epi != EPI_GRU_ZR || gru_ch % kB2TN == 0)) {
+  if (band_ok && band2_shape(epi, B, H, W, Cout, gru_ch)) {
     if (epi == EPI_GRU_ZR) return pre ? launch_band2_kernel<EPI_GRU_ZRP>(a, stream) : launch_band2_kernel<EPI_GRU_ZR>(a, stream);
     if (epi == EPI_GRU_Q) return pre ? launch_band2_kernel<EPI_GRU_QP>(a, stream) : launch_band2_kernel<EPI_GRU_Q>(a, stream);
     return launch_band2_kernel<EPI_ACT>(a, stream);
@@ -2583,6 +2592,34 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
   if (TN == 128) return launch_conv<128>(a, stream);
   if (TN == 64) return launch_conv<64>(a, stream);
   return launch_conv<16>(a, stream);
+}
+
+// Tile policy of the W == 64 3x3 convs: -1 = default (plain convs and small
+// gate-conv grids on the two-workgroups-per-CU tile, C3-sized gate convs on the
+// 8-wave band tiles), 0 = 8-wave band tiles only, 1 = the two-workgroup tile
+// wherever it applies.  Returns the previous policy.  Process-wide, not
+// thread-safe by design (tests and A/B runs).
+int droid_conv_set_tile(int mode) {
+  if (mode < -1 || mode > 1) return -2;
+  const int prev = band2_mode();
+  band2_mode() = mode;
+  return prev;
+}
+
+// Which kernel droid_conv_gru_pre_f16 runs for a ConvGRU gate conv (epi 1: z|r,
+// Cout 256; epi 2: q, Cout 128) over B images of H x W under the current tile
+// policy: 1 = conv_band2_kernel, 0 = the 8-wave band tile (<256,256> for z|r,
+// <384,128> for q), 2 = the opt-in 4-wave z|r tile (DROID_CONV_NW4=1), -1 = no
+// band tile for the shape.
+int droid_conv_gate_tile(int epi, int B, int H, int W) {
+  if ((epi != EPI_GRU_ZR && epi != EPI_GRU_Q) || B < 0 || H <= 0 || W <= 0) return -1;
+  if (band_version() <= 0 || W % 16 || 64 % W) return -1;
+  const int Cout = epi == EPI_GRU_ZR ? 256 : 128;
+  if (band2_shape(epi, B, H, W, Cout, 128)) return 1;
+  int ns_, nh_;
+  if (epi == EPI_GRU_ZR && band_nw4() && (H * W) % 256 == 0 && band_fits<256, 256, 4>(W, &ns_, &nh_)) return 2;
+  if (epi == EPI_GRU_ZR) return ((H * W) % 256 == 0 && band_fits<256, 256>(W, &ns_, &nh_)) ? 0 : -1;
+  return ((H * W) % 384 == 0 && band_fits<384, 128>(W, &ns_, &nh_)) ? 0 : -1;
 }
 
 int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc,

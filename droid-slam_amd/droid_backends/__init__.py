@@ -250,6 +250,22 @@ def alt_set_variant(v):
     check(lib.droid_alt_set_variant(int(v)), "alt_set_variant")
 
 
+def conv_set_tile(mode):
+    """Tile policy of the W=64 3x3 band convs (droid_conv_set_tile): -1 default,
+    0 = 8-wave band tiles only, 1 = the two-workgroups-per-CU tile wherever it
+    applies.  Returns the previous policy."""
+    prev = lib.droid_conv_set_tile(int(mode))
+    if prev == -2:
+        raise RuntimeError("conv_set_tile: mode must be -1, 0 or 1")
+    return prev
+
+
+def conv_gate_tile(epi, B, H, W):
+    """droid_conv_gate_tile: the kernel a gate conv of this shape runs on
+    (1 band2, 0 the 8-wave band tile, 2 the 4-wave z|r tile, -1 none)."""
+    return int(lib.droid_conv_gate_tile(int(epi), int(B), int(H), int(W)))
+
+
 EPI_ACT, EPI_GRU_ZR, EPI_GRU_Q, EPI_HEAD, EPI_GLO = 0, 1, 2, 3, 4
 
 
@@ -854,6 +870,19 @@ class BaPlan:
                                             _ptr(intrinsics), _ptr(disps_sens), _ptr(targets), _ptr(weights),
                                             _ptr(eta), float(lm), float(ep), _ptr(dx), _ptr(dz), _stream(poses)),
                   "ba solve_update")
+
+    def solve_system(self, lm, ep, dx):
+        """damping + Cholesky of the (all-reduced) system -> dx and status word 0."""
+        with torch.cuda.device(self.device):
+            check(lib.droid_ba_solve_system(self._h, _ptr(self.workspace), float(lm), float(ep), _ptr(dx),
+                                            _stream(self.workspace)), "ba solve_system")
+
+    def apply_update(self, poses, disps, intrinsics, disps_sens, targets, weights, eta, dx, dz):
+        """back-substitution + retraction, skipped when status bit 1 is set."""
+        with torch.cuda.device(self.device):
+            check(lib.droid_ba_apply_update(self._h, _ptr(self.workspace), _ptr(poses), _ptr(disps),
+                                            _ptr(intrinsics), _ptr(disps_sens), _ptr(targets), _ptr(weights),
+                                            _ptr(eta), _ptr(dx), _ptr(dz), _stream(poses)), "ba apply_update")
 
     def status_words(self):
         """the device status words (int32 [this solve, sticky]), a view."""

@@ -34,6 +34,8 @@ _SIGS = {
     "droid_conv_set_profile": ([_p], _i),
     "droid_alt_set_profile": ([_p], _i),
     "droid_alt_set_variant": ([_i], _i),
+    "droid_conv_set_tile": ([_i], _i),
+    "droid_conv_gate_tile": ([_i, _i, _i, _i], _i),
     "droid_corr_volume_pyramid": ([_p, _p, _p, _i, _i, _i, _i, _p, _i, _p], _i),
     "droid_corr_alt_ce0": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_conv_nhwc_f16": ([_p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _i, _i,
@@ -78,6 +80,8 @@ _SIGS = {
     "droid_ba_plan_upload": ([_p, _p, _p], _i),
     "droid_ba_build_system": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _p], _i),
     "droid_ba_solve_update": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p], _i),
+    "droid_ba_solve_system": ([_p, _p, _f, _f, _p, _p], _i),
+    "droid_ba_apply_update": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p], _i),
     "droid_chol_plan_create": ([_i, ctypes.POINTER(_p)], _i),
     "droid_chol_plan_info": ([_p, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),
                               ctypes.POINTER(_i)], _i),

@@ -55,64 +55,70 @@ class DepthVideo:
     def get_lock(self):
         return self.counter.get_lock()
 
-    def __item_setter(self, index, item):
-        if isinstance(index, int) and index >= self.counter.value:
-            self.counter.value = index + 1
-        elif isinstance(index, torch.Tensor) and index.max().item() > self.counter.value:
-            self.counter.value = index.max().item() + 1
-        self.tstamp[index] = item[0]
-        self.images[index] = item[1]
-        if item[2] is not None:
-            self.poses[index] = item[2]
-        if item[3] is not None:
-            self.disps[index] = item[3]
-        if item[4] is not None:
-            depth = item[4][3::8, 3::8]
-            self.disps_sens[index] = torch.where(depth > 0, 1.0 / depth, depth)
-        if item[5] is not None:
-            self.intrinsics[index] = item[5]
-        if len(item) > 6:
-            self.fmaps[index] = item[6]
-        if len(item) > 7:
-            self.nets[index] = item[7]
-        if len(item) > 8:
-            self.inps[index] = item[8]
+    # the item tuple the frontend writes (depth_video.py:46-77): (tstamp, image,
+    # pose, disp, depth, intrinsics[, fmap, net, inp]); pose / disp / depth /
+    # intrinsics may be None (kept), the trailing features may be absent
+    _ITEM_FIELDS = ("tstamp", "images", "poses", "disps", None, "intrinsics", "fmaps", "nets", "inps")
+    _OPTIONAL = frozenset(("poses", "disps", "intrinsics"))
+
+    def _grow_counter(self, index):
+        """the frame count follows the highest slot written (an int slot at or
+        past the end, or an index tensor whose largest entry exceeds it)."""
+        if isinstance(index, int):
+            top = index if index >= self.counter.value else None
+        elif isinstance(index, torch.Tensor):
+            hi = int(index.max().item())
+            top = hi if hi > self.counter.value else None
+        else:
+            top = None
+        if top is not None:
+            self.counter.value = top + 1
+
+    def _write(self, index, item):
+        self._grow_counter(index)
+        for k, value in enumerate(item[:len(self._ITEM_FIELDS)]):
+            name = self._ITEM_FIELDS[k]
+            if name is None:      # a full-resolution depth map -> sensor disparity at 1/8 resolution
+                if value is not None:
+                    d8 = value[3::8, 3::8]
+                    self.disps_sens[index] = torch.where(d8 > 0, 1.0 / d8, d8)
+            elif value is not None or name not in self._OPTIONAL:
+                getattr(self, name)[index] = value
 
     def __setitem__(self, index, item):
         with self.get_lock():
-            self.__item_setter(index, item)
+            self._write(index, item)
 
     def __getitem__(self, index):
         with self.get_lock():
-            if isinstance(index, int) and index < 0:
-                index = self.counter.value + index
-            return (self.poses[index], self.disps[index], self.intrinsics[index],
-                    self.fmaps[index], self.nets[index], self.inps[index])
+            slot = self.counter.value + index if isinstance(index, int) and index < 0 else index
+            return tuple(getattr(self, name)[slot] for name in ("poses", "disps", "intrinsics", "fmaps", "nets",
+                                                                  "inps"))
 
     def append(self, *item):
         with self.get_lock():
-            self.__item_setter(self.counter.value, item)
+            self._write(self.counter.value, item)
 
     @staticmethod
     def format_indicies(ii, jj, device="cuda"):
-        if not isinstance(ii, torch.Tensor):
-            ii = torch.as_tensor(ii)
-        if not isinstance(jj, torch.Tensor):
-            jj = torch.as_tensor(jj)
-        return (ii.to(device=device, dtype=torch.long).reshape(-1),
-                jj.to(device=device, dtype=torch.long).reshape(-1))
+        """edge index lists (any sequence or tensor) -> flat int64 tensors on device."""
+        def flat(x):
+            return torch.as_tensor(x).to(device=device, dtype=torch.long).reshape(-1)
+        return flat(ii), flat(jj)
 
     def upsample(self, ix, mask):
-        disps_up = cvx_upsample(self.disps[ix].unsqueeze(-1), mask)
-        self.disps_up[ix] = disps_up.squeeze()
+        """convex upsampling of the 1/8 disparities of frames ix (depth_video.py:123-127)."""
+        self.disps_up[ix] = cvx_upsample(self.disps[ix].unsqueeze(-1), mask).squeeze()
 
     def normalize(self):
+        """rescale so the mean disparity of the stored frames is 1 (poses' translations
+        scaled alike), depth_video.py:129-136."""
         with self.get_lock():
-            n = self.counter.value
-            s = self.disps[:n].mean()
-            self.disps[:n] /= s
-            self.poses[:n, :3] *= s
-            self.dirty[:n] = True
+            live = slice(0, self.counter.value)
+            scale = self.disps[live].mean()
+            self.disps[live].div_(scale)
+            self.poses[live, :3].mul_(scale)
+            self.dirty[live] = True
 
     def reproject(self, ii, jj, target=None):
         """project pixels of ii into jj (depth_video.py:139-147) -> coords
@@ -183,10 +189,12 @@ def ba_sharded(poses, disps, intrinsics, disps_sens, target, weight, eta, ii_hos
     structurally nonzero 64x64 tiles of A - S and the rhs row cross the links
     (9.6 MB at C3, 66 MB at C5 instead of the dense 603 MB).
 
-    Failures are agreed on, not per rank: the solves' status words are
-    all-reduced (MAX) on the device after the last GN iteration, and every rank
-    raises at its next BA call (or droid_backends.check_status()) if any rank's
-    dataflow Cholesky timed out - no rank is left waiting in a collective."""
+    Failures are agreed on, not per rank: after each GN iteration's Cholesky
+    the status words are all-reduced (MAX, 8 bytes) on the device BEFORE the
+    back-substitution and retraction, so if any rank's dataflow solve timed out
+    every rank skips that step (the replicated poses never diverge), and every
+    rank raises at its next BA call (or droid_backends.check_status()) - no
+    rank is left waiting in a collective."""
     import torch.distributed as dist
     group = comm.get("group")
     N, H, W = disps.shape
@@ -200,6 +208,7 @@ def ba_sharded(poses, disps, intrinsics, disps_sens, target, weight, eta, ii_hos
     dx = torch.empty((plan.P, 6), dtype=torch.float32, device=poses.device)
     dz = None if motion_only else torch.empty((plan.K, H * W), dtype=torch.float32, device=poses.device)
     flat = plan.system.view(-1)
+    status = plan.status_words()     # a view of the device status words [this solve, sticky]
     plan.clear_status()
     timing = comm.get("_ar_events")   # bench: HIP events around each all-reduce, or None
     for _ in range(itrs):
@@ -211,11 +220,14 @@ def ba_sharded(poses, disps, intrinsics, disps_sens, target, weight, eta, ii_hos
         if timing is not None:
             ev[1].record()
             timing.append(ev + (flat.numel() * flat.element_size(),))
-        plan.solve_update(poses, disps, intrinsics, disps_sens, target, weight, eta, lm, ep, dx, dz)
-    # status values are 0..3 per word, so MAX keeps the timeout bit (value >= 2) of any rank
-    status = plan.status_words().clone()
-    dist.all_reduce(status, op=dist.ReduceOp.MAX, group=group)
-    plan._record_status(status)
+        plan.solve_system(lm, ep, dx)
+        # the status words agreed before the step is applied (status values are
+        # 0..3 per word, so MAX keeps the timeout bit, value >= 2, of any rank):
+        # a rank whose dataflow solve timed out makes EVERY rank skip this step's
+        # back-substitution and retraction, so the replicated poses stay equal
+        dist.all_reduce(status, op=dist.ReduceOp.MAX, group=group)
+        plan.apply_update(poses, disps, intrinsics, disps_sens, target, weight, eta, dx, dz)
+    plan._record_status()     # the agreed words (identical on every rank)
     comm["_last_plan"] = plan
     return [dx, dz]
 
@@ -238,18 +250,21 @@ def global_edges(ii_host, jj_host, comm, call_key):
     key = None if version is None else (version,) + tuple(call_key)
     cache = comm.setdefault("_gedges", {})
     hit = cache.get(key) if key is not None else None
+    local = (ii_host.tobytes(), jj_host.tobytes())
     if hit is None:
         parts = [None] * dist.get_world_size(group)
         dist.all_gather_object(parts, (ii_host, jj_host), group=group)
-        hit = (np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
+        hit = (np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]), {local})
         if key is not None:
             if len(cache) >= 4:
                 cache.pop(next(iter(cache)))
             cache[key] = hit
-    elif len(ii_host):
+    elif len(ii_host) and local not in hit[2]:
+        # validated once per (cached list, local edge list): later hits skip the set test
         n = int(max(hit[0].max(), hit[1].max(), ii_host.max(), jj_host.max())) + 1
         have = np.unique(hit[0] * n + hit[1])
         if not np.isin(ii_host * n + jj_host, have).all():
             raise RuntimeError("ba (sharded): this rank's edges are not in the global edge list of edge-set "
                                "version %r - edge edits must be issued on every rank" % (version,))
-    return hit
+        hit[2].add(local)
+    return hit[0], hit[1]

@@ -142,6 +142,12 @@ class PendingAltLookup:
         self.coords = coords
 
 
+def _version_of(t):
+    """t's autograd version counter, or None for an inference tensor (created
+    under torch.inference_mode: no counter, reading _version raises)."""
+    return None if t.is_inference() else t._version
+
+
 def edge_segments(inverse, num_unique):
     """CSR (seg_ptr (U+1), seg_idx (E)) int64 of the edges per source-frame slot.
     `inverse` may be a numpy array (built on the host) or a device tensor."""
@@ -327,11 +333,15 @@ class FusedUpdateModule(torch.nn.Module):
             # the weights only: it is the same in every update() of an edge set,
             # so it is computed once per inp_frames tensor (the graph caches that
             # tensor per edge set) instead of once per update
+            # keyed on the tensor's identity AND its version counter, so a caller
+            # that refills the same buffer in place gets a fresh term (inference
+            # tensors carry no version counter: their term is recomputed per call)
+            ver = _version_of(inp_frames)
             c = self._pre
-            if c is None or c[0] is not inp_frames or c[1] is not P:
+            if c is None or c[0] is not inp_frames or c[1] is not P or ver is None or c[3] != ver:
                 pre = torch.empty((inp_frames.shape[0], H, W, 384), dtype=torch.float16, device=dev)
                 conv3([(inp_frames, 0, 128)], "inp_zrq", 384, None, pre, act=0)
-                self._pre = c = (inp_frames, P, pre)
+                self._pre = c = (inp_frames, P, pre, ver)
             pre = c[2]
             pidx = inverse if inverse.dtype == torch.int64 else inverse.long()
             if wino:
@@ -438,17 +448,18 @@ class ReferenceLayoutUpdateModule(torch.nn.Module):
         # the caller's inp is the same tensor until its edge set changes, and the
         # net it passes back is usually the one this module returned: their
         # channels-last copies are reused then (tensor identity + version counter)
+        # (inference tensors have no version counter: no reuse for them)
         c = self._net
-        if c is not None and c[0] is net and c[1] == net._version:
+        if c is not None and c[0] is net and c[1] is not None and c[1] == _version_of(net):
             net_cl = c[2]
         else:
             net_cl = cl(net)
         c = self._inp
-        if c is not None and c[0] is inp and c[1] == inp._version:
+        if c is not None and c[0] is inp and c[1] is not None and c[1] == _version_of(inp):
             inp_cl = c[2]
         else:
             inp_cl = cl(inp)
-            self._inp = (inp, inp._version, inp_cl)
+            self._inp = (inp, _version_of(inp), inp_cl)
         c200 = cl(corr, 200)
         motn = (torch.zeros((num, 4, ht, wd), device=dev) if flow is None
                 else flow.reshape(num, 4, ht, wd).float().contiguous())
@@ -463,5 +474,5 @@ class ReferenceLayoutUpdateModule(torch.nn.Module):
         upmask = droid_backends.transpose_f16(upmask.contiguous(), ht * wd, upmask.shape[-1]).unsqueeze(0)
         upmask = upmask.view(1, upmask.shape[1], -1, ht, wd)
         net_out = droid_backends.transpose_f16(n, ht * wd, 128).view(1, num, 128, ht, wd)
-        self._net = (net_out, net_out._version, n)
+        self._net = (net_out, _version_of(net_out), n)
         return net_out, d, w, eta, upmask

@@ -82,6 +82,18 @@ int droid_alt_set_profile(void* buf);
  * default; env DROID_ALT_VARIANT=1 selects 1 at load).  Outputs are bitwise
  * equal; tests compare the two. */
 int droid_alt_set_variant(int v);
+/* Tile policy of the W == 64 3x3 band convs (not part of the reference
+ * interface; tests run both tiles in one process): -1 = default (the plain
+ * convs and small gate-conv grids on the two-workgroups-per-CU tile, larger
+ * gate-conv grids on the 8-wave band tiles), 0 = 8-wave band tiles only, 1 = the
+ * two-workgroup tile wherever it applies.  Returns the previous policy, -2 for
+ * a bad mode.  Process-wide. */
+int droid_conv_set_tile(int mode);
+/* Which kernel droid_conv_gru_pre_f16 takes for a ConvGRU gate conv (epi 1 =
+ * z|r, 2 = q) over B images of H x W under the current policy: 1 =
+ * conv_band2_kernel, 0 = the 8-wave band tile, 2 = the opt-in 4-wave z|r tile,
+ * -1 = none (DROID_UNSUPPORTED).  Queries the device's CU count. */
+int droid_conv_gate_tile(int epi, int B, int H, int W);
 /* profiling builds only (make prof): Cholesky task timeline, 8 int64 per task */
 int droid_chol_set_profile(void* buf);
 
@@ -382,6 +394,14 @@ int droid_ba_solve_update(void* plan, void* workspace, float* poses, float* disp
                           const float* intrinsics, const float* disps_sens, const float* targets,
                           const float* weights, const float* eta, float lm, float ep, float* dx,
                           float* dz, hipStream_t stream);
+/* droid_ba_solve_update in two steps: solve_system = damping + Cholesky (dx,
+ * status word 0), apply_update = back substitution + retraction, both skipped
+ * when status bit 1 (timeout) is set.  A sharded caller all-reduces (MAX) the
+ * status words between them so every rank skips or applies the step alike. */
+int droid_ba_solve_system(void* plan, void* workspace, float lm, float ep, float* dx, hipStream_t stream);
+int droid_ba_apply_update(void* plan, void* workspace, float* poses, float* disps, const float* intrinsics,
+                          const float* disps_sens, const float* targets, const float* weights,
+                          const float* eta, float* dx, float* dz, hipStream_t stream);
 /* `iterations` x (build_system + solve_update): droid_backends.ba on one device.
  * poses (N,7) f32, disps (N,H,W) f32 mutated in place; intrinsics (4); disps_sens (N,H,W);
  * targets/weights (E,2,H,W); eta (K or 1,H,W); dx (P,6) and dz (K,H*W) outputs. */

@@ -684,8 +684,11 @@ def test_fused_update_inp_frames_matches_per_edge_inp():
 
 
 def test_fused_update_matches_reference_module_48x64():
-    """The bench shape (48x64: W=64 band tiles, the per-frame gate term, fused
-    delta/weight heads) with E=10 edges over 4 source frames."""
+    """The bench's feature-map size (48x64, the per-frame gate term, fused
+    delta/weight heads) with E=10 edges over 4 source frames.  At this edge
+    count the gate convs run on the two-workgroup tile (conv_band2_kernel);
+    the 8-wave W=64 band tiles the C3 bench takes are covered at 192-256
+    edges by tests/test_gpu_conv_c3.py."""
     from droid_mi355x.fused import FusedUpdateModule
     from droid_mi355x.update import UpdateModule
     E, H, W = 10, 48, 64
@@ -752,3 +755,68 @@ def test_reference_layout_module_matches_update_module(H, W, E):
     assert len(n3) == 3 and torch.equal(n3[0], dn) and torch.equal(n3[1], dd) and torch.equal(n3[2], dw)
     for a, b in ((an, dn), (ad, dd), (aw, dw), (ae, de), (au, du)):
         assert torch.equal(a, b)
+
+
+def test_reference_layout_module_under_inference_mode():
+    """The drop-in called under torch.inference_mode() (inference tensors carry
+    no version counter, so its channels-last caches must not read one) gives
+    the no_grad results bit for bit, on repeated calls and with the net it
+    returned passed back."""
+    from droid_mi355x.fused import FusedUpdateModule, ReferenceLayoutUpdateModule
+    from droid_mi355x.update import UpdateModule
+    E, H, W = 10, 48, 64
+    m = UpdateModule().to(DEV).eval()
+    det_fill(m)
+    g = torch.Generator(device=DEV).manual_seed(41)
+    net = torch.tanh(torch.randn((1, E, 128, H, W), generator=g, device=DEV)).half()
+    inp = torch.relu(torch.randn((1, E, 128, H, W), generator=g, device=DEV)).half()
+    corr = (2 * torch.randn((1, E, 196, H, W), generator=g, device=DEV)).half()
+    flow = (4 * torch.randn((1, E, 4, H, W), generator=g, device=DEV)).clamp(-64, 64)
+    ii = torch.tensor([0, 0, 1, 2, 2, 3, 1, 3, 0, 2], device=DEV)
+    jj = torch.tensor([1, 2, 0, 1, 3, 2, 3, 0, 3, 0], device=DEV)
+    with torch.no_grad():
+        d = ReferenceLayoutUpdateModule(m)
+        a1 = d(net, inp, corr, flow, ii, jj)
+        a2 = d(a1[0], inp, corr, flow, ii, jj)
+    with torch.inference_mode():
+        d = ReferenceLayoutUpdateModule(m)
+        ni, ip, co, fl = net.clone(), inp.clone(), corr.clone(), flow.clone()
+        assert ni.is_inference()
+        b1 = d(ni, ip, co, fl, ii, jj)
+        b2 = d(b1[0], ip, co, fl, ii, jj)
+        # the per-frame gate term on an inference inp_frames tensor
+        f = FusedUpdateModule(m)
+        nhwc = lambda t: t[0].permute(0, 2, 3, 1).contiguous()
+        c200 = torch.zeros((E, H, W, 200), dtype=torch.float16, device=DEV)
+        c200[..., :196] = nhwc(co)
+        uq, inv = torch.unique(ii, return_inverse=True)
+        inpf = nhwc(ip)[:4]
+        r1 = f(nhwc(ni), None, c200, fl[0], inv, len(uq), inp_frames=inpf)
+        r2 = f(nhwc(ni), None, c200, fl[0], inv, len(uq), inp_frames=inpf)
+    for x, y in list(zip(a1, b1)) + list(zip(a2, b2)) + list(zip(r1, r2)):
+        assert torch.equal(x, y)
+
+
+def test_fused_pre_term_follows_in_place_refill():
+    """The per-frame gate-term cache is keyed on the inp_frames tensor's version:
+    refilling the same buffer in place gives the term of the new contents."""
+    from droid_mi355x.fused import FusedUpdateModule
+    from droid_mi355x.update import UpdateModule
+    E, H, W = 6, 48, 64
+    m = UpdateModule().to(DEV).eval()
+    det_fill(m)
+    f = FusedUpdateModule(m)
+    g = torch.Generator(device=DEV).manual_seed(43)
+    net = torch.tanh(torch.randn((E, H, W, 128), generator=g, device=DEV)).half()
+    c200 = (2 * torch.randn((E, H, W, 200), generator=g, device=DEV)).half()
+    flow = (4 * torch.randn((E, 4, H, W), generator=g, device=DEV)).clamp(-64, 64)
+    inv = torch.tensor([0, 0, 1, 1, 2, 2], device=DEV)
+    buf = torch.relu(torch.randn((3, H, W, 128), generator=g, device=DEV)).half()
+    other = torch.relu(torch.randn((3, H, W, 128), generator=g, device=DEV)).half()
+    with torch.no_grad():
+        f(net, None, c200, flow, inv, 3, inp_frames=buf)
+        buf.copy_(other)
+        a = f(net, None, c200, flow, inv, 3, inp_frames=buf)
+        b = FusedUpdateModule(m)(net, None, c200, flow, inv, 3, inp_frames=other)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)

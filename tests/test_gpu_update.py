@@ -295,9 +295,32 @@ def test_update_lowmem_matches_oracle_composition():
               damping=host(g.damping[:n]))
     inp = host(video.inps[:n].float())[g._ii]
     params = {k: host(v.float()) for k, v in m.state_dict().items()}
-    with torch.no_grad():
-        g.update_lowmem(steps=1)
+    import droid_backends
+    from oracle import ba as oba
+    captured = {}
+    orig = droid_backends.ba
+
+    def spy(*a, **k):
+        captured["a"] = [x.detach().clone() if isinstance(x, torch.Tensor) else x for x in a]
+        return orig(*a, **k)
+
+    droid_backends.ba = spy
+    try:
+        with torch.no_grad():
+            g.update_lowmem(steps=1)
+    finally:
+        droid_backends.ba = orig
     torch.cuda.synchronize()
+    # the BA update_lowmem drives, on the very inputs it handed over, within the
+    # north star's 1e-4 of the oracle (the composition below is looser: its
+    # targets come from the fp32 operator, the device's from the fp16 one)
+    a = captured["a"]
+    assert (a[9], a[10], a[12], a[13], a[14]) == (1, n, 1e-5, 1e-2, False)
+    ba_ref = oba.ba(poses=host(a[0]), disps=host(a[1]), intrinsics=host(a[2]), disps_sens=host(a[3]),
+                    targets=host(a[4]), weights=host(a[5]), eta=host(a[6]), ii=host(a[7]), jj=host(a[8]),
+                    t0=a[9], t1=a[10], iterations=a[11], lm=a[12], ep=a[13], motion_only=False)
+    np.testing.assert_allclose(host(video.poses[:n]), ba_ref["poses"][:n], atol=1e-4)
+    np.testing.assert_allclose(host(video.disps[:n]), np.maximum(ba_ref["disps"][:n], 1e-3), atol=1e-4)
     ref = ofg.update(params, st["poses"], st["disps"], st["disps_sens"], st["intrinsics"], st["fmaps"], g._ii,
                      g._jj, st["net"], inp, st["target"], st["weight"], st["damping"], t0=1, t1=n, lm=1e-5, ep=1e-2)
     np.testing.assert_allclose(host(g.net.float()).transpose(0, 3, 1, 2), ref["net"], atol=2e-2)
