@@ -295,6 +295,255 @@ __global__ void __launch_bounds__(512) corr_volume_pyramid_kernel(VolArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Round 4: corr_volume_pyramid2_kernel, the same pyramid with the MFMA operands
+// swapped so that pooling is (mostly) register-local, and no store drain per
+// patch.  Measured cost of the kernel above (34.4 ms at 2048 edges, 1.5 TB/s
+// of writes): per patch and wave 192 cross-lane shuffles (ds_bpermute on the
+// LDS pipe) for the two lower pooling levels, 64 two-byte LDS staging writes,
+// and a vmcnt(0) wait at every patch that drains the previous patch's 8 global
+// stores (gfx9 counts stores in vmcnt, in order with the LDS-DMA) before the
+// next patch may start.
+//   * D = target x query (A = the patch's target rows from LDS, B = the wave's
+//     query rows in registers): lane (fq, fr) holds targets 4 fq + i (i < 4) of
+//     an N-block for query fr, and the patch buffer orders an N-block's 16
+//     target rows so that those four are a 2x2 window (row c = 4 fq + i ->
+//     sub-patch (2 (fq >> 1) + (i >> 1), 2 (fq & 1) + (i & 1))): level 1 is
+//     pooled inside the lane, level 2 takes 3 shuffles per (row block, N-block)
+//     (lanes l ^ 16, ^ 32, ^ 48), level 3 is register-local across N-blocks -
+//     24 shuffles per patch instead of 192; same arithmetic and summation order.
+//   * level 0 is staged as 4-byte pairs (16 ds_write_b32 instead of 32
+//     ds_write_b16), the 16-B tile rows of query q XOR-swizzled by q & 7
+//     (2-way bank conflicts instead of 8), so that two workgroups fit a CU
+//     (80.5 KB of LDS each, 108 VGPRs: 4 waves per SIMD instead of 2).
+//   * every store is an unconditional buffer store (an out-of-range offset is
+//     dropped), so each wave issues exactly kVol2Stores per patch and the patch
+//     hand-off waits with vmcnt(kVol2Stores): the LDS-DMA of the next patch,
+//     issued before this patch's stores, is awaited without draining them.
+// ---------------------------------------------------------------------------
+constexpr int kVol2S0 = 64;    // staging row (halves): level 0, one 8x8 tile, 16-B row pieces XOR-swizzled by q & 7
+constexpr int kVol2S1 = 20;    // level 1, 4x4 + pad (8-B aligned rows)
+constexpr int kVol2StageWave = 32 * kVol2S0 * 2 + 32 * kVol2S1 * 2 + 32 * 4 * 2 + 32 * 2;
+constexpr int kVol2Lds = kVolStage + 8 * kVol2StageWave;
+static_assert(2 * kVol2Lds <= 160 * 1024, "corr_volume_pyramid2: two workgroups per CU");
+constexpr int kVol2Stores = 8;  // per wave and patch: 4 (level 0) + 2 (level 1) + 1 + 1
+
+// target pixel of N-block b, row c (= 4 fq + i) inside an 8x8 patch
+__device__ __forceinline__ int vol2_ty(int b, int c) { return 4 * (b >> 1) + 2 * (c >> 3) + ((c >> 1) & 1); }
+__device__ __forceinline__ int vol2_tx(int b, int c) { return 4 * (b & 1) + 2 * ((c >> 2) & 1) + (c & 1); }
+
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned pack2h(float lo, float hi) {
+  return (unsigned)__half_as_ushort(__float2half(lo)) | ((unsigned)__half_as_ushort(__float2half(hi)) << 16);
+}
+
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) corr_volume_pyramid2_kernel(VolArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int H = a.H, W = a.W, HW = H * W;
+  const int e = __builtin_amdgcn_readfirstlane((int)(blockIdx.x / a.qblocks));
+  const int qb = (int)(blockIdx.x % a.qblocks);
+  const int fa = __builtin_amdgcn_readfirstlane(a.f1[e]);
+  const int fb = __builtin_amdgcn_readfirstlane(a.f2[e]);
+  const unsigned lds_a = lds_addr(lds);
+  char* stage = lds + kVolStage + wave * kVol2StageWave;
+  _Float16* s0 = reinterpret_cast<_Float16*>(stage);                   // [32][kVol2S0]
+  _Float16* s1 = s0 + 32 * kVol2S0;                                    // [32][kVol2S1]
+  _Float16* s2 = s1 + 32 * kVol2S1;                                    // [32][4]
+  _Float16* s3 = s2 + 32 * 4;                                          // [32]
+
+  // this wave's 32 query rows: B fragments (lane: query fr, channels 8 fq ..) x 4 K-steps
+  const int q0 = qb * kVolQ + wave * 32;
+  half8 qf[2][4];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int q = min(q0 + 16 * r + fr, HW - 1);
+    const __half* row = a.f + ((long)fa * HW + q) * 128;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[r][ks] = *reinterpret_cast<const half8*>(row + ks * 32 + fq * 8);
+  }
+
+  // level geometry and this edge's output slices (one descriptor per level:
+  // offsets past a query pixel that does not exist are dropped)
+  int Hl[4], Wl[4], TR[4];
+  long slice[4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    Hl[l] = H >> l;
+    Wl[l] = W >> l;
+    TR[l] = (Hl[l] + 7) / 8;  // tile rows (tiled layout)
+    slice[l] = a.tiled ? (long)TR[l] * (Wl[l] / 8) * 64 : (long)Hl[l] * Wl[l];
+  }
+  __amdgpu_buffer_rsrc_t ro[4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l)
+    ro[l] = __builtin_amdgcn_make_buffer_rsrc(a.lvl[l] + (long)e * HW * slice[l], (short)0,
+                                              (int)(HW * slice[l] * 2), kBufFlags);
+
+  const rsrc_t rsb = make_rsrc(a.f + (long)fb * HW * 128, (unsigned)(HW * 256));
+  const int pcols = W / 8, npatch = (H / 8) * pcols;
+  (void)npatch;
+  auto patch_yx = [&](int p, int& py, int& px) {
+    const int gcols = (pcols + 1) / 2;
+    const int g = p >> 2, k = p & 3;
+    int gy = g / gcols, gx = g - gy * gcols;
+    py = 2 * gy + (k >> 1);
+    px = 2 * gx + (k & 1);
+  };
+  const int gslots = ((H / 8 + 1) / 2) * ((pcols + 1) / 2) * 4;
+  auto patch_dma = [&](int p, int buf) {
+    int py, px;
+    patch_yx(p, py, px);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int ins = wave_u + 8 * k;
+      const int row = ins * 4 + (lane >> 4);
+      const int b = row >> 4, c = row & 15;
+      const int t = (8 * py + vol2_ty(b, c)) * W + 8 * px + vol2_tx(b, c);
+      const int piece = (lane & 15) ^ (row & 15);
+      dma16(rsb, lds_a + kVolB + buf * 16384 + ins * 1024, (unsigned)((t * 128 + piece * 8) * 2));
+    }
+  };
+  auto valid = [&](int p) {
+    int py, px;
+    patch_yx(p, py, px);
+    return py < H / 8 && px < pcols;
+  };
+  int first = 0;
+  while (first < gslots && !valid(first)) ++first;
+  if (first < gslots) patch_dma(first, 0);
+  int buf = 0;
+  bool stores_out = false;   // this wave has kVol2Stores stores in flight after the last DMA
+  for (int p = first; p < gslots;) {
+    int nxt = p + 1;
+    while (nxt < gslots && !valid(nxt)) ++nxt;
+    if (stores_out) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // == kVol2Stores
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // patch p landed in buf; every wave done with buf ^ 1
+    if (nxt < gslots) patch_dma(nxt, buf ^ 1);
+    int py, px;
+    patch_yx(p, py, px);
+    const int ty0 = 8 * py, tx0 = 8 * px;
+
+    // per N-block b and row block r: V0 = targets (4 fq + i) for query 16 r + fr,
+    // rounded to fp16, staged as the lane's 2x2 window (two 4-B pairs of the 8x8
+    // tile, row-major), and its level-1 value pooled in place ((h, w) order;
+    // level-1 pixel (2 (b >> 1) + (fq >> 1), 2 (b & 1) + (fq & 1)) of the patch's
+    // 4x4 block) - only four V0 values are live at a time
+    float u[2][4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      half8 tf[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int row = b * 16 + fr, piece = ks * 4 + fq;
+        tf[ks] = *reinterpret_cast<const half8*>(lds + kVolB + buf * 16384 + row * 256 + ((piece ^ (row & 15)) << 4));
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(tf[ks], qf[r][ks], c, 0, 0, 0);
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = rnd16(c[i]);
+        const int q = 16 * r + fr;
+        const int y = 4 * (b >> 1) + 2 * (fq >> 1), x = 4 * (b & 1) + 2 * (fq & 1);
+        *reinterpret_cast<unsigned*>(s0 + q * kVol2S0 + ((y ^ (q & 7)) << 3) + x) = pack2h(v[0], v[1]);
+        *reinterpret_cast<unsigned*>(s0 + q * kVol2S0 + (((y + 1) ^ (q & 7)) << 3) + x) = pack2h(v[2], v[3]);
+        u[r][b] = vol_pool4(v[0], v[1], v[2], v[3]);
+        s1[q * kVol2S1 + (2 * (b >> 1) + (fq >> 1)) * 4 + 2 * (b & 1) + (fq & 1)] = (_Float16)u[r][b];
+      }
+    }
+    // level 2: the four level-1 values of an N-block sit in lanes fq = 0..3 ((h, w)
+    // order = fq order); level 3: the four N-blocks of a lane
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      float w2[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        w2[b] = vol_pool4(u[r][b], __shfl_xor(u[r][b], 16), __shfl_xor(u[r][b], 32), __shfl_xor(u[r][b], 48));
+      if (fq == 0) {
+        const int q = 16 * r + fr;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) s2[q * 4 + b] = (_Float16)w2[b];
+        s3[q] = (_Float16)vol_pool4(w2[0], w2[1], w2[2], w2[3]);
+      }
+    }
+    // stores (the staging area is this wave's own: a wave barrier suffices)
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // level 0: 32 q x 128 B, 8 lanes per query pixel
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = 8 * k + (lane >> 3), seg = lane & 7;   // seg = tile row
+      const int qg = q0 + q;
+      const u32x4_t val = *reinterpret_cast<const u32x4_t*>(s0 + q * kVol2S0 + ((seg ^ (q & 7)) << 3));
+      const long off = a.tiled ? ((long)qg * TR[0] * (Wl[0] / 8) + py * (Wl[0] / 8) + px) * 64 + seg * 8
+                               : (long)qg * HW + (long)(ty0 + seg) * W + tx0;
+      __builtin_amdgcn_raw_buffer_store_b128(val, ro[0], qg < HW ? (int)(off * 2) : (int)kOob, 0, 0);
+    }
+    // level 1: 32 q x 4 rows x 8 B (the patch's 4x4 level-1 block)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = 16 * k + (lane >> 2), rr = lane & 3;
+      const int qg = q0 + q;
+      const u32x2_t val = *reinterpret_cast<const u32x2_t*>(s1 + q * kVol2S1 + rr * 4);
+      const int y = ty0 / 2 + rr, x = tx0 / 2;
+      const long off = a.tiled ? ((long)qg * TR[1] * (Wl[1] / 8) + (y >> 3) * (Wl[1] / 8) + (x >> 3)) * 64 +
+                                     (y & 7) * 8 + (x & 7)
+                               : (long)qg * (Hl[1] * Wl[1]) + (long)y * Wl[1] + x;
+      __builtin_amdgcn_raw_buffer_store_b64(val, ro[1], qg < HW ? (int)(off * 2) : (int)kOob, 0, 0);
+    }
+    // level 2: 32 q x 2 rows x 4 B; level 3: 32 q x 2 B
+    {
+      const int q = lane >> 1, rr = lane & 1;
+      const int qg = q0 + q;
+      const unsigned val = *reinterpret_cast<const unsigned*>(s2 + q * 4 + rr * 2);
+      const int y = ty0 / 4 + rr, x = tx0 / 4;
+      const long off = a.tiled ? ((long)qg * TR[2] * (Wl[2] / 8) + (y >> 3) * (Wl[2] / 8) + (x >> 3)) * 64 +
+                                     (y & 7) * 8 + (x & 7)
+                               : (long)qg * (Hl[2] * Wl[2]) + (long)y * Wl[2] + x;
+      __builtin_amdgcn_raw_buffer_store_b32(val, ro[2], qg < HW ? (int)(off * 2) : (int)kOob, 0, 0);
+    }
+    {
+      const int qg = q0 + (lane & 31);
+      const int y = ty0 / 8, x = tx0 / 8;
+      const long off = a.tiled ? ((long)qg * TR[3] * (Wl[3] / 8) + (y >> 3) * (Wl[3] / 8) + (x >> 3)) * 64 +
+                                     (y & 7) * 8 + (x & 7)
+                               : (long)qg * (Hl[3] * Wl[3]) + (long)y * Wl[3] + x;
+      const short val = (short)__half_as_ushort(*reinterpret_cast<const __half*>(s3 + (lane & 31)));
+      __builtin_amdgcn_raw_buffer_store_b16(val, ro[3], (lane < 32 && qg < HW) ? (int)(off * 2) : (int)kOob, 0, 0);
+    }
+    stores_out = true;
+    buf ^= 1;
+    p = nxt;
+  }
+  // tiled layout: rows of the last tile row past H_l are zero (levels whose height is not a multiple of 8)
+  if (a.tiled) {
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+      const int pad = TR[l] * 8 - Hl[l];
+      if (pad == 0) continue;
+      const int tcols = Wl[l] / 8;
+      const int pieces = tcols * pad;
+      for (int idx = lane; idx < 32 * pieces; idx += 64) {
+        const int q = idx / pieces, k = idx - q * pieces;
+        const int tc = k / pad, rr = Hl[l] - (TR[l] - 1) * 8 + (k - tc * pad);
+        const int qg = q0 + q;
+        if (qg < HW) {
+          const long off = (((long)e * HW + qg) * TR[l] * tcols + (TR[l] - 1) * tcols + tc) * 64 + rr * 8;
+          *reinterpret_cast<uint4*>(a.lvl[l] + off) = uint4{0u, 0u, 0u, 0u};
+        }
+      }
+    }
+  }
+}
+
 }  // namespace droid
 
 using namespace droid;
@@ -328,13 +577,30 @@ int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, i
   const long grid = (long)E * a.qblocks;
   if (grid == 0) return kOk;
   if (grid > 0x7fffffffL) return fail(kUnsupported, "corr_volume_pyramid: too many edges");
-  static bool attr = false;
-  if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid_kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, kVolLds));
-    attr = true;
+  // DROID_VOL_V1=1: the round-3 kernel (A/B runs); the default is corr_volume_pyramid2_kernel
+  static const bool v1 = [] {
+    const char* e = getenv("DROID_VOL_V1");
+    return e && e[0] == '1';
+  }();
+  if (v1) {
+    static bool attr = false;
+    if (!attr) {
+      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid_kernel),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kVolLds));
+      attr = true;
+    }
+    corr_volume_pyramid_kernel<<<dim3((unsigned)grid), 512, kVolLds, stream>>>(a);
+  } else {
+    if ((long)H * W * H * W * 2 >= 0x7fffffffL)
+      return fail(kUnsupported, "corr_volume_pyramid: an edge's level-0 volume must stay below 2 GB");
+    static bool attr2 = false;
+    if (!attr2) {
+      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kVol2Lds));
+      attr2 = true;
+    }
+    corr_volume_pyramid2_kernel<<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
   }
-  corr_volume_pyramid_kernel<<<dim3((unsigned)grid), 512, kVolLds, stream>>>(a);
   DROID_LAUNCH_CHECK();
   return kOk;
 }

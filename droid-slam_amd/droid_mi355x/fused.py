@@ -418,12 +418,40 @@ class ReferenceLayoutUpdateModule(torch.nn.Module):
         self.fused = module if isinstance(module, FusedUpdateModule) else FusedUpdateModule(module)
         self._inp = None   # (the caller's inp tensor, its version, the channels-last copy)
         self._net = None   # (the net tensor last returned, its version, our channels-last copy)
+        self._frames = None   # (key, inp, ii, per-source-frame inp rows or None), see _inp_frames
 
     def load_state_dict(self, *a, **k):
         return self.fused.load_state_dict(*a, **k)
 
     def state_dict(self, *a, **k):
         return self.fused.state_dict(*a, **k)
+
+    def _inp_frames(self, inp, inp_cl, ii, inverse, num_unique):
+        """The context features per source frame, (U,H,W,128) channels-last, or
+        None.  The reference's graph gathers inp = video.inps[ii] per edge
+        (factor_graph.py:118), so every edge leaving a frame carries the same
+        rows and the gate convs' inp term can be computed once per frame
+        (FusedUpdateModule's factored gates) - but the drop-in must equal
+        UpdateModule for ANY inputs, so this is checked, not assumed: every
+        edge's rows are compared with the first edge of its source frame (a
+        read of inp, once per (inp, ii) pair - the caller's tensors are the same
+        objects across the updates of an edge set); when any edge differs, the
+        per-edge gates run."""
+        key = (id(inp), _version_of(inp), id(ii), _version_of(ii), num_unique)
+        c = getattr(self, "_frames", None)
+        if (c is not None and c[0] == key and c[1] is inp and c[2] is ii and key[1] is not None
+                and key[3] is not None):
+            return c[3]
+        E = inp_cl.shape[0]
+        first = torch.full((num_unique,), E, dtype=torch.int64, device=inp_cl.device)
+        first.scatter_reduce_(0, inverse, torch.arange(E, device=inp_cl.device), "amin")
+        frames = None
+        if bool((first < E).all()):
+            cand = inp_cl.index_select(0, first)
+            if torch.equal(cand.index_select(0, inverse), inp_cl):
+                frames = cand
+        self._frames = (key, inp, ii, frames)
+        return frames
 
     @torch.no_grad()
     def forward(self, net, inp, corr, flow=None, ii=None, jj=None, inverse=None, num_unique=None):
@@ -470,7 +498,12 @@ class ReferenceLayoutUpdateModule(torch.nn.Module):
         if inverse is None:   # GraphAgg's torch.unique (droid_net.py:64), as the reference does
             uniq, inverse = torch.unique(ii.to(dev), return_inverse=True)
             num_unique = int(uniq.shape[0])
-        n, d, w, eta, upmask = self.fused(net_cl, inp_cl, c200, motn, inverse, num_unique, want_upmask=True)
+        frames = self._inp_frames(inp, inp_cl, ii, inverse, num_unique)
+        if frames is not None:   # the gates' inp term once per source frame (cached across updates)
+            n, d, w, eta, upmask = self.fused(net_cl, None, c200, motn, inverse, num_unique, want_upmask=True,
+                                              inp_frames=frames)
+        else:
+            n, d, w, eta, upmask = self.fused(net_cl, inp_cl, c200, motn, inverse, num_unique, want_upmask=True)
         upmask = droid_backends.transpose_f16(upmask.contiguous(), ht * wd, upmask.shape[-1]).unsqueeze(0)
         upmask = upmask.view(1, upmask.shape[1], -1, ht, wd)
         net_out = droid_backends.transpose_f16(n, ht * wd, 128).view(1, num, 128, ht, wd)

@@ -720,13 +720,16 @@ def test_fused_update_matches_reference_module_48x64():
     np.testing.assert_allclose(host(fe), host(re), atol=1e-3 + 2e-2 * float(re.abs().max()))
 
 
-@pytest.mark.parametrize("H,W,E", [(16, 24, 6), (48, 64, 10)])   # generic kernels / band tiles + fused heads
-def test_reference_layout_module_matches_update_module(H, W, E):
+@pytest.mark.parametrize("H,W,E,per_frame", [(16, 24, 6, False), (48, 64, 10, False), (48, 64, 10, True)])
+def test_reference_layout_module_matches_update_module(H, W, E, per_frame):
     """ReferenceLayoutUpdateModule is called exactly as the reference's
     factor_graph.update() calls UpdateModule (factor_graph.py:207-208: NCHW
     state, materialised 196-channel lookup, 5 outputs incl. upmask) and agrees
     with the torch module (pinned to the reference by update_module.npz) at
-    fp16 tolerance; without ii it returns the 3-output form."""
+    fp16 tolerance; without ii it returns the 3-output form.  per_frame: inp
+    gathered per source frame as the reference's graph builds it
+    (factor_graph.py:118), so the drop-in takes the factored gates (checked,
+    not assumed - random per-edge inp takes the per-edge gates)."""
     from droid_mi355x.fused import ReferenceLayoutUpdateModule
     from droid_mi355x.update import UpdateModule
     m = UpdateModule().to(DEV).eval()
@@ -739,6 +742,8 @@ def test_reference_layout_module_matches_update_module(H, W, E):
     flow = (4 * torch.randn((1, E, 4, H, W), generator=g, device=DEV)).clamp(-64, 64)
     ii = torch.tensor([0, 0, 1, 2, 2, 3, 1, 3, 0, 2][:E], device=DEV)
     jj = torch.tensor([1, 2, 0, 1, 3, 2, 3, 0, 3, 0][:E], device=DEV)
+    if per_frame:
+        inp = inp[:, :4][:, ii].contiguous()
     with torch.no_grad():
         rn, rd, rw, re, ru = m(net.float(), inp.float(), corr.float(), flow, ii, jj)
         dn, dd, dw, de, du = d(net, inp, corr, flow, ii, jj)
@@ -752,7 +757,9 @@ def test_reference_layout_module_matches_update_module(H, W, E):
     np.testing.assert_allclose(host(dw), host(rw), atol=1.5e-2)
     np.testing.assert_allclose(host(de), host(re), atol=1e-3 + 2e-2 * float(re.abs().max()))
     np.testing.assert_allclose(host(du.float()), host(ru), atol=3e-2 * max(1.0, float(ru.abs().max())))
-    assert len(n3) == 3 and torch.equal(n3[0], dn) and torch.equal(n3[1], dd) and torch.equal(n3[2], dw)
+    if not per_frame:
+        assert len(n3) == 3 and torch.equal(n3[0], dn) and torch.equal(n3[1], dd) and torch.equal(n3[2], dw)
+    assert (d._frames[3] is not None) == per_frame
     for a, b in ((an, dn), (ad, dd), (aw, dw), (ae, de), (au, du)):
         assert torch.equal(a, b)
 
