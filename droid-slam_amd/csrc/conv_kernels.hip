@@ -1662,7 +1662,13 @@ __device__ __forceinline__ int b2_slot(int r, int kq) { return kq ^ (((r >> 2) &
 #endif
 constexpr bool kB2Swap = DROID_B2_SWAP != 0;
 
-template <int EPI>
+// REUSE (round 4): the taps run column-major (tx outer, ty inner) and a wave
+// reads the A fragments of a tap column once: fragment i of tap (ty, tx) is band
+// row 2 wm + (i >> 2) + ty + 1, column group i & 3, so the three ty taps of one
+// tx use band rows 2 wm .. 2 wm + 3 - 16 fragments for 96 MFMAs instead of 24.
+// LDS reads per MFMA fall from 12 KB / 32 to 28 KB / 96 (-22 %); the weights
+// stay one (half chunk, tap) stage per DMA step, issued in the same tap order.
+template <int EPI, bool REUSE = true>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_band2_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
   char* lds = reinterpret_cast<char*>(smem);
@@ -1721,9 +1727,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   unsigned woff[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) woff[q] = (unsigned)((((wave + 4 * q) * 16 + (lane >> 2)) * nst9 * BK + lpiece * 8) * 2);
-  // loop stage s = (half chunk bg = s / 9, tap t = s % 9): packed stage (bg >> 1) * 9 + t, K half bg & 1
+  // loop stage s = (half chunk bg = s / 9, step u = s % 9) -> tap t = tap_of(u): packed
+  // stage (bg >> 1) * 9 + t, K half bg & 1 (REUSE: column-major tap order)
+  auto tap_of = [](int u) { return REUSE ? (u % 3) * 3 + u / 3 : u; };
   auto issue_w = [&](int s, int buf) {
-    const int bg = s / 9, t = s - 9 * bg;
+    const int bg = s / 9, t = tap_of(s - 9 * bg);
     const unsigned sb = (unsigned)((((bg >> 1) * 9 + t) * BK + (bg & 1) * 32) * 2);
     const unsigned dst = Bl_a + buf * kB2Wst;
 #pragma unroll
@@ -1763,9 +1771,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   int s = 0, wbuf = 0;
   for (int bg = 0; bg < nb; ++bg) {
     const char* Hb = Hl + (bg & 1) * kB2Band + wm * 2 * 4096;
+    half8 a16[REUSE ? 16 : 1];   // REUSE: band rows 2 wm .. + 3 x 4 column groups of this tap column
 #pragma unroll
     for (int t = 0; t < 9; ++t, ++s) {
-      const int ty = t / 3 - 1, tx = t % 3 - 1;
+      // t = step within the half chunk; tap = tap_of(t)
+      const int tap = tap_of(t);
+      const int ty = tap / 3 - 1, tx = tap % 3 - 1;
       // this wave's DMAs issued after W(s): W(s+1) (2, one stage ago) and the
       // bands issued at stages s-1 / s-2 (6 each, at the first stage of a group)
       const int nafter = (s + 1 < nst ? 2 : 0) + ((t == 1 && bg + 1 < nb) ? 6 : 0) + ((t == 2 && bg + 1 < nb) ? 6 : 0);
@@ -1774,19 +1785,38 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       __builtin_amdgcn_s_barrier();
       if (s + 2 < nst) issue_w(s + 2, wbuf == 0 ? 2 : wbuf - 1);
       if (t == 0 && bg + 1 < nb) issue_band(bg + 1);
-      const char* Ab = Hb + (ty + 1) * 4096;
       const char* Bb = Bl + wbuf * kB2Wst + bbase;
-      half8 af[8], bf[4];
+      half8 bf[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8*>(Bb + j * 1024);
+      if constexpr (REUSE) {
+        if (t % 3 == 0) {   // a new tap column: its 16 A fragments
 #pragma unroll
-      for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const half8*>(Ab + aoff(i & 3, tx) + (i >> 2) * 4096);
+          for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+            for (int c4 = 0; c4 < 4; ++c4)
+              a16[r * 4 + c4] = *reinterpret_cast<const half8*>(Hb + r * 4096 + aoff(c4, tx));
+        }
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = kB2Swap ? __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0)
-                              : __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const half8 af = a16[((i >> 2) + ty + 1) * 4 + (i & 3)];
+            acc[i][j] = kB2Swap ? __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af, acc[i][j], 0, 0, 0)
+                                : __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], acc[i][j], 0, 0, 0);
+          }
+      } else {
+        const char* Ab = Hb + (ty + 1) * 4096;
+        half8 af[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const half8*>(Ab + aoff(i & 3, tx) + (i >> 2) * 4096);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = kB2Swap ? __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0)
+                                : __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
       wbuf = wbuf == 2 ? 0 : wbuf + 1;
     }
   }
@@ -1794,12 +1824,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 }
 
 // Which convs take the two-workgroups-per-CU tile (profiles/r03/band2_r03bh.txt,
-// band2_c2_r03bl.txt): the plain 128-channel-tile convs (EPI_ACT:
-// corr_encoder[2], GraphAgg conv1 / conv2, the per-frame gate term) always
-// (C3: 1.59 vs 1.66 ms); the gate convs only on small grids - at C3 they are
-// slower on it (z|r 7.66 vs 7.41 ms, q 4.12 = 4.12), but on the frontend window
-// (C2, 96 edges: 1152 z|r tiles = 4.5 rounds of the 8-wave tile over 256 CUs)
-// its finer tiles fill the last round: update() 1.252 vs 1.308 ms.
+// band2_c2_r03bl.txt; round 4 with the tap-column A reuse, profiles/r04/
+// gate_tiles_r04b.txt): the plain 128-channel-tile convs (EPI_ACT:
+// corr_encoder[2], GraphAgg conv1 / conv2, the per-frame gate term) and the q
+// gate always (C3: 128->128 1.57 vs 1.67 ms, q 4.08 vs 4.43); the z|r gates
+// only on small grids - at C3 the two tiles tie (7.42 / 7.42 ms), and on the
+// frontend window (C2, 96 edges: 1152 z|r tiles = 4.5 rounds of the 8-wave tile
+// over 256 CUs) the finer tiles fill the last round: update() 1.252 vs 1.308 ms.
 // DROID_CONV_BAND2=0 / 1: none / every shape it takes (A/B runs), read at load;
 // droid_conv_set_tile changes it per call (tests compare both tiles in one process).
 static int& band2_mode() {
@@ -1811,7 +1842,7 @@ static int& band2_mode() {
 }
 static bool band2_for(int epi, long px) {
   const int mode = band2_mode();
-  return mode == 1 || (mode < 0 && (epi == EPI_ACT || px / 256 <= 8L * device_cu_count()));
+  return mode == 1 || (mode < 0 && (epi == EPI_ACT || epi == EPI_GRU_Q || px / 256 <= 8L * device_cu_count()));
 }
 // a band-eligible 3x3 conv of this shape runs on the two-workgroup tile
 static bool band2_shape(int epi, int B, int H, int W, int Cout, int gru_ch) {

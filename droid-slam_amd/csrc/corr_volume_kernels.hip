@@ -46,6 +46,7 @@ struct VolArgs {
   int H, W;          // query and target maps are H x W
   int tiled;         // 1: (E,H,W,ceil(H_l/8),W_l/8,8,8) 8x8 tiles; 0: (E,H,W,H_l,W_l)
   int qblocks;       // ceil(HW / 256)
+  int ablate;        // timing experiments only (DROID_VOL_ABLATE, results invalid): bit 0 no stores, bit 1 no DMA after the first patch
 };
 
 constexpr int kVolQ = 256;                 // query pixels per workgroup
@@ -424,7 +425,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     if (stores_out) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // == kVol2Stores
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();   // patch p landed in buf; every wave done with buf ^ 1
-    if (nxt < gslots) patch_dma(nxt, buf ^ 1);
+    if (nxt < gslots && !(a.ablate & 2)) patch_dma(nxt, buf ^ 1);
     int py, px;
     patch_yx(p, py, px);
     const int ty0 = 8 * py, tx0 = 8 * px;
@@ -477,6 +478,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     // stores (the staging area is this wave's own: a wave barrier suffices)
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int qlim = (a.ablate & 1) ? 0 : HW;   // ablation: every offset out of range (no bytes written)
     // level 0: 32 q x 128 B, 8 lanes per query pixel
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -485,7 +487,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
       const u32x4_t val = *reinterpret_cast<const u32x4_t*>(s0 + q * kVol2S0 + ((seg ^ (q & 7)) << 3));
       const long off = a.tiled ? ((long)qg * TR[0] * (Wl[0] / 8) + py * (Wl[0] / 8) + px) * 64 + seg * 8
                                : (long)qg * HW + (long)(ty0 + seg) * W + tx0;
-      __builtin_amdgcn_raw_buffer_store_b128(val, ro[0], qg < HW ? (int)(off * 2) : (int)kOob, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(val, ro[0], qg < qlim ? (int)(off * 2) : (int)kOob, 0, 0);
     }
     // level 1: 32 q x 4 rows x 8 B (the patch's 4x4 level-1 block)
 #pragma unroll
@@ -497,7 +499,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
       const long off = a.tiled ? ((long)qg * TR[1] * (Wl[1] / 8) + (y >> 3) * (Wl[1] / 8) + (x >> 3)) * 64 +
                                      (y & 7) * 8 + (x & 7)
                                : (long)qg * (Hl[1] * Wl[1]) + (long)y * Wl[1] + x;
-      __builtin_amdgcn_raw_buffer_store_b64(val, ro[1], qg < HW ? (int)(off * 2) : (int)kOob, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(val, ro[1], qg < qlim ? (int)(off * 2) : (int)kOob, 0, 0);
     }
     // level 2: 32 q x 2 rows x 4 B; level 3: 32 q x 2 B
     {
@@ -508,7 +510,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
       const long off = a.tiled ? ((long)qg * TR[2] * (Wl[2] / 8) + (y >> 3) * (Wl[2] / 8) + (x >> 3)) * 64 +
                                      (y & 7) * 8 + (x & 7)
                                : (long)qg * (Hl[2] * Wl[2]) + (long)y * Wl[2] + x;
-      __builtin_amdgcn_raw_buffer_store_b32(val, ro[2], qg < HW ? (int)(off * 2) : (int)kOob, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(val, ro[2], qg < qlim ? (int)(off * 2) : (int)kOob, 0, 0);
     }
     {
       const int qg = q0 + (lane & 31);
@@ -517,7 +519,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
                                      (y & 7) * 8 + (x & 7)
                                : (long)qg * (Hl[3] * Wl[3]) + (long)y * Wl[3] + x;
       const short val = (short)__half_as_ushort(*reinterpret_cast<const __half*>(s3 + (lane & 31)));
-      __builtin_amdgcn_raw_buffer_store_b16(val, ro[3], (lane < 32 && qg < HW) ? (int)(off * 2) : (int)kOob, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b16(val, ro[3], (lane < 32 && qg < qlim) ? (int)(off * 2) : (int)kOob, 0, 0);
     }
     stores_out = true;
     buf ^= 1;
@@ -574,6 +576,7 @@ int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, i
   a.W = W;
   a.tiled = tiled ? 1 : 0;
   a.qblocks = ceil_div(H * W, kVolQ);
+  if (const char* ab = getenv("DROID_VOL_ABLATE")) a.ablate = atoi(ab);   // timing experiments only
   const long grid = (long)E * a.qblocks;
   if (grid == 0) return kOk;
   if (grid > 0x7fffffffL) return fail(kUnsupported, "corr_volume_pyramid: too many edges");

@@ -5,6 +5,8 @@ R="${GRAFT_REPO_ROOT:-$(pwd)}"
 O="$R/gpurun_out/r04b"
 mkdir -p "$O"
 cd "$R"
+timeout -k 10 300 python -u scripts/gate_tiles.py > "$O/gate_tiles.txt" 2>&1 || { tail -20 "$O/gate_tiles.txt"; exit 1; }
+cat "$O/gate_tiles.txt"
 timeout -k 10 300 python -u scripts/vol_bench.py > "$O/vol_v2.txt" 2>&1 || { tail -20 "$O/vol_v2.txt"; exit 1; }
 cat "$O/vol_v2.txt"
 DROID_VOL_V1=1 timeout -k 10 300 python -u scripts/vol_bench.py > "$O/vol_v1.txt" 2>&1 || { tail -20 "$O/vol_v1.txt"; exit 1; }

@@ -1,12 +1,14 @@
 """The update operator's gate convs at the benchmark's shape (C3/C4: 48x64
 feature maps, thousands of edges), on BOTH W=64 tiles the library can pick.
 
-The band-conv entry points route a ConvGRU gate conv to the two-workgroups-
-per-CU tile (conv_band2_kernel) on small grids and to the 8-wave band tiles
-(conv_band_kernel<256,256,..,ZRP> for z|r, <384,128,..,QP> for q) above
-8 x 256 tiles of 256 pixels, i.e. above 170 edges at 48x64 - the C3 bench
-path.  droid_conv_set_tile forces either tile per call, so both are compared
-with torch fp32 in one process here (reference: modules/gru.py:19-32,
+The band-conv entry points route the ConvGRU z|r gate conv to the two-
+workgroups-per-CU tile (conv_band2_kernel) on small grids and to the 8-wave
+band tile (conv_band_kernel<256,256,..,ZRP>) above 8 x 256 tiles of 256
+pixels, i.e. above 170 edges at 48x64 - the C3 bench path; the q gate takes
+conv_band2_kernel at every size since round 4 (its 8-wave tile,
+conv_band_kernel<384,128,..,QP>, stays reachable with policy 0).
+droid_conv_set_tile forces either tile per call, so both are compared with
+torch fp32 in one process here (reference: modules/gru.py:19-32,
 droid_net.py:111-143)."""
 import numpy as np
 import pytest
@@ -50,17 +52,25 @@ def _gates(B, H, W, F_, seed):
     return dict(idx=idx, inp_f=inp_f, h=h, cf=cf, ff=ff, wzr=wzr, wq=wq, bzr=bzr, bq=bq, bbzr=bbzr, bbq=bbq)
 
 
-def _run_gates(t, H, W):
+def _pre_term(t, H, W):
+    """the per-source-frame gate term conv3x3(inp_frames) (a plain conv: its own
+    tile choice, so it is computed once and shared by the runs compared)."""
+    import droid_backends
+    from droid_mi355x.fused import pack_conv
+    pre = torch.empty((t["inp_f"].shape[0], H, W, 384), dtype=torch.float16, device=DEV)
+    droid_backends.conv_nhwc_f16([(t["inp_f"], 0, 128)],
+                                 pack_conv(torch.cat([t["wzr"][:, 128:256], t["wq"][:, 128:256]]), [128]),
+                                 384, 3, out=pre)
+    return pre
+
+
+def _run_gates(t, H, W, pre):
     """z, r*h and the GRU update through droid_conv_gru_pre_f16 (per-frame inp term)."""
     import droid_backends
     from droid_backends import EPI_GRU_Q, EPI_GRU_ZR
     from droid_mi355x.fused import pack_conv
     B = t["h"].shape[0]
     keep = lambda w: torch.cat([w[:, :128], w[:, 256:]], 1)
-    pre = torch.empty((t["inp_f"].shape[0], H, W, 384), dtype=torch.float16, device=DEV)
-    droid_backends.conv_nhwc_f16([(t["inp_f"], 0, 128)],
-                                 pack_conv(torch.cat([t["wzr"][:, 128:256], t["wq"][:, 128:256]]), [128]),
-                                 384, 3, out=pre)
     z = torch.empty((B, H, W, 128), dtype=torch.float16, device=DEV)
     rn = torch.empty_like(z)
     droid_backends.conv_gru_pre_f16([(t["h"], 0, 128), (t["cf"], 0, 128), (t["ff"], 0, 64)],
@@ -86,32 +96,35 @@ def test_conv_gru_gates_c3_shape_both_tiles(B, tile_policy):
     t = _gates(B, H, W, B // 8, seed=31)
     xs = [t["h"], t["inp_f"][t["idx"]].contiguous(), t["cf"], t["ff"]]
     gates = torch.sigmoid(_conv_ref(xs, t["wzr"], t["bzr"], t["bbzr"]))
+    pre = _pre_term(t, H, W)
     outs = {}
-    for mode, tile in ((0, 0), (1, 1), (-1, 0)):
+    # (mode, z|r tile, q tile): the default runs z|r on the 8-wave tile and q on
+    # the two-workgroup tile at this size
+    for mode, tzr, tq in ((0, 0, 0), (1, 1, 1), (-1, 0, 1)):
         tile_policy(mode)
         # the kernel each gate conv is routed to (the rocprof trace of this test,
         # profiles/r04/, shows conv_band_kernel<256,256,..,6,8> / <384,128,..,7,8>)
-        assert droid_backends.conv_gate_tile(EPI_GRU_ZR, B, H, W) == tile, mode
-        assert droid_backends.conv_gate_tile(EPI_GRU_Q, B, H, W) == tile, mode
-        outs[mode] = _run_gates(t, H, W)
-    for mode in (0, 1):
+        assert droid_backends.conv_gate_tile(EPI_GRU_ZR, B, H, W) == tzr, mode
+        assert droid_backends.conv_gate_tile(EPI_GRU_Q, B, H, W) == tq, mode
+        outs[mode] = _run_gates(t, H, W, pre)
+    for mode in (0, 1, -1):
         z, rn, hn = outs[mode]
         assert _maxdiff(z, gates[..., :128]) < 3e-3, mode
         assert _maxdiff(rn, gates[..., 128:] * t["h"].float()) < 3e-3, mode
     del gates
-    for mode in (0, 1):
+    for mode in (0, 1, -1):
         z, rn, hn = outs[mode]
         q = torch.tanh(_conv_ref([rn] + xs[1:], t["wq"], t["bq"], t["bbq"]))
         ref = (1 - z.float()) * t["h"].float() + z.float() * q
         assert _maxdiff(hn, ref) < 4e-3, mode
         del q, ref
-    # the default policy takes the 8-wave tiles at this size: bitwise policy 0
-    # (the two tiles also agree to the fp16 bit on these inputs: the same MFMA
-    # products, fp32 sums in a different order, one fp16 rounding of the gate)
-    for a, b in zip(outs[-1], outs[0]):
+    # the default's z|r is policy 0's bit for bit; the two tiles sum the same
+    # MFMA products in a different order (fp32), so they agree to an fp16 ulp
+    # or two of the gates
+    for a, b in zip(outs[-1][:2], outs[0][:2]):
         assert torch.equal(a, b)
     for a, b in zip(outs[1], outs[0]):
-        assert _maxdiff(a, b) < 2e-3
+        assert _maxdiff(a, b) < 4e-3
 
 
 def test_conv_gru_gates_small_grid_default_is_band2(tile_policy):
@@ -120,12 +133,13 @@ def test_conv_gru_gates_small_grid_default_is_band2(tile_policy):
     from droid_backends import EPI_GRU_Q, EPI_GRU_ZR
     H, W, B = 48, 64, 96
     t = _gates(B, H, W, 12, seed=37)
+    pre = _pre_term(t, H, W)
     outs = {}
     for mode in (1, -1):
         tile_policy(mode)
         assert droid_backends.conv_gate_tile(EPI_GRU_ZR, B, H, W) == 1
         assert droid_backends.conv_gate_tile(EPI_GRU_Q, B, H, W) == 1
-        outs[mode] = _run_gates(t, H, W)
+        outs[mode] = _run_gates(t, H, W, pre)
     for a, b in zip(outs[-1], outs[1]):
         assert torch.equal(a, b)
 
