@@ -1,7 +1,7 @@
 """Time droid_corr_volume_pyramid (add_factors' per-edge volume build) at the C3
 shape: 2048 edges of 48x64 over 256 frames, tiled layout, HIP events.  Prints
 ms, written GB/s and a hash of a 64-edge build (compare kernels across runs:
-DROID_VOL_V1=1 selects the round-3 kernel)."""
+DROID_VOL_VARIANT=1 / 2 / 3 selects the kernel)."""
 import hashlib
 import os
 import sys
@@ -36,5 +36,5 @@ for rep in range(3):
     torch.cuda.synchronize()
     ms = s.elapsed_time(e)
     print("variant %s rep %d: %.2f ms, %.2f GB written, %.0f GB/s" % (
-        "v1" if os.environ.get("DROID_VOL_V1") == "1" else "v2", rep, ms, bytes_ / 1e9, bytes_ / ms / 1e6), flush=True)
+        "v" + os.environ.get("DROID_VOL_VARIANT", "3"), rep, ms, bytes_ / 1e9, bytes_ / ms / 1e6), flush=True)
     del lv
