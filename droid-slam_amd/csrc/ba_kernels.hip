@@ -904,6 +904,85 @@ __device__ __forceinline__ void panel_factor(double* T, double* dinv, int c0, in
   if (bad && lane == 0) atomicOr(flag, 1);
 }
 
+// 1/sqrt(x) in fp64 with ONE Newton step after v_rsq_f64 (~2^-23 relative ->
+// ~2^-46): the pivot chain of the blocked panel below; far inside the 1e-4 parity bar
+__device__ __forceinline__ double rsqrt_f64_1(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  return y * fma(-0.5 * x * y, y, 1.5);
+}
+
+// Round 4: the 16-wide panel in blocks of 4 columns.  The column-at-a-time
+// panel above pays per column an LDS broadcast round trip AND the pivot chain
+// (readlane -> rsqrt -> scale -> next diagonal -> readlane; ~270 clk per column,
+// profiles/r02/chol_timeline_c3_r02af.txt: 2.08 us per 16 columns).  Here, per
+// block of 4 columns: the block's 4x4 diagonal (10 values) reaches every lane by
+// v_readlane, every lane factors it redundantly (4 chained rsqrts, no cross-lane
+// traffic inside the chain), each lane forms its own row of the block's 4
+// columns, and ONE LDS broadcast of those rows updates the panel's later
+// columns - one cross-lane round trip per 4 columns instead of per column.
+// Same outputs as panel_factor: L in T (upper triangle: junk, never read), dinv,
+// unit pivots past Bp, flag bit 0 on a non-SPD pivot.
+__device__ __forceinline__ void panel_factor4(double* T, double* dinv, int c0, int Bp, int lane, int* flag,
+                                              double* xb) {
+  double v[16], invs[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = T[lane * LT + c0 + q];
+  bool bad = false;
+#pragma unroll
+  for (int jb = 0; jb < 16; jb += 4) {
+    double D[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b <= a; ++b) D[a][b] = bcast_lane(v[jb + b], c0 + jb + a);
+    double Lb[4][4], iv[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+#pragma unroll
+      for (int b = 0; b < a; ++b) {
+        double s = D[a][b];
+#pragma unroll
+        for (int c = 0; c < b; ++c) s = fma(-Lb[a][c], Lb[b][c], s);
+        Lb[a][b] = s * iv[b];
+      }
+      double p = D[a][a];
+#pragma unroll
+      for (int c = 0; c < a; ++c) p = fma(-Lb[a][c], Lb[a][c], p);
+      if (c0 + jb + a >= Bp) p = 1.0;   // wave-uniform: unit pivot past the block's real columns
+      bad |= !(p > 0.0 && p < 1e300);
+      iv[a] = rsqrt_f64_1(p);
+      invs[jb + a] = iv[a];
+    }
+    double x[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      double s = v[jb + a];
+#pragma unroll
+      for (int b = 0; b < a; ++b) s = fma(-x[b], Lb[a][b], s);
+      x[a] = s * iv[a];
+      v[jb + a] = x[a];
+    }
+    if (jb < 12) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) xb[lane * 4 + a] = x[a];
+#pragma unroll
+      for (int q = jb + 4; q < 16; ++q)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) v[q] = fma(-x[a], xb[(c0 + q) * 4 + a], v[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) T[lane * LT + c0 + q] = v[q];
+  double mine = 0.0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) mine = (lane == q) ? invs[q] : mine;
+  if (lane < 16) dinv[c0 + lane] = mine;
+  if (bad && lane == 0) atomicOr(flag, 1);
+}
+#ifndef DROID_CHOL_PANEL4
+#define DROID_CHOL_PANEL4 1
+#endif
+
 __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* T0 = sm;
@@ -1002,7 +1081,10 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       __syncthreads();
       CH_STAMP(2);
       for (int c0 = 0; c0 < Bp; c0 += 16) {  // whole 16-wide panels (unit-padded)
-        if (wave == 0) panel_factor(T0, vec + 128, c0, Bp, lane, d.flag, scr);
+        if (wave == 0) {
+          if (DROID_CHOL_PANEL4) panel_factor4(T0, vec + 128, c0, Bp, lane, d.flag, scr);
+          else panel_factor(T0, vec + 128, c0, Bp, lane, d.flag, scr);
+        }
         if (c0 == 0) CH_STAMP(6);
         __syncthreads();
         const int s0 = c0 + 16;
