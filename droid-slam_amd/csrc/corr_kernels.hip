@@ -232,6 +232,116 @@ corr_pyramid_f16_r3_kernel(PyramidArgs args, const float* __restrict__ coords,
 }
 
 // ---------------------------------------------------------------------------
+// Round 4: fp16 radius-3 lookup of ONE level per thread (grid z = level) in the
+// reference layout - the reference-layout drop-in's lookup (CorrBlock.__call__,
+// modules/corr.py:40-50, and the per-level corr_index_forward it calls).  The
+// 4-level kernel above walks a pixel's levels one after another with 16 loads
+// in flight per thread and guarded loads (divergent branches + waits); here each
+// (pixel, level) is its own thread, its 8 window rows (2 aligned 16-B pieces
+// each) are 16 branch-free buffer loads against a per-block descriptor (pieces
+// outside the slice use an out-of-range offset and load zeros), all in flight
+// at once - 4x the memory-level parallelism.  Arithmetic identical to
+// corr_pyramid_f16_r3_kernel (bit-exact at::Half semantics).  Needs W2 % 8 == 0
+// and 16-B aligned levels; PLANAR: coords (B,2,H,W) (corr_index_forward),
+// else (E,H,W,2) at level-0 scale.
+// ---------------------------------------------------------------------------
+struct LookupLvlArgs {
+  const __half* vol[4];
+  int H2[4], W2[4];
+  const float* coords;
+  __half* out;
+  long out_estride;   // output halves per edge
+  int H, W;
+  float coord_scale;  // PLANAR: coordinates already at the level's scale (1); else 1 / 2^l per level
+};
+
+template <bool PLANAR>
+__global__ void __launch_bounds__(256) corr_lookup_lvl_kernel(LookupLvlArgs a) {
+  constexpr int R = 3, RD = 7;
+  const int HW = a.H * a.W;
+  const int p0 = blockIdx.x * 256;
+  const int p = p0 + threadIdx.x;
+  const int e = blockIdx.y;
+  const int lvl = blockIdx.z;
+  const int H2 = a.H2[lvl], W2 = a.W2[lvl], nch = W2 >> 3;
+  const long slice = (long)H2 * W2;
+  const bool live = p < HW;
+  const int pc = live ? p : HW - 1;
+  float cx, cy;
+  if (PLANAR) {
+    cx = a.coords[((long)e * 2 + 0) * HW + pc];
+    cy = a.coords[((long)e * 2 + 1) * HW + pc];
+  } else {
+    cx = a.coords[((long)e * HW + pc) * 2 + 0];
+    cy = a.coords[((long)e * HW + pc) * 2 + 1];
+  }
+  const float s = PLANAR ? a.coord_scale : 1.0f / (float)(1 << lvl);
+  const float x0 = cx * s, y0 = cy * s;
+  const float fx0 = floorf(x0), fy0 = floorf(y0);
+  const float dx = x0 - fx0, dy = y0 - fy0;
+  const int xi0 = (int)fx0, yi0 = (int)fy0;
+  const float w11 = rnd16(dx * dy);
+  const float w10 = rnd16(dx * (1.0f - dy));
+  const float w01 = rnd16((1.0f - dx) * dy);
+  const float w00 = rnd16((1.0f - dx) * (1.0f - dy));
+  // the block's 256 pixel slices as one descriptor (wave-uniform base)
+  const long nblk = min(256, HW - p0);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__half*>(a.vol[lvl] + ((long)e * HW + p0) * slice), (short)0, (int)(nblk * slice * 2), kBufFlags);
+  const unsigned pbase = (unsigned)((p - p0) * slice) * 2u;
+  const int xs = xi0 - R;
+  const int c0 = (xs >= 0) ? (xs >> 3) : -((-xs + 7) >> 3);
+  const int off = xs - 8 * c0;
+  const bool ok0 = live && c0 >= 0 && c0 < nch, ok1 = live && c0 + 1 >= 0 && c0 + 1 < nch;
+  uint4 raw[8][2];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int y1 = yi0 - R + j;
+    const bool yok = y1 >= 0 && y1 < H2;
+    const unsigned o0 = (yok && ok0) ? pbase + (unsigned)(y1 * W2 + 8 * c0) * 2u : kOob;
+    const unsigned o1 = (yok && ok1) ? pbase + (unsigned)(y1 * W2 + 8 * (c0 + 1)) * 2u : kOob;
+    raw[j][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o0, 0, 0));
+    raw[j][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, 0));
+  }
+  __half* o = a.out + (long)e * a.out_estride + (long)lvl * RD * RD * HW + pc;
+  auto taps = [&](int j, float* t) {
+    // taps x = xs .. xs+7 of row j: dwords off/2 .. of the two pieces, funnel-shifted
+    const uint4 p0v = raw[j][0], p1v = raw[j][1];
+    const unsigned u[8] = {p0v.x, p0v.y, p0v.z, p0v.w, p1v.x, p1v.y, p1v.z, p1v.w};
+    const int k = off >> 1;
+    unsigned v[6], w[5];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v[i] = (k & 2) ? u[i + 2] : u[i];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) w[i] = (k & 1) ? v[i + 1] : v[i];
+    const unsigned sh = (off & 1) ? 16u : 0u;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const unsigned q = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
+      t[2 * m + 0] = __half2float(__ushort_as_half((unsigned short)(q & 0xffffu)));
+      t[2 * m + 1] = __half2float(__ushort_as_half((unsigned short)(q >> 16)));
+    }
+  };
+  float prev[8], cur[8];
+  taps(0, prev);
+#pragma unroll
+  for (int j = 1; j <= RD; ++j) {
+    taps(j, cur);
+    const int b = j - 1;
+#pragma unroll
+    for (int x = 0; x < RD; ++x) {
+      float acc = 0.f + rnd16(prev[x] * w00);
+      acc = rnd16(acc + rnd16(cur[x] * w01));
+      acc = rnd16(acc + rnd16(prev[x + 1] * w10));
+      acc = rnd16(acc + rnd16(cur[x + 1] * w11));
+      if (live) o[(long)(x * RD + b) * HW] = __float2half(acc);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) prev[i] = cur[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // corr_index_backward: scatter bilinear-weighted gradients into the volume
 // (correlation_kernels.cu:73-124).  Each (n,y,x) owns its volume slice, so no
 // atomics are needed.
@@ -378,6 +488,15 @@ altcorr_bwd_kernel(const float* __restrict__ fmap1, const float* __restrict__ fm
 // ===========================================================================
 using namespace droid;
 
+// DROID_LOOKUP_V1=1: the round-3 lookup kernels for the reference-layout paths (A/B runs)
+static bool lookup_lvl_on() {
+  static const bool on = [] {
+    const char* e = getenv("DROID_LOOKUP_V1");
+    return !(e && e[0] == '1');
+  }();
+  return on;
+}
+
 extern "C" {
 
 // dtype codes: 0 = fp16, 1 = fp32, 2 = fp64
@@ -388,6 +507,22 @@ int droid_corr_index_forward(int dtype, const void* volume, const float* coords,
   if (B == 0) return kOk;
   const int rd = 2 * radius + 1;
   const long bstride = (long)rd * rd * H * W;
+  if (dtype == 0 && radius == 3 && W2 % 8 == 0 && !(reinterpret_cast<uintptr_t>(volume) & 15) && lookup_lvl_on() &&
+      (long)256 * H2 * W2 * 2 < 0x7fffffffL) {
+    LookupLvlArgs a{};
+    a.vol[0] = (const __half*)volume;
+    a.H2[0] = H2;
+    a.W2[0] = W2;
+    a.coords = coords;
+    a.out = (__half*)corr;
+    a.out_estride = bstride;
+    a.H = H;
+    a.W = W;
+    a.coord_scale = 1.0f;
+    corr_lookup_lvl_kernel<true><<<dim3(ceil_div(H * W, 256), B, 1), 256, 0, stream>>>(a);
+    DROID_LAUNCH_CHECK();
+    return kOk;
+  }
   dim3 grid(ceil_div(H * W, 256), B);
   switch (dtype) {
     case 0: corr_index_fwd_kernel<__half><<<grid, 256, 0, stream>>>((const __half*)volume, coords, 0, 1.0f, (__half*)corr, bstride, B, H, W, H2, W2, radius); break;
@@ -428,6 +563,25 @@ int droid_corr_pyramid_lookup(int dtype, const void* const* levels, const int* H
     if (W2s[l] % 8 != 0 || (reinterpret_cast<uintptr_t>(levels[l]) & 15u)) fast = false;
   }
   dim3 grid(ceil_div(H * W, 256), E);
+  long maxslice = 0;
+  for (int l = 0; l < num_levels; ++l) maxslice = std::max(maxslice, (long)H2s[l] * W2s[l]);
+  if (fast && lookup_lvl_on() && 256 * maxslice * 2 < 0x7fffffffL) {
+    LookupLvlArgs a{};
+    for (int l = 0; l < num_levels; ++l) {
+      a.vol[l] = (const __half*)levels[l];
+      a.H2[l] = H2s[l];
+      a.W2[l] = W2s[l];
+    }
+    a.coords = coords;
+    a.out = (__half*)out;
+    a.out_estride = (long)num_levels * rd * rd * H * W;
+    a.H = H;
+    a.W = W;
+    a.coord_scale = 1.0f;
+    corr_lookup_lvl_kernel<false><<<dim3(ceil_div(H * W, 256), E, num_levels), 256, 0, stream>>>(a);
+    DROID_LAUNCH_CHECK();
+    return kOk;
+  }
   if (fast) {
     PyramidArgs a;
     for (int l = 0; l < 4; ++l) {

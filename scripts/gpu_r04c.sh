@@ -19,7 +19,3 @@ rc=$?
 grep -E "FAILED|ERROR" "$O/pytest.txt" | head -20
 tail -2 "$O/pytest.txt"
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u bench.py --no-cpu-baseline > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
-cat "$O/bench.json"
-timeout -k 10 600 python -u bench.py --reference-layout --no-cpu-baseline > "$O/bench_reflayout.json" 2> "$O/bench_reflayout.err" || { tail -20 "$O/bench_reflayout.err"; exit 1; }
-cat "$O/bench_reflayout.json"
