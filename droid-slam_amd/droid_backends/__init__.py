@@ -418,6 +418,25 @@ def transpose_f16(src, R, C, ldd=None, out=None):
     return out
 
 
+def conv1x1_nchw_f16(src, w, bias, relu=True, out=None):
+    """corr_encoder[0] on an NCHW lookup (include/droid_backends.h:
+    droid_conv1x1_nchw_f16): src (E, C, H, W) fp16 contiguous, w [128][K] fp16
+    (K % 32 == 0, columns >= C zero), bias [128] f32 -> (E, H, W, 128) fp16."""
+    _check_inputs(("src", "w", "bias"), (src, w, bias))
+    _need(src, torch.float16, "src")
+    _need(w, torch.float16, "w")
+    _need(bias, torch.float32, "bias")
+    E, C, H, W = src.shape
+    if w.dim() != 2 or w.shape[0] != 128 or bias.numel() != 128:
+        raise RuntimeError("conv1x1_nchw_f16: w must be (128, K) and bias (128,)")
+    if out is None:
+        out = torch.empty((E, H, W, 128), dtype=torch.float16, device=src.device)
+    with torch.cuda.device(src.device):
+        check(lib.droid_conv1x1_nchw_f16(_ptr(src), int(C), _ptr(w), int(w.shape[1]), _ptr(bias), _ptr(out), int(E),
+                                         int(H * W), int(bool(relu)), _stream(src)), "conv1x1_nchw_f16")
+    return out
+
+
 def dw_head_supported(H, W):
     """Shapes droid_conv_dw_head_f16 accepts (the band tile: W in {16,32,64}, H*W % 256 == 0)."""
     return W in (16, 32, 64) and (H * W) % 256 == 0

@@ -45,6 +45,7 @@ _SIGS = {
     "droid_conv_wino_f16": ([_p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _p, _i,
                              _p, _p, _i, _p, _p, _i, _i, _p], _i),
     "droid_transpose_f16": ([_p, _p, _i, _i, _i, _i, _p], _i),
+    "droid_conv1x1_nchw_f16": ([_p, _i, _p, _i, _p, _p, _i, _i, _i, _p], _i),
     "droid_conv_dw_head_f16": ([_p, _p, _p, _i, _p, _p, _i, _i, _i, _p, _p, _p], _i),
     "droid_flow_enc0_f16": ([_p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_gru_global_f16": ([_p, _p, _p, _p, _i, _i, _p], _i),

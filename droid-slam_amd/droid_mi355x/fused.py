@@ -142,6 +142,15 @@ class PendingAltLookup:
         self.coords = coords
 
 
+class EncodedCorr:
+    """corr_encoder[0]'s output (E,H,W,128) fp16 computed by the caller (the
+    reference-layout drop-in runs it straight on the NCHW lookup,
+    droid_conv1x1_nchw_f16): FusedUpdateModule starts from it."""
+
+    def __init__(self, c1):
+        self.c1 = c1
+
+
 def _version_of(t):
     """t's autograd version counter, or None for an inference tensor (created
     under torch.inference_mode: no counter, reading _version raises)."""
@@ -282,7 +291,9 @@ class FusedUpdateModule(torch.nn.Module):
         levels = (corr.block.pool_levels() if pooled else corr.block.corr_pyramid) if isinstance(corr, PendingLookup) \
             else None
         tiled = levels is not None and getattr(corr.block, "tiled", False)
-        if isinstance(corr, PendingAltLookup):
+        if isinstance(corr, EncodedCorr):
+            c1 = corr.c1
+        elif isinstance(corr, PendingAltLookup):
             coords = corr.coords.reshape(E, H, W, 2).float().contiguous()
             c1 = droid_backends.corr_alt_ce0(corr.pyramid, corr.f1, corr.f2, coords, P["ce0_224"], P["ce0_b"])
         elif levels is not None and droid_backends.corr_lookup_ce0_supported(levels, H, W):
@@ -488,7 +499,16 @@ class ReferenceLayoutUpdateModule(torch.nn.Module):
         else:
             inp_cl = cl(inp)
             self._inp = (inp, _version_of(inp), inp_cl)
-        c200 = cl(corr, 200)
+        # the lookup straight into corr_encoder[0] from its NCHW layout (no
+        # channels-last copy of the 196-channel tensor), else the transposed copy
+        if (corr.dtype == torch.float16 and corr.is_contiguous() and (ht * wd) % 128 == 0
+                and corr.shape[2] <= 224):
+            if self.fused._packed is None:
+                self.fused.pack()
+            P = self.fused._packed
+            c200 = EncodedCorr(droid_backends.conv1x1_nchw_f16(corr[0], P["ce0_224"], P["ce0_b"]))
+        else:
+            c200 = cl(corr, 200)
         motn = (torch.zeros((num, 4, ht, wd), device=dev) if flow is None
                 else flow.reshape(num, 4, ht, wd).float().contiguous())
         if ii is None:

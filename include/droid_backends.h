@@ -204,6 +204,15 @@ int droid_conv_wino_f16(const void* const* srcs, const int* C, const int* cstrid
  * zero-pads the channels); NHWC -> NCHW: R = H*W, C = channels. */
 int droid_transpose_f16(const void* src, void* dst, int B, int R, int C, int ldd, hipStream_t stream);
 
+/* corr_encoder[0] (droid_net.py:84-86: 1x1 conv 196 -> 128, bias, ReLU) read
+ * straight from the reference's NCHW lookup (modules/corr.py:40-50 returns
+ * (1, E, 196, H, W)): src (E, C, HW) fp16, w [128][K] fp16 (K % 32 == 0, K >= C,
+ * columns >= C zero), bias [128] f32 -> out (E, HW, 128) fp16 = act(w . src +
+ * bias), act = ReLU when relu != 0.  The reference-layout drop-in's path (no
+ * channels-last copy of the lookup).  Needs HW % 128 == 0, C <= 256. */
+int droid_conv1x1_nchw_f16(const void* src, int C, const void* w, int K, const float* bias, void* out, int E,
+                           int HW, int relu, hipStream_t stream);
+
 /* UpdateModule delta/weight heads fused (droid_net.py:95-103, 132-133): conv3x3
  * srcs -> 256 (wp, bias, ReLU; the delta.0 || weight.0 hidden map) feeding the
  * block-diagonal conv3x3 256 -> 4 (hw [48][256] fp16, row = tap*4 + c, tap =

@@ -827,3 +827,30 @@ def test_fused_pre_term_follows_in_place_refill():
         b = FusedUpdateModule(m)(net, None, c200, flow, inv, 3, inp_frames=other)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("E,C,H,W", [(3, 196, 48, 64), (2, 196, 16, 24), (5, 100, 8, 16)])
+def test_conv1x1_nchw_matches_torch(E, C, H, W):
+    """corr_encoder[0] straight from the NCHW lookup (droid_conv1x1_nchw_f16)
+    vs torch fp32 (droid_net.py:84-86), and vs the channels-last 1x1 conv the
+    fused path runs on the transposed tensor."""
+    import droid_backends
+    from droid_mi355x.fused import pack_conv
+    g = torch.Generator(device=DEV).manual_seed(47)
+    src = (2 * torch.randn((E, C, H, W), generator=g, device=DEV)).half()
+    w = torch.randn((128, C), generator=g, device=DEV) / C ** 0.5
+    b = torch.randn(128, generator=g, device=DEV)
+    K = (C + 31) // 32 * 32
+    wk = torch.zeros((128, K), device=DEV)
+    wk[:, :C] = w
+    out = droid_backends.conv1x1_nchw_f16(src, wk.half().contiguous(), b)
+    ref = torch.relu(torch.einsum("oc,echw->ehwo", w.half().float(), src.float()) + b)
+    np.testing.assert_allclose(host(out.float()), host(ref), atol=2e-2, rtol=1e-2)
+    nhwc = torch.zeros((E, H, W, (C + 7) // 8 * 8), dtype=torch.float16, device=DEV)
+    nhwc[..., :C] = src.permute(0, 2, 3, 1)
+    cl = torch.empty((E, H, W, 128), dtype=torch.float16, device=DEV)
+    wp = torch.zeros((128, nhwc.shape[-1], 1, 1), device=DEV)
+    wp[:, :C, 0, 0] = w
+    droid_backends.conv_nhwc_f16([(nhwc, 0, nhwc.shape[-1])], pack_conv(wp, [nhwc.shape[-1]]), 128, 1, bias=b, act=1,
+                                 out=cl)
+    assert float((out.float() - cl.float()).abs().max()) < 2e-3
