@@ -913,17 +913,27 @@ class BaPlan:
                                                       dtype=torch.float32, device=poses.device)
         if iterations <= 0:
             return dx.zero_(), dz
-        self.check_status()
+        capturing = torch.cuda.is_current_stream_capturing()
+        if not capturing:
+            self.check_status()
         with torch.cuda.device(poses.device):
             check(lib.droid_ba_run(self._h, _ptr(self.workspace), _ptr(poses), _ptr(disps), _ptr(intrinsics),
                                    _ptr(disps_sens), _ptr(targets), _ptr(weights), _ptr(eta), int(iterations),
                                    float(lm), float(ep), _ptr(dx), _ptr(dz), _stream(poses)), "ba")
-            self._record_status()
+            if not capturing:   # a captured run's status is recorded after each replay
+                self._record_status()
         return dx, dz
 
 
 _PLAN_CACHE = OrderedDict()
 _PLAN_CACHE_SIZE = 8
+_LAST_PLAN = [None]
+
+
+def last_plan():
+    """the plan of the last ba() call (a caller replaying a captured ba keeps it
+    alive with the graph and records its status after each replay)."""
+    return _LAST_PLAN[0]
 
 
 def check_status():
@@ -972,6 +982,10 @@ def get_plan(ii_host, jj_host, num_frames, ht, wd, t0, t1, eta_rows, motion_only
            int(eta_rows), bool(motion_only), str(device), own, gkey)
     plan = _PLAN_CACHE.get(key)
     if plan is None:
+        if torch.cuda.is_current_stream_capturing():
+            # its workspace would live in the graph's pool and its upload be a
+            # captured host copy: a plan must exist before a capture
+            raise RuntimeError("ba: no plan for this edge set inside a HIP graph capture")
         plan = BaPlan(ii_host, jj_host, num_frames, ht, wd, t0, t1, eta_rows, motion_only, device, own, gedges)
         _PLAN_CACHE[key] = plan
         while len(_PLAN_CACHE) > _PLAN_CACHE_SIZE:
@@ -1012,6 +1026,7 @@ def ba(poses, disps, intrinsics, disps_sens, targets, weights, eta, ii, jj, t0, 
         jj_host = jj.cpu().numpy()
     eta_rows = eta.numel() // (H * W) if eta.numel() else 0
     plan = get_plan(ii_host, jj_host, N, H, W, int(t0), int(t1), eta_rows, motion_only, poses.device)
+    _LAST_PLAN[0] = plan
     dx, dz = plan.run(poses, disps, intrinsics, disps_sens, targets, weights, eta, int(iterations), lm, ep)
     if sync:
         plan.check_status()

@@ -78,6 +78,10 @@ def upload(arr, device):
     pinned memory and copied asynchronously."""
     t = torch.from_numpy(np.ascontiguousarray(arr))
     if torch.device(device).type == "cuda":
+        if torch.cuda.is_current_stream_capturing():
+            # a captured copy would re-read this staging buffer at every replay,
+            # after the host allocator has recycled it (FactorGraph._update_graphed)
+            raise RuntimeError("upload() inside a HIP graph capture")
         t = t.pin_memory()
     return t.to(device, non_blocking=True)
 

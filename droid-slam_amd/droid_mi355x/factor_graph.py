@@ -62,6 +62,13 @@ class FactorGraph:
         self.tiled_volume = os.environ.get("DROID_TILED_VOLUME", "1") != "0"
         self._version = 0          # bumped by every edge edit
         self._ba_tw = None         # (key, BA target rows, BA weight rows), see _ba_inputs
+        # HIP-graph replay of update() per edge set (fused operator, one device,
+        # frontend-sized graphs where host issue and launch gaps dominate):
+        # DROID_UPDATE_GRAPHS=1 enables it (off by default; see _update_graphed)
+        self.graphs = os.environ.get("DROID_UPDATE_GRAPHS", "0") == "1"
+        self._graph = None         # captured update: dict(key, graph, plan, state, keep)
+        self._graph_warm = None    # key of the last eager call (the capture follows it)
+        self._cap_stream = None
 
     # -- per-edge state layout ------------------------------------------------
     @property
@@ -114,8 +121,10 @@ class FactorGraph:
     def _edited(self):
         """edge-set version (sharded BA: the global-edge cache key) - every edit,
         issued in lockstep on all ranks even when it leaves this rank's shard
-        unchanged, bumps it, so all ranks agree on when to re-gather."""
+        unchanged, bumps it, so all ranks agree on when to re-gather.  Drops a
+        captured update graph."""
         self._version += 1
+        self._drop_graph()
         if self.comm is not None:
             self.comm["version"] = self.comm.get("version", 0) + 1
 
@@ -246,6 +255,99 @@ class FactorGraph:
 
     # -- the hot path (factor_graph.py:196-242) -------------------------------
     def update(self, t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, motion_only=False):
+        args = (t0, t1, itrs, use_inactive, EP, motion_only)
+        if self.graphs and self.fused and self.comm is None and 0 < len(self._ii) <= 512:
+            return self._update_graphed(args)
+        self._update(*args)
+
+    def _drop_graph(self):
+        """Release the captured update graph.  The caller's stream is synchronised
+        first: no replay may still be running when the graph's executable and its
+        private memory pool go."""
+        if self._graph is not None:
+            torch.cuda.current_stream(self.device).synchronize()
+            self._graph = None
+        self._graph_warm = None
+
+    def _graph_keep(self):
+        """Strong references to every tensor the captured body reads or writes
+        by raw pointer (caches that a later call could replace and free while
+        the graph still holds their addresses)."""
+        keep = dict(dev=dict(self._dev_cache), inp=self.inp, inp_frames=self._inp_frames, ba_tw=self._ba_tw,
+                    damping=self.damping, target_inac=self.target_inac, weight_inac=self.weight_inac,
+                    pre=getattr(self.update_op, "_pre", None), packed=getattr(self.update_op, "_packed", None))
+        if self.corr is not None:
+            keep["corr"] = (list(getattr(self.corr, "_pyr", [])), getattr(self.corr, "_slot_dev", None))
+        return keep
+
+    def _update_graphed(self, args):
+        """update() through a HIP graph of this edge set: the first call is eager
+        (it fills every cache the body reads: edge-list uploads, the BA plan,
+        the per-frame inp rows and gate term), the second captures the body and
+        replays it, later ones only replay.  The per-edge state (net, target,
+        weight) lives in static buffers the graph reads and refills, so replay
+        t+1 sees replay t's output; an edge edit drops the graph.
+
+        Capture safety (round 4): nothing may be uploaded or
+        allocated for the body's inputs inside the capture - a host-to-device
+        copy captured from a pinned staging buffer would re-read that buffer at
+        every replay after the host allocator had recycled it (stale indices),
+        and a BA plan built inside the capture would live in the graph's pool.
+        upload() and get_plan() raise during a capture; the capture then falls
+        back to eager for good.  Every tensor the graph addresses is kept alive
+        by the graph record, and a graph is only released after its stream is
+        synchronised."""
+        key = (self._version, self.video.counter.value) + args
+        g = self._graph
+        if g is not None and g["key"] == key:
+            for name in ("net", "target", "weight"):      # state replaced from outside: copy it in
+                cur = getattr(self, name)
+                if cur is not g[name]:
+                    g[name].copy_(cur)
+                    setattr(self, name, g[name])
+            g["graph"].replay()
+            g["plan"]._record_status()
+            self.age += 1
+            return
+        if self._cap_stream is None:
+            self._cap_stream = torch.cuda.Stream(device=self.device)
+        cs, main = self._cap_stream, torch.cuda.current_stream(self.device)
+        if self._graph_warm != key:
+            # eager warm-up on the capture stream (torch's rule: lazily created
+            # per-stream state must not be born inside the capture), ordered both ways
+            self._drop_graph()
+            self._graph_warm = key
+            cs.wait_stream(main)
+            with torch.cuda.stream(cs):
+                self._update(*args)
+            main.wait_stream(cs)
+            return
+        droid_backends.check_status()        # no host wait may happen inside the capture
+        saved = (self.net, self.target, self.weight)
+        static = dict(net=self.net, target=self.target, weight=self.weight.clone())
+        self.weight = static["weight"]
+        graph = torch.cuda.CUDAGraph()
+        cs.wait_stream(main)
+        try:
+            with torch.cuda.graph(graph, stream=cs):
+                plan = self._update(*args, age=False)
+                for name in ("net", "target", "weight"):   # this update's state -> the static inputs
+                    static[name].copy_(getattr(self, name))
+        except Exception:
+            # capture unsupported here (an upload, a plan build, an op that syncs): stay eager
+            main.wait_stream(cs)
+            self.net, self.target, self.weight = saved
+            self.graphs = False
+            self._update(*args)
+            return
+        main.wait_stream(cs)
+        self.net, self.target, self.weight = static["net"], static["target"], static["weight"]
+        self._graph = dict(key=key, graph=graph, plan=plan, keep=self._graph_keep(), **static)
+        graph.replay()
+        plan._record_status()
+        self.age += 1
+
+    def _update(self, t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, motion_only=False, age=True):
         ht, wd = self.ht, self.wd
         E = len(self._ii)
         ii, jj = self.ii, self.jj
@@ -340,7 +442,9 @@ class FactorGraph:
                           t0, t1, itrs=itrs, lm=1e-4, ep=0.1, motion_only=motion_only,
                           ii_host=ii_h, jj_host=jj_h, comm=self.comm,
                           edge_tag="update+inactive" if use_inactive else "update")
-        self.age += 1
+        if age:
+            self.age += 1
+        return droid_backends.last_plan()
 
     def _ba_inputs(self, m, E):
         """The BA's target / weight inputs (rows,2,H,W) f32 for update(): the

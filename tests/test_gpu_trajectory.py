@@ -41,7 +41,8 @@ def _report(name, rep):
 
 
 @pytest.mark.timeout(600)
-def test_frontend_sequence_matches_oracle():
+@pytest.mark.parametrize("graphs", [False, True])
+def test_frontend_sequence_matches_oracle(graphs):
     from droid_mi355x import DepthVideo, FactorGraph, UpdateModule
     from droid_mi355x.fused import FusedUpdateModule
     torch.backends.cudnn.allow_tf32 = False
@@ -51,11 +52,14 @@ def test_frontend_sequence_matches_oracle():
     params = {k: v.detach().float().cpu().numpy() for k, v in m.state_dict().items()}
     video = DepthVideo(image_size=(8 * H, 8 * W), buffer=FRAMES + 2, device="cuda")
     g = FactorGraph(video, FusedUpdateModule(m), device="cuda", max_factors=48)
+    g.graphs = graphs   # the HIP-graph replay of update() per edge set (FactorGraph._update_graphed)
     dev = DeviceSide(video, g)
     ref = oracle_side(params, H, W, FRAMES + 2, device="cuda")
     with torch.no_grad():
         rep = replay(dev, ref, synthetic_stream(H, W), FRAMES, keyframe_thresh=KEYFRAME_THRESH)
-    _report("trajectory_parity.json", rep)
+    _report("trajectory_parity%s.json" % ("_graphs" if graphs else ""), rep)
+    if graphs:
+        assert g.graphs, "the capture fell back to eager"
     summary = {k: v for k, v in rep.items() if k != "steps"}
     print(summary)
     # the sequence exercised what it should

@@ -372,3 +372,40 @@ def test_reference_update_structure_with_dropin_module():
     ref = oba.ba(**prob, iterations=a[11], lm=a[12], ep=a[13], motion_only=a[14])
     np.testing.assert_allclose(host(vb.poses[:n]), ref["poses"][:n], atol=1e-4)
     np.testing.assert_allclose(host(vb.disps[:n]), np.maximum(ref["disps"][:n], 0.001), atol=1e-4)
+
+
+def test_update_graph_replay_matches_eager():
+    """update() replayed from a captured HIP graph (FactorGraph.graphs,
+    DROID_UPDATE_GRAPHS=1) gives the eager body's results bit for bit, across
+    replays, an edge edit (graph dropped, eager, re-captured), use_inactive and
+    a keyframe removal (the capture's safety rules)."""
+    from droid_mi355x import FactorGraph, UpdateModule, synthetic
+    from droid_mi355x.fused import FusedUpdateModule
+    m = UpdateModule().to("cuda").eval()
+    det_fill(m)
+    ii, jj = synthetic.c2_edges()
+    runs = []
+    for graphs in (True, False):
+        video = _c2_video(48, 64, seed=57)
+        g = FactorGraph(video, FusedUpdateModule(m), device="cuda")
+        g.graphs = graphs
+        with torch.no_grad():
+            g.add_factors(ii, jj)
+            for _ in range(4):
+                g.update()
+            g.rm_factors(g._ii < 7, store=True)
+            for _ in range(3):
+                g.update(use_inactive=True)
+            g.add_factors(np.array([15, 4]), np.array([4, 15]))
+            for _ in range(3):
+                g.update(use_inactive=True)
+            g.rm_keyframe(12)
+            for _ in range(3):
+                g.update(use_inactive=True)
+        torch.cuda.synchronize()
+        runs.append((g, video))
+    (ga, va), (gb, vb) = runs
+    assert ga.graphs and ga._graph is not None and gb._graph is None
+    for x, y in ((va.poses, vb.poses), (va.disps, vb.disps), (ga.net, gb.net), (ga.target, gb.target),
+                 (ga.weight, gb.weight), (ga.damping, gb.damping), (ga.age, gb.age)):
+        np.testing.assert_array_equal(host(x), host(y))
