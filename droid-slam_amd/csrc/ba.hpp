@@ -108,7 +108,7 @@ struct BaPlan {
   std::vector<int> perm, outmap;
   int order_kind = 0;                   // 0 identity, 1 reverse Cuthill-McKee, 2 minimum degree, 3 nested dissection
   CholStructure cs;
-  size_t sync_bytes = 0;                // ticket, abort, tile versions, y versions, x flags
+  size_t sync_bytes = 0;                // ticket, abort, tile versions, y versions, x flags, L^-1 flags
   // device layout (byte offsets into the workspace)
   size_t off_ints = 0, off_hpart = 0, off_gram = 0, off_qw = 0, off_ei = 0, off_M = 0, off_x = 0,
          off_flag = 0, off_sync = 0, off_linv = 0, off_ybuf = 0, total = 0;

@@ -696,7 +696,7 @@ struct CholDev {
   const int* ycnt;    // [nbc] final version of y_c
   const int* outmap;  // [n] permuted variable -> dx index
   int nslots;
-  int* sync;    // [0] ticket [1] abort [4..] ver[nslots] | yver[nbc] | xdone[nbc]
+  int* sync;    // [0] ticket [1] abort [4..] ver[nslots] | yver[nbc] | xdone[nbc] | lver[nbc]
   int* flag;    // bit 0: factorisation failed (dx = 0), bit 1: spin timeout
   double* linv; // [nbc][64][64]
   double* ybuf; // [nbc*64]
@@ -1005,6 +1005,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
   int* ver = d.sync + 4;
   int* yver = ver + d.nslots;
   int* xdone = yver + nbc;
+  int* lver = xdone + nbc;  // L_kk^-1 stored (published after the pivot tiles)
   auto SL = [&](int i, int j) { return d.slot[i * nbc + j]; };
   if (d.inject && blockIdx.x == 0 && tid == 0) {
     __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1030,8 +1031,8 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           break;
         }
         case kTrsm: {
-          const int s = SL(i, k), sk = SL(k, k);
-          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&ver[sk], d.fin[sk], abort_w, d.flag);
+          const int s = SL(i, k);
+          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&lver[k], 1, abort_w, d.flag);
           break;
         }
         case kUpdate: {
@@ -1041,8 +1042,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           break;
         }
         case kBsolve: {
-          const int s = SL(i, i);
-          ok = poll_ge(&ver[s], d.fin[s], abort_w, d.flag) && poll_ge(&yver[i], d.ycnt[i], abort_w, d.flag);
+          ok = poll_ge(&lver[i], 1, abort_w, d.flag) && poll_ge(&yver[i], d.ycnt[i], abort_w, d.flag);
           break;
         }
         default: {  // kBupd (r = i, c = j)
@@ -1108,7 +1108,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       const int R1 = R0 + 64, nr1 = below ? min(64, n + 1 - R1) : 0;
       const int sb = below ? SL(k + 1, k) : 0;
       if (below && tid == 0) shi[2] = poll_ge(&ver[sb], d.fin[sb] - 1, abort_w, d.flag) ? 1 : 0;
-      // Linv of the Bp x Bp pivot block (unit-diagonal padding past Bp)
+      // lower-triangular copy of the Bp x Bp pivot block (unit-diagonal padding past Bp)
       for (int idx = tid; idx < 64 * 64; idx += 256) {
         const int r = idx >> 6, c = idx & 63;
         T2[r * LT + c] = (r < Bp) ? (c <= r ? T0[r * LT + c] : 0.0) : (r == c ? 1.0 : 0.0);
@@ -1118,9 +1118,12 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       __syncthreads();
       if (below) {
         if (!__builtin_amdgcn_readfirstlane(shi[2])) break;
-        tile_issue(rM, sb, nr1, Bp, pre);  // lands during the Linv work
+        tile_issue(rM, sb, nr1, Bp, pre);  // lands during the diagonal-block inverses
       }
-      if (wave == 0) {  // the four 16x16 diagonal blocks; lane = 16 * block + column
+      tile_store(rM, skk, Br, Bp, T0);
+      const bool rhs = Br > Bp;
+      if (rhs && tid < 32) st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[Bp * LT + 2 * tid]));
+      if (wave == 0) {  // the four 16x16 diagonal blocks of L^-1; lane = 16 * block + column
         const int base = 16 * (lane >> 4), cc = lane & 15;
         double xv[16];
 #pragma unroll
@@ -1133,7 +1136,49 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
 #pragma unroll
         for (int t = 0; t < 16; ++t) T1[(base + t) * LT + base + cc] = xv[t];
       }
-      __syncthreads();
+      if (below) {
+        // trsm(k+1, k) by blocked forward substitution, L(k+1,k) L_kk^T = A(k+1,k):
+        // X_p = (A_p - sum_{j<p} X_j L_pj^T) D_p^-T per 16-column block p, with D_p^-1
+        // the diagonal blocks just formed.  Each wave owns 16 rows, so the four
+        // block steps need no barrier, and the full L_kk^-1 (consumed only by the
+        // trsm/back-solve tasks of later tiles) is finished AFTER the publish below:
+        // it is off the critical chain potrf(k) -> update(k+2, k+1, k) -> potrf(k+1).
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();  // T0's store reads are done; D_p^-1 is in T1
+        tile_commit(pre, T0);
+        __syncthreads();
+        const int r0 = 16 * wave;
+        double* sw = scr + wave * 272;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          dbl4 S;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) S[q] = T0[(r0 + 4 * q + fk) * LT + 16 * p + fr];
+#pragma unroll
+          for (int j = 0; j < p; ++j)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+              S = mfma64(-T0[(r0 + fr) * LT + 16 * j + 4 * kk + fk], T2[(16 * p + fr) * LT + 16 * j + 4 * kk + fk], S);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sw[(4 * q + fk) * 17 + fr] = S[q];
+          asm volatile("" ::: "memory");
+          dbl4 X = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+            X = mfma64(sw[fr * 17 + 4 * kk + fk], T1[(16 * p + fr) * LT + 16 * p + 4 * kk + fk], X);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) T0[(r0 + 4 * q + fk) * LT + 16 * p + fr] = X[q];
+          asm volatile("" ::: "memory");
+        }
+        __syncthreads();
+        CH_STAMP(5);
+        tile_store(rM, sb, nr1, Bp, T0);
+        const bool rhs1 = (k + 1 == nbr - 1);
+        if (rhs1 && tid < 32) st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[(n - R1) * LT + 2 * tid]));
+        publish(&ver[skk], d.fin[skk], &ver[sb], d.fin[sb], rhs1 ? &yver[k] : nullptr, 1);
+      } else {
+        publish(&ver[skk], d.fin[skk], rhs ? &yver[k] : nullptr, 1);
+      }
       for (int I = 1; I < 4; ++I) {  // Linv[I][J] = -Dinv_I sum_{K=J}^{I-1} L[I][K] Linv[K][J]
         if (wave < I) {
           const int J = wave;
@@ -1156,28 +1201,8 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         __syncthreads();
       }
       CH_STAMP(4);
-      tile_store(rM, skk, Br, Bp, T0);
       tile_store(rL, k, 64, 64, T1);
-      const bool rhs = Br > Bp;
-      if (rhs && tid < 32) st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[Bp * LT + 2 * tid]));
-      if (below) {  // trsm(k+1, k): L(k+1,k) = A(k+1,k) L_kk^-T with L_kk^-1 still in T1
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __syncthreads();  // T0's store reads are done
-        tile_commit(pre, T0);
-        __syncthreads();
-        dbl4 acc[2][2] = {};
-        gemm_nt64(T0, T1, acc, wr, wc, lane, 1.0);
-        __syncthreads();
-        acc_store(T0, acc, wr, wc, lane);
-        __syncthreads();
-        CH_STAMP(5);
-        tile_store(rM, sb, nr1, Bp, T0);
-        const bool rhs1 = (k + 1 == nbr - 1);
-        if (rhs1 && tid < 32) st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[(n - R1) * LT + 2 * tid]));
-        publish(&ver[skk], d.fin[skk], &ver[sb], d.fin[sb], rhs1 ? &yver[k] : nullptr, 1);
-      } else {
-        publish(&ver[skk], d.fin[skk], rhs ? &yver[k] : nullptr, 1);
-      }
+      publish(&lver[k], 1);
     } else if (type == kTrsm) {
       const int R0 = 64 * i, C0 = 64 * k, nr = min(64, n + 1 - R0), nc = min(64, n - C0);
       const int s = SL(i, k);

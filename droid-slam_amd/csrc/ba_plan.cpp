@@ -766,7 +766,7 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, co
   p.o_widef = put(p.wide_f); p.o_wideeoff = put(p.wide_eoff); p.o_widetasks = put(p.wide_tasks);
   if (p.ints.empty()) p.ints.push_back(0);
   const int nbc = p.cs.nbc;
-  p.sync_bytes = align_up((size_t)(4 + p.cs.nslots + 2 * nbc) * 4, 16);
+  p.sync_bytes = align_up((size_t)(4 + p.cs.nslots + 3 * nbc) * 4, 16);
   if ((size_t)std::max(p.cs.nslots, 1) * kTile * 8 >= 0x80000000ull)
     return fail(kUnsupported, "ba: factor tiles exceed the 2 GB buffer-resource range");
 
@@ -840,7 +840,7 @@ int droid_chol_plan_create(int n, void** plan_out) {
   p->o_slot = put(p->cs.slot); p->o_fin = put(p->cs.fin); p->o_ycnt = put(p->cs.ycnt);
   p->o_outmap = put(p->outmap);
   if (p->ints.empty()) p->ints.push_back(0);
-  p->sync_bytes = align_up((size_t)(4 + p->cs.nslots + 2 * nbc) * 4, 16);
+  p->sync_bytes = align_up((size_t)(4 + p->cs.nslots + 3 * nbc) * 4, 16);
   size_t off = 0;
   p->off_ints = off; off = align_up(off + p->ints.size() * 4, 256);
   p->off_M = off; off = align_up(off + (size_t)std::max(p->cs.nslots, 1) * kTile * 8, 256);

@@ -42,12 +42,14 @@ t0 = p[p[:, 0] > 0, 0].min()
 print("%s: n=%d tasks=%d, Cholesky span %.1f us" % (cfg, plan.P * 6, plan.ntasks, p[:, 7].max() - t0))
 pot = np.nonzero(p[:, 3] > 0)[0]
 pot = pot[np.argsort(p[pot, 0])]
-names = ["wait deps", "last update", "panels", "Linv", "stores+trsm(k+1,k)", "publish"]
+# stamps: 0 ticket, 1 deps met, 2 last update applied, 6 first panel, 3 panels done,
+# 5 trsm(k+1,k) done (pivot tiles published right after), 4 L_kk^-1 done, 7 task end
+names = ["wait deps", "last update", "panels", "diag inv + trsm(k+1,k)", "stores+publish+Linv", "Linv store"]
 rows = []
 for a, k in enumerate(pot):
     r = p[k]
-    b5 = r[5] if r[5] > 0 else r[4]
-    ph = [r[1] - r[0], r[2] - r[1], r[3] - r[2], r[4] - r[3], b5 - r[4], r[7] - b5]
+    b5 = r[5] if r[5] > 0 else r[3]
+    ph = [r[1] - r[0], r[2] - r[1], r[3] - r[2], b5 - r[3], r[4] - b5, r[7] - r[4]]
     step = (p[pot[a + 1], 2] - r[2]) if a + 1 < len(pot) else np.nan
     rows.append(ph + [r[7] - r[0], step])
 rows = np.array(rows)
@@ -58,8 +60,8 @@ print("first panel_factor (wave 0, 16 columns) median %.2f us" % np.median(pf))
 other = np.setdiff1d(np.nonzero(p[:, 7] > 0)[0], pot)
 dur = p[other, 7] - p[other, 1]
 print("other tasks (%d): median work %.2f us, median wait %.2f us" % (len(other), np.median(dur), np.median(p[other, 1] - p[other, 0])))
-# where the chain waits: potrf(k+1)'s other updates done (its stamp 1) vs potrf(k)'s publish (stamp 7)
-late = np.array([p[pot[a + 1], 1] - p[pot[a], 7] for a in range(len(pot) - 1)])
+# where the chain waits: potrf(k+1)'s other updates done (its stamp 1) vs potrf(k)'s trsm(k+1,k) (stamp 5)
+late = np.array([p[pot[a + 1], 1] - p[pot[a], 5] for a in range(len(pot) - 1)])
 print("other updates of A(k+1,k+1) done after potrf(k) published: %d of %d steps, median %.2f us (p90 %.2f); "
       "last-update phase when not late: median %.2f us" % ((late > 0).sum(), len(late), np.median(late),
                                                             np.percentile(late, 90),

@@ -81,6 +81,7 @@ def emulate(M, n, st):
     ver = np.zeros(st["nslots"], int)
     yver = np.zeros(nbc, int)
     xdone = np.zeros(nbc, int)
+    lver = np.zeros(nbc, int)     # L_kk^-1 stored: published by potrf(k) after its pivot tiles
     linv = {}
     y = np.zeros(nbc * 64)
     x = np.zeros(n)
@@ -113,16 +114,18 @@ def emulate(M, n, st):
             if b:                                                    # trsm(k+1, k)
                 sb = S(k + 1, k)
                 assert sb >= 0 and ver[sb] >= fin[sb] - 1
-                M[blk(k + 1), col(k)] = M[blk(k + 1), col(k)] @ linv[k].T
+                # blocked forward substitution against L_kk itself (not via L_kk^-1)
+                M[blk(k + 1), col(k)] = np.linalg.solve(L, M[blk(k + 1), col(k)].T).T
                 if k + 1 == nbr - 1:
                     y[64 * k:64 * k + Bp] = M[n, col(k)]
                     yver[k] = 1
                 ver[sb] = fin[sb]
             else:
                 assert k + 1 >= nbr or S(k + 1, k) < 0
+            lver[k] = 1
         elif t == TRSM:
             s = S(i, k)
-            assert s >= 0 and ver[s] >= fin[s] - 1 and ver[S(k, k)] >= fin[S(k, k)]
+            assert s >= 0 and ver[s] >= fin[s] - 1 and lver[k]
             M[blk(i), col(k)] = M[blk(i), col(k)] @ linv[k].T
             if i == nbr - 1:
                 y[64 * k:64 * k + (col(k).stop - col(k).start)] = M[n, col(k)]
@@ -136,7 +139,7 @@ def emulate(M, n, st):
             ver[s] = a + 1
         elif t == BSOLVE:                                            # + bupd(c, c-1) when fused
             c = i
-            assert ver[S(c, c)] >= fin[S(c, c)] and yver[c] >= ycnt[c]
+            assert lver[c] and yver[c] >= ycnt[c]
             Bp = col(c).stop - col(c).start
             x[col(c)] = linv[c].T @ y[64 * c:64 * c + Bp]
             xdone[c] = 1
@@ -149,7 +152,7 @@ def emulate(M, n, st):
             assert xdone[r] and ver[S(r, c)] >= fin[S(r, c)] and yver[c] == 1 + a
             y[64 * c:64 * c + 64] -= M[col(r), col(c)].T @ x[col(r)]
             yver[c] = 2 + a
-    assert np.all(ver == fin) and np.all(yver == ycnt) and np.all(xdone == 1)
+    assert np.all(ver == fin) and np.all(yver == ycnt) and np.all(xdone == 1) and np.all(lver == 1)
     return x, len(seen)
 
 
