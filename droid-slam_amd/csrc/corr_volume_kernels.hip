@@ -800,12 +800,14 @@ int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, i
   const long grid = (long)E * a.qblocks;
   if (grid == 0) return kOk;
   if (grid > 0x7fffffffL) return fail(kUnsupported, "corr_volume_pyramid: too many edges");
-  // DROID_VOL_VARIANT=1 / 2: the round-3 kernel / corr_volume_pyramid2_kernel (A/B
-  // runs); the default is corr_volume_pyramid3_kernel (DROID_VOL_V1=1 = variant 1)
+  // DROID_VOL_VARIANT=1 / 3: the round-3 kernel / corr_volume_pyramid3_kernel (A/B
+  // runs); the default is corr_volume_pyramid2_kernel (DROID_VOL_V1=1 = variant 1).
+  // C3, 2048 edges (profiles/r04/vol_v*.txt): v1 33.3 ms, v2 19.9 ms, v3 23.6 ms,
+  // identical bytes (hash64)
   static const int variant = [] {
     const char* e = getenv("DROID_VOL_VARIANT");
     const char* e1 = getenv("DROID_VOL_V1");
-    return e ? atoi(e) : (e1 && e1[0] == '1') ? 1 : 3;
+    return e ? atoi(e) : (e1 && e1[0] == '1') ? 1 : 2;
   }();
   if ((long)H * W * H * W * 2 >= 0x7fffffffL && variant != 1)
     return fail(kUnsupported, "corr_volume_pyramid: an edge's level-0 volume must stay below 2 GB");

@@ -16,7 +16,7 @@ tail -2 "$O/pytest.txt"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u scripts/ba_bench.py C3 C5 > "$O/ba_new.txt" 2>&1 || { tail -20 "$O/ba_new.txt"; exit 1; }
 cat "$O/ba_new.txt"
-for v in t0 p1; do
+for v in t0; do
   DROID_HIP_LIB="$R/droid-slam_amd/lib/ab/libdroid_hip_$v.so" timeout -k 10 300 python -u scripts/ba_bench.py C3 C5 > "$O/ba_$v.txt" 2>&1 || { tail -20 "$O/ba_$v.txt"; exit 1; }
   echo "== $v"; cat "$O/ba_$v.txt"
 done

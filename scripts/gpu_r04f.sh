@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 4: Cholesky chain timelines (profiling build), then the HIP-graph replay
+# of update(): the bitwise unit test first, the trajectory with replay on last
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(pwd)}"
+O="$R/gpurun_out/r04f"
+mkdir -p "$O"
+cd "$R"
+for c in C3 C5; do
+  timeout -k 10 300 python -u scripts/chol_timeline.py $c > "$O/timeline_$c.txt" 2>&1 || { tail -20 "$O/timeline_$c.txt"; exit 1; }
+  cat "$O/timeline_$c.txt"
+done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_update.py -m gpu -k graph_replay -v --timeout 240 --timeout-method thread \
+  > "$O/pytest_graph_unit.txt" 2>&1
+rc=$?; tail -3 "$O/pytest_graph_unit.txt"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u -m pytest "tests/test_gpu_trajectory.py::test_frontend_sequence_matches_oracle[True]" -m gpu -v --timeout 360 --timeout-method thread \
+  > "$O/pytest_graph_traj.txt" 2>&1
+rc=$?; tail -3 "$O/pytest_graph_traj.txt"; exit $rc
