@@ -456,7 +456,11 @@ def main():
         ms = 1000.0 * elapsed / args.steps
         bytes_per_launch = (LOOKUP_BYTES_PER_EDGE if args.reference_op else LOOKUP_CE0_BYTES_PER_EDGE) * e_local
         achieved = bytes_per_launch / (lookup_ms * 1e-3) / 1e9 if lookup_ms else None
-        lookup_roof = {"kernel": ("corr_pyramid_f16_r3_kernel<NCHW> (4-level lookup)" if args.reference_op else
+        ref_lookup = ("corr_lookup_lvl_kernel<false, true> (4-level lookup, NCHW out, 8x8-tiled volume pool)"
+                      if os.environ.get("DROID_TILED_VOLUME", "1") != "0" else
+                      "corr_pyramid_f16_r3_kernel<NCHW> (4-level lookup)" if os.environ.get("DROID_LOOKUP_V1") == "1"
+                      else "corr_lookup_lvl_kernel<false> (4-level lookup, NCHW out)")
+        lookup_roof = {"kernel": (ref_lookup if args.reference_op else
                                   "corr_ce0_kernel (4-level lookup fused with corr_encoder[0] 1x1 196->128)"),
                        "bound": "hbm",
                        "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -248,6 +248,7 @@ corr_pyramid_f16_r3_kernel(PyramidArgs args, const float* __restrict__ coords,
 struct LookupLvlArgs {
   const __half* vol[4];
   int H2[4], W2[4];
+  const int* slot;    // TILED: volume row of each edge (a slot pool) or null = e
   const float* coords;
   __half* out;
   long out_estride;   // output halves per edge
@@ -255,7 +256,13 @@ struct LookupLvlArgs {
   float coord_scale;  // PLANAR: coordinates already at the level's scale (1); else 1 / 2^l per level
 };
 
-template <bool PLANAR>
+// TILED (round 4): the same lookup reading the 8x8-tiled slot pool of the fused
+// path, (R,H,W,ceil(H2/8),W2/8,8,8): a window row is still two 16-B pieces (one
+// tile row of tile columns c0, c0 + 1), but a window's 8 rows lie in at most
+// 2 x 2 tiles = four 128-B lines instead of 8-16 lines of the row-major slice -
+// the reference API's lookup (CorrBlock.__call__, NCHW output) at the fused
+// path's line efficiency.
+template <bool PLANAR, bool TILED = false>
 __global__ void __launch_bounds__(256) corr_lookup_lvl_kernel(LookupLvlArgs a) {
   constexpr int R = 3, RD = 7;
   const int HW = a.H * a.W;
@@ -264,7 +271,8 @@ __global__ void __launch_bounds__(256) corr_lookup_lvl_kernel(LookupLvlArgs a) {
   const int e = blockIdx.y;
   const int lvl = blockIdx.z;
   const int H2 = a.H2[lvl], W2 = a.W2[lvl], nch = W2 >> 3;
-  const long slice = (long)H2 * W2;
+  const long slice = TILED ? (long)((H2 + 7) >> 3) * 8 * W2 : (long)H2 * W2;
+  const long vrow = (TILED && a.slot) ? (long)a.slot[e] : (long)e;
   const bool live = p < HW;
   const int pc = live ? p : HW - 1;
   float cx, cy;
@@ -287,7 +295,7 @@ __global__ void __launch_bounds__(256) corr_lookup_lvl_kernel(LookupLvlArgs a) {
   // the block's 256 pixel slices as one descriptor (wave-uniform base)
   const long nblk = min(256, HW - p0);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<__half*>(a.vol[lvl] + ((long)e * HW + p0) * slice), (short)0, (int)(nblk * slice * 2), kBufFlags);
+      const_cast<__half*>(a.vol[lvl] + (vrow * HW + p0) * slice), (short)0, (int)(nblk * slice * 2), kBufFlags);
   const unsigned pbase = (unsigned)((p - p0) * slice) * 2u;
   const int xs = xi0 - R;
   const int c0 = (xs >= 0) ? (xs >> 3) : -((-xs + 7) >> 3);
@@ -298,8 +306,11 @@ __global__ void __launch_bounds__(256) corr_lookup_lvl_kernel(LookupLvlArgs a) {
   for (int j = 0; j < 8; ++j) {
     const int y1 = yi0 - R + j;
     const bool yok = y1 >= 0 && y1 < H2;
-    const unsigned o0 = (yok && ok0) ? pbase + (unsigned)(y1 * W2 + 8 * c0) * 2u : kOob;
-    const unsigned o1 = (yok && ok1) ? pbase + (unsigned)(y1 * W2 + 8 * (c0 + 1)) * 2u : kOob;
+    // piece (row y1, tile column c): row-major y1 * W2 + 8 c; tiled (tile (y1/8, c), row y1 % 8)
+    const int rb = TILED ? (y1 >> 3) * 8 * W2 + (y1 & 7) * 8 : y1 * W2;
+    const int cm = TILED ? 64 : 8;
+    const unsigned o0 = (yok && ok0) ? pbase + (unsigned)(rb + cm * c0) * 2u : kOob;
+    const unsigned o1 = (yok && ok1) ? pbase + (unsigned)(rb + cm * (c0 + 1)) * 2u : kOob;
     raw[j][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o0, 0, 0));
     raw[j][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, 0));
   }
@@ -546,6 +557,40 @@ int droid_corr_index_backward(int dtype, const float* coords, const void* corr_g
     case 2: corr_index_bwd_kernel<double><<<grid, 256, 0, stream>>>(coords, (const double*)corr_grad, (double*)volume_grad, B, H, W, H2, W2, radius); break;
     default: return fail(kUnsupported, "corr_index_backward: dtype must be fp16/fp32/fp64");
   }
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
+// CorrBlock.__call__ over the fused path's 8x8-tiled slot pool (see
+// corr_lookup_lvl_kernel<.., TILED>): fp16, radius 3, levels[l] (R,H,W,
+// ceil(H2/8),W2/8,8,8), edge e's volume at row slot[e] (slot null: row e);
+// out (E, L*49, H, W) fp16, bit-exact with droid_corr_pyramid_lookup on the
+// row-major volume.
+int droid_corr_pyramid_lookup_tiled(const void* const* levels, const int* H2s, const int* W2s, const int* slot,
+                                    int num_levels, const float* coords, void* out, int E, int H, int W,
+                                    hipStream_t stream) {
+  if (num_levels < 1 || num_levels > 4 || E < 0 || H <= 0 || W <= 0)
+    return fail(kInvalidArgument, "corr_pyramid_lookup_tiled: bad arguments");
+  if (E == 0) return kOk;
+  long maxslice = 0;
+  LookupLvlArgs a{};
+  for (int l = 0; l < num_levels; ++l) {
+    if (H2s[l] <= 0 || W2s[l] <= 0 || W2s[l] % 8 != 0 || (reinterpret_cast<uintptr_t>(levels[l]) & 15u))
+      return fail(kInvalidArgument, "corr_pyramid_lookup_tiled: levels need W2 % 8 == 0 and 16-B alignment");
+    maxslice = std::max(maxslice, (long)((H2s[l] + 7) / 8) * 8 * W2s[l]);
+    a.vol[l] = (const __half*)levels[l];
+    a.H2[l] = H2s[l];
+    a.W2[l] = W2s[l];
+  }
+  if (256 * maxslice * 2 >= 0x7fffffffL) return fail(kInvalidArgument, "corr_pyramid_lookup_tiled: slice too large");
+  a.slot = slot;
+  a.coords = coords;
+  a.out = (__half*)out;
+  a.out_estride = (long)num_levels * 49 * H * W;
+  a.H = H;
+  a.W = W;
+  a.coord_scale = 1.0f;
+  corr_lookup_lvl_kernel<false, true><<<dim3(ceil_div(H * W, 256), E, num_levels), 256, 0, stream>>>(a);
   DROID_LAUNCH_CHECK();
   return kOk;
 }

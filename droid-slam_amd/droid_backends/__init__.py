@@ -114,6 +114,35 @@ def corr_pyramid_lookup(levels, coords, radius, out=None):
     return out
 
 
+def corr_pyramid_lookup_tiled(levels, level_shapes, coords, slots=None, out=None):
+    """CorrBlock.__call__ over the 8x8-tiled slot pool (fp16, r=3): levels[l]
+    (R,H,W,ceil(H2/8),W2/8,8,8), level_shapes [(H2, W2)], slots (E) int32 device
+    volume rows (None: row e), coords (E,H,W,2) f32 -> (E, L*49, H, W) fp16."""
+    _check_inputs(["level%d" % i for i in range(len(levels))] + ["coords"], list(levels) + [coords])
+    _need(coords, torch.float32, "coords")
+    for lv in levels:
+        _need(lv, torch.float16, "levels")
+    E, H, W = coords.shape[:3]
+    if slots is not None:
+        _check_inputs(("slots",), (slots,))
+        _need(slots, torch.int32, "slots")
+        if slots.numel() != E:
+            raise RuntimeError("corr_pyramid_lookup_tiled: one slot per edge")
+    elif levels[0].shape[0] < E:
+        raise RuntimeError("corr_pyramid_lookup_tiled: fewer volume rows than edges")
+    L = len(levels)
+    if out is None:
+        out = torch.empty((E, L * 49, H, W), dtype=torch.float16, device=coords.device)
+    ptrs = (ctypes.c_void_p * L)(*[lv.data_ptr() for lv in levels])
+    h2s = (ctypes.c_int * L)(*[int(h) for h, _ in level_shapes])
+    w2s = (ctypes.c_int * L)(*[int(w) for _, w in level_shapes])
+    with torch.cuda.device(coords.device):
+        check(lib.droid_corr_pyramid_lookup_tiled(ptrs, h2s, w2s, _ptr(slots) if slots is not None else None, L,
+                                                  _ptr(coords), _ptr(out), E, H, W, _stream(coords)),
+              "corr_pyramid_lookup_tiled")
+    return out
+
+
 def corr_pyramid_lookup_nhwc(levels, coords, out_cstride=200, out=None):
     """CorrBlock lookup (fp16, r=3, 4 levels) -> channels-last (E,H,W,out_cstride)
     rows, zero past channel 196 (A operand of the fused update operator)."""

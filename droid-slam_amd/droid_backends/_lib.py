@@ -27,6 +27,7 @@ _SIGS = {
     "droid_corr_index_forward": ([_i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p], _i),
     "droid_corr_index_backward": ([_i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p], _i),
     "droid_corr_pyramid_lookup": ([_i, _p, _p, _p, _i, _p, _p, _i, _i, _i, _i, _p], _i),
+    "droid_corr_pyramid_lookup_tiled": ([_p, _p, _p, _p, _i, _p, _p, _i, _i, _i, _p], _i),
     "droid_corr_pyramid_lookup_nhwc": ([_p, _p, _p, _i, _p, _p, _i, _i, _i, _i, _p], _i),
     "droid_corr_lookup_ce0": ([_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_corr_lookup_ce0_tiled": ([_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),

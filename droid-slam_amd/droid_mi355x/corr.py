@@ -145,6 +145,12 @@ class CorrBlock:
 
     def __call__(self, coords):
         batch, num, ht, wd, _ = coords.shape
+        if (self.tiled and self.radius == 3 and not torch.is_grad_enabled()
+                and self._pyr[0].dtype == torch.float16):
+            # the tiled slot pool read in place (no untile / gather copy), NCHW out
+            c = coords.reshape(batch * num, ht, wd, 2).float().contiguous()
+            out = droid_backends.corr_pyramid_lookup_tiled(self._pyr, self.level_shapes, c, self.slot_tensor())
+            return out.view(batch, num, -1, ht, wd)
         pyr = self.reference_pyramid()
         if torch.is_grad_enabled() and any(v.requires_grad for v in pyr):
             c = coords.permute(0, 1, 4, 2, 3).contiguous().view(batch * num, 2, ht, wd)

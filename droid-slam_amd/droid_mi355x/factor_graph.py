@@ -58,7 +58,10 @@ class FactorGraph:
         # fused (MI355X) operator: per-edge hidden state kept channels-last (E,H,W,128)
         from .fused import FusedUpdateModule
         self.fused = isinstance(update_op, FusedUpdateModule)
-        # CorrBlock(tiled=...) for the fused lookup (DROID_TILED_VOLUME=0: reference row-major layout)
+        # CorrBlock(tiled=...): the volume pool in 8x8 tiles for every operator - the
+        # fused lookup reads it, and so does CorrBlock.__call__ (the reference
+        # operators' NCHW lookup, droid_corr_pyramid_lookup_tiled); the layout is
+        # internal to the block (DROID_TILED_VOLUME=0: reference row-major layout)
         self.tiled_volume = os.environ.get("DROID_TILED_VOLUME", "1") != "0"
         self._version = 0          # bumped by every edge edit
         self._ba_tw = None         # (key, BA target rows, BA weight rows), see _ba_inputs
@@ -181,7 +184,7 @@ class FactorGraph:
             frames = torch.empty((len(used), ht, wd, ch), dtype=torch.float16, device=self.device)
             torch.mul(fm.permute(0, 2, 3, 1), 0.25, out=frames)     # NHWC / 4 in one pass (exact in fp16)
             f1, f2 = up[len(used):len(used) + len(ii)], up[len(used) + len(ii):]
-            tiled = self.fused and self.tiled_volume
+            tiled = self.tiled_volume
             if droid_backends.corr_volume_pyramid_supported(ht, wd, tiled and wd // 8 % 8 == 0):
                 corr = CorrBlock.from_frames(frames, f1, f2, tiled=tiled)
             else:

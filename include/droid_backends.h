@@ -57,6 +57,15 @@ int droid_corr_pyramid_lookup(int dtype, const void* const* levels, const int* H
                               int num_levels, const float* coords, void* out, int E, int H, int W,
                               int radius, hipStream_t stream);
 
+/* CorrBlock.__call__ (modules/corr.py:40-50; fp16, r=3) over the 8x8-tiled slot
+ * pool of CorrBlock(tiled=True): levels[l] (R,H,W,ceil(H2s[l]/8),W2s[l]/8,8,8),
+ * edge e's volume at row slot[e] (slot null: row e), coords (E,H,W,2) f32 ->
+ * out (E, num_levels*49, H, W) fp16, bit-exact with droid_corr_pyramid_lookup
+ * on the row-major volume.  W2s[l] % 8 == 0, 16-B aligned levels. */
+int droid_corr_pyramid_lookup_tiled(const void* const* levels, const int* H2s, const int* W2s, const int* slot,
+                                    int num_levels, const float* coords, void* out, int E, int H, int W,
+                                    hipStream_t stream);
+
 /* CorrBlock lookup (fp16, r=3, 4 levels) writing channels-last rows
  * out (E,H,W,out_cstride) with zeros past channel 196: the A operand of the
  * fused update operator's first (1x1) conv. */

@@ -1,11 +1,17 @@
 #!/bin/bash
-# round 4: Cholesky chain timelines (profiling build), then the HIP-graph replay
-# of update(): the bitwise unit test first, the trajectory with replay on last
+# round 4: tiled-pool NCHW lookup test + reference-layout bench, Cholesky chain
+# timelines (profiling build), then the HIP-graph replay of update(): the bitwise
+# unit test first, the trajectory with replay on last
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 O="$R/gpurun_out/r04f"
 mkdir -p "$O"
 cd "$R"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_corr.py tests/test_gpu_update.py -m gpu -v --timeout 240 --timeout-method thread \
+  -k "not graph_replay" > "$O/pytest_corr_update.txt" 2>&1
+rc=$?; grep -E "FAILED|ERROR" "$O/pytest_corr_update.txt" | head; tail -2 "$O/pytest_corr_update.txt"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u bench.py --reference-layout --no-cpu-baseline > "$O/bench_reflayout.json" 2> "$O/bench_reflayout.err" || { tail -20 "$O/bench_reflayout.err"; exit 1; }
+cat "$O/bench_reflayout.json"
 for c in C3 C5; do
   timeout -k 10 300 python -u scripts/chol_timeline.py $c > "$O/timeline_$c.txt" 2>&1 || { tail -20 "$O/timeline_$c.txt"; exit 1; }
   cat "$O/timeline_$c.txt"

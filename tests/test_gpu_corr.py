@@ -59,6 +59,42 @@ def test_pyramid_lookup_bitexact_and_equals_per_level():
     np.testing.assert_array_equal(host(fused).view(np.uint16), ref.view(np.uint16))
 
 
+def test_tiled_pool_lookup_bitexact():
+    """CorrBlock.__call__ on the 8x8-tiled slot pool (droid_corr_pyramid_lookup_tiled,
+    the reference operators' NCHW lookup) == the row-major lookup of a block built
+    from the final edge list, bit for bit, after drop / append edits (rows freed
+    and refilled, pool growth), at 48x64 (levels 2 and 3 are 12 and 6 rows: a
+    partial tile row) with off-map coordinates; == the oracle."""
+    from droid_mi355x.corr import CorrBlock
+    rng = np.random.default_rng(14)
+    C, H, W = 128, 48, 64
+    feats = [dev(rng.normal(size=(1, 1, C, H, W)).astype(np.float16)) for _ in range(9)]
+    pairs = [(0, 1), (1, 2), (2, 0), (3, 4), (4, 5)]
+    with torch.no_grad():
+        mk = lambda ps, tiled: CorrBlock(torch.cat([feats[a] for a, _ in ps], 1),
+                                         torch.cat([feats[b] for _, b in ps], 1), tiled=tiled)
+        cb = mk(pairs, True)
+        assert cb.tiled
+        keep = np.array([True, False, True, False, True])
+        cb = cb.select(keep)
+        more = [(5, 6), (6, 7), (7, 8), (8, 0)]
+        cb = cb.cat(mk(more, True))
+        final = [p for p, k in zip(pairs, keep) if k] + more
+        ref_blk = mk(final, False)
+        E = len(final)
+        coords = np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None, None].astype(np.float32)
+        coords = np.repeat(coords, E, axis=1) + rng.normal(0, 4.0, (1, E, H, W, 2)).astype(np.float32)
+        coords[0, 0, 0, 0] = [-40.0, 100.0]
+        coords[0, 1, 2, 3] = [63.7, 47.9]
+        coords[0, 2, 5, 5] = [-3.5, -3.5]
+        got = cb(dev(coords))
+        ref = ref_blk(dev(coords))
+    assert got.shape == (1, E, 196, H, W)
+    np.testing.assert_array_equal(host(got).view(np.uint16), host(ref).view(np.uint16))
+    ora = oc.lookup_pyramid([host(v)[:2] for v in ref_blk.corr_pyramid], coords[:, :2], 3)
+    np.testing.assert_array_equal(host(got)[:, :2].view(np.uint16), ora.view(np.uint16))
+
+
 def test_corr_index_backward_vs_oracle():
     import droid_backends
     rng = np.random.default_rng(13)
