@@ -97,6 +97,8 @@ _SIGS = {
 EXPORTS = tuple(_SIGS)
 
 for _name, (_args, _res) in _SIGS.items():
+    if os.environ.get("DROID_HIP_LIB") and not hasattr(lib, _name):
+        continue   # an older A/B build: entry points it predates stay unbound
     _fn = getattr(lib, _name)
     _fn.argtypes = _args
     _fn.restype = _res
