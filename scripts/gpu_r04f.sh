@@ -16,6 +16,11 @@ for c in C3 C5; do
   timeout -k 10 300 python -u scripts/chol_timeline.py $c > "$O/timeline_$c.txt" 2>&1 || { tail -20 "$O/timeline_$c.txt"; exit 1; }
   cat "$O/timeline_$c.txt"
 done
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_c3" -o r04f --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --steps 10 --warmup 3 > "$O/bench_c3_rocprof.json" 2> "$O/bench_c3_rocprof.err" || { tail -20 "$O/bench_c3_rocprof.err"; exit 1; }
+cd "$R"
+find "$O/prof_c3" -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} "$O/r04f_c3_kernel_stats.csv"
+head -25 "$O/r04f_c3_kernel_stats.csv" | cut -c1-220
 timeout -k 10 300 python -u -m pytest tests/test_gpu_update.py -m gpu -k graph_replay -v --timeout 240 --timeout-method thread \
   > "$O/pytest_graph_unit.txt" 2>&1
 rc=$?; tail -3 "$O/pytest_graph_unit.txt"; [ $rc -eq 0 ] || exit $rc
