@@ -1042,7 +1042,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           break;
         }
         case kBsolve: {
-          ok = poll_ge(&lver[i], 1, abort_w, d.flag) && poll_ge(&yver[i], d.ycnt[i], abort_w, d.flag);
+          ok = poll_ge(&lver[i], 1, abort_w, d.flag);   // y_i is awaited after the tile loads are issued
           break;
         }
         default: {  // kBupd (r = i, c = j)
@@ -1065,9 +1065,9 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       tile_issue(rM, skk, Br, Bp, pre);  // A(k,k) is final but for (k,k,klast): load while L(k,klast) is awaited
       if (ta >= 0) {  // the tile's last update (k, k, klast): T0 -= L(k,klast) L(k,klast)^T
         const int sl = SL(k, ta);
-        if (tid == 0) shi[1] = poll_ge(&ver[sl], d.fin[sl], abort_w, d.flag) ? 1 : 0;
+        if (tid == 0) shi[3] = poll_ge(&ver[sl], d.fin[sl], abort_w, d.flag) ? 1 : 0;
         __syncthreads();
-        if (!__builtin_amdgcn_readfirstlane(shi[1])) break;
+        if (!__builtin_amdgcn_readfirstlane(shi[3])) break;
         tile_load(rM, sl, Br, 64, T1);
         tile_commit(pre, T0);
         __syncthreads();
@@ -1235,8 +1235,16 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       publish(&ver[s], ta + 1);
     } else if (type == kBsolve) {  // x_i = L_ii^-T y_i, then (fused) y_{i-1} -= L(i,i-1)^T x_i
       const int C0 = 64 * i, Bp = min(64, n - C0);
-      tile_load(rL, i, 64, 64, T1);
-      if (ta) tile_load(rM, SL(i, i - 1), Bp, 64, T0);
+      // the back-solve chain is bsolve(i) -> y_{i-1} -> bsolve(i-1): L_ii^-1 and
+      // L(i,i-1) (final long before) are in flight while y_i is awaited
+      dbl2 pl[8], pb[8];
+      tile_issue(rL, i, 64, 64, pl);
+      if (ta) tile_issue(rM, SL(i, i - 1), Bp, 64, pb);
+      if (tid == 0) shi[3] = poll_ge(&yver[i], d.ycnt[i], abort_w, d.flag) ? 1 : 0;
+      __syncthreads();
+      if (!__builtin_amdgcn_readfirstlane(shi[3])) break;
+      tile_commit(pl, T1);
+      if (ta) tile_commit(pb, T0);
       if (tid < 32) {
         const dbl2 yv = ld2(rY, 2 * tid < Bp ? (unsigned)((C0 + 2 * tid) * 8) : kOobOff);
         vec[2 * tid] = yv[0];
