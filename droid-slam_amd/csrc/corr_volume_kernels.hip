@@ -46,7 +46,7 @@ struct VolArgs {
   int H, W;          // query and target maps are H x W
   int tiled;         // 1: (E,H,W,ceil(H_l/8),W_l/8,8,8) 8x8 tiles; 0: (E,H,W,H_l,W_l)
   int qblocks;       // ceil(HW / 256)
-  int ablate;        // timing experiments only (DROID_VOL_ABLATE, results invalid): bit 0 no stores, bit 1 no DMA after the first patch
+  int ablate;        // timing experiments only (DROID_VOL_ABLATE, results invalid): bit 0 no stores, bit 1 no DMA after the first patch, (v2) bit 2 no level 1-3 stores, bit 3 no level-0 stores
 };
 
 constexpr int kVolQ = 256;                 // query pixels per workgroup
@@ -478,7 +478,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     // stores (the staging area is this wave's own: a wave barrier suffices)
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const int qlim = (a.ablate & 1) ? 0 : HW;   // ablation: every offset out of range (no bytes written)
+    // ablations: every offset out of range (no bytes written) - bit 0 all levels,
+    // bit 2 levels 1..3 only, bit 3 level 0 only
+    const int qlim0 = (a.ablate & 9) ? 0 : HW;
+    const int qlim = (a.ablate & 5) ? 0 : HW;
     // level 0: 32 q x 128 B, 8 lanes per query pixel
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -487,7 +490,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
       const u32x4_t val = *reinterpret_cast<const u32x4_t*>(s0 + q * kVol2S0 + ((seg ^ (q & 7)) << 3));
       const long off = a.tiled ? ((long)qg * TR[0] * (Wl[0] / 8) + py * (Wl[0] / 8) + px) * 64 + seg * 8
                                : (long)qg * HW + (long)(ty0 + seg) * W + tx0;
-      __builtin_amdgcn_raw_buffer_store_b128(val, ro[0], qg < qlim ? (int)(off * 2) : (int)kOob, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(val, ro[0], qg < qlim0 ? (int)(off * 2) : (int)kOob, 0, 0);
     }
     // level 1: 32 q x 4 rows x 8 B (the patch's 4x4 level-1 block)
 #pragma unroll

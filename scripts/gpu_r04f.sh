@@ -10,6 +10,10 @@ cd "$R"
 timeout -k 10 300 python -u -m pytest tests/test_gpu_corr.py tests/test_gpu_update.py -m gpu -v --timeout 240 --timeout-method thread \
   -k "not graph_replay" > "$O/pytest_corr_update.txt" 2>&1
 rc=$?; grep -E "FAILED|ERROR" "$O/pytest_corr_update.txt" | head; tail -2 "$O/pytest_corr_update.txt"; [ $rc -eq 0 ] || exit $rc
+for ab in 0 1 4 8; do
+  DROID_VOL_VARIANT=2 DROID_VOL_ABLATE=$ab VOL_EDGES=1024 timeout -k 10 300 python -u scripts/vol_bench.py > "$O/vol2_ablate$ab.txt" 2>&1 || { tail -20 "$O/vol2_ablate$ab.txt"; exit 1; }
+  echo "v2 ablate $ab (1024 edges)"; grep variant "$O/vol2_ablate$ab.txt"
+done
 timeout -k 10 600 python -u bench.py --reference-layout --no-cpu-baseline > "$O/bench_reflayout.json" 2> "$O/bench_reflayout.err" || { tail -20 "$O/bench_reflayout.err"; exit 1; }
 cat "$O/bench_reflayout.json"
 for c in C3 C5; do
