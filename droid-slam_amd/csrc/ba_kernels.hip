@@ -979,6 +979,39 @@ __device__ __forceinline__ void panel_factor4(double* T, double* dinv, int c0, i
   if (lane < 16) dinv[c0 + lane] = mine;
   if (bad && lane == 0) atomicOr(flag, 1);
 }
+// X <- X L^-T for a 64-row tile X in T (trsm against a factored pivot block) by
+// blocked forward substitution, X_p = (A_p - sum_{j<p} X_j L_pj^T) D_p^-T per
+// 16-column block p: L's strictly-lower 16x16 blocks are read from Lt, the
+// diagonal-block inverses D_p = L_pp^-1 from the diagonal blocks of Dt.  Each
+// wave owns 16 rows, so the four block steps need no barrier (caller syncs
+// before and after).  f64 MFMA: 40 per wave, vs 64 for the product with L^-1.
+__device__ __forceinline__ void tall_solve(double* T, const double* Lt, const double* Dt, double* scr, int wave,
+                                           int fr, int fk) {
+  const int r0 = 16 * wave;
+  double* sw = scr + wave * 272;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    dbl4 S;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S[q] = T[(r0 + 4 * q + fk) * LT + 16 * p + fr];
+#pragma unroll
+    for (int j = 0; j < p; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        S = mfma64(-T[(r0 + fr) * LT + 16 * j + 4 * kk + fk], Lt[(16 * p + fr) * LT + 16 * j + 4 * kk + fk], S);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sw[(4 * q + fk) * 17 + fr] = S[q];
+    asm volatile("" ::: "memory");
+    dbl4 X = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      X = mfma64(sw[fr * 17 + 4 * kk + fk], Dt[(16 * p + fr) * LT + 16 * p + 4 * kk + fk], X);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) T[(r0 + 4 * q + fk) * LT + 16 * p + fr] = X[q];
+    asm volatile("" ::: "memory");
+  }
+}
+
 #ifndef DROID_CHOL_PANEL4
 #define DROID_CHOL_PANEL4 1
 #endif
@@ -1032,7 +1065,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         }
         case kTrsm: {
           const int s = SL(i, k);
-          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&lver[k], 1, abort_w, d.flag);
+          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&ver[SL(k, k)], d.fin[SL(k, k)], abort_w, d.flag);
           break;
         }
         case kUpdate: {
@@ -1136,40 +1169,19 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
 #pragma unroll
         for (int t = 0; t < 16; ++t) T1[(base + t) * LT + base + cc] = xv[t];
       }
+      // the diagonal blocks of L_kk^-1 (the rest of T1 is still zero) go out with
+      // the pivot tile: the trsm tasks of column k solve against L_kk and these
+      // blocks, so L_kk^-1 itself - finished below, after the publish - is
+      // needed only by the back solve and is off the factorisation's chain
+      __syncthreads();
+      tile_store(rL, k, 64, 64, T1);
       if (below) {
-        // trsm(k+1, k) by blocked forward substitution, L(k+1,k) L_kk^T = A(k+1,k):
-        // X_p = (A_p - sum_{j<p} X_j L_pj^T) D_p^-T per 16-column block p, with D_p^-1
-        // the diagonal blocks just formed.  Each wave owns 16 rows, so the four
-        // block steps need no barrier, and the full L_kk^-1 (consumed only by the
-        // trsm/back-solve tasks of later tiles) is finished AFTER the publish below:
-        // it is off the critical chain potrf(k) -> update(k+2, k+1, k) -> potrf(k+1).
+        // trsm(k+1, k) in this task, by the same blocked forward substitution
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __syncthreads();  // T0's store reads are done; D_p^-1 is in T1
+        __syncthreads();  // T0's store reads are done
         tile_commit(pre, T0);
         __syncthreads();
-        const int r0 = 16 * wave;
-        double* sw = scr + wave * 272;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          dbl4 S;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) S[q] = T0[(r0 + 4 * q + fk) * LT + 16 * p + fr];
-#pragma unroll
-          for (int j = 0; j < p; ++j)
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-              S = mfma64(-T0[(r0 + fr) * LT + 16 * j + 4 * kk + fk], T2[(16 * p + fr) * LT + 16 * j + 4 * kk + fk], S);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) sw[(4 * q + fk) * 17 + fr] = S[q];
-          asm volatile("" ::: "memory");
-          dbl4 X = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk)
-            X = mfma64(sw[fr * 17 + 4 * kk + fk], T1[(16 * p + fr) * LT + 16 * p + 4 * kk + fk], X);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) T0[(r0 + 4 * q + fk) * LT + 16 * p + fr] = X[q];
-          asm volatile("" ::: "memory");
-        }
+        tall_solve(T0, T2, T1, scr, wave, fr, fk);
         __syncthreads();
         CH_STAMP(5);
         tile_store(rM, sb, nr1, Bp, T0);
@@ -1206,13 +1218,14 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
     } else if (type == kTrsm) {
       const int R0 = 64 * i, C0 = 64 * k, nr = min(64, n + 1 - R0), nc = min(64, n - C0);
       const int s = SL(i, k);
+      dbl2 pl[8], pd[8];
+      tile_issue(rM, SL(k, k), nc, nc, pl);   // L_kk (rows / columns past nc load zeros)
+      tile_issue(rL, k, 64, 64, pd);          // diagonal blocks of L_kk^-1
       tile_load(rM, s, nr, nc, T0);
-      tile_load(rL, k, 64, 64, T1);
+      tile_commit(pl, T2);
+      tile_commit(pd, T1);
       __syncthreads();
-      dbl4 acc[2][2] = {};
-      gemm_nt64(T0, T1, acc, wr, wc, lane, 1.0);
-      __syncthreads();
-      acc_store(T0, acc, wr, wc, lane);
+      tall_solve(T0, T2, T1, scr, wave, fr, fk);
       __syncthreads();
       tile_store(rM, s, nr, nc, T0);
       const bool rhs = (i == nbr - 1);

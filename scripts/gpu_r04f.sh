@@ -7,7 +7,7 @@ R="${GRAFT_REPO_ROOT:-$(pwd)}"
 O="$R/gpurun_out/r04f"
 mkdir -p "$O"
 cd "$R"
-timeout -k 10 300 python -u -m pytest tests/test_gpu_corr.py tests/test_gpu_update.py -m gpu -v --timeout 240 --timeout-method thread \
+timeout -k 10 500 python -u -m pytest tests/test_gpu_corr.py tests/test_gpu_update.py tests/test_gpu_chol.py tests/test_gpu_ba.py tests/test_gpu_ba_scale.py -m gpu -v --timeout 240 --timeout-method thread \
   -k "not graph_replay" > "$O/pytest_corr_update.txt" 2>&1
 rc=$?; grep -E "FAILED|ERROR" "$O/pytest_corr_update.txt" | head; tail -2 "$O/pytest_corr_update.txt"; [ $rc -eq 0 ] || exit $rc
 for ab in 0 1 4 8; do
@@ -16,6 +16,12 @@ for ab in 0 1 4 8; do
 done
 timeout -k 10 600 python -u bench.py --reference-layout --no-cpu-baseline > "$O/bench_reflayout.json" 2> "$O/bench_reflayout.err" || { tail -20 "$O/bench_reflayout.err"; exit 1; }
 cat "$O/bench_reflayout.json"
+timeout -k 10 300 python -u scripts/ba_bench.py C3 C5 > "$O/ba_new.txt" 2>&1 || { tail -20 "$O/ba_new.txt"; exit 1; }
+cat "$O/ba_new.txt"
+for v in t1 t0; do
+  DROID_HIP_LIB="$R/droid-slam_amd/lib/ab/libdroid_hip_$v.so" timeout -k 10 300 python -u scripts/ba_bench.py C3 C5 > "$O/ba_$v.txt" 2>&1 || { tail -20 "$O/ba_$v.txt"; exit 1; }
+  echo "== $v"; cat "$O/ba_$v.txt"
+done
 for c in C3 C5; do
   timeout -k 10 300 python -u scripts/chol_timeline.py $c > "$O/timeline_$c.txt" 2>&1 || { tail -20 "$O/timeline_$c.txt"; exit 1; }
   cat "$O/timeline_$c.txt"
