@@ -36,4 +36,8 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_update.py -m gpu -k graph_r
 rc=$?; tail -3 "$O/pytest_graph_unit.txt"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u -m pytest "tests/test_gpu_trajectory.py::test_frontend_sequence_matches_oracle[True]" -m gpu -v --timeout 360 --timeout-method thread \
   > "$O/pytest_graph_traj.txt" 2>&1
-rc=$?; tail -3 "$O/pytest_graph_traj.txt"; exit $rc
+rc=$?; tail -3 "$O/pytest_graph_traj.txt"; [ $rc -eq 0 ] || exit $rc
+for gr in 0 1; do
+  DROID_UPDATE_GRAPHS=$gr timeout -k 10 300 python -u bench.py --config C2 --no-cpu-baseline > "$O/bench_C2_graphs$gr.json" 2> "$O/bench_C2_graphs$gr.err" || { tail -20 "$O/bench_C2_graphs$gr.err"; exit 1; }
+  echo "C2 graphs=$gr"; cut -c1-300 "$O/bench_C2_graphs$gr.json"
+done
