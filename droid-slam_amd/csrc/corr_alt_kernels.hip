@@ -666,6 +666,47 @@ __device__ __forceinline__ void b2_corr(char* lds, int T, int qmask, const half8
   }
 }
 
+// Round 4 (V3): C of tap rows [0, T) with the blocks split over the waves
+// instead of the query pixels: wave w takes blocks w, w + 4, .. and multiplies
+// each by all 64 query pixels (the tile's query rows in registers four times,
+// from L2), so every box row is read from LDS ONCE per workgroup instead of
+// once per wave (the C phase was LDS-read bound: 4 x 54 KB per level-0 box).
+// The MFMA runs transposed (query pixels as rows), so a lane holds 4
+// consecutive pixels of one tap: one 8-B LDS write per (block, M-block) instead
+// of four 2-B writes.  A wave overwrites only rows it alone has read, so no
+// barrier is needed before the writes.  Same products, same fp16 rounding: C is
+// bitwise the V2 values.
+__device__ __forceinline__ void b2_corr3(char* lds, int T, int qmask, const half8 (&af)[4][4], int wave_u, int fr,
+                                         int fq) {
+  constexpr int NBW = (kB2Rows / 16 + 3) / 4;
+  const int nb = (T + 15) >> 4;
+#pragma unroll 1
+  for (int j = 0; j < NBW; ++j) {
+    const int b = wave_u + 4 * j;
+    if (b < nb) {
+      half8 bf[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        bf[ks] = *reinterpret_cast<const half8*>(lds + (b * 16 + fr) * 256 + (((ks * 4 + fq) ^ fr) << 4));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if ((qmask >> q) & 1) {
+          floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[q][ks], bf[ks], c, 0, 0, 0);
+          // lane (fr, fq): C[pixel q*16 + 4 fq + k][tap b*16 + fr], k < 4
+          half4_t h;
+          h[0] = (_Float16)c[0];
+          h[1] = (_Float16)c[1];
+          h[2] = (_Float16)c[2];
+          h[3] = (_Float16)c[3];
+          *reinterpret_cast<half4_t*>(lds + (b * 16 + fr) * 256 + (q * 16 + 4 * fq) * 2) = h;
+        }
+      }
+    }
+  }
+}
+
 // bilinear windows of level l for the pixels of the M-blocks in qmask (only
 // pixel gpix when >= 0; the others' rows are zeroed) -> lookup tile slot `as`.
 // Thread = (wave w, pixel lane): window rows w and w + 4 (< 7) with the
@@ -753,9 +794,97 @@ __device__ __forceinline__ void b2_bilinear(char* lds, const float* cxy, int l, 
   }
 }
 
+// V3: the same windows with the lookup tile's K order changed to k = 8 iy + ix
+// (ix < 7; k = 8 iy + 7 and the row iy = 7 are zero, the encoder weights of
+// build_wl3 zero there too): a thread's 7 outputs of window row iy are one
+// 16-B piece, so a level costs a lane 2 ds_write_b128 instead of 14
+// ds_write_b16.  Every piece of every pixel in qmask is written (wave 3 writes
+// the zero row 7), so the encoder needs no padding mask.  Same arithmetic as
+// b2_bilinear, value for value.
+__device__ __forceinline__ void b2_bilinear3(char* lds, const float* cxy, int l, int Hl, int Wl, int bx0, int by0,
+                                             int bw, int toff, int as, int qmask, int gpix, int wave_u, int lane) {
+  const int p = lane;
+  if (!((qmask >> (p >> 4)) & 1)) return;
+  char* arow = lds + (as * 64 + p) * 256 + 128;
+  const int sw = p & 7;
+  auto put_row = [&](int iy, uint4 v) { *reinterpret_cast<uint4*>(arow + ((iy ^ sw) << 4)) = v; };
+  const uint4 zero4 = uint4{0u, 0u, 0u, 0u};
+  if (gpix >= 0 && gpix != p) {   // a single-pixel group: the M-block's other rows are zero
+    put_row(wave_u, zero4);
+    put_row(wave_u + 4, zero4);
+    return;
+  }
+  const float scl = 1.0f / (float)(1 << l);
+  const float x0 = cxy[2 * p] * scl, y0 = cxy[2 * p + 1] * scl;
+  const float fx0 = floorf(x0), fy0 = floorf(y0);
+  const float dx = x0 - fx0, dy = y0 - fy0;
+  const int xi0 = alt_floor(x0), yi0 = alt_floor(y0);
+  const _Float16 w11 = (_Float16)rnd16(dx * dy);
+  const _Float16 w10 = (_Float16)rnd16(dx * (1.0f - dy));
+  const _Float16 w01 = (_Float16)rnd16((1.0f - dx) * dy);
+  const _Float16 w00 = (_Float16)rnd16((1.0f - dx) * (1.0f - dy));
+  const int xs = xi0 - 3;
+  const int lo = min(max(-xs, 0), 8), hi = max(min(Wl - xs, 8), 0);
+  const unsigned cmask = hi > lo ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
+  const bool any_partial = __builtin_amdgcn_ballot_w64(cmask != 0xffu) != 0;
+  auto rowbase = [&](int y) {
+    return (y >= 0 && y < Hl) ? (unsigned)((toff + (y - by0) * bw + xs - bx0) * 256 + 2 * p) : kB2Zero;
+  };
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  const int nr = wave_u == 3 ? 1 : 2;
+  unsigned pe[2][2][4];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int ya = yi0 - 3 + wave_u + 4 * r;
+#pragma unroll
+    for (int ab = 0; ab < 2; ++ab) {
+      const unsigned base = rowbase(ya + ab);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        pe[r][ab][q] = __builtin_bit_cast(unsigned, h2_t{b2_ldh(lds, base + (2 * q) * 256),
+                                                         b2_ldh(lds, base + (2 * q + 1) * 256)});
+    }
+  }
+  if (any_partial) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned m = (((cmask >> (2 * q)) & 1) ? 0xffffu : 0u) | (((cmask >> (2 * q + 1)) & 1) ? 0xffff0000u : 0u);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        pe[r][0][q] &= m;
+        pe[r][1][q] &= m;
+      }
+    }
+  }
+  const _Float16 z = (_Float16)0.f;
+  const h2_t W00 = {w00, w00}, W01 = {w01, w01}, W10 = {w10, w10}, W11 = {w11, w11}, Z2 = {z, z};
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (r >= nr) {   // wave 3: window row 7 does not exist - its piece is zero
+      put_row(7, zero4);
+      break;
+    }
+    unsigned o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // outputs 2q, 2q + 1 (output 7 is the zero pad)
+      const h2_t ae = __builtin_bit_cast(h2_t, pe[r][0][q]), be = __builtin_bit_cast(h2_t, pe[r][1][q]);
+      const unsigned an = q < 3 ? pe[r][0][q + 1] : 0u, bn = q < 3 ? pe[r][1][q + 1] : 0u;
+      const h2_t ao = __builtin_bit_cast(h2_t, __builtin_amdgcn_alignbit(an, pe[r][0][q], 16));
+      const h2_t bo = __builtin_bit_cast(h2_t, __builtin_amdgcn_alignbit(bn, pe[r][1][q], 16));
+      h2_t v = Z2 + ae * W00;
+      v = v + be * W01;
+      v = v + ao * W10;
+      v = v + bo * W11;
+      o[q] = __builtin_bit_cast(unsigned, v);
+    }
+    o[3] &= 0xffffu;
+    put_row(wave_u + 4 * r, uint4{o[0], o[1], o[2], o[3]});
+  }
+}
+
 // corr_encoder[0] slice of level L for the M-blocks in qmask from lookup tile slot `as`;
 // acc[q][n] = out^T: lane (fr, fq) holds out[pixel q*16 + fr][co 32 w + 16 n + 4 fq + k]
-template <int L>
+template <int L, bool V3 = false>
 __device__ __forceinline__ void b2_encode(const char* lds, int as, int qmask, const half8 (&wl)[4][2][2],
                                           floatx4 (&acc)[4][2], int fq, const int (&eoff)[2]) {
 #pragma unroll
@@ -764,7 +893,7 @@ __device__ __forceinline__ void b2_encode(const char* lds, int as, int qmask, co
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       half8 x = *reinterpret_cast<const half8*>(lds + (as * 64 + q * 16) * 256 + eoff[s]);
-      if (s == 1) {   // columns 49..63 (lanes fq 2: k 48..55, fq 3: k 56..63) are padding
+      if (!V3 && s == 1) {   // columns 49..63 (lanes fq 2: k 48..55, fq 3: k 56..63) are padding
         uint4 u = __builtin_bit_cast(uint4, x);
         u.x &= fq == 3 ? 0u : fq == 2 ? 0xffffu : 0xffffffffu;
         u.y = fq >= 2 ? 0u : u.y;
@@ -823,6 +952,7 @@ __device__ __forceinline__ void b2_plan_groups(const AltArgs& a, const float* cx
   if (lane == 0) grp[0] = hcnt(0) + hcnt(1);
 }
 
+template <bool V3>
 __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int* grp = reinterpret_cast<int*>(lds + kB2Grp);
@@ -851,7 +981,11 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int k = 32 * s + 8 * fq + i;
-          v[i] = k < 49 ? (_Float16)a.w[(wave * 32 + 16 * n + fr) * 224 + 49 * l + k] : (_Float16)0.f;
+          // V3 lookup-tile order k = 8 iy + ix <-> the reference channel 7 ix + iy
+          const int iy = k >> 3, ix = k & 7;
+          const bool ok = V3 ? (ix < 7 && iy < 7) : k < 49;
+          const int ch = V3 ? 7 * ix + iy : k;
+          v[i] = ok ? (_Float16)a.w[(wave * 32 + 16 * n + fr) * 224 + 49 * l + ch] : (_Float16)0.f;
         }
         wl[l][n][s] = v;
       }
@@ -880,20 +1014,24 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
     }
   };
   // this wave's 16 query feature rows (M-block `wave`) straight into the MFMA B fragments
-  auto load_f1 = [&](const Tile& T, half8 (&af)[4]) {
+  // V2: M-block `wave` into af[0]; V3: all four M-blocks
+  auto load_f1 = [&](const Tile& T, half8 (&af)[4][4]) {
     const unsigned long long pa =
         (unsigned long long)(a.pyr[0] + (long)__builtin_amdgcn_readfirstlane(T.f1) * HW * 128);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(pa), (short)0, HW * 256, 0x00020000);
-    const int p = wave * 16 + fr;
-    const int pix = (T.ty0 + alt_py(p)) * W + T.tx0 + alt_px(p);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      af[ks] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rs, (int)((pix * 128 + (ks * 4 + fq) * 8) * 2), 0, 0));
+    for (int m = 0; m < (V3 ? 4 : 1); ++m) {
+      const int p = (V3 ? m : wave) * 16 + fr;
+      const int pix = (T.ty0 + alt_py(p)) * W + T.tx0 + alt_px(p);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        af[m][ks] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rs, (int)((pix * 128 + (ks * 4 + fq) * 8) * 2), 0, 0));
+    }
   };
 
-  half8 af[4];
+  half8 af[4][4];
   floatx4 acc[4][2];
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q][0] = acc[q][1] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -909,10 +1047,10 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
   };
   auto encode = [&](int L, int as, int qmask) {
     switch (L) {
-      case 3: b2_encode<3>(lds, as, qmask, wl, acc, fq, eoff); break;
-      case 2: b2_encode<2>(lds, as, qmask, wl, acc, fq, eoff); break;
-      case 1: b2_encode<1>(lds, as, qmask, wl, acc, fq, eoff); break;
-      default: b2_encode<0>(lds, as, qmask, wl, acc, fq, eoff); break;
+      case 3: b2_encode<3, V3>(lds, as, qmask, wl, acc, fq, eoff); break;
+      case 2: b2_encode<2, V3>(lds, as, qmask, wl, acc, fq, eoff); break;
+      case 1: b2_encode<1, V3>(lds, as, qmask, wl, acc, fq, eoff); break;
+      default: b2_encode<0, V3>(lds, as, qmask, wl, acc, fq, eoff); break;
     }
   };
   // level L of tile T: its tile box if it fits the region, else the fallback groups
@@ -936,10 +1074,12 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
       if (L == 0) B2_STAMP(8);
       wait_bar();
       if (L == 0) B2_STAMP(9);
-      b2_corr(lds, gw * gh, qmask, af, wave_u, fr, fq);
+      if (V3) b2_corr3(lds, gw * gh, qmask, af, wave_u, fr, fq);
+      else b2_corr(lds, gw * gh, qmask, af[0], wave_u, fr, fq);
       if (L == 0) B2_STAMP(10);
       __syncthreads();
-      b2_bilinear(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, 0, qmask, gpix, wave_u, lane);
+      if (V3) b2_bilinear3(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, 0, qmask, gpix, wave_u, lane);
+      else b2_bilinear(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, 0, qmask, gpix, wave_u, lane);
       if (side && gi == ng - 1 && wave_u == 3 && more)   // the next tile's boxes, on the wave with one window row
         alt_tile_boxes(a, reinterpret_cast<const float*>(lds + kB2Coord + nslot * 512),
                        reinterpret_cast<int*>(lds + kB2Lvl) + nslot * 16, lane);
@@ -987,22 +1127,28 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
       B2_STAMP(1);
       wait_bar();
       B2_STAMP(2);
-      b2_corr(lds, T321, 15, af, wave_u, fr, fq);
+      if (V3) b2_corr3(lds, T321, 15, af, wave_u, fr, fq);
+      else b2_corr(lds, T321, 15, af[0], wave_u, fr, fq);
       B2_STAMP(3);
       __syncthreads();
       B2_STAMP(4);
       for (int i = 0; i < 3; ++i) {
         const int L = 3 - i;
-        b2_bilinear(lds, cxy, L, a.Hl[L], a.Wl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
-                    __builtin_amdgcn_readfirstlane(lv[4 * L + 1]), __builtin_amdgcn_readfirstlane(lv[4 * L + 2]),
-                    toffs[i], i, 15, -1, wave_u, lane);
+        if (V3)
+          b2_bilinear3(lds, cxy, L, a.Hl[L], a.Wl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
+                       __builtin_amdgcn_readfirstlane(lv[4 * L + 1]), __builtin_amdgcn_readfirstlane(lv[4 * L + 2]),
+                       toffs[i], i, 15, -1, wave_u, lane);
+        else
+          b2_bilinear(lds, cxy, L, a.Hl[L], a.Wl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
+                      __builtin_amdgcn_readfirstlane(lv[4 * L + 1]), __builtin_amdgcn_readfirstlane(lv[4 * L + 2]),
+                      toffs[i], i, 15, -1, wave_u, lane);
       }
       B2_STAMP(5);
       __syncthreads();
       B2_STAMP(6);
-      b2_encode<3>(lds, 0, 15, wl, acc, fq, eoff);
-      b2_encode<2>(lds, 1, 15, wl, acc, fq, eoff);
-      b2_encode<1>(lds, 2, 15, wl, acc, fq, eoff);
+      b2_encode<3, V3>(lds, 0, 15, wl, acc, fq, eoff);
+      b2_encode<2, V3>(lds, 1, 15, wl, acc, fq, eoff);
+      b2_encode<1, V3>(lds, 2, 15, wl, acc, fq, eoff);
       __syncthreads();
       B2_STAMP(7);
     } else {
@@ -1057,7 +1203,7 @@ static long long* g_alt_prof = nullptr;
 static int& alt_variant() {
   static int v = [] {
     const char* e = getenv("DROID_ALT_VARIANT");
-    return (e && e[0] == '1') ? 1 : 2;
+    return (e && e[0] == '1') ? 1 : (e && e[0] == '3') ? 3 : 2;
   }();
   return v;
 }
@@ -1114,7 +1260,9 @@ int droid_corr_alt_ce0(const void* const* pyr, const int* Hl, const int* Wl, con
   } else {
     static bool attr2 = false;
     if (!attr2) {
-      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel),
+      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<false>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
+      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<true>),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
       attr2 = true;
     }
@@ -1123,16 +1271,17 @@ int droid_corr_alt_ce0(const void* const* pyr, const int* Hl, const int* Wl, con
       return (e && e[0] == '1') ? 1 : 2;
     }();
     const long grid = std::min<long>(a.ntiles, (long)per_cu * device_cu_count());
-    corr_alt2_kernel<<<dim3((unsigned)grid), 256, kB2Lds, stream>>>(a);
+    if (alt_variant() == 3) corr_alt2_kernel<true><<<dim3((unsigned)grid), 256, kB2Lds, stream>>>(a);
+    else corr_alt2_kernel<false><<<dim3((unsigned)grid), 256, kB2Lds, stream>>>(a);
   }
   DROID_LAUNCH_CHECK();
   return kOk;
 }
 
-// A/B hook: 1 = the one-workgroup-per-CU kernel, 2 = corr_alt2_kernel (default;
-// env DROID_ALT_VARIANT sets the initial value)
+// A/B hook: 1 = the one-workgroup-per-CU kernel, 2 = corr_alt2_kernel (default),
+// 3 = corr_alt2_kernel<V3> (env DROID_ALT_VARIANT sets the initial value)
 int droid_alt_set_variant(int v) {
-  if (v != 1 && v != 2) return fail(kInvalidArgument, "alt_set_variant: 1 or 2");
+  if (v < 1 || v > 3) return fail(kInvalidArgument, "alt_set_variant: 1, 2 or 3");
   alt_variant() = v;
   return kOk;
 }

@@ -275,7 +275,7 @@ def corr_alt_ce0(pyramid, f1, f2, coords, w, bias, out=None):
 
 
 def alt_set_variant(v):
-    """A/B hook (droid_alt_set_variant): 1 = corr_alt_ce0_kernel, 2 = corr_alt2_kernel."""
+    """A/B hook (droid_alt_set_variant): 1 = corr_alt_ce0_kernel, 2 = corr_alt2_kernel, 3 = corr_alt2_kernel<V3>."""
     check(lib.droid_alt_set_variant(int(v)), "alt_set_variant")
 
 

@@ -14,7 +14,7 @@ from c3_alt_inputs import c3_alt_inputs  # noqa: E402
 dev = torch.device("cuda:0")
 pyr, f1, f2, c, w, b = c3_alt_inputs(dev)
 outs = {}
-for variant in (1, 2):   # droid_alt_set_variant: the one-workgroup kernel, corr_alt2_kernel
+for variant in (1, 2, 3):   # droid_alt_set_variant: the one-workgroup kernel, corr_alt2_kernel, <V3>
     droid_backends.alt_set_variant(variant)
     ts = []
     for it in range(8):
@@ -27,4 +27,7 @@ for variant in (1, 2):   # droid_alt_set_variant: the one-workgroup kernel, corr
     outs[variant] = o
     print("%s variant %d: median %.3f ms (min %.3f)" % (os.environ.get("DROID_HIP_LIB", "default"), variant,
                                                         float(np.median(ts[2:])), min(ts)))
-print("C3 outputs bitwise equal:", bool(torch.equal(outs[1], outs[2])))
+print("C3 outputs bitwise equal (1, 2):", bool(torch.equal(outs[1], outs[2])))
+d = (outs[3].float() - outs[2].float()).abs()
+print("V3 vs V2: max diff %.3g of scale %.3g, identical fraction %.4f" % (float(d.max()), float(outs[2].float().abs().max()),
+                                                                     float((d == 0).float().mean())))

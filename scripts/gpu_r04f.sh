@@ -7,6 +7,10 @@ R="${GRAFT_REPO_ROOT:-$(pwd)}"
 O="$R/gpurun_out/r04f"
 mkdir -p "$O"
 cd "$R"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_fused.py -m gpu -k "alt2" -v --timeout 240 --timeout-method thread > "$O/pytest_alt.txt" 2>&1
+rc=$?; grep -E "FAILED|ERROR" "$O/pytest_alt.txt" | head; tail -2 "$O/pytest_alt.txt"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u scripts/alt_time.py > "$O/alt_time.txt" 2>&1 || { tail -20 "$O/alt_time.txt"; exit 1; }
+cat "$O/alt_time.txt"
 timeout -k 10 500 python -u -m pytest tests/test_gpu_corr.py tests/test_gpu_update.py tests/test_gpu_chol.py tests/test_gpu_ba.py tests/test_gpu_ba_scale.py -m gpu -v --timeout 240 --timeout-method thread \
   -k "not graph_replay" > "$O/pytest_corr_update.txt" 2>&1
 rc=$?; grep -E "FAILED|ERROR" "$O/pytest_corr_update.txt" | head; tail -2 "$O/pytest_corr_update.txt"; [ $rc -eq 0 ] || exit $rc

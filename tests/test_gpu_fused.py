@@ -402,6 +402,52 @@ def test_corr_alt2_bitwise_equals_alt1(noise, H, W, E, far):
     assert torch.equal(out, ref), (float(diff.max()), int((diff > 0).sum()))
 
 
+@pytest.mark.parametrize("noise,H,W,E,far", [(1.5, 16, 24, 6, 0.0), (40.0, 16, 24, 6, 0.0), (1.5, 48, 64, 300, 0.0),
+                                             (4.0, 48, 64, 200, 0.1), (0.3, 32, 64, 64, 0.0)])
+def test_corr_alt2_v3_matches_v2(noise, H, W, E, far):
+    """corr_alt2_kernel<V3> (box blocks split over the waves, transposed C
+    MFMA, lookup tile in the k = 8 iy + ix order with the encoder weights
+    permuted to match): the C values and the bilinear windows are the V2 values;
+    only corr_encoder[0]'s fp32 summation order differs (a permuted K), so the
+    fp16 outputs agree to a few ulps and are mostly identical; every fallback
+    (incoherent, off-map coordinates) included."""
+    import droid_backends
+    from droid_mi355x.corr import AltCorrBlock
+    rng = np.random.default_rng(43)
+    NF = 8
+    fm = torch.from_numpy(rng.normal(size=(NF, 128, H, W)).astype(np.float16)).to(DEV)
+    ii = rng.integers(0, NF, E).astype(np.int32)
+    jj = rng.integers(0, NF, E).astype(np.int32)
+    pyr = [lv.view((-1,) + tuple(lv.shape[2:])) for lv in AltCorrBlock(fm[None]).pyramid]
+    grid = np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None].astype(np.float32)
+    coords = grid + rng.normal(0, noise, (E, H, W, 2)).astype(np.float32) + rng.uniform(-3, 3, (E, 1, 1, 2)).astype(np.float32)
+    if far:
+        m = rng.random((E, H, W)) < far
+        coords[m] += rng.uniform(30, 200, (int(m.sum()), 2)).astype(np.float32) * rng.choice([-1, 1], (int(m.sum()), 2))
+    c = torch.from_numpy(coords).to(DEV).contiguous()
+    g = torch.Generator(device=DEV).manual_seed(44)
+    w224 = torch.zeros((128, 224), device=DEV)
+    w224[:, :196] = torch.randn((128, 196), generator=g, device=DEV) / 14.0
+    w224 = w224.half().contiguous()
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    f1, f2 = torch.as_tensor(ii, device=DEV), torch.as_tensor(jj, device=DEV)
+    try:
+        droid_backends.alt_set_variant(2)
+        ref = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
+        droid_backends.alt_set_variant(3)
+        out = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
+        out2 = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
+    finally:
+        droid_backends.alt_set_variant(2)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)                      # deterministic
+    assert bool(torch.isfinite(out.float()).all())
+    scale = float(ref.float().abs().max())
+    diff = (out.float() - ref.float()).abs()
+    assert float(diff.max()) <= 4e-3 * scale, float(diff.max()) / scale
+    assert float((diff == 0).float().mean()) > 0.9
+
+
 def test_corr_volume_slot_pool_matches_fresh_block():
     """The tiled CorrBlock as a slot pool (frontend edge edits: append, drop,
     append again, pool growth) looked up in place through
