@@ -1047,8 +1047,11 @@ __device__ __forceinline__ void tall_solve(double* T, const double* Lt, const do
   }
 }
 
+// panel_factor4 measured no faster than the column panel (first 16-column panel
+// 2.20 vs 2.08 us, profiles/r04/r04f_timeline_C3.txt: the single wave's f64
+// VALU issue, not the pivot chain, bounds it); the column panel stays default
 #ifndef DROID_CHOL_PANEL4
-#define DROID_CHOL_PANEL4 1
+#define DROID_CHOL_PANEL4 0
 #endif
 
 __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
@@ -1100,7 +1103,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         }
         case kTrsm: {
           const int s = SL(i, k);
-          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&ver[SL(k, k)], d.fin[SL(k, k)], abort_w, d.flag);
+          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&lver[k], 1, abort_w, d.flag);
           break;
         }
         case kUpdate: {
@@ -1201,12 +1204,8 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
 #pragma unroll
         for (int t = 0; t < 16; ++t) T1[(base + t) * LT + base + cc] = xv[t];
       }
-      // the diagonal blocks of L_kk^-1 (the rest of T1 is still zero) go out with
-      // the pivot tile: the trsm tasks of column k solve against L_kk and these
-      // blocks, so L_kk^-1 itself - finished below, after the publish - is
-      // needed only by the back solve and is off the factorisation's chain
-      __syncthreads();
-      tile_store(rL, k, 64, 64, T1);
+      // L_kk^-1 itself is finished below, after the publish: only the trsm and
+      // back-solve tasks of later tiles read it, off the factorisation's chain
       if (below) {
         // trsm(k+1, k) in this task, by the same blocked forward substitution
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1250,14 +1249,19 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
     } else if (type == kTrsm) {
       const int R0 = 64 * i, C0 = 64 * k, nr = min(64, n + 1 - R0), nc = min(64, n - C0);
       const int s = SL(i, k);
-      dbl2 pl[8], pd[8];
-      tile_issue(rM, SL(k, k), nc, nc, pl);   // L_kk (rows / columns past nc load zeros)
-      tile_issue(rL, k, 64, 64, pd);          // diagonal blocks of L_kk^-1
+      // the product with L_kk^-1 (64 f64 MFMAs per wave, two tile loads); the
+      // blocked forward substitution against L_kk and its diagonal-block
+      // inverses (tall_solve, as potrf does for (k+1, k)) measured slower here:
+      // C3 BA(itrs=2) 2.44 vs 2.34 ms (profiles/r04/r04f_ba_*.txt) - these tiles
+      // are off the factorisation's chain, where the extra load and the four
+      // serial block steps cost more than the MFMAs they save
       tile_load(rM, s, nr, nc, T0);
-      tile_commit(pl, T2);
-      tile_commit(pd, T1);
+      tile_load(rL, k, 64, 64, T1);
       __syncthreads();
-      tall_solve(T0, T2, T1, scr, wave, fr, fk);
+      dbl4 acc[2][2] = {};
+      gemm_nt64(T0, T1, acc, wr, wc, lane, 1.0);
+      __syncthreads();
+      acc_store(T0, acc, wr, wc, lane);
       __syncthreads();
       tile_store(rM, s, nr, nc, T0);
       const bool rhs = (i == nbr - 1);

@@ -125,8 +125,8 @@ def emulate(M, n, st):
             lver[k] = 1
         elif t == TRSM:
             s = S(i, k)
-            assert s >= 0 and ver[s] >= fin[s] - 1 and ver[S(k, k)] >= fin[S(k, k)]
-            M[blk(i), col(k)] = np.linalg.solve(np.tril(M[col(k), col(k)]), M[blk(i), col(k)].T).T
+            assert s >= 0 and ver[s] >= fin[s] - 1 and lver[k]
+            M[blk(i), col(k)] = M[blk(i), col(k)] @ linv[k].T
             if i == nbr - 1:
                 y[64 * k:64 * k + (col(k).stop - col(k).start)] = M[n, col(k)]
                 yver[k] = 1
