@@ -10,6 +10,7 @@ features come out of the fused reprojection kernel; the correlation lookup
 is one kernel for all levels; BA runs fully on the GPU.
 """
 import os
+import sys
 
 import numpy as np
 import torch
@@ -24,6 +25,9 @@ def _coords_grid(ht, wd, device):
     y, x = torch.meshgrid(torch.arange(ht, device=device, dtype=torch.float),
                           torch.arange(wd, device=device, dtype=torch.float), indexing="ij")
     return torch.stack([x, y], dim=-1)
+
+
+_GRAPH_DEBUG = os.environ.get("DROID_GRAPH_DEBUG", "0") == "1"
 
 
 class FactorGraph:
@@ -301,6 +305,12 @@ class FactorGraph:
         by the graph record, and a graph is only released after its stream is
         synchronised."""
         key = (self._version, self.video.counter.value) + args
+        dbg = _GRAPH_DEBUG
+
+        def trace(phase):
+            if dbg:   # diagnostics: each phase synchronised and named (never inside a capture)
+                torch.cuda.synchronize(self.device)
+                print("[update graph] %s key=%s" % (phase, key), file=sys.stderr, flush=True)
         g = self._graph
         if g is not None and g["key"] == key:
             for name in ("net", "target", "weight"):      # state replaced from outside: copy it in
@@ -308,9 +318,11 @@ class FactorGraph:
                 if cur is not g[name]:
                     g[name].copy_(cur)
                     setattr(self, name, g[name])
+            trace("replay begin")
             g["graph"].replay()
             g["plan"]._record_status()
             self.age += 1
+            trace("replay done")
             return
         if self._cap_stream is None:
             self._cap_stream = torch.cuda.Stream(device=self.device)
@@ -318,13 +330,16 @@ class FactorGraph:
         if self._graph_warm != key:
             # eager warm-up on the capture stream (torch's rule: lazily created
             # per-stream state must not be born inside the capture), ordered both ways
+            trace("warm begin")
             self._drop_graph()
             self._graph_warm = key
             cs.wait_stream(main)
             with torch.cuda.stream(cs):
                 self._update(*args)
             main.wait_stream(cs)
+            trace("warm done")
             return
+        trace("capture begin")
         droid_backends.check_status()        # no host wait may happen inside the capture
         saved = (self.net, self.target, self.weight)
         static = dict(net=self.net, target=self.target, weight=self.weight.clone())
@@ -344,11 +359,13 @@ class FactorGraph:
             self._update(*args)
             return
         main.wait_stream(cs)
+        trace("captured")
         self.net, self.target, self.weight = static["net"], static["target"], static["weight"]
         self._graph = dict(key=key, graph=graph, plan=plan, keep=self._graph_keep(), **static)
         graph.replay()
         plan._record_status()
         self.age += 1
+        trace("first replay done")
 
     def _update(self, t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, motion_only=False, age=True):
         ht, wd = self.ht, self.wd

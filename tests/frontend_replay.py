@@ -18,6 +18,8 @@ on the device, fp32 convs + fp64 BA in the oracle).  The discrete decisions
 ORACLE and applied to both sides, so the trajectories stay comparable; each
 side's own decision is recorded and the mismatches reported.
 """
+import os
+import sys
 import time
 
 import numpy as np
@@ -123,9 +125,15 @@ def replay(dev, ref, stream, num_frames, warmup=8, beta=0.3, nms=1, keyframe_thr
         if log:
             log(rec)
 
+    debug = os.environ.get("DROID_GRAPH_DEBUG", "0") == "1"
+
     def update(tag, **kw):
         for s in sides:
             s.g.update(**kw)
+            if debug:   # diagnostics: attribute a device fault to its side and update
+                torch.cuda.synchronize()
+                print("[replay] update %d (%s) %s done" % (rep["updates"], tag, type(s).__name__), file=sys.stderr,
+                      flush=True)
         rep["updates"] += 1
         compare(tag)
 
