@@ -394,7 +394,8 @@ def main():
         log("setup %.1fs (local edges %d)" % (time.time() - t_setup, e_local))
 
     import droid_backends
-    LOOKUP_FN[0] = ("corr_pyramid_lookup" if args.reference_op else
+    tiled_ref = graph.corr is not None and getattr(graph.corr, "tiled", False)
+    LOOKUP_FN[0] = (("corr_pyramid_lookup_tiled" if tiled_ref else "corr_pyramid_lookup") if args.reference_op else
                     "corr_alt_ce0" if args.corr == "pyramid" or args.lowmem else "corr_lookup_ce0")
     lookup = KernelTimer(droid_backends, LOOKUP_FN[0])
     zr = zrp = None
@@ -457,7 +458,7 @@ def main():
         bytes_per_launch = (LOOKUP_BYTES_PER_EDGE if args.reference_op else LOOKUP_CE0_BYTES_PER_EDGE) * e_local
         achieved = bytes_per_launch / (lookup_ms * 1e-3) / 1e9 if lookup_ms else None
         ref_lookup = ("corr_lookup_lvl_kernel<false, true> (4-level lookup, NCHW out, 8x8-tiled volume pool)"
-                      if os.environ.get("DROID_TILED_VOLUME", "1") != "0" else
+                      if LOOKUP_FN[0] == "corr_pyramid_lookup_tiled" else
                       "corr_pyramid_f16_r3_kernel<NCHW> (4-level lookup)" if os.environ.get("DROID_LOOKUP_V1") == "1"
                       else "corr_lookup_lvl_kernel<false> (4-level lookup, NCHW out)")
         lookup_roof = {"kernel": (ref_lookup if args.reference_op else
