@@ -340,6 +340,9 @@ __device__ __forceinline__ unsigned pack2h(float lo, float hi) {
   return (unsigned)__half_as_ushort(__float2half(lo)) | ((unsigned)__half_as_ushort(__float2half(hi)) << 16);
 }
 
+// L23 = false (round 4, variant 4): levels 2 and 3 are neither pooled nor
+// stored here - corr_volume_pool23_kernel forms them from the stored level 1
+template <bool L23>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) corr_volume_pyramid2_kernel(VolArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -422,8 +425,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
   for (int p = first; p < gslots;) {
     int nxt = p + 1;
     while (nxt < gslots && !valid(nxt)) ++nxt;
-    if (stores_out) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // == kVol2Stores
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (stores_out) {
+      if (L23) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // == kVol2Stores
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");       // levels 0 and 1 only
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();   // patch p landed in buf; every wave done with buf ^ 1
     if (nxt < gslots && !(a.ablate & 2)) patch_dma(nxt, buf ^ 1);
     int py, px;
@@ -463,7 +470,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     // level 2: the four level-1 values of an N-block sit in lanes fq = 0..3 ((h, w)
     // order = fq order); level 3: the four N-blocks of a lane
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < (L23 ? 2 : 0); ++r) {
       float w2[4];
 #pragma unroll
       for (int b = 0; b < 4; ++b)
@@ -505,7 +512,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
       __builtin_amdgcn_raw_buffer_store_b64(val, ro[1], qg < qlim ? (int)(off * 2) : (int)kOob, 0, 0);
     }
     // level 2: 32 q x 2 rows x 4 B; level 3: 32 q x 2 B
-    {
+    if (L23) {
       const int q = lane >> 1, rr = lane & 1;
       const int qg = q0 + q;
       const unsigned val = *reinterpret_cast<const unsigned*>(s2 + q * 4 + rr * 2);
@@ -515,7 +522,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
                                : (long)qg * (Hl[2] * Wl[2]) + (long)y * Wl[2] + x;
       __builtin_amdgcn_raw_buffer_store_b32(val, ro[2], qg < qlim ? (int)(off * 2) : (int)kOob, 0, 0);
     }
-    {
+    if (L23) {
       const int qg = q0 + (lane & 31);
       const int y = ty0 / 8, x = tx0 / 8;
       const long off = a.tiled ? ((long)qg * TR[3] * (Wl[3] / 8) + (y >> 3) * (Wl[3] / 8) + (x >> 3)) * 64 +
@@ -531,7 +538,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
   // tiled layout: rows of the last tile row past H_l are zero (levels whose height is not a multiple of 8)
   if (a.tiled) {
 #pragma unroll
-    for (int l = 1; l < 4; ++l) {
+    for (int l = 1; l < (L23 ? 4 : 2); ++l) {
       const int pad = TR[l] * 8 - Hl[l];
       if (pad == 0) continue;
       const int tcols = Wl[l] / 8;
@@ -769,6 +776,93 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
   }
 }
 
+// ---------------------------------------------------------------------------
+// corr_volume_pool23_kernel (round 4, variant 4): levels 2 and 3 of every
+// (edge, query pixel) from its stored level 1, with the pyramid kernel's
+// arithmetic (vol_pool4 over the four fp16 values in (h, w) order - the same
+// values in the same order, so the bytes are those of variant 2).  Written
+// this way because the per-patch level-2/3 pieces (2-8 B of lines completed
+// over 16-48 patches) left the L2 partial and cost more than the whole level-0
+// stream (profiles/r04/r04f_vol2_ablate*.txt).  One wave per query pixel: a
+// level is walked in its storage order, so each wave-instruction stores 128
+// contiguous bytes (one tiled-layout tile or a 64-element row run) and the
+// padding rows of the tiled layout are written as zeros; level 2 is kept in
+// LDS for level 3.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ long vol_elem(bool tiled, int tcols, int W, int y, int x) {
+  return tiled ? ((long)((y >> 3) * tcols + (x >> 3)) << 6) + ((y & 7) << 3) + (x & 7) : (long)y * W + x;
+}
+
+__global__ void __launch_bounds__(256) corr_volume_pool23_kernel(VolArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int H = a.H, W = a.W, HW = H * W;
+  const long nq = a.qblocks;   // = E * H * W (set by the launcher)
+  const bool tiled = a.tiled != 0;
+  int Hl[4], Wl[4], TR[4], TC[4];
+  long slice[4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    Hl[l] = H >> l;
+    Wl[l] = W >> l;
+    TR[l] = (Hl[l] + 7) / 8;
+    TC[l] = Wl[l] / 8;
+    slice[l] = tiled ? (long)TR[l] * TC[l] * 64 : (long)Hl[l] * Wl[l];
+  }
+  _Float16* s2 = reinterpret_cast<_Float16*>(lds) + (long)wave * Hl[2] * Wl[2];
+  // persistent: wave w of the grid takes (edge, query pixel) w, w + 4 G, ..
+  for (long qp = (long)blockIdx.x * 4 + wave; qp < nq; qp += 4L * gridDim.x) {
+  const __half* l1 = a.lvl[1] + qp * slice[1];
+  __half* l2 = a.lvl[2] + qp * slice[2];
+  __half* l3 = a.lvl[3] + qp * slice[3];
+  // level 2, in storage order
+  for (long s = lane; s < slice[2]; s += 64) {
+    int y, x;
+    if (tiled) {
+      const int t = (int)(s >> 6), r = (int)(s & 63);
+      y = (t / TC[2]) * 8 + (r >> 3);
+      x = (t % TC[2]) * 8 + (r & 7);
+    } else {
+      y = (int)(s / Wl[2]);
+      x = (int)(s % Wl[2]);
+    }
+    float v = 0.0f;
+    if (y < Hl[2]) {
+      const unsigned top = *reinterpret_cast<const unsigned*>(l1 + vol_elem(tiled, TC[1], Wl[1], 2 * y, 2 * x));
+      const unsigned bot = *reinterpret_cast<const unsigned*>(l1 + vol_elem(tiled, TC[1], Wl[1], 2 * y + 1, 2 * x));
+      v = vol_pool4(__half2float(__ushort_as_half((unsigned short)(top & 0xffffu))),
+                    __half2float(__ushort_as_half((unsigned short)(top >> 16))),
+                    __half2float(__ushort_as_half((unsigned short)(bot & 0xffffu))),
+                    __half2float(__ushort_as_half((unsigned short)(bot >> 16))));
+      s2[y * Wl[2] + x] = (_Float16)v;
+    }
+    l2[s] = __float2half(v);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // level 3 from level 2
+  for (long s = lane; s < slice[3]; s += 64) {
+    int y, x;
+    if (tiled) {
+      const int t = (int)(s >> 6), r = (int)(s & 63);
+      y = (t / TC[3]) * 8 + (r >> 3);
+      x = (t % TC[3]) * 8 + (r & 7);
+    } else {
+      y = (int)(s / Wl[3]);
+      x = (int)(s % Wl[3]);
+    }
+    float v = 0.0f;
+    if (y < Hl[3]) {
+      const _Float16* r0 = s2 + (2 * y) * Wl[2] + 2 * x;
+      v = vol_pool4((float)r0[0], (float)r0[1], (float)r0[Wl[2]], (float)r0[Wl[2] + 1]);
+    }
+    l3[s] = __float2half(v);
+  }
+  __builtin_amdgcn_wave_barrier();   // s2 is rewritten by the next query's level 2
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 }  // namespace droid
 
 using namespace droid;
@@ -810,7 +904,7 @@ int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, i
   static const int variant = [] {
     const char* e = getenv("DROID_VOL_VARIANT");
     const char* e1 = getenv("DROID_VOL_V1");
-    return e ? atoi(e) : (e1 && e1[0] == '1') ? 1 : 2;
+    return e ? atoi(e) : (e1 && e1[0] == '1') ? 1 : 2;   // 4: variant 2 + corr_volume_pool23_kernel
   }();
   if ((long)H * W * H * W * 2 >= 0x7fffffffL && variant != 1)
     return fail(kUnsupported, "corr_volume_pyramid: an edge's level-0 volume must stay below 2 GB");
@@ -833,11 +927,25 @@ int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, i
   } else {
     static bool attr2 = false;
     if (!attr2) {
-      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel),
+      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel<true>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kVol2Lds));
+      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel<false>),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, kVol2Lds));
       attr2 = true;
     }
-    corr_volume_pyramid2_kernel<<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
+    if (variant == 4) {
+      corr_volume_pyramid2_kernel<false><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
+      DROID_LAUNCH_CHECK();
+      VolArgs b = a;
+      const long nq = (long)E * H * W;
+      b.qblocks = (int)nq;   // the pooling pass reads its (edge, pixel) count from qblocks
+      const long g2 = std::min<long>((nq + 3) / 4, 16L * device_cu_count());
+      if (g2 > 0x7fffffffL || nq > 0x7fffffffL) return fail(kUnsupported, "corr_volume_pyramid: too many pixels");
+      const int lds2 = 4 * (H / 4) * (W / 4) * 2;
+      corr_volume_pool23_kernel<<<dim3((unsigned)g2), 256, lds2, stream>>>(b);
+    } else {
+      corr_volume_pyramid2_kernel<true><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
+    }
   }
   DROID_LAUNCH_CHECK();
   return kOk;
