@@ -342,9 +342,15 @@ __device__ __forceinline__ unsigned pack2h(float lo, float hi) {
 
 // L23 = false (round 4, variant 4): levels 2 and 3 are neither pooled nor
 // stored here - corr_volume_pool23_kernel forms them from the stored level 1
-template <bool L23>
+// MODE 0: every level stored per patch.  MODE 1 (tiled layout): a 2x2 patch
+// group is one level-1 tile, so the group's level-1 values are held in
+// registers (16 VGPRs of packed pairs) and stored as whole tiles when the group
+// ends; MODE 2: level 1 per patch.  MODEs 1 and 2 leave levels 2 and 3 to
+// corr_volume_pool23_kernel.
+template <int MODE>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) corr_volume_pyramid2_kernel(VolArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr bool L23 = MODE == 0, GRP = MODE == 1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
@@ -420,14 +426,19 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
   int first = 0;
   while (first < gslots && !valid(first)) ++first;
   if (first < gslots) patch_dma(first, 0);
+  unsigned l1g[4][2][2];   // MODE 1: the group's level-1 values, [patch k][row block r][pair (b, b + 1)]
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) l1g[kk][0][0] = l1g[kk][0][1] = l1g[kk][1][0] = l1g[kk][1][1] = 0u;
   int buf = 0;
   bool stores_out = false;   // this wave has kVol2Stores stores in flight after the last DMA
   for (int p = first; p < gslots;) {
     int nxt = p + 1;
     while (nxt < gslots && !valid(nxt)) ++nxt;
     if (stores_out) {
-      if (L23) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // == kVol2Stores
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");       // levels 0 and 1 only
+      // the stores issued after the next patch's DMA: MODE 0 4 + 2 + 1 + 1, MODE 1
+      // 4 + 4 (the group's level-1 rows, out of range but at its last patch), MODE 2 4 + 2
+      if (MODE != 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -464,7 +475,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
         *reinterpret_cast<unsigned*>(s0 + q * kVol2S0 + ((y ^ (q & 7)) << 3) + x) = pack2h(v[0], v[1]);
         *reinterpret_cast<unsigned*>(s0 + q * kVol2S0 + (((y + 1) ^ (q & 7)) << 3) + x) = pack2h(v[2], v[3]);
         u[r][b] = vol_pool4(v[0], v[1], v[2], v[3]);
-        s1[q * kVol2S1 + (2 * (b >> 1) + (fq >> 1)) * 4 + 2 * (b & 1) + (fq & 1)] = (_Float16)u[r][b];
+        if (!GRP) s1[q * kVol2S1 + (2 * (b >> 1) + (fq >> 1)) * 4 + 2 * (b & 1) + (fq & 1)] = (_Float16)u[r][b];
+        if (GRP && (b & 1)) {   // the pair (b - 1, b) into the group's registers (select chain: k is a runtime value)
+          const unsigned pk = pack2h(u[r][b - 1], u[r][b]);
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) l1g[kk][r][b >> 1] = ((p & 3) == kk) ? pk : l1g[kk][r][b >> 1];
+        }
       }
     }
     // level 2: the four level-1 values of an N-block sit in lanes fq = 0..3 ((h, w)
@@ -501,7 +517,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     }
     // level 1: 32 q x 4 rows x 8 B (the patch's 4x4 level-1 block)
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < (GRP ? 0 : 2); ++k) {
       const int q = 16 * k + (lane >> 2), rr = lane & 3;
       const int qg = q0 + q;
       const u32x2_t val = *reinterpret_cast<const u32x2_t*>(s1 + q * kVol2S1 + rr * 4);
@@ -510,6 +526,43 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
                                      (y & 7) * 8 + (x & 7)
                                : (long)qg * (Hl[1] * Wl[1]) + (long)y * Wl[1] + x;
       __builtin_amdgcn_raw_buffer_store_b64(val, ro[1], qg < qlim ? (int)(off * 2) : (int)kOob, 0, 0);
+    }
+    if (GRP) {
+      // at the group's last patch: its 8x8 level-1 tile per query through the
+      // level-0 staging rows (free once the level-0 stores above have read
+      // them), then 4 x 16-B row pieces per lane = whole 128-B tiles
+      const bool flush = nxt >= gslots || (nxt >> 2) != (p >> 2);
+      if (flush) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const int q = 16 * r + fr;
+              const int y1 = 4 * (kk >> 1) + 2 * (b >> 1) + (fq >> 1), x1 = 4 * (kk & 1) + 2 * (b & 1) + (fq & 1);
+              const unsigned pk = l1g[kk][r][b >> 1];
+              s0[q * kVol2S0 + ((y1 ^ (q & 7)) << 3) + x1] =
+                  __builtin_bit_cast(_Float16, (unsigned short)((b & 1) ? (pk >> 16) : (pk & 0xffffu)));
+            }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      const int g = p >> 2, gcols = (pcols + 1) / 2;
+      const int gy = g / gcols, gx = g - gy * gcols;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = 8 * k + (lane >> 3), seg = lane & 7;
+        const int qg = q0 + q;
+        const u32x4_t val = flush ? *reinterpret_cast<const u32x4_t*>(s0 + q * kVol2S0 + ((seg ^ (q & 7)) << 3))
+                                  : u32x4_t{0u, 0u, 0u, 0u};
+        const long off = ((long)qg * TR[1] * (Wl[1] / 8) + gy * (Wl[1] / 8) + gx) * 64 + seg * 8;
+        __builtin_amdgcn_raw_buffer_store_b128(val, ro[1], (flush && qg < qlim) ? (int)(off * 2) : (int)kOob, 0, 0);
+      }
+      if (flush) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) l1g[kk][0][0] = l1g[kk][0][1] = l1g[kk][1][0] = l1g[kk][1][1] = 0u;
+      }
     }
     // level 2: 32 q x 2 rows x 4 B; level 3: 32 q x 2 B
     if (L23) {
@@ -927,14 +980,17 @@ int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, i
   } else {
     static bool attr2 = false;
     if (!attr2) {
-      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel<true>),
+      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel<0>),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, kVol2Lds));
-      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel<false>),
+      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel<1>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kVol2Lds));
+      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel<2>),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, kVol2Lds));
       attr2 = true;
     }
     if (variant == 4) {
-      corr_volume_pyramid2_kernel<false><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
+      if (tiled) corr_volume_pyramid2_kernel<1><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
+      else corr_volume_pyramid2_kernel<2><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
       DROID_LAUNCH_CHECK();
       VolArgs b = a;
       const long nq = (long)E * H * W;
@@ -944,7 +1000,7 @@ int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, i
       const int lds2 = 4 * (H / 4) * (W / 4) * 2;
       corr_volume_pool23_kernel<<<dim3((unsigned)g2), 256, lds2, stream>>>(b);
     } else {
-      corr_volume_pyramid2_kernel<true><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
+      corr_volume_pyramid2_kernel<0><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
     }
   }
   DROID_LAUNCH_CHECK();
