@@ -807,41 +807,6 @@ __device__ __forceinline__ void acc_store(double* T, const dbl4 (&acc)[2][2], in
         T[(wr + 16 * a + 4 * q + (lane >> 4)) * LT + wc + 16 * b + (lane & 15)] = acc[a][b][q];
 }
 
-// C += sgn * A A^T on the ten lower 16x16 tiles of a 64x64 tile (the strictly
-// upper quadrant the 2x2-per-wave gemm_nt64 also computes is never read): waves
-// take row-sharing tile sets of 3, 3, 2, 2 - 48 f64 MFMAs on the longest wave
-// instead of 64.  C and A in LDS (LT pitch); the caller syncs before and after.
-__device__ __forceinline__ void syrk_lower64(double* C, const double* A, int wave, int lane, double sgn) {
-  const int fr = lane & 15, fk = lane >> 4;
-  // (row, col) tile blocks per wave; nt tiles, the first nt listed
-  const int nt = wave < 2 ? 3 : 2;
-  int tr[3], tc[3];
-  if (wave == 0) { tr[0] = tr[1] = tr[2] = 3; tc[0] = 0; tc[1] = 1; tc[2] = 2; }
-  else if (wave == 1) { tr[0] = tr[1] = tr[2] = 2; tc[0] = 0; tc[1] = 1; tc[2] = 2; }
-  else if (wave == 2) { tr[0] = tr[1] = tr[2] = 1; tc[0] = 0; tc[1] = 1; tc[2] = 1; }
-  else { tr[0] = 0; tc[0] = 0; tr[1] = tr[2] = 3; tc[1] = tc[2] = 3; }
-  dbl4 acc[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[t][q] = t < nt ? C[(16 * tr[t] + 4 * q + fk) * LT + 16 * tc[t] + fr] : 0.0;
-#pragma unroll 4
-  for (int k0 = 0; k0 < 64; k0 += 4) {
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      if (t < nt) {
-        const double a = sgn * A[(16 * tr[t] + fr) * LT + k0 + fk], b = A[(16 * tc[t] + fr) * LT + k0 + fk];
-        acc[t] = mfma64(a, b, acc[t]);
-      }
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < 3; ++t)
-    if (t < nt)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) C[(16 * tr[t] + 4 * q + fk) * LT + 16 * tc[t] + fr] = acc[t][q];
-}
-
 // every storing wave drains, then one lane publishes (Guideline 16 R1)
 __device__ __forceinline__ void publish(int* w, int v, int* w2 = nullptr, int v2 = 0, int* w3 = nullptr, int v3 = 0) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1142,7 +1107,10 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         tile_load(rM, sl, Br, 64, T1);
         tile_commit(pre, T0);
         __syncthreads();
-        syrk_lower64(T0, T1, wave, lane, -1.0);
+        dbl4 acc[2][2];
+        acc_load(T0, acc, wr, wc, lane);
+        gemm_nt64(T1, T1, acc, wr, wc, lane, -1.0);
+        acc_store(T0, acc, wr, wc, lane);
       } else {
         tile_commit(pre, T0);
       }
@@ -1272,17 +1240,13 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       const int nri = min(64, n + 1 - Ri), ncj = min(64, n - Rj), nck = min(64, n - Ck);
       const int s = SL(i, j);
       tile_load(rM, SL(i, k), nri, nck, T0);
-      if (i != j) tile_load(rM, SL(j, k), ncj, nck, T1);
+      tile_load(rM, SL(j, k), ncj, nck, T1);
       tile_load(rM, s, nri, ncj, T2);
       __syncthreads();
-      if (i == j) {   // a diagonal tile: A(i,i) -= L(i,k) L(i,k)^T, lower tiles only
-        syrk_lower64(T2, T0, wave, lane, -1.0);
-      } else {
-        dbl4 acc[2][2];
-        acc_load(T2, acc, wr, wc, lane);
-        gemm_nt64(T0, T1, acc, wr, wc, lane, -1.0);
-        acc_store(T2, acc, wr, wc, lane);
-      }
+      dbl4 acc[2][2];
+      acc_load(T2, acc, wr, wc, lane);
+      gemm_nt64(T0, T1, acc, wr, wc, lane, -1.0);
+      acc_store(T2, acc, wr, wc, lane);
       __syncthreads();
       tile_store(rM, s, nri, ncj, T2);
       publish(&ver[s], ta + 1);

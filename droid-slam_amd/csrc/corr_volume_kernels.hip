@@ -950,14 +950,15 @@ int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, i
   const long grid = (long)E * a.qblocks;
   if (grid == 0) return kOk;
   if (grid > 0x7fffffffL) return fail(kUnsupported, "corr_volume_pyramid: too many edges");
-  // DROID_VOL_VARIANT=1 / 3: the round-3 kernel / corr_volume_pyramid3_kernel (A/B
-  // runs); the default is corr_volume_pyramid2_kernel (DROID_VOL_V1=1 = variant 1).
-  // C3, 2048 edges (profiles/r04/vol_v*.txt): v1 33.3 ms, v2 19.9 ms, v3 23.6 ms,
-  // identical bytes (hash64)
+  // DROID_VOL_VARIANT (A/B runs; DROID_VOL_V1=1 = variant 1): 1 the round-3 kernel,
+  // 2 corr_volume_pyramid2_kernel<0> (every level per patch), 3 the ring variant,
+  // 4 (default) corr_volume_pyramid2_kernel<1 / 2> + corr_volume_pool23_kernel.
+  // C3, 2048 edges, identical bytes (hash64): v1 33.3 ms, v2 19.9-23.2, v3 23.6,
+  // v4 15.6-16.1 (profiles/r04/vol_v*.txt, r04g_vol_v*.txt)
   static const int variant = [] {
     const char* e = getenv("DROID_VOL_VARIANT");
     const char* e1 = getenv("DROID_VOL_V1");
-    return e ? atoi(e) : (e1 && e1[0] == '1') ? 1 : 2;   // 4: variant 2 + corr_volume_pool23_kernel
+    return e ? atoi(e) : (e1 && e1[0] == '1') ? 1 : 4;
   }();
   if ((long)H * W * H * W * 2 >= 0x7fffffffL && variant != 1)
     return fail(kUnsupported, "corr_volume_pyramid: an edge's level-0 volume must stay below 2 GB");

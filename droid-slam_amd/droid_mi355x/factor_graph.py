@@ -287,6 +287,45 @@ class FactorGraph:
             keep["corr"] = (list(getattr(self.corr, "_pyr", [])), getattr(self.corr, "_slot_dev", None))
         return keep
 
+    def _graph_pool_report(self, graph, static):
+        """Diagnostics (DROID_GRAPH_DEBUG=1): every live CUDA tensor whose memory
+        lies in the just-captured graph's private pool (an allocation made inside
+        the capture that outlived it), named by where this graph, its module,
+        correlation block, video or droid_backends hold it.  With
+        DROID_GRAPH_DEBUG_STOP=n the n-th capture raises after the report."""
+        import gc
+        torch.cuda.synchronize(self.device)
+        pid = tuple(graph.pool())
+        segs = [(sg["address"], sg["total_size"]) for sg in torch.cuda.memory_snapshot()
+                if tuple(sg.get("segment_pool_id", ())) == pid]
+        inpool = lambda t: any(a <= t.data_ptr() < a + n for a, n in segs)
+        live = [t for t in gc.get_objects() if isinstance(t, torch.Tensor) and t.is_cuda and inpool(t)]
+        owners = dict(graph=self.__dict__, update_op=self.update_op.__dict__, video=self.video.__dict__,
+                      backends=vars(droid_backends))
+        if self.corr is not None:
+            owners["corr"] = self.corr.__dict__
+
+        def walk(x, path, out, depth=0):
+            if isinstance(x, torch.Tensor):
+                if x.is_cuda and inpool(x):
+                    out.append(path)
+            elif depth < 4 and isinstance(x, dict):
+                for k, v in list(x.items())[:200]:
+                    walk(v, "%s[%r]" % (path, k), out, depth + 1)
+            elif depth < 4 and isinstance(x, (list, tuple)):
+                for i, v in enumerate(list(x)[:200]):
+                    walk(v, "%s[%d]" % (path, i), out, depth + 1)
+        named = []
+        for nm, d in owners.items():
+            for k, v in list(d.items()):
+                walk(v, "%s.%s" % (nm, k), named)
+        print("[update graph] pool %s: %d segments, %d live tensors in the pool; held by: %s" % (
+            pid, len(segs), len(live), named[:40]), file=sys.stderr, flush=True)
+        self._n_captures = getattr(self, "_n_captures", 0) + 1
+        stop = int(os.environ.get("DROID_GRAPH_DEBUG_STOP", "0"))
+        if stop and self._n_captures >= stop:
+            raise RuntimeError("graph debug stop after capture %d" % self._n_captures)
+
     def _update_graphed(self, args):
         """update() through a HIP graph of this edge set: the first call is eager
         (it fills every cache the body reads: edge-list uploads, the BA plan,
@@ -360,6 +399,8 @@ class FactorGraph:
             return
         main.wait_stream(cs)
         trace("captured")
+        if dbg:
+            self._graph_pool_report(graph, static)
         self.net, self.target, self.weight = static["net"], static["target"], static["weight"]
         self._graph = dict(key=key, graph=graph, plan=plan, keep=self._graph_keep(), **static)
         graph.replay()
