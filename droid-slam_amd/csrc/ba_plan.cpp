@@ -924,6 +924,14 @@ int droid_ba_plan_kx(const void* plan, int64_t* out) {
 // the assembly writes, rhs row included) inside the workspace: the contiguous
 // buffer a multi-GPU caller all-reduces.  Fill tiles follow it and are zero
 // before the factorisation.
+int droid_ba_plan_ints_region(const void* plan, size_t* offset, size_t* bytes) {
+  auto* p = static_cast<const BaPlan*>(plan);
+  if (!p) return fail(kInvalidArgument, "ba_plan_ints_region: null plan");
+  *offset = p->off_ints;
+  *bytes = p->ints.size() * sizeof(int);
+  return kOk;
+}
+
 int droid_ba_plan_system_region(const void* plan, size_t* offset, size_t* bytes) {
   auto* p = static_cast<const BaPlan*>(plan);
   if (!p) return fail(kInvalidArgument, "ba_plan_system_region: null plan");

@@ -932,6 +932,13 @@ class BaPlan:
                                             _ptr(intrinsics), _ptr(disps_sens), _ptr(targets), _ptr(weights),
                                             _ptr(eta), _ptr(dx), _ptr(dz), _stream(poses)), "ba apply_update")
 
+    def ints_region(self):
+        """the plan's packed int section in the workspace (a uint8 view; read-only
+        after the upload - diagnostics compare it across calls)."""
+        off, sz = ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib.droid_ba_plan_ints_region(self._h, ctypes.byref(off), ctypes.byref(sz)), "ba_plan_ints_region")
+        return self.workspace[off.value:off.value + sz.value]
+
     def status_words(self):
         """the device status words (int32 [this solve, sticky]), a view."""
         return self._flag

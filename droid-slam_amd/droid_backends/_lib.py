@@ -79,6 +79,7 @@ _SIGS = {
                             ctypes.POINTER(_i)], _i),
     "droid_ba_plan_kx": ([_p, _p], _i),
     "droid_ba_plan_system_region": ([_p, ctypes.POINTER(_sz), ctypes.POINTER(_sz)], _i),
+    "droid_ba_plan_ints_region": ([_p, ctypes.POINTER(_sz), ctypes.POINTER(_sz)], _i),
     "droid_ba_plan_upload": ([_p, _p, _p], _i),
     "droid_ba_build_system": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _p], _i),
     "droid_ba_solve_update": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p], _i),

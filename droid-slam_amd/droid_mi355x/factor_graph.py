@@ -322,9 +322,6 @@ class FactorGraph:
         print("[update graph] pool %s: %d segments, %d live tensors in the pool; held by: %s" % (
             pid, len(segs), len(live), named[:40]), file=sys.stderr, flush=True)
         self._n_captures = getattr(self, "_n_captures", 0) + 1
-        stop = int(os.environ.get("DROID_GRAPH_DEBUG_STOP", "0"))
-        if stop and self._n_captures >= stop:
-            raise RuntimeError("graph debug stop after capture %d" % self._n_captures)
 
     def _update_graphed(self, args):
         """update() through a HIP graph of this edge set: the first call is eager
@@ -399,14 +396,27 @@ class FactorGraph:
             return
         main.wait_stream(cs)
         trace("captured")
+        self.net, self.target, self.weight = static["net"], static["target"], static["weight"]
         if dbg:
             self._graph_pool_report(graph, static)
-        self.net, self.target, self.weight = static["net"], static["target"], static["weight"]
         self._graph = dict(key=key, graph=graph, plan=plan, keep=self._graph_keep(), **static)
+        if dbg:   # integrity of what the graph only reads: unchanged by a replay?
+            ro = {"plan.ints": plan.ints_region()}
+            for nm, (_, t) in self._dev_cache.items():
+                ro["dev." + nm] = t
+            if self.corr is not None and getattr(self.corr, "_slot_dev", None) is not None:
+                ro["corr.slots"] = self.corr._slot_dev
+            before = {nm: t.clone() for nm, t in ro.items()}
         graph.replay()
         plan._record_status()
         self.age += 1
         trace("first replay done")
+        if dbg:
+            changed = [nm for nm, t in ro.items() if not torch.equal(t, before[nm])]
+            print("[update graph] read-only inputs changed by the replay: %s" % (changed,), file=sys.stderr, flush=True)
+            stop = int(os.environ.get("DROID_GRAPH_DEBUG_STOP", "0"))
+            if stop and self._n_captures >= stop:
+                raise RuntimeError("graph debug stop after capture %d" % self._n_captures)
 
     def _update(self, t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, motion_only=False, age=True):
         ht, wd = self.ht, self.wd

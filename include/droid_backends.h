@@ -387,6 +387,11 @@ int droid_ba_plan_kx(const void* plan, int64_t* kx_host);
  * dissection (tile-aligned); perm[pose] =
  * elimination position (P ints); frames on the wide Schur path; tile tasks */
 int droid_ba_plan_order(const void* plan, int* kind, int* perm, int* num_wide, int* ntasks);
+/* The plan's packed int section (edge lists, assembly lists, task records,
+ * slot map) inside the workspace: uploaded once by droid_ba_plan_upload and
+ * only read afterwards (diagnostics: an integrity check of the section). */
+int droid_ba_plan_ints_region(const void* plan, size_t* offset, size_t* bytes);
+
 /* the reduced system's input tiles inside the workspace: 64x64 fp64 tiles of
  * the permuted lower triangle of A - S with the rhs as row n; the contiguous
  * region a multi-GPU caller all-reduces (SUM) between build and solve */
