@@ -30,6 +30,62 @@ def _coords_grid(ht, wd, device):
 _GRAPH_DEBUG = os.environ.get("DROID_GRAPH_DEBUG", "0") == "1"
 
 
+class _PointerRecorder:
+    """Diagnostics (DROID_GRAPH_DEBUG=1): every device pointer the captured body
+    hands the C library (scalar arguments and pointer arrays), checked after the
+    capture against the caching allocator's blocks - a pointer into a block that
+    is no longer allocated is one the graph's replays would read or write stale."""
+
+    def __init__(self):
+        import ctypes
+        self.ct = ctypes
+        self.calls = []
+
+    def install(self):
+        real = droid_backends.lib
+        rec = self
+
+        class Proxy:
+            def __getattr__(self, name):
+                fn = getattr(real, name)
+                if not name.startswith("droid_"):
+                    return fn
+
+                def wrapped(*a):
+                    ptrs = []
+                    for i, x in enumerate(a):
+                        if isinstance(x, rec.ct.c_void_p) and x.value:
+                            ptrs.append((i, x.value))
+                        elif isinstance(x, rec.ct.Array) and getattr(x, "_type_", None) is rec.ct.c_void_p:
+                            ptrs.extend((("%d[%d]" % (i, j)), v) for j, v in enumerate(x) if v)
+                    rec.calls.append((name, ptrs))
+                    return fn(*a)
+                return wrapped
+        self.real = real
+        droid_backends.lib = Proxy()
+
+    def remove(self):
+        droid_backends.lib = self.real
+
+    def report(self):
+        blocks = []
+        for sg in torch.cuda.memory_snapshot():
+            for b in sg.get("blocks", []):
+                blocks.append((b["address"], b["size"], b["state"]))
+        blocks.sort()
+        import bisect
+        starts = [b[0] for b in blocks]
+        bad = []
+        for name, ptrs in self.calls:
+            for arg, v in ptrs:
+                k = bisect.bisect_right(starts, v) - 1
+                state = "outside every segment" if k < 0 or v >= blocks[k][0] + blocks[k][1] else blocks[k][2]
+                if state != "active_allocated":
+                    bad.append((name, arg, hex(v), state))
+        print("[update graph] %d library calls captured; pointers not in an allocated block: %s" % (
+            len(self.calls), bad[:30]), file=sys.stderr, flush=True)
+
+
 class FactorGraph:
     def __init__(self, video, update_op, device="cuda:0", corr_impl="volume", max_factors=-1):
         self.video = video
@@ -382,12 +438,19 @@ class FactorGraph:
         self.weight = static["weight"]
         graph = torch.cuda.CUDAGraph()
         cs.wait_stream(main)
+        rec = _PointerRecorder() if dbg else None
         try:
             with torch.cuda.graph(graph, stream=cs):
+                if rec is not None:
+                    rec.install()
                 plan = self._update(*args, age=False)
                 for name in ("net", "target", "weight"):   # this update's state -> the static inputs
                     static[name].copy_(getattr(self, name))
+                if rec is not None:
+                    rec.remove()
         except Exception:
+            if rec is not None:
+                rec.remove()
             # capture unsupported here (an upload, a plan build, an op that syncs): stay eager
             main.wait_stream(cs)
             self.net, self.target, self.weight = saved
@@ -399,6 +462,9 @@ class FactorGraph:
         self.net, self.target, self.weight = static["net"], static["target"], static["weight"]
         if dbg:
             self._graph_pool_report(graph, static)
+            rec.report()
+            if os.environ.get("DROID_GRAPH_DEBUG_STOP_BEFORE_REPLAY", "0") == "1":
+                raise RuntimeError("graph debug stop before the first replay")
         self._graph = dict(key=key, graph=graph, plan=plan, keep=self._graph_keep(), **static)
         if dbg:   # integrity of what the graph only reads: unchanged by a replay?
             ro = {"plan.ints": plan.ints_region()}
