@@ -67,23 +67,28 @@ class _PointerRecorder:
     def remove(self):
         droid_backends.lib = self.real
 
-    def report(self):
+    def report(self, pool):
         blocks = []
         for sg in torch.cuda.memory_snapshot():
+            pid = tuple(sg.get("segment_pool_id", ()))
             for b in sg.get("blocks", []):
-                blocks.append((b["address"], b["size"], b["state"]))
+                blocks.append((b["address"], b["size"], b["state"], pid))
         blocks.sort()
         import bisect
         starts = [b[0] for b in blocks]
-        bad = []
+        bad, n = [], 0
         for name, ptrs in self.calls:
             for arg, v in ptrs:
+                n += 1
                 k = bisect.bisect_right(starts, v) - 1
-                state = "outside every segment" if k < 0 or v >= blocks[k][0] + blocks[k][1] else blocks[k][2]
-                if state != "active_allocated":
-                    bad.append((name, arg, hex(v), state))
-        print("[update graph] %d library calls captured; pointers not in an allocated block: %s" % (
-            len(self.calls), bad[:30]), file=sys.stderr, flush=True)
+                if k < 0 or v >= blocks[k][0] + blocks[k][1]:
+                    if v < (1 << 40):   # a host handle (the stream), not device memory
+                        continue
+                    bad.append((name, arg, hex(v), "outside every segment"))
+                elif blocks[k][2] != "active_allocated" and blocks[k][3] != tuple(pool):
+                    bad.append((name, arg, hex(v), blocks[k][2], blocks[k][3]))
+        print("[update graph] %d library calls, %d device pointers captured; stale (free outside the graph's "
+              "pool): %s" % (len(self.calls), n, bad[:40]), file=sys.stderr, flush=True)
 
 
 class FactorGraph:
@@ -462,7 +467,7 @@ class FactorGraph:
         self.net, self.target, self.weight = static["net"], static["target"], static["weight"]
         if dbg:
             self._graph_pool_report(graph, static)
-            rec.report()
+            rec.report(graph.pool())
             if os.environ.get("DROID_GRAPH_DEBUG_STOP_BEFORE_REPLAY", "0") == "1":
                 raise RuntimeError("graph debug stop before the first replay")
         self._graph = dict(key=key, graph=graph, plan=plan, keep=self._graph_keep(), **static)
