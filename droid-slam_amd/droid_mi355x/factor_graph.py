@@ -468,8 +468,6 @@ class FactorGraph:
         if dbg:
             self._graph_pool_report(graph, static)
             rec.report(graph.pool())
-            if os.environ.get("DROID_GRAPH_DEBUG_STOP_BEFORE_REPLAY", "0") == "1":
-                raise RuntimeError("graph debug stop before the first replay")
         self._graph = dict(key=key, graph=graph, plan=plan, keep=self._graph_keep(), **static)
         if dbg:   # integrity of what the graph only reads: unchanged by a replay?
             ro = {"plan.ints": plan.ints_region()}
@@ -478,6 +476,18 @@ class FactorGraph:
             if self.corr is not None and getattr(self.corr, "_slot_dev", None) is not None:
                 ro["corr.slots"] = self.corr._slot_dev
             before = {nm: t.clone() for nm, t in ro.items()}
+            # do allocations made after the capture land in the graph's private pool?
+            pid = tuple(graph.pool())
+            segs = [(sg["address"], sg["total_size"]) for sg in torch.cuda.memory_snapshot()
+                    if tuple(sg.get("segment_pool_id", ())) == pid]
+            probe = [torch.empty(n, dtype=torch.uint8, device=self.device) for n in (512, 4096, 65536, 1 << 20, 4 << 20)]
+            inside = [nm for nm, t in list(before.items()) + [("probe%d" % i, t) for i, t in enumerate(probe)]
+                      if any(a <= t.data_ptr() < a + n for a, n in segs)]
+            print("[update graph] post-capture allocations inside the graph's pool: %s" % (inside,), file=sys.stderr,
+                  flush=True)
+            del probe
+            if os.environ.get("DROID_GRAPH_DEBUG_STOP_BEFORE_REPLAY", "0") == "1":
+                raise RuntimeError("graph debug stop before the first replay")
         graph.replay()
         plan._record_status()
         self.age += 1
