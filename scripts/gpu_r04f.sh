@@ -38,7 +38,7 @@ head -25 "$O/r04f_c3_kernel_stats.csv" | cut -c1-220
 timeout -k 10 300 python -u -m pytest tests/test_gpu_update.py -m gpu -k graph_replay -v --timeout 240 --timeout-method thread \
   > "$O/pytest_graph_unit.txt" 2>&1
 rc=$?; tail -3 "$O/pytest_graph_unit.txt"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python -u -m pytest "tests/test_gpu_trajectory.py::test_frontend_sequence_matches_oracle[True]" -m gpu -v --timeout 360 --timeout-method thread \
+DROID_TEST_GRAPH_TRAJECTORY=1 timeout -k 10 400 python -u -m pytest "tests/test_gpu_trajectory.py::test_frontend_sequence_matches_oracle[True]" -m gpu -v --timeout 360 --timeout-method thread \
   > "$O/pytest_graph_traj.txt" 2>&1
 rc=$?; tail -3 "$O/pytest_graph_traj.txt"; [ $rc -eq 0 ] || exit $rc
 for gr in 0 1; do

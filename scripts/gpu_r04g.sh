@@ -20,7 +20,7 @@ timeout -k 10 300 python -u scripts/ba_bench.py C3 C5 > "$O/ba_new.txt" 2>&1 || 
 cat "$O/ba_new.txt"
 DROID_HIP_LIB="$R/droid-slam_amd/lib/ab/libdroid_hip_t1.so" timeout -k 10 300 python -u scripts/ba_bench.py C3 C5 > "$O/ba_t1.txt" 2>&1 || { tail -20 "$O/ba_t1.txt"; exit 1; }
 echo "== t1"; cat "$O/ba_t1.txt"
-DROID_GRAPH_DEBUG=1 timeout -k 10 300 python -u -m pytest "tests/test_gpu_trajectory.py::test_frontend_sequence_matches_oracle[True]" -m gpu -v -s --timeout 240 --timeout-method thread \
+DROID_TEST_GRAPH_TRAJECTORY=1 DROID_GRAPH_DEBUG=1 timeout -k 10 300 python -u -m pytest "tests/test_gpu_trajectory.py::test_frontend_sequence_matches_oracle[True]" -m gpu -v -s --timeout 240 --timeout-method thread \
   > "$O/pytest_graph_traj_debug.txt" 2>&1
 rc=$?
 grep -E "^\[update graph\]|^\[replay\]" "$O/pytest_graph_traj_debug.txt" | tail -30
