@@ -115,6 +115,26 @@ __device__ __forceinline__ void wave_transpose_reduce128(float* v, int lane) {
 // Kernel A: per-edge 12x12 Hessian (upper triangle, reference order) and
 // gradient, reduced over a pixel split.  grid = (nsplit, E), 256 threads.
 // ---------------------------------------------------------------------------
+// Zero-fill of a workspace region as a kernel (16-B stores; sizes and offsets
+// here are multiples of 16 B): in a captured HIP graph the solve's resets are
+// then kernel nodes like the rest of the chain, not runtime memset nodes.
+__global__ void __launch_bounds__(256) ba_zero_kernel(uint4* __restrict__ p, long n16) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) p[i] = uint4{0u, 0u, 0u, 0u};
+}
+
+static int ba_zero(void* p, size_t bytes, hipStream_t stream) {
+  if (bytes == 0) return kOk;
+  if ((reinterpret_cast<uintptr_t>(p) & 15u) || (bytes & 15u)) {
+    DROID_HIP_CHECK(hipMemsetAsync(p, 0, bytes, stream));
+    return kOk;
+  }
+  const long n16 = (long)(bytes / 16);
+  const long grid = std::min<long>((n16 + 255) / 256, 1024);
+  ba_zero_kernel<<<dim3((unsigned)grid), 256, 0, stream>>>(static_cast<uint4*>(p), n16);
+  DROID_LAUNCH_CHECK();
+  return kOk;
+}
+
 __global__ void __launch_bounds__(256) ba_edge_hessian_kernel(BaDev d) {
   __shared__ float red[4][128];
   const int e = blockIdx.y, split = blockIdx.x;
@@ -1506,7 +1526,7 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kCholLds));
     attr = true;
   }
-  DROID_HIP_CHECK(hipMemsetAsync(c.sync, 0, p.sync_bytes, stream));
+  if (int st = ba_zero(c.sync, p.sync_bytes, stream)) return st;
   // one worker per two CUs: the same makespan at C3 (2.38 vs 2.41 ms for
   // BA(itrs=2)) and 10 % less at C5 (11.6 vs 12.9 ms) than one per CU - fewer
   // workers polling the hand-off counters (profiles/r02/chol_grid_r02dn.txt)
@@ -1579,7 +1599,7 @@ int droid_ba_build_system(void* plan, void* workspace, float* poses, float* disp
     st = launch_wide(*p, d, stream);
     if (st) return st;
   }
-  DROID_HIP_CHECK(hipMemsetAsync(d.M, 0, (size_t)p->cs.nslots * kTile * sizeof(double), stream));
+  if (int st = ba_zero(d.M, (size_t)p->cs.nslots * kTile * sizeof(double), stream)) return st;
   if (d.nblk + p->P > 0) {
     ba_assemble_kernel<<<d.nblk + p->P, 256, 0, stream>>>(d);
     DROID_LAUNCH_CHECK();
@@ -1667,7 +1687,7 @@ int droid_ba_plan_clear_status(void* plan, void* workspace, hipStream_t stream) 
   auto* p = static_cast<BaPlan*>(plan);
   int st = check_ready(p, workspace);
   if (st) return st;
-  DROID_HIP_CHECK(hipMemsetAsync(static_cast<char*>(workspace) + p->off_flag, 0, 8, stream));
+  if (int st = ba_zero(static_cast<char*>(workspace) + p->off_flag, 16, stream)) return st;   // the two status words (+ 8 unused bytes of the 64-B flag region)
   return kOk;
 }
 
@@ -1693,7 +1713,7 @@ int droid_chol_set_system(void* plan, void* workspace, const double* A, int lda,
   if (lda < p->n) return fail(kInvalidArgument, "chol_set_system: lda < n");
   char* ws = static_cast<char*>(workspace);
   double* M = reinterpret_cast<double*>(ws + p->off_M);
-  DROID_HIP_CHECK(hipMemsetAsync(M, 0, (size_t)std::max(p->cs.nslots, 1) * kTile * sizeof(double), stream));
+  if (int st = ba_zero(M, (size_t)std::max(p->cs.nslots, 1) * kTile * sizeof(double), stream)) return st;
   if (p->n == 0) return kOk;
   const long total = (long)(p->n + 1) * p->n;
   chol_scatter_kernel<<<(int)((total + 255) / 256), 256, 0, stream>>>(
