@@ -1141,7 +1141,6 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           if (DROID_CHOL_PANEL4) panel_factor4(T0, vec + 128, c0, Bp, lane, d.flag, scr);
           else panel_factor(T0, vec + 128, c0, Bp, lane, d.flag, scr);
         }
-        if (c0 == 0) CH_STAMP(6);
         __syncthreads();
         const int s0 = c0 + 16;
         const int nt = (64 - s0) / 16;
@@ -1164,6 +1163,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       const int R1 = R0 + 64, nr1 = below ? min(64, n + 1 - R1) : 0;
       const int sb = below ? SL(k + 1, k) : 0;
       if (below && tid == 0) shi[2] = poll_ge(&ver[sb], d.fin[sb] - 1, abort_w, d.flag) ? 1 : 0;
+      CH_STAMP(6);   // profiling: A(k+1,k) has all its updates but this task's (tid 0 polled it)
       // lower-triangular copy of the Bp x Bp pivot block (unit-diagonal padding past Bp)
       for (int idx = tid; idx < 64 * 64; idx += 256) {
         const int r = idx >> 6, c = idx & 63;

@@ -42,7 +42,7 @@ t0 = p[p[:, 0] > 0, 0].min()
 print("%s: n=%d tasks=%d, Cholesky span %.1f us" % (cfg, plan.P * 6, plan.ntasks, p[:, 7].max() - t0))
 pot = np.nonzero(p[:, 3] > 0)[0]
 pot = pot[np.argsort(p[pot, 0])]
-# stamps: 0 ticket, 1 deps met, 2 last update applied, 6 first panel, 3 panels done,
+# stamps: 0 ticket, 1 deps met, 2 last update applied, 3 panels done, 6 A(k+1,k) ready,
 # 5 trsm(k+1,k) done (pivot tiles published right after), 4 L_kk^-1 done, 7 task end
 names = ["wait deps", "last update", "panels", "diag inv + trsm(k+1,k)", "stores+publish+Linv", "Linv store"]
 rows = []
@@ -55,8 +55,10 @@ for a, k in enumerate(pot):
 rows = np.array(rows)
 print("potrf tasks (%d): median us: " % len(pot) + ", ".join("%s %.2f" % (nm, v) for nm, v in zip(
     names + ["total", "chain step (panels start -> next panels start)"], np.nanmedian(rows, 0))))
-pf = p[pot, 6] - p[pot, 2]
-print("first panel_factor (wave 0, 16 columns) median %.2f us" % np.median(pf))
+below = p[pot, 5] > 0
+wa = (p[pot, 6] - p[pot, 3])[below]
+print("wait for A(k+1,k)'s other updates after the panels: median %.2f us, p90 %.2f, %d of %d > 0.5 us" % (
+    np.median(wa), np.percentile(wa, 90), int((wa > 0.5).sum()), len(wa)))
 other = np.setdiff1d(np.nonzero(p[:, 7] > 0)[0], pot)
 dur = p[other, 7] - p[other, 1]
 print("other tasks (%d): median work %.2f us, median wait %.2f us" % (len(other), np.median(dur), np.median(p[other, 1] - p[other, 0])))
