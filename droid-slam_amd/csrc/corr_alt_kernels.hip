@@ -62,6 +62,7 @@ struct AltArgs {
   int H, W;
   long ntiles;           // E * (H / 8) * (W / 8)
   long long* prof;       // profiling builds: s_memtime per (workgroup, stage < 32, phase < 8), or null
+  const int* order;      // (E) edge processed in the k-th slot of the tile walk (edges grouped by target frame), or null
 };
 
 #ifndef DROID_CONV_PROFILE
@@ -245,8 +246,9 @@ __global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
   struct Tile { int e, ty0, tx0, f1, f2; };
   auto tile_of = [&](int t) {
     Tile r;
-    r.e = __builtin_amdgcn_readfirstlane(t / tpe);
-    const int tt = t - r.e * tpe;
+    const int slot = t / tpe;   // the walk's edge slot; the tile inside the edge is the same either way
+    r.e = __builtin_amdgcn_readfirstlane(a.order ? a.order[slot] : slot);
+    const int tt = t - slot * tpe;
     r.ty0 = (tt / tcols) * 8;
     r.tx0 = (tt - (tt / tcols) * tcols) * 8;
     // plain loads: the compiler waits for them at their first use (the next
@@ -997,8 +999,9 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
   struct Tile { int e, ty0, tx0, f1, f2; };
   auto tile_of = [&](int t) {
     Tile r;
-    r.e = __builtin_amdgcn_readfirstlane(t / tpe);
-    const int tt = t - r.e * tpe;
+    const int slot = t / tpe;   // the walk's edge slot; the tile inside the edge is the same either way
+    r.e = __builtin_amdgcn_readfirstlane(a.order ? a.order[slot] : slot);
+    const int tt = t - slot * tpe;
     r.ty0 = (tt / tcols) * 8;
     r.tx0 = (tt - (tt / tcols) * tcols) * 8;
     r.f1 = a.f1[r.e];
@@ -1223,10 +1226,24 @@ int droid_alt_set_profile(void* buf) {
 #endif
 }
 
+int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int* Wl, const int* f1, const int* f2,
+                               const int* order, const float* coords, const void* w, const float* bias, void* out,
+                               int E, int H, int W, hipStream_t stream);
+
 // On-the-fly CorrBlock lookup fused with corr_encoder[0] (corr_alt_ce0_kernel).
 int droid_corr_alt_ce0(const void* const* pyr, const int* Hl, const int* Wl, const int* f1, const int* f2,
                        const float* coords, const void* w, const float* bias, void* out, int E, int H, int W,
                        hipStream_t stream) {
+  return droid_corr_alt_ce0_ordered(pyr, Hl, Wl, f1, f2, nullptr, coords, w, bias, out, E, H, W, stream);
+}
+
+// The same with the edges walked in `order` (a permutation of 0..E-1, device
+// int32; null = 0..E-1): grouping the edges that share a target frame keeps
+// that frame's pyramid rows in the XCD's L2 across their tiles' box DMAs.
+// Outputs are the same bytes in the same places whatever the order.
+int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int* Wl, const int* f1, const int* f2,
+                               const int* order, const float* coords, const void* w, const float* bias, void* out,
+                               int E, int H, int W, hipStream_t stream) {
   if (E < 0 || H <= 0 || W <= 0 || !coords || !w || !bias || !out || !f1 || !f2)
     return fail(kInvalidArgument, "corr_alt_ce0: bad arguments");
   if (H % 8 || W % 8) return fail(kUnsupported, "corr_alt_ce0: H and W must be multiples of 8");
@@ -1241,7 +1258,7 @@ int droid_corr_alt_ce0(const void* const* pyr, const int* Hl, const int* Wl, con
   }
   if (Hl[0] != H || Wl[0] != W) return fail(kInvalidArgument, "corr_alt_ce0: level 0 must be H x W");
   if ((long)H * W * 8 > 0x7fffffffL) return fail(kUnsupported, "corr_alt_ce0: coordinate plane too large");
-  a.f1 = f1; a.f2 = f2; a.coords = coords;
+  a.f1 = f1; a.f2 = f2; a.coords = coords; a.order = order;
   a.w = (const __half*)w; a.bias = bias; a.out = (__half*)out;
   a.H = H; a.W = W;
   a.ntiles = (long)E * (H / 8) * (W / 8);

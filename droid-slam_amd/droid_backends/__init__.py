@@ -248,11 +248,12 @@ def corr_lookup_ce0(levels, coords, w, bias, out=None, tiled_shapes=None, slots=
     return out
 
 
-def corr_alt_ce0(pyramid, f1, f2, coords, w, bias, out=None):
+def corr_alt_ce0(pyramid, f1, f2, coords, w, bias, out=None, order=None):
     """On-the-fly correlation lookup + corr_encoder[0] (include/droid_backends.h:
     droid_corr_alt_ce0): pyramid 4 x (NF,H_l,W_l,128) fp16 (AltCorrBlock layout),
     f1/f2 (E) int32 pyramid rows, coords (E,H,W,2) f32, w [128][224] fp16,
-    bias [128] f32 -> (E,H,W,128) fp16."""
+    bias [128] f32 -> (E,H,W,128) fp16.  order: optional (E) int32 device
+    permutation the tiles are walked in (droid_corr_alt_ce0_ordered; same output)."""
     _check_inputs(["level%d" % i for i in range(len(pyramid))] + ["f1", "f2", "coords", "w", "bias"],
                   list(pyramid) + [f1, f2, coords, w, bias])
     _need(coords, torch.float32, "coords")
@@ -268,9 +269,14 @@ def corr_alt_ce0(pyramid, f1, f2, coords, w, bias, out=None):
     ptrs = (ctypes.c_void_p * 4)(*[lv.data_ptr() for lv in pyramid])
     hs = (ctypes.c_int * 4)(*[lv.shape[-3] for lv in pyramid])
     ws = (ctypes.c_int * 4)(*[lv.shape[-2] for lv in pyramid])
+    if order is not None:
+        _check_inputs(("order",), (order,))
+        _need(order, torch.int32, "order")
+        if order.numel() != E:
+            raise RuntimeError("corr_alt_ce0: order must hold one entry per edge")
     with torch.cuda.device(coords.device):
-        check(lib.droid_corr_alt_ce0(ptrs, hs, ws, _ptr(f1), _ptr(f2), _ptr(coords), _ptr(w), _ptr(bias), _ptr(out),
-                                     E, H, W, _stream(coords)), "corr_alt_ce0")
+        check(lib.droid_corr_alt_ce0_ordered(ptrs, hs, ws, _ptr(f1), _ptr(f2), _ptr(order), _ptr(coords), _ptr(w),
+                                             _ptr(bias), _ptr(out), E, H, W, _stream(coords)), "corr_alt_ce0")
     return out
 
 

@@ -39,6 +39,7 @@ _SIGS = {
     "droid_conv_gate_tile": ([_i, _i, _i, _i], _i),
     "droid_corr_volume_pyramid": ([_p, _p, _p, _i, _i, _i, _i, _p, _i, _p], _i),
     "droid_corr_alt_ce0": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
+    "droid_corr_alt_ce0_ordered": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_conv_nhwc_f16": ([_p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _i, _i,
                              _p, _i, _p, _i, _p, _p, _i, _p, _p], _i),
     "droid_conv_gru_pre_f16": ([_p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _p, _i,

@@ -638,8 +638,17 @@ class FactorGraph:
             blk = AltCorrBlock(f.reshape((1, n * rig) + tuple(f.shape[2:])))
             self._alt_pyr = (n, [lv.view((-1,) + tuple(lv.shape[2:])) for lv in blk.pyramid])
         f1 = self._dev("alt_f1", (rig * self._ii).astype(np.int32))
-        f2 = self._dev("alt_f2", (rig * self._jj + ((self._ii == self._jj) & (rig > 1))).astype(np.int32))
-        return PendingAltLookup(self._alt_pyr[1], f1, f2, coords1)
+        f2h = (rig * self._jj + ((self._ii == self._jj) & (rig > 1))).astype(np.int32)
+        f2 = self._dev("alt_f2", f2h)
+        return PendingAltLookup(self._alt_pyr[1], f1, f2, coords1, order=self._alt_order(f2h))
+
+    def _alt_order(self, f2h):
+        """the on-demand lookup's tile walk: edges grouped by target frame (stable
+        sort), so the tiles that read one frame's pyramid rows run together and
+        find them in L2 (DROID_ALT_ORDER=0: edge order)"""
+        if os.environ.get("DROID_ALT_ORDER", "1") == "0":
+            return None
+        return self._dev("alt_order", np.argsort(f2h, kind="stable").astype(np.int32))
 
     def update_lowmem(self, t0=None, t1=None, itrs=2, use_inactive=False, EP=1e-7, steps=8):
         """factor_graph.py:245-290: `steps` x [reprojection, on-the-fly (alt)
@@ -660,7 +669,9 @@ class FactorGraph:
             blk = AltCorrBlock(f.reshape((1, num * rig) + tuple(f.shape[2:])))
             pyr = [lv.view((-1,) + tuple(lv.shape[2:])) for lv in blk.pyramid]
             f1 = self._dev("alt_f1", (rig * self._ii).astype(np.int32))
-            f2 = self._dev("alt_f2", (rig * self._jj + ((self._ii == self._jj) & (rig > 1))).astype(np.int32))
+            f2h = (rig * self._jj + ((self._ii == self._jj) & (rig > 1))).astype(np.int32)
+            f2 = self._dev("alt_f2", f2h)
+            alt_order = self._alt_order(f2h)
             uniq, inverse = np.unique(self._ii, return_inverse=True)
             dinv = self._dev("inverse", inverse.astype(np.int64))
             ptr, idx = edge_segments(inverse, len(uniq))
@@ -679,7 +690,7 @@ class FactorGraph:
                 coords1 = coords1.view(1, E, ht, wd, 2)
                 motn = motn.view(1, E, 4, ht, wd)
             if self.fused:
-                corr = PendingAltLookup(pyr, f1, f2, coords1)
+                corr = PendingAltLookup(pyr, f1, f2, coords1, order=alt_order)
                 self.net, delta, weight, damping = self.update_op(self.net, None, corr, motn[0], dinv, len(uniq),
                                                                   segments=segs, inp_frames=inp_frames)
                 with torch.autocast("cuda", enabled=False):

@@ -135,11 +135,12 @@ class PendingAltLookup:
     correlation windows on demand on MFMA, fused with corr_encoder[0]
     (droid_backends.corr_alt_ce0); no volume exists."""
 
-    def __init__(self, pyramid, f1, f2, coords):
+    def __init__(self, pyramid, f1, f2, coords, order=None):
         self.pyramid = pyramid
         self.f1 = f1
         self.f2 = f2
         self.coords = coords
+        self.order = order   # (E) int32: the tile walk's edge order (edges sharing a target frame together)
 
 
 class EncodedCorr:
@@ -295,7 +296,8 @@ class FusedUpdateModule(torch.nn.Module):
             c1 = corr.c1
         elif isinstance(corr, PendingAltLookup):
             coords = corr.coords.reshape(E, H, W, 2).float().contiguous()
-            c1 = droid_backends.corr_alt_ce0(corr.pyramid, corr.f1, corr.f2, coords, P["ce0_224"], P["ce0_b"])
+            c1 = droid_backends.corr_alt_ce0(corr.pyramid, corr.f1, corr.f2, coords, P["ce0_224"], P["ce0_b"],
+                                             order=corr.order)
         elif levels is not None and droid_backends.corr_lookup_ce0_supported(levels, H, W):
             coords = corr.coords.reshape(E, H, W, 2).float().contiguous()
             c1 = droid_backends.corr_lookup_ce0(levels, coords, P["ce0_224"], P["ce0_b"],

@@ -156,6 +156,14 @@ int droid_corr_alt_ce0(const void* const* pyr, const int* Hl, const int* Wl, con
                        const float* coords, const void* w, const float* bias, void* out, int E, int H, int W,
                        hipStream_t stream);
 
+/* droid_corr_alt_ce0 with the edges walked in `order` (device int32, a
+ * permutation of 0..E-1; null = edge order): grouping edges that share a
+ * target frame keeps its pyramid rows in L2 across their tiles.  Outputs are
+ * identical for any order. */
+int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int* Wl, const int* f1, const int* f2,
+                               const int* order, const float* coords, const void* w, const float* bias, void* out,
+                               int E, int H, int W, hipStream_t stream);
+
 /* ---- update operator ----------------------------------------------------
  * Implicit-GEMM convolution on MFMA (UpdateModule / ConvGRU convs,
  * droid_net.py:78-143, modules/gru.py:19-32), NHWC fp16 in, fp32 accumulate.

@@ -31,3 +31,16 @@ print("C3 outputs bitwise equal (1, 2):", bool(torch.equal(outs[1], outs[2])))
 d = (outs[3].float() - outs[2].float()).abs()
 print("V3 vs V2: max diff %.3g of scale %.3g, identical fraction %.4f" % (float(d.max()), float(outs[2].float().abs().max()),
                                                                      float((d == 0).float().mean())))
+# the tile walk grouped by target frame (droid_corr_alt_ce0_ordered)
+droid_backends.alt_set_variant(2)
+order = torch.argsort(f2.long(), stable=True).to(torch.int32)
+ts = []
+for it in range(8):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    o = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w, b, order=order)
+    e.record()
+    torch.cuda.synchronize()
+    ts.append(s.elapsed_time(e))
+print("variant 2, edges grouped by target frame: median %.3f ms (min %.3f); bitwise equal to edge order: %s" % (
+    float(np.median(ts[2:])), min(ts), bool(torch.equal(o, outs[2]))))

@@ -448,6 +448,40 @@ def test_corr_alt2_v3_matches_v2(noise, H, W, E, far):
     assert float((diff == 0).float().mean()) > 0.9
 
 
+def test_corr_alt_ordered_walk_is_bitwise_the_same():
+    """droid_corr_alt_ce0_ordered: walking the tiles in an edge permutation
+    (edges grouped by target frame, FactorGraph._alt_order) changes only which
+    workgroup computes a tile - the outputs are the same bytes in the same
+    places, for the default and the V3 kernel."""
+    import droid_backends
+    from droid_mi355x.corr import AltCorrBlock
+    rng = np.random.default_rng(45)
+    NF, H, W, E = 8, 48, 64, 40
+    fm = torch.from_numpy(rng.normal(size=(NF, 128, H, W)).astype(np.float16)).to(DEV)
+    ii = rng.integers(0, NF, E).astype(np.int32)
+    jj = rng.integers(0, NF, E).astype(np.int32)
+    pyr = [lv.view((-1,) + tuple(lv.shape[2:])) for lv in AltCorrBlock(fm[None]).pyramid]
+    grid = np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None].astype(np.float32)
+    coords = grid + rng.normal(0, 2.0, (E, H, W, 2)).astype(np.float32)
+    c = torch.from_numpy(coords).to(DEV).contiguous()
+    g = torch.Generator(device=DEV).manual_seed(46)
+    w224 = torch.zeros((128, 224), device=DEV)
+    w224[:, :196] = torch.randn((128, 196), generator=g, device=DEV) / 14.0
+    w224 = w224.half().contiguous()
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    f1, f2 = torch.as_tensor(ii, device=DEV), torch.as_tensor(jj, device=DEV)
+    order = torch.as_tensor(np.argsort(jj, kind="stable").astype(np.int32), device=DEV)
+    try:
+        for v in (2, 3):
+            droid_backends.alt_set_variant(v)
+            ref = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
+            out = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b, order=order)
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref), v
+    finally:
+        droid_backends.alt_set_variant(2)
+
+
 def test_corr_volume_slot_pool_matches_fresh_block():
     """The tiled CorrBlock as a slot pool (frontend edge edits: append, drop,
     append again, pool growth) looked up in place through
