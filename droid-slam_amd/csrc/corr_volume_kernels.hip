@@ -355,8 +355,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
   const int fr = lane & 15, fq = lane >> 4;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int H = a.H, W = a.W, HW = H * W;
-  const int e = __builtin_amdgcn_readfirstlane((int)(blockIdx.x / a.qblocks));
-  const int qb = (int)(blockIdx.x % a.qblocks);
+  // XCD-aware order: the hardware deals consecutive workgroups to the 8 XCDs in
+  // turn, so an edge's workgroups (its query blocks, which all read the same
+  // target frame's patches) would land on 8 different L2s and fetch that frame
+  // from HBM up to 8 times; remapped, each XCD takes a contiguous run of edges
+  const int G = (int)gridDim.x;
+  const int bid = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  const int e = __builtin_amdgcn_readfirstlane(bid / a.qblocks);
+  const int qb = bid % a.qblocks;
   const int fa = __builtin_amdgcn_readfirstlane(a.f1[e]);
   const int fb = __builtin_amdgcn_readfirstlane(a.f2[e]);
   const unsigned lds_a = lds_addr(lds);
