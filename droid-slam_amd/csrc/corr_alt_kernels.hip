@@ -966,9 +966,24 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
   const unsigned lds_a = lds_addr(lds);
 
   // XCD-aware order: the workgroups of one XCD (blockIdx % 8) walk adjacent tiles
+  // XCD-aware walk: XCD x (the workgroups blockIdx % 8 == x) sweeps its own
+  // contiguous eighth of the tiles, its workgroups interleaved inside it, so
+  // consecutive edges - grouped by target frame when a.order is given - run on
+  // one L2 and the frame's pyramid rows are fetched from HBM about once
   const int G = gridDim.x;
-  const int b0 = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  if (b0 >= a.ntiles) return;
+  int b0, step;
+  long tend;
+  if (G % 8 == 0) {
+    const long per = (a.ntiles + 7) / 8;
+    b0 = (int)((blockIdx.x % 8) * per + blockIdx.x / 8);
+    step = G / 8;
+    tend = std::min<long>(a.ntiles, (long)(blockIdx.x % 8 + 1) * per);
+  } else {
+    b0 = (int)blockIdx.x;
+    step = G;
+    tend = a.ntiles;
+  }
+  if (b0 >= tend) return;
 
   // corr_encoder[0] B fragments of this wave's 32 output channels (2 N-blocks):
   // per level K = 49 real columns padded to 64 (2 K-steps of 32)
@@ -1107,8 +1122,8 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
   __syncthreads();
 
   for (;;) {
-    const int tn_ = t + G;
-    const bool more = tn_ < a.ntiles;
+    const int tn_ = t + step;
+    const bool more = tn_ < tend;
     const Tile nxt = more ? tile_of(tn_) : cur;
     const float* cxy = reinterpret_cast<const float*>(lds + kB2Coord + slot * 512);
     const int* lv = reinterpret_cast<const int*>(lds + kB2Lvl) + slot * 16;
