@@ -12,6 +12,7 @@ cd "$R" || exit 1
 export PYTHONUNBUFFERED=1
 export DROID_REPORT_DIR="$R/gpurun_out/$TAG"
 O="gpurun_out/$TAG"
+PYN=0
 mkdir -p "$O"
 
 fail() { echo "step $1 failed (rc=$2)"; tail -40 "$3"; exit "$2"; }
@@ -77,8 +78,9 @@ for step in "$@"; do
       # export K=V for the steps that follow (A/B runs: env:DROID_OVERLAP_GLO=0 bench:C3)
       export "${step#env:}"; echo "export ${step#env:}" ;;
     py:*)
-      timeout -k 10 600 python -u ${step#py:} > "$O/py.txt" 2>&1 || fail "$step" $? "$O/py.txt"
-      tail -30 "$O/py.txt" ;;
+      PYN=$((PYN+1)); PO="$O/py$PYN.txt"
+      timeout -k 10 600 python -u ${step#py:} > "$PO" 2>&1 || fail "$step" $? "$PO"
+      tail -30 "$PO" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
