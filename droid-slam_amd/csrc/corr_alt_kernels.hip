@@ -63,6 +63,7 @@ struct AltArgs {
   long ntiles;           // E * (H / 8) * (W / 8)
   long long* prof;       // profiling builds: s_memtime per (workgroup, stage < 32, phase < 8), or null
   const int* order;      // (E) edge processed in the k-th slot of the tile walk (edges grouped by target frame), or null
+  int chunk;             // corr_alt2_kernel: tiles per XCD chunk (0 = the plain interleaved walk)
 };
 
 #ifndef DROID_CONV_PROFILE
@@ -965,25 +966,23 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
   const int tcols = W / 8, tpe = (H / 8) * tcols;
   const unsigned lds_a = lds_addr(lds);
 
-  // XCD-aware order: the workgroups of one XCD (blockIdx % 8) walk adjacent tiles
-  // XCD-aware walk: XCD x (the workgroups blockIdx % 8 == x) sweeps its own
-  // contiguous eighth of the tiles, its workgroups interleaved inside it, so
-  // consecutive edges - grouped by target frame when a.order is given - run on
-  // one L2 and the frame's pyramid rows are fetched from HBM about once
+  // XCD-aware walk: the tile walk is cut into chunks of a.chunk tiles (a few
+  // edges), dealt round-robin to the 8 XCDs (the workgroups blockIdx % 8 == x);
+  // an XCD's workgroups interleave inside its chunks.  The edges of a chunk -
+  // grouped by target frame when a.order is given - then share one L2, and all
+  // XCDs still progress through the walk together (per-edge costs differ with
+  // the motion, so contiguous per-XCD eighths finish unevenly).  Local step j of
+  // XCD x is tile ((j / C) * 8 + x) * C + j % C, increasing in j.
   const int G = gridDim.x;
-  int b0, step;
-  long tend;
-  if (G % 8 == 0) {
-    const long per = (a.ntiles + 7) / 8;
-    b0 = (int)((blockIdx.x % 8) * per + blockIdx.x / 8);
-    step = G / 8;
-    tend = std::min<long>(a.ntiles, (long)(blockIdx.x % 8 + 1) * per);
-  } else {
-    b0 = (int)blockIdx.x;
-    step = G;
-    tend = a.ntiles;
-  }
-  if (b0 >= tend) return;
+  const bool chunked = (G % 8 == 0) && a.chunk > 0;
+  const int nx = chunked ? 8 : 1, xcd = (int)blockIdx.x % nx, step = G / nx;
+  const int C = chunked ? a.chunk : 1;
+  auto walk = [&](int j) -> int {
+    return chunked ? ((j / C) * 8 + xcd) * C + j % C : j;
+  };
+  int j = (int)blockIdx.x / nx;
+  const int b0 = walk(j);
+  if (b0 >= a.ntiles) return;
 
   // corr_encoder[0] B fragments of this wave's 32 output channels (2 N-blocks):
   // per level K = 49 real columns padded to 64 (2 K-steps of 32)
@@ -1122,8 +1121,9 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
   __syncthreads();
 
   for (;;) {
-    const int tn_ = t + step;
-    const bool more = tn_ < tend;
+    j += step;
+    const int tn_ = walk(j);
+    const bool more = tn_ < a.ntiles;
     const Tile nxt = more ? tile_of(tn_) : cur;
     const float* cxy = reinterpret_cast<const float*>(lds + kB2Coord + slot * 512);
     const int* lv = reinterpret_cast<const int*>(lds + kB2Lvl) + slot * 16;
@@ -1218,6 +1218,13 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
 using namespace droid;
 
 static long long* g_alt_prof = nullptr;
+static int& alt_chunk_edges() {
+  static int v = [] {
+    const char* e = getenv("DROID_ALT_CHUNK");
+    return e ? std::max(0, atoi(e)) : 8;
+  }();
+  return v;
+}
 static int& alt_variant() {
   static int v = [] {
     const char* e = getenv("DROID_ALT_VARIANT");
@@ -1279,6 +1286,10 @@ int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int*
   a.ntiles = (long)E * (H / 8) * (W / 8);
   if (a.ntiles + device_cu_count() >= 0x7fffffffL) return fail(kUnsupported, "corr_alt_ce0: too many tiles");
   a.prof = g_alt_prof;
+  // corr_alt2_kernel's XCD chunks: DROID_ALT_CHUNK edges' tiles (default 8, about
+  // the edges per target frame of a DROID graph; 0 = the plain interleaved walk)
+  const long chunk = (long)alt_chunk_edges() * (H / 8) * (W / 8);
+  a.chunk = (chunk > 0 && 8 * chunk + a.ntiles < 0x7fffffffL) ? (int)chunk : 0;
   if (a.ntiles == 0) return kOk;
   static bool attr = false;
   if (!attr) {
@@ -1312,6 +1323,14 @@ int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int*
 
 // A/B hook: 1 = the one-workgroup-per-CU kernel, 2 = corr_alt2_kernel (default),
 // 3 = corr_alt2_kernel<V3> (env DROID_ALT_VARIANT sets the initial value)
+// A/B hook: corr_alt2_kernel's XCD chunk in edges (0 = the plain interleaved
+// walk; env DROID_ALT_CHUNK sets the initial value, default 8)
+int droid_alt_set_chunk(int edges) {
+  if (edges < 0) return fail(kInvalidArgument, "alt_set_chunk: edges >= 0");
+  alt_chunk_edges() = edges;
+  return kOk;
+}
+
 int droid_alt_set_variant(int v) {
   if (v < 1 || v > 3) return fail(kInvalidArgument, "alt_set_variant: 1, 2 or 3");
   alt_variant() = v;

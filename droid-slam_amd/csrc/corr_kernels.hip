@@ -245,6 +245,33 @@ corr_pyramid_f16_r3_kernel(PyramidArgs args, const float* __restrict__ coords,
 // and 16-B aligned levels; PLANAR: coords (B,2,H,W) (corr_index_forward),
 // else (E,H,W,2) at level-0 scale.
 // ---------------------------------------------------------------------------
+// window row taps x = xs .. xs + 7: dwords off/2 .. of the row's two 16-B pieces, funnel-shifted
+__device__ __forceinline__ void coop_taps(uint4 p0v, uint4 p1v, int off, float* t) {
+  // plain values and selects (an array indexed under a select becomes a
+  // scratch-memory array)
+  const bool k2 = off & 4, k1 = off & 2;
+  const unsigned v0 = k2 ? p0v.z : p0v.x, v1 = k2 ? p0v.w : p0v.y, v2 = k2 ? p1v.x : p0v.z;
+  const unsigned v3 = k2 ? p1v.y : p0v.w, v4 = k2 ? p1v.z : p1v.x, v5 = k2 ? p1v.w : p1v.y;
+  const unsigned w0 = k1 ? v1 : v0, w1 = k1 ? v2 : v1, w2 = k1 ? v3 : v2, w3 = k1 ? v4 : v3, w4 = k1 ? v5 : v4;
+  const unsigned sh = (off & 1) ? 16u : 0u;
+  const unsigned q0 = __builtin_amdgcn_alignbit(w1, w0, sh), q1 = __builtin_amdgcn_alignbit(w2, w1, sh);
+  const unsigned q2 = __builtin_amdgcn_alignbit(w3, w2, sh), q3 = __builtin_amdgcn_alignbit(w4, w3, sh);
+  const unsigned q[4] = {q0, q1, q2, q3};
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    t[2 * m + 0] = __half2float(__ushort_as_half((unsigned short)(q[m] & 0xffffu)));
+    t[2 * m + 1] = __half2float(__ushort_as_half((unsigned short)(q[m] >> 16)));
+  }
+}
+__device__ __forceinline__ uint4 dpp_next_lane(uint4 v) {   // lane + 1's value (DPP row_shl:1)
+  uint4 r;
+  r.x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.x, 0x101, 0xF, 0xF, false);
+  r.y = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.y, 0x101, 0xF, 0xF, false);
+  r.z = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.z, 0x101, 0xF, 0xF, false);
+  r.w = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.w, 0x101, 0xF, 0xF, false);
+  return r;
+}
+
 struct LookupLvlArgs {
   const __half* vol[4];
   int H2[4], W2[4];
@@ -315,24 +342,7 @@ __global__ void __launch_bounds__(256) corr_lookup_lvl_kernel(LookupLvlArgs a) {
     raw[j][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, 0));
   }
   __half* o = a.out + (long)e * a.out_estride + (long)lvl * RD * RD * HW + pc;
-  auto taps = [&](int j, float* t) {
-    // taps x = xs .. xs+7 of row j: dwords off/2 .. of the two pieces, funnel-shifted
-    const uint4 p0v = raw[j][0], p1v = raw[j][1];
-    const unsigned u[8] = {p0v.x, p0v.y, p0v.z, p0v.w, p1v.x, p1v.y, p1v.z, p1v.w};
-    const int k = off >> 1;
-    unsigned v[6], w[5];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) v[i] = (k & 2) ? u[i + 2] : u[i];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) w[i] = (k & 1) ? v[i + 1] : v[i];
-    const unsigned sh = (off & 1) ? 16u : 0u;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const unsigned q = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
-      t[2 * m + 0] = __half2float(__ushort_as_half((unsigned short)(q & 0xffffu)));
-      t[2 * m + 1] = __half2float(__ushort_as_half((unsigned short)(q >> 16)));
-    }
-  };
+  auto taps = [&](int j, float* t) { coop_taps(raw[j][0], raw[j][1], off, t); };
   float prev[8], cur[8];
   taps(0, prev);
 #pragma unroll
@@ -349,6 +359,107 @@ __global__ void __launch_bounds__(256) corr_lookup_lvl_kernel(LookupLvlArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) prev[i] = cur[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Cooperative NCHW lookup (round 4, the reference-layout CorrBlock.__call__):
+// the same (pixel, level) arithmetic as corr_lookup_lvl_kernel, bit for bit,
+// with the fused path's cooperative gather and staged stores.  A wave owns 64
+// consecutive pixels of one edge and level; in round r lane (pp = lane >> 3,
+// j = lane & 7) loads window row j (two 16-B pieces) of pixel 8 r + pp, so a
+// load instruction touches 8 pixels x <= 2 lines each instead of 64 pixels x
+// 4 lines (the per-thread kernel's TA / line pressure).  Window row j + 1 comes
+// from the next lane (DPP row_shl:1, the 8-lane groups never straddle a DPP
+// row), lane j < 7 forms the 7 outputs of window row j, and they go through
+// an LDS tile [49 channels][64 px] so every global store is a 16-B piece of a
+// 128-B channel row.  Needs H*W % 64 == 0 and a 16-B aligned output.
+// ---------------------------------------------------------------------------
+constexpr int kCoopPitch = 72;   // staging row pitch in halves (144 B: 16-B aligned rows)
+template <bool TILED>
+__global__ void __launch_bounds__(256) corr_lookup_coop_kernel(LookupLvlArgs a) {
+  constexpr int R = 3, RD = 7, SP = kCoopPitch;
+  __shared__ __attribute__((aligned(16))) __half stage[4][RD * RD * SP];
+  const int HW = a.H * a.W;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int pw0 = blockIdx.x * 256 + wave * 64;
+  if (pw0 >= HW) return;   // wave-uniform (HW % 64 == 0); no workgroup barrier below
+  const int e = blockIdx.y, lvl = blockIdx.z;
+  const int H2 = a.H2[lvl], W2 = a.W2[lvl], nch = W2 >> 3;
+  const long slice = TILED ? (long)((H2 + 7) >> 3) * 8 * W2 : (long)H2 * W2;
+  const long vrow = (TILED && a.slot) ? (long)a.slot[e] : (long)e;
+  const int pp = lane >> 3, j = lane & 7;
+  const float s = 1.0f / (float)(1 << lvl);
+  float2 cc[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+    cc[r] = *reinterpret_cast<const float2*>(a.coords + ((long)e * HW + pw0 + 8 * r + pp) * 2);
+  // the wave's 64 pixel slices as one descriptor
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__half*>(a.vol[lvl] + (vrow * HW + pw0) * slice), (short)0, (int)(64 * slice * 2), kBufFlags);
+  auto geom = [&](int r, int& xs, int& c0, float& dx, float& dy, int& yi0) {
+    const float x0 = cc[r].x * s, y0 = cc[r].y * s;
+    const float fx0 = floorf(x0), fy0 = floorf(y0);
+    dx = x0 - fx0;
+    dy = y0 - fy0;
+    yi0 = (int)fy0;
+    xs = (int)fx0 - R;
+    c0 = (xs >= 0) ? (xs >> 3) : -((-xs + 7) >> 3);
+  };
+  uint4 raw[8][2];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    int xs, c0, yi0;
+    float dx, dy;
+    geom(r, xs, c0, dx, dy, yi0);
+    const bool ok0 = c0 >= 0 && c0 < nch, ok1 = c0 + 1 >= 0 && c0 + 1 < nch;
+    const int y1 = yi0 - R + j;
+    const bool yok = y1 >= 0 && y1 < H2;
+    const unsigned pbase = (unsigned)((8 * r + pp) * slice) * 2u;
+    const int rb = TILED ? (y1 >> 3) * 8 * W2 + (y1 & 7) * 8 : y1 * W2;
+    const int cm = TILED ? 64 : 8;
+    const unsigned o0 = (yok && ok0) ? pbase + (unsigned)(rb + cm * c0) * 2u : kOob;
+    const unsigned o1 = (yok && ok1) ? pbase + (unsigned)(rb + cm * (c0 + 1)) * 2u : kOob;
+    raw[r][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o0, 0, 0));
+    raw[r][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, 0));
+  }
+  __half* const st = stage[wave];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    int xs, c0, yi0;
+    float dx, dy;
+    geom(r, xs, c0, dx, dy, yi0);
+    const int off = xs - 8 * c0;
+    const float w11 = rnd16(dx * dy);
+    const float w10 = rnd16(dx * (1.0f - dy));
+    const float w01 = rnd16((1.0f - dx) * dy);
+    const float w00 = rnd16((1.0f - dx) * (1.0f - dy));
+    // window row j + 1 of the same pixel is lane + 1's row
+    const uint4 n0 = dpp_next_lane(raw[r][0]), n1 = dpp_next_lane(raw[r][1]);
+    float prev[8], cur[8];
+    coop_taps(raw[r][0], raw[r][1], off, prev);
+    coop_taps(n0, n1, off, cur);
+    if (j < RD) {
+#pragma unroll
+      for (int x = 0; x < RD; ++x) {
+        float acc = 0.f + rnd16(prev[x] * w00);
+        acc = rnd16(acc + rnd16(cur[x] * w01));
+        acc = rnd16(acc + rnd16(prev[x + 1] * w10));
+        acc = rnd16(acc + rnd16(cur[x + 1] * w11));
+        st[(x * RD + j) * SP + 8 * r + pp] = __float2half(acc);   // channel x*7 + b, b = j
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  __half* const o = a.out + (long)e * a.out_estride + (long)lvl * RD * RD * HW + pw0;
+#pragma unroll
+  for (int k0 = 0; k0 < RD * RD * 8; k0 += 64) {
+    const int k = k0 + lane;
+    if (k < RD * RD * 8) {
+      const int ch = k >> 3, seg = k & 7;
+      *reinterpret_cast<uint4*>(o + (long)ch * HW + seg * 8) = *reinterpret_cast<const uint4*>(&st[ch * SP + seg * 8]);
+    }
   }
 }
 
@@ -508,7 +619,26 @@ static bool lookup_lvl_on() {
   return on;
 }
 
+// the cooperative NCHW lookup (corr_lookup_coop_kernel) for the 4-level
+// reference lookups; DROID_LOOKUP_COOP=0 / droid_lookup_set_coop(0) for the
+// per-thread kernel (A/B and the bitwise test)
+static int& lookup_coop() {
+  static int v = [] {
+    const char* e = getenv("DROID_LOOKUP_COOP");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+static bool coop_ok(int HW, const void* out, long maxslice) {
+  return lookup_coop() && HW % 64 == 0 && !(reinterpret_cast<uintptr_t>(out) & 15u) && 64 * maxslice * 2 < 0x7fffffffL;
+}
+
 extern "C" {
+
+int droid_lookup_set_coop(int on) {
+  lookup_coop() = on ? 1 : 0;
+  return kOk;
+}
 
 // dtype codes: 0 = fp16, 1 = fp32, 2 = fp64
 int droid_corr_index_forward(int dtype, const void* volume, const float* coords, void* corr,
@@ -590,7 +720,10 @@ int droid_corr_pyramid_lookup_tiled(const void* const* levels, const int* H2s, c
   a.H = H;
   a.W = W;
   a.coord_scale = 1.0f;
-  corr_lookup_lvl_kernel<false, true><<<dim3(ceil_div(H * W, 256), E, num_levels), 256, 0, stream>>>(a);
+  if (coop_ok(H * W, out, maxslice))
+    corr_lookup_coop_kernel<true><<<dim3(ceil_div(H * W, 256), E, num_levels), 256, 0, stream>>>(a);
+  else
+    corr_lookup_lvl_kernel<false, true><<<dim3(ceil_div(H * W, 256), E, num_levels), 256, 0, stream>>>(a);
   DROID_LAUNCH_CHECK();
   return kOk;
 }
@@ -623,7 +756,10 @@ int droid_corr_pyramid_lookup(int dtype, const void* const* levels, const int* H
     a.H = H;
     a.W = W;
     a.coord_scale = 1.0f;
-    corr_lookup_lvl_kernel<false><<<dim3(ceil_div(H * W, 256), E, num_levels), 256, 0, stream>>>(a);
+    if (coop_ok(H * W, out, maxslice))
+      corr_lookup_coop_kernel<false><<<dim3(ceil_div(H * W, 256), E, num_levels), 256, 0, stream>>>(a);
+    else
+      corr_lookup_lvl_kernel<false><<<dim3(ceil_div(H * W, 256), E, num_levels), 256, 0, stream>>>(a);
     DROID_LAUNCH_CHECK();
     return kOk;
   }

@@ -285,6 +285,16 @@ def alt_set_variant(v):
     check(lib.droid_alt_set_variant(int(v)), "alt_set_variant")
 
 
+def lookup_set_coop(on):
+    """A/B hook (droid_lookup_set_coop): the cooperative NCHW lookup (1, default) or the per-thread kernel (0)."""
+    check(lib.droid_lookup_set_coop(1 if on else 0), "lookup_set_coop")
+
+
+def alt_set_chunk(edges):
+    """A/B hook (droid_alt_set_chunk): edges per XCD chunk of corr_alt2_kernel's walk, 0 = interleaved."""
+    check(lib.droid_alt_set_chunk(int(edges)), "alt_set_chunk")
+
+
 def conv_set_tile(mode):
     """Tile policy of the W=64 3x3 band convs (droid_conv_set_tile): -1 default,
     0 = 8-wave band tiles only, 1 = the two-workgroups-per-CU tile wherever it

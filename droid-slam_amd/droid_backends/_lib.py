@@ -35,6 +35,8 @@ _SIGS = {
     "droid_conv_set_profile": ([_p], _i),
     "droid_alt_set_profile": ([_p], _i),
     "droid_alt_set_variant": ([_i], _i),
+    "droid_alt_set_chunk": ([_i], _i),
+    "droid_lookup_set_coop": ([_i], _i),
     "droid_conv_set_tile": ([_i], _i),
     "droid_conv_gate_tile": ([_i, _i, _i, _i], _i),
     "droid_corr_volume_pyramid": ([_p, _p, _p, _i, _i, _i, _i, _p, _i, _p], _i),

@@ -91,6 +91,11 @@ int droid_alt_set_profile(void* buf);
  * default; env DROID_ALT_VARIANT=1 selects 1 at load).  Outputs are bitwise
  * equal; tests compare the two. */
 int droid_alt_set_variant(int v);
+/* Tuning hook: edges per XCD chunk of corr_alt2_kernel's tile walk (0 = interleaved; default 8). */
+int droid_alt_set_chunk(int edges);
+/* Tuning hook: 1 = the cooperative NCHW lookup for droid_corr_pyramid_lookup(_tiled) (default),
+ * 0 = the per-thread kernel; outputs are bitwise equal. */
+int droid_lookup_set_coop(int on);
 /* Tile policy of the W == 64 3x3 band convs (not part of the reference
  * interface; tests run both tiles in one process): -1 = default (the plain
  * convs and small gate-conv grids on the two-workgroups-per-CU tile, larger

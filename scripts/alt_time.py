@@ -1,5 +1,7 @@
 """Median launch time of corr_alt_ce0 on the C3 bench coordinates (2048 edges,
-48x64) for the library in $DROID_HIP_LIB (scripts/alt_ablate.sh variants)."""
+48x64) for the library in $DROID_HIP_LIB (scripts/alt_ablate.sh variants), and
+corr_alt2_kernel's walk: edge order vs edges grouped by target frame, times the
+XCD chunk size (droid_alt_set_chunk)."""
 import os
 import sys
 
@@ -13,34 +15,35 @@ from c3_alt_inputs import c3_alt_inputs  # noqa: E402
 
 dev = torch.device("cuda:0")
 pyr, f1, f2, c, w, b = c3_alt_inputs(dev)
-outs = {}
-for variant in (1, 2, 3):   # droid_alt_set_variant: the one-workgroup kernel, corr_alt2_kernel, <V3>
-    droid_backends.alt_set_variant(variant)
+
+
+def timed(**kw):
     ts = []
     for it in range(8):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        o = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w, b)
+        o = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w, b, **kw)
         e.record()
         torch.cuda.synchronize()
         ts.append(s.elapsed_time(e))
-    outs[variant] = o
-    print("%s variant %d: median %.3f ms (min %.3f)" % (os.environ.get("DROID_HIP_LIB", "default"), variant,
-                                                        float(np.median(ts[2:])), min(ts)))
+    return o, float(np.median(ts[2:])), min(ts)
+
+
+outs = {}
+for variant in (1, 2, 3):   # droid_alt_set_variant: the one-workgroup kernel, corr_alt2_kernel, <V3>
+    droid_backends.alt_set_variant(variant)
+    outs[variant], med, mn = timed()
+    print("%s variant %d: median %.3f ms (min %.3f)" % (os.environ.get("DROID_HIP_LIB", "default"), variant, med, mn))
 print("C3 outputs bitwise equal (1, 2):", bool(torch.equal(outs[1], outs[2])))
 d = (outs[3].float() - outs[2].float()).abs()
 print("V3 vs V2: max diff %.3g of scale %.3g, identical fraction %.4f" % (float(d.max()), float(outs[2].float().abs().max()),
                                                                      float((d == 0).float().mean())))
-# the tile walk grouped by target frame (droid_corr_alt_ce0_ordered)
 droid_backends.alt_set_variant(2)
 order = torch.argsort(f2.long(), stable=True).to(torch.int32)
-ts = []
-for it in range(8):
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    o = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w, b, order=order)
-    e.record()
-    torch.cuda.synchronize()
-    ts.append(s.elapsed_time(e))
-print("variant 2, edges grouped by target frame: median %.3f ms (min %.3f); bitwise equal to edge order: %s" % (
-    float(np.median(ts[2:])), min(ts), bool(torch.equal(o, outs[2]))))
+for chunk in (0, 1, 2, 4, 8, 16, 32):
+    droid_backends.alt_set_chunk(chunk)
+    for name, o_ in (("edge order", None), ("by target frame", order)):
+        o, med, mn = timed(order=o_)
+        print("variant 2, chunk %2d edges, %-15s: median %.3f ms (min %.3f) bitwise %s" % (
+            chunk, name, med, mn, bool(torch.equal(o, outs[2]))))
+droid_backends.alt_set_chunk(8)

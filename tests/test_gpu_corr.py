@@ -95,6 +95,39 @@ def test_tiled_pool_lookup_bitexact():
     np.testing.assert_array_equal(host(got)[:, :2].view(np.uint16), ora.view(np.uint16))
 
 
+def test_coop_lookup_bitwise_equals_per_thread_kernel():
+    """droid_corr_pyramid_lookup(_tiled)'s cooperative NCHW kernel (a wave per
+    64 pixels, staged 16-B stores) == the per-thread kernel (droid_lookup_set_coop(0)),
+    bit for bit, on the row-major and the tiled volume, with coordinates far off
+    the map and on the borders; a 40x56 image (H*W % 64 == 0, 35 waves) and a
+    20x36 one (H*W % 64 != 0: the per-thread kernel either way)."""
+    import droid_backends
+    from droid_mi355x.corr import CorrBlock
+    rng = np.random.default_rng(15)
+    try:
+        for H, W, E in ((40, 56, 12), (20, 40, 5)):
+            f1 = dev(rng.normal(size=(1, E, 128, H, W)).astype(np.float16))
+            f2 = dev(rng.normal(size=(1, E, 128, H, W)).astype(np.float16))
+            coords = np.stack(np.meshgrid(np.arange(W), np.arange(H)), -1)[None, None].astype(np.float32)
+            coords = np.repeat(coords, E, axis=1) + rng.normal(0, 6.0, (1, E, H, W, 2)).astype(np.float32)
+            coords[0, 0, :4, :4] = [[-40.0, 100.0]]
+            coords[0, 1, 2, 3] = [W - 0.3, H - 0.1]
+            coords[0, 2, 5] = [-3.5, -3.5]
+            coords[0, 3, 7] = [W + 2.5, 1.25]
+            c = dev(coords)
+            with torch.no_grad():
+                for tiled in (False, True):
+                    blk = CorrBlock(f1, f2, tiled=tiled)
+                    droid_backends.lookup_set_coop(1)
+                    got = blk(c)
+                    droid_backends.lookup_set_coop(0)
+                    ref = blk(c)
+                    torch.cuda.synchronize()
+                    assert torch.equal(got, ref), (H, W, tiled)
+    finally:
+        droid_backends.lookup_set_coop(1)
+
+
 def test_corr_index_backward_vs_oracle():
     import droid_backends
     rng = np.random.default_rng(13)

@@ -478,8 +478,19 @@ def test_corr_alt_ordered_walk_is_bitwise_the_same():
             out = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b, order=order)
             torch.cuda.synchronize()
             assert torch.equal(out, ref), v
+        # the XCD chunking of the walk (droid_alt_set_chunk): interleaved, one
+        # edge, a chunk that does not divide the 40 edges, more than all of them
+        droid_backends.alt_set_variant(2)
+        ref = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
+        for chunk in (0, 1, 3, 64):
+            droid_backends.alt_set_chunk(chunk)
+            for o in (None, order):
+                out = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b, order=o)
+                torch.cuda.synchronize()
+                assert torch.equal(out, ref), (chunk, o is None)
     finally:
         droid_backends.alt_set_variant(2)
+        droid_backends.alt_set_chunk(8)
 
 
 def test_corr_volume_slot_pool_matches_fresh_block():
