@@ -457,7 +457,9 @@ def main():
         ms = 1000.0 * elapsed / args.steps
         bytes_per_launch = (LOOKUP_BYTES_PER_EDGE if args.reference_op else LOOKUP_CE0_BYTES_PER_EDGE) * e_local
         achieved = bytes_per_launch / (lookup_ms * 1e-3) / 1e9 if lookup_ms else None
-        ref_lookup = ("corr_lookup_lvl_kernel<false, true> (4-level lookup, NCHW out, 8x8-tiled volume pool)"
+        coop = os.environ.get("DROID_LOOKUP_COOP") != "0" and (args.ht // 8) * (args.wd // 8) % 64 == 0
+        ref_lookup = (("corr_lookup_coop_kernel<true> (cooperative 4-level lookup, NCHW out, 8x8-tiled volume pool)"
+                       if coop else "corr_lookup_lvl_kernel<false, true> (4-level lookup, NCHW out, 8x8-tiled volume pool)")
                       if LOOKUP_FN[0] == "corr_pyramid_lookup_tiled" else
                       "corr_pyramid_f16_r3_kernel<NCHW> (4-level lookup)" if os.environ.get("DROID_LOOKUP_V1") == "1"
                       else "corr_lookup_lvl_kernel<false> (4-level lookup, NCHW out)")
@@ -466,8 +468,9 @@ def main():
                        "bound": "hbm",
                        "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                        "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
-                       "traffic": load_traffic("corr_lookup", e_local, "corr_pyramid_f16_r3_kernel" if args.reference_op
-                                               else "corr_ce0_kernel<true>"), "launch_ms": lookup_ms,
+                       "traffic": (load_traffic("corr_lookup_nchw", e_local, "corr_lookup_coop_kernel")
+                                   if args.reference_op else load_traffic("corr_lookup", e_local, "corr_ce0_kernel<true>")),
+                       "launch_ms": lookup_ms,
                        "algorithmic_bytes_per_launch": bytes_per_launch}
         if zr_ms:
             flops = (ZR_PRE_FLOPS_PER_PIXEL if factored else ZR_FLOPS_PER_PIXEL) * e_local * (args.ht // 8) * (args.wd // 8)

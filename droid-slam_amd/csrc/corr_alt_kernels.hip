@@ -1221,7 +1221,7 @@ static long long* g_alt_prof = nullptr;
 static int& alt_chunk_edges() {
   static int v = [] {
     const char* e = getenv("DROID_ALT_CHUNK");
-    return e ? std::max(0, atoi(e)) : 8;
+    return e ? std::max(0, atoi(e)) : 0;
   }();
   return v;
 }
@@ -1286,8 +1286,9 @@ int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int*
   a.ntiles = (long)E * (H / 8) * (W / 8);
   if (a.ntiles + device_cu_count() >= 0x7fffffffL) return fail(kUnsupported, "corr_alt_ce0: too many tiles");
   a.prof = g_alt_prof;
-  // corr_alt2_kernel's XCD chunks: DROID_ALT_CHUNK edges' tiles (default 8, about
-  // the edges per target frame of a DROID graph; 0 = the plain interleaved walk)
+  // corr_alt2_kernel's XCD chunks: DROID_ALT_CHUNK edges' tiles (0, the default:
+  // the plain interleaved walk - chunks of 1-32 edges measured 0-12 % slower at
+  // C3, with or without the target-frame order, profiles/r04/r04n_alt_time.txt)
   const long chunk = (long)alt_chunk_edges() * (H / 8) * (W / 8);
   a.chunk = (chunk > 0 && 8 * chunk + a.ntiles < 0x7fffffffL) ? (int)chunk : 0;
   if (a.ntiles == 0) return kOk;

@@ -854,7 +854,8 @@ __device__ __forceinline__ long vol_elem(bool tiled, int tcols, int W, int y, in
 
 __global__ void __launch_bounds__(256) corr_volume_pool23_kernel(VolArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave-uniform in an SGPR: the per-query buffer descriptors below stay scalar
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int H = a.H, W = a.W, HW = H * W;
   const long nq = a.qblocks;   // = E * H * W (set by the launcher)
   const bool tiled = a.tiled != 0;
@@ -867,6 +868,106 @@ __global__ void __launch_bounds__(256) corr_volume_pool23_kernel(VolArgs a) {
     TR[l] = (Hl[l] + 7) / 8;
     TC[l] = Wl[l] / 8;
     slice[l] = tiled ? (long)TR[l] * TC[l] * 64 : (long)Hl[l] * Wl[l];
+  }
+  const int n2 = (int)slice[2], n3 = (int)slice[3], n1 = (int)slice[1];
+  if (n2 <= 8 * 64 && n3 <= 64) {
+    // the common shapes (C3's 48x64: 256 + 64 halves): two query pixels per wave
+    // step with every level-1 load of both in flight before the first use (the
+    // generic loop below waits for each 64-element run's loads in turn), all
+    // through per-query buffer descriptors with out-of-range offsets for the
+    // elements a query does not have - branch-free, fixed instruction counts
+    constexpr int QPW = 2;
+    _Float16* s2q = reinterpret_cast<_Float16*>(lds) + (long)wave * QPW * Hl[2] * Wl[2];
+    for (long qp0 = ((long)blockIdx.x * 4 + wave) * QPW; qp0 < nq; qp0 += 4L * QPW * gridDim.x) {
+      unsigned top[QPW][8], bot[QPW][8];
+#pragma unroll
+      for (int k = 0; k < QPW; ++k) {
+        const long qp = qp0 + k;
+        const bool qok = qp < nq;
+        const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<__half*>(a.lvl[1] + (qok ? qp : 0) * slice[1]), (short)0, qok ? n1 * 2 : 0, kBufFlags);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int s = lane + 64 * i;
+          int y, x;
+          if (tiled) {
+            const int t = s >> 6, r = s & 63;
+            y = (t / TC[2]) * 8 + (r >> 3);
+            x = (t % TC[2]) * 8 + (r & 7);
+          } else {
+            y = s / Wl[2];
+            x = s % Wl[2];
+          }
+          const bool ok = s < n2 && y < Hl[2];
+          const unsigned ot = ok ? (unsigned)vol_elem(tiled, TC[1], Wl[1], 2 * y, 2 * x) * 2u : kOob;
+          const unsigned ob = ok ? (unsigned)vol_elem(tiled, TC[1], Wl[1], 2 * y + 1, 2 * x) * 2u : kOob;
+          top[k][i] = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(r1, (int)ot, 0, 0);
+          bot[k][i] = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(r1, (int)ob, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < QPW; ++k) {
+        const long qp = qp0 + k;
+        const bool qok = qp < nq;
+        const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(
+            a.lvl[2] + (qok ? qp : 0) * slice[2], (short)0, qok ? n2 * 2 : 0, kBufFlags);
+        _Float16* s2 = s2q + k * Hl[2] * Wl[2];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int s = lane + 64 * i;
+          int y, x;
+          if (tiled) {
+            const int t = s >> 6, r = s & 63;
+            y = (t / TC[2]) * 8 + (r >> 3);
+            x = (t % TC[2]) * 8 + (r & 7);
+          } else {
+            y = s / Wl[2];
+            x = s % Wl[2];
+          }
+          float v = 0.0f;
+          if (s < n2 && y < Hl[2]) {
+            const unsigned t0 = top[k][i], b0 = bot[k][i];
+            v = vol_pool4(__half2float(__ushort_as_half((unsigned short)(t0 & 0xffffu))),
+                          __half2float(__ushort_as_half((unsigned short)(t0 >> 16))),
+                          __half2float(__ushort_as_half((unsigned short)(b0 & 0xffffu))),
+                          __half2float(__ushort_as_half((unsigned short)(b0 >> 16))));
+            s2[y * Wl[2] + x] = (_Float16)v;
+          }
+          __builtin_amdgcn_raw_buffer_store_b16((short)__half_as_ushort(__float2half(v)), r2,
+                                                s < n2 ? s * 2 : (int)kOob, 0, 0);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < QPW; ++k) {
+        const long qp = qp0 + k;
+        const bool qok = qp < nq;
+        const __amdgpu_buffer_rsrc_t r3 = __builtin_amdgcn_make_buffer_rsrc(
+            a.lvl[3] + (qok ? qp : 0) * slice[3], (short)0, qok ? n3 * 2 : 0, kBufFlags);
+        const _Float16* s2 = s2q + k * Hl[2] * Wl[2];
+        const int s = lane;
+        int y, x;
+        if (tiled) {
+          const int t = s >> 6, r = s & 63;
+          y = (t / TC[3]) * 8 + (r >> 3);
+          x = (t % TC[3]) * 8 + (r & 7);
+        } else {
+          y = s / Wl[3];
+          x = s % Wl[3];
+        }
+        float v = 0.0f;
+        if (s < n3 && y < Hl[3]) {
+          const _Float16* r0 = s2 + (2 * y) * Wl[2] + 2 * x;
+          v = vol_pool4((float)r0[0], (float)r0[1], (float)r0[Wl[2]], (float)r0[Wl[2] + 1]);
+        }
+        __builtin_amdgcn_raw_buffer_store_b16((short)__half_as_ushort(__float2half(v)), r3,
+                                              s < n3 ? s * 2 : (int)kOob, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();   // s2 is rewritten by the next step's level 2
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return;
   }
   _Float16* s2 = reinterpret_cast<_Float16*>(lds) + (long)wave * Hl[2] * Wl[2];
   // persistent: wave w of the grid takes (edge, query pixel) w, w + 4 G, ..
@@ -1004,7 +1105,7 @@ int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, i
       b.qblocks = (int)nq;   // the pooling pass reads its (edge, pixel) count from qblocks
       const long g2 = std::min<long>((nq + 3) / 4, 16L * device_cu_count());
       if (g2 > 0x7fffffffL || nq > 0x7fffffffL) return fail(kUnsupported, "corr_volume_pyramid: too many pixels");
-      const int lds2 = 4 * (H / 4) * (W / 4) * 2;
+      const int lds2 = 2 * 4 * (H / 4) * (W / 4) * 2;   // two query pixels' level 2 per wave
       corr_volume_pool23_kernel<<<dim3((unsigned)g2), 256, lds2, stream>>>(b);
     } else {
       corr_volume_pyramid2_kernel<0><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);

@@ -643,10 +643,12 @@ class FactorGraph:
         return PendingAltLookup(self._alt_pyr[1], f1, f2, coords1, order=self._alt_order(f2h))
 
     def _alt_order(self, f2h):
-        """the on-demand lookup's tile walk: edges grouped by target frame (stable
-        sort), so the tiles that read one frame's pyramid rows run together and
-        find them in L2 (DROID_ALT_ORDER=0: edge order)"""
-        if os.environ.get("DROID_ALT_ORDER", "1") == "0":
+        """the on-demand lookup's tile walk, opt-in (DROID_ALT_ORDER=1): edges
+        grouped by target frame (stable sort), so the tiles that read one frame's
+        pyramid rows run together.  Measured at C3 (profiles/r04/r04n_alt_time.txt):
+        within +-3 % of edge order for every XCD chunk size - the kernel is bound
+        by its per-tile phases, not by L2 misses - so edge order is the default."""
+        if os.environ.get("DROID_ALT_ORDER", "0") != "1":
             return None
         return self._dev("alt_order", np.argsort(f2h, kind="stable").astype(np.int32))
 

@@ -91,7 +91,7 @@ int droid_alt_set_profile(void* buf);
  * default; env DROID_ALT_VARIANT=1 selects 1 at load).  Outputs are bitwise
  * equal; tests compare the two. */
 int droid_alt_set_variant(int v);
-/* Tuning hook: edges per XCD chunk of corr_alt2_kernel's tile walk (0 = interleaved; default 8). */
+/* Tuning hook: edges per XCD chunk of corr_alt2_kernel's tile walk (0 = interleaved, the default). */
 int droid_alt_set_chunk(int edges);
 /* Tuning hook: 1 = the cooperative NCHW lookup for droid_corr_pyramid_lookup(_tiled) (default),
  * 0 = the per-thread kernel; outputs are bitwise equal. */

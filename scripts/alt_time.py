@@ -46,4 +46,4 @@ for chunk in (0, 1, 2, 4, 8, 16, 32):
         o, med, mn = timed(order=o_)
         print("variant 2, chunk %2d edges, %-15s: median %.3f ms (min %.3f) bitwise %s" % (
             chunk, name, med, mn, bool(torch.equal(o, outs[2]))))
-droid_backends.alt_set_chunk(8)
+droid_backends.alt_set_chunk(0)

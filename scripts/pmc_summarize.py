@@ -31,6 +31,7 @@ def per_kernel(counter):
                "zr" if ("conv_band_kernel<256, 256, false, false, 6>" in name or
                         "conv_band_kernel<256, 256, false, false, 6, 8>" in name) else
                "lookup" if ("corr_ce0_kernel" in name or "corr_pyramid_f16_r3_kernel" in name) else
+               "lookup_nchw" if "corr_lookup_coop_kernel" in name else
                "alt" if ("corr_alt_ce0_kernel" in name or "corr_alt2_kernel" in name) else None)
         if key:
             out.setdefault(key, []).append(float(r["Counter_Value"]))
@@ -50,7 +51,10 @@ LOOKUP_CE0 = 4 * 64 * 2 * 3072 + 2 * 4 * 3072 + 128 * 2 * 3072
 # z|r gates with the inp term per source frame: 3x3 over net | corr | flow (320 channels)
 # on-demand lookup: query + target feature-pyramid rows, coords, 128-channel fp16 output per edge (bench.py)
 ALT = 786432 + 1044480 + 24576 + 128 * 2 * 3072
+# the reference API's NCHW lookup: SURVEY.md §8d's volume-API bytes (bench.py LOOKUP_BYTES_PER_EDGE)
+LOOKUP_NCHW = 2801664
 for key, name, algo in (("zr", "conv_zr", 2 * 256 * 320 * 9 * 3072 * E), ("lookup", "corr_lookup", LOOKUP_CE0 * E),
+                        ("lookup_nchw", "corr_lookup_nchw", LOOKUP_NCHW * E),
                         ("alt", "corr_alt", ALT * E)):
     fb = kf * min(fetch[key])
     wb = kw * min(write[key])

@@ -3,7 +3,8 @@ scripts/pmc_traffic.sh): a 1 GiB device copy (calibration of the FETCH/WRITE
 counters on a known byte count), then the C3 ZR gate conv as update() runs it
 (over net | corr | flow, the inp term per source frame of bench.py's C3 edge
 list: droid_conv_gru_pre_f16) and the C3 4-level
-correlation lookup fused with corr_encoder[0] (corr_lookup_ce0 on the 8x8-tiled volume), then the
+correlation lookup fused with corr_encoder[0] (corr_lookup_ce0 on the 8x8-tiled volume) and the
+reference API's NCHW lookup on the same volume (corr_pyramid_lookup_tiled), then the
 on-demand lookup (corr_alt_ce0) on the C3 graph's reprojected coordinates, each
 launched 3 times on synthetic data."""
 import os
@@ -61,6 +62,9 @@ c = coords.view(E, H, W, 2).contiguous()
 with torch.no_grad():
     for _ in range(3):
         droid_backends.corr_lookup_ce0(cb.corr_pyramid, c, w224, b128, tiled_shapes=cb.level_shapes)
+    torch.cuda.synchronize()
+    for _ in range(3):   # the reference API's NCHW lookup on the same pool (corr_lookup_coop_kernel)
+        droid_backends.corr_pyramid_lookup_tiled(cb.corr_pyramid, cb.level_shapes, c)
 torch.cuda.synchronize()
 del cb, f
 

@@ -490,7 +490,7 @@ def test_corr_alt_ordered_walk_is_bitwise_the_same():
                 assert torch.equal(out, ref), (chunk, o is None)
     finally:
         droid_backends.alt_set_variant(2)
-        droid_backends.alt_set_chunk(8)
+        droid_backends.alt_set_chunk(0)
 
 
 def test_corr_volume_slot_pool_matches_fresh_block():
