@@ -2281,41 +2281,46 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
 // not the 13 of the 8-channel packing (half of whose K was zero padding).
 // The weights keep the ABI layout w[co][tap*8 + c] (K = 52 x 8) and are
 // re-packed to [co][7 rows x 4 pairs x 8] while staged into LDS.
-constexpr int kFeTP = 128, kFeK = 416, kFeK2 = 224, kFeKS = kFeK2 + 8, kFeOS = 136;
+// Round 4: TP = 256-pixel tiles on 16 waves where the shape allows (C3's 48x64:
+// twice the bytes in flight per CU and four waves per SIMD to cover the
+// tile's barriers; the 128-pixel, 8-wave tile measured 2.6 TB/s of output).
+constexpr int kFeK = 416, kFeK2 = 224, kFeKS = kFeK2 + 8, kFeOS = 136;
 
-__host__ __device__ constexpr int fe_lds_bytes(int W) {
-  return 128 * kFeKS * 2 + (kFeTP / W + 6) * (W + 8) * 8 + kFeTP * kFeOS * 2;
+__host__ __device__ constexpr int fe_lds_bytes(int W, int TP) {
+  return 128 * kFeKS * 2 + (TP / W + 6) * (W + 8) * 8 + TP * kFeOS * 2;
 }
 
-__global__ void __launch_bounds__(512) flow_enc0_kernel(const float* __restrict__ motn, const __half* __restrict__ w,
+template <int TP>
+__global__ void __launch_bounds__(4 * TP) flow_enc0_kernel(const float* __restrict__ motn, const __half* __restrict__ w,
                                                         const float* __restrict__ bias, __half* __restrict__ out,
                                                         int H, int W, long ntiles) {
   extern __shared__ __attribute__((aligned(16))) _Float16 smem_fe[];
   // band rows; padded row length: 3 columns left, 5 right (the pair (6, 7) of
   // a row reads column x + 7, whose weights are zero)
-  const int RB = kFeTP / W + 6, PW = W + 8;
+  constexpr int NT = 4 * TP;
+  const int RB = TP / W + 6, PW = W + 8;
   _Float16* Ws = smem_fe;                    // [128][kFeKS]: [row 7][pair 4][tap 2][ch 4]
   _Float16* In = Ws + 128 * kFeKS;           // [RB][PW][4]
   _Float16* Os = In + RB * PW * 4;           // [128][kFeOS]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int HW = H * W, tpe = HW / kFeTP;
-  for (int idx = tid; idx < 128 * 28 * 2; idx += 512) {  // (co, row, pair, tap of the pair)
+  const int HW = H * W, tpe = HW / TP;
+  for (int idx = tid; idx < 128 * 28 * 2; idx += NT) {  // (co, row, pair, tap of the pair)
     const int co = idx / 56, q = idx - co * 56, kb = q >> 1, h2 = q & 1;
     const int ty = kb >> 2, tx = 2 * (kb & 3) + h2;
     const uint2 v = tx < 7 ? *reinterpret_cast<const uint2*>(w + co * kFeK + (ty * 7 + tx) * 8) : make_uint2(0, 0);
     *reinterpret_cast<uint2*>(&Ws[co * kFeKS + kb * 8 + h2 * 4]) = v;
   }
-  for (int idx = tid; idx < RB * PW; idx += 512)
+  for (int idx = tid; idx < RB * PW; idx += NT)
     *reinterpret_cast<uint2*>(&In[idx * 4]) = make_uint2(0, 0);  // padding columns stay zero
   // input staging: thread -> band pixel (row idx / W, column idx % W), several per thread
-  const int nin = (RB * W + 511) / 512;  // <= 2 for W <= 128
+  const int nin = (RB * W + NT - 1) / NT;  // <= 2 for W <= 128
   float v[2][4];
   auto load_in = [&](long t) {
     const long e = t / tpe;
-    const int y0 = (int)(t - e * tpe) * (kFeTP / W);
+    const int y0 = (int)(t - e * tpe) * (TP / W);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int idx = tid + 512 * u;
+      const int idx = tid + NT * u;
       const int ry = idx / W, x = idx - ry * W, y = y0 - 3 + ry;
       const bool ok = u < nin && ry < RB && t < ntiles && y >= 0 && y < H;
 #pragma unroll
@@ -2325,7 +2330,7 @@ __global__ void __launch_bounds__(512) flow_enc0_kernel(const float* __restrict_
   auto store_in = [&]() {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int idx = tid + 512 * u;
+      const int idx = tid + NT * u;
       const int ry = idx / W, x = idx - ry * W;
       if (u < nin && ry < RB) {
         half4_t h;
@@ -2388,8 +2393,8 @@ __global__ void __launch_bounds__(512) flow_enc0_kernel(const float* __restrict_
       }
     __syncthreads();
     const long e = t / tpe;
-    const long pix0 = e * HW + (t - e * tpe) * kFeTP;
-    for (int idx = tid; idx < kFeTP * 16; idx += 512) {
+    const long pix0 = e * HW + (t - e * tpe) * TP;
+    for (int idx = tid; idx < TP * 16; idx += NT) {
       const int r = idx >> 4, q = idx & 15;
       *reinterpret_cast<uint4*>(out + (pix0 + r) * 128 + q * 8) = *reinterpret_cast<const uint4*>(&Os[r * kFeOS + q * 8]);
     }
@@ -2857,19 +2862,33 @@ int droid_flow_enc0_f16(const float* motn, const void* w, const float* bias, voi
                         hipStream_t stream) {
   if (E < 0 || H <= 0 || W <= 0 || !motn || !w || !bias || !out || (reinterpret_cast<uintptr_t>(bias) & 15))
     return fail(kInvalidArgument, "flow_enc0_f16: bad arguments (bias must be 16-B aligned)");
-  if (W % 16 || kFeTP % W || (H * W) % kFeTP || (long)E * H * W * 4 > 0x7fffffffL)
+  if (W % 16 || 128 % W || (H * W) % 128 || (long)E * H * W * 4 > 0x7fffffffL)
     return fail(kUnsupported, "flow_enc0_f16: needs W in {16,32,64,128} and H*W % 128 == 0");
   if (E == 0) return kOk;
-  const int lds = fe_lds_bytes(W);
   static bool attr = false;
   if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&flow_enc0_kernel),
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&flow_enc0_kernel<128>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&flow_enc0_kernel<256>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     attr = true;
   }
-  const long ntiles = (long)E * H * W / kFeTP;
-  const long grid = std::min<long>(ntiles, device_cu_count());
-  flow_enc0_kernel<<<dim3((unsigned)grid), 512, lds, stream>>>(motn, (const __half*)w, bias, (__half*)out, H, W, ntiles);
+  // DROID_FE_TP=128: the 128-pixel tile on a shape that allows 256 (A/B runs)
+  static const int tp_env = [] {
+    const char* e = getenv("DROID_FE_TP");
+    return e ? atoi(e) : 256;
+  }();
+  if (tp_env == 256 && (H * W) % 256 == 0 && fe_lds_bytes(W, 256) <= kLdsMax) {
+    const long ntiles = (long)E * H * W / 256;
+    const long grid = std::min<long>(ntiles, device_cu_count());
+    flow_enc0_kernel<256><<<dim3((unsigned)grid), 1024, fe_lds_bytes(W, 256), stream>>>(
+        motn, (const __half*)w, bias, (__half*)out, H, W, ntiles);
+  } else {
+    const long ntiles = (long)E * H * W / 128;
+    const long grid = std::min<long>(ntiles, device_cu_count());
+    flow_enc0_kernel<128><<<dim3((unsigned)grid), 512, fe_lds_bytes(W, 128), stream>>>(
+        motn, (const __half*)w, bias, (__half*)out, H, W, ntiles);
+  }
   DROID_LAUNCH_CHECK();
   return kOk;
 }

@@ -33,6 +33,7 @@
 #include "lds_dma.hpp"
 
 #include <algorithm>
+#include <type_traits>
 
 #pragma clang fp contract(off)
 
@@ -878,95 +879,111 @@ __global__ void __launch_bounds__(256) corr_volume_pool23_kernel(VolArgs a) {
     // elements a query does not have - branch-free, fixed instruction counts
     constexpr int QPW = 2;
     _Float16* s2q = reinterpret_cast<_Float16*>(lds) + (long)wave * QPW * Hl[2] * Wl[2];
-    for (long qp0 = ((long)blockIdx.x * 4 + wave) * QPW; qp0 < nq; qp0 += 4L * QPW * gridDim.x) {
-      unsigned top[QPW][8], bot[QPW][8];
+    // each lane forms two horizontally adjacent level-2 values (x even): their
+    // 2x2 level-1 sources are one 8-B load per row (four consecutive halves of a
+    // tile row / a row run) and the pair is one 4-B store, so a wave-instruction
+    // moves 512 / 256 B instead of 256 / 128; NI pair rounds cover the slice
+    // (C3's 256 halves: 2 rounds, no out-of-range rounds issued)
+    auto run = [&](auto nic) {
+      constexpr int NI = decltype(nic)::value;
+      for (long qp0 = ((long)blockIdx.x * 4 + wave) * QPW; qp0 < nq; qp0 += 4L * QPW * gridDim.x) {
+        u32x2_t top[QPW][NI], bot[QPW][NI];
 #pragma unroll
-      for (int k = 0; k < QPW; ++k) {
-        const long qp = qp0 + k;
-        const bool qok = qp < nq;
-        const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<__half*>(a.lvl[1] + (qok ? qp : 0) * slice[1]), (short)0, qok ? n1 * 2 : 0, kBufFlags);
+        for (int k = 0; k < QPW; ++k) {
+          const long qp = qp0 + k;
+          const bool qok = qp < nq;
+          const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+              const_cast<__half*>(a.lvl[1] + (qok ? qp : 0) * slice[1]), (short)0, qok ? n1 * 2 : 0, kBufFlags);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int s = lane + 64 * i;
-          int y, x;
-          if (tiled) {
-            const int t = s >> 6, r = s & 63;
-            y = (t / TC[2]) * 8 + (r >> 3);
-            x = (t % TC[2]) * 8 + (r & 7);
-          } else {
-            y = s / Wl[2];
-            x = s % Wl[2];
+          for (int i = 0; i < NI; ++i) {
+            const int s = 2 * (lane + 64 * i);
+            int y, x;
+            if (tiled) {
+              const int t = s >> 6, r = s & 63;
+              y = (t / TC[2]) * 8 + (r >> 3);
+              x = (t % TC[2]) * 8 + (r & 7);
+            } else {
+              y = s / Wl[2];
+              x = s % Wl[2];
+            }
+            const bool ok = s < n2 && y < Hl[2];
+            const unsigned ot = ok ? (unsigned)vol_elem(tiled, TC[1], Wl[1], 2 * y, 2 * x) * 2u : kOob;
+            const unsigned ob = ok ? (unsigned)vol_elem(tiled, TC[1], Wl[1], 2 * y + 1, 2 * x) * 2u : kOob;
+            top[k][i] = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(r1, (int)ot, 0, 0));
+            bot[k][i] = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(r1, (int)ob, 0, 0));
           }
-          const bool ok = s < n2 && y < Hl[2];
-          const unsigned ot = ok ? (unsigned)vol_elem(tiled, TC[1], Wl[1], 2 * y, 2 * x) * 2u : kOob;
-          const unsigned ob = ok ? (unsigned)vol_elem(tiled, TC[1], Wl[1], 2 * y + 1, 2 * x) * 2u : kOob;
-          top[k][i] = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(r1, (int)ot, 0, 0);
-          bot[k][i] = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(r1, (int)ob, 0, 0);
         }
-      }
 #pragma unroll
-      for (int k = 0; k < QPW; ++k) {
-        const long qp = qp0 + k;
-        const bool qok = qp < nq;
-        const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(
-            a.lvl[2] + (qok ? qp : 0) * slice[2], (short)0, qok ? n2 * 2 : 0, kBufFlags);
-        _Float16* s2 = s2q + k * Hl[2] * Wl[2];
+        for (int k = 0; k < QPW; ++k) {
+          const long qp = qp0 + k;
+          const bool qok = qp < nq;
+          const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(
+              a.lvl[2] + (qok ? qp : 0) * slice[2], (short)0, qok ? n2 * 2 : 0, kBufFlags);
+          _Float16* s2 = s2q + k * Hl[2] * Wl[2];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int s = lane + 64 * i;
+          for (int i = 0; i < NI; ++i) {
+            const int s = 2 * (lane + 64 * i);
+            int y, x;
+            if (tiled) {
+              const int t = s >> 6, r = s & 63;
+              y = (t / TC[2]) * 8 + (r >> 3);
+              x = (t % TC[2]) * 8 + (r & 7);
+            } else {
+              y = s / Wl[2];
+              x = s % Wl[2];
+            }
+            float v0 = 0.0f, v1 = 0.0f;
+            if (s < n2 && y < Hl[2]) {
+              const u32x2_t t0 = top[k][i], b0 = bot[k][i];
+              v0 = vol_pool4(__half2float(__ushort_as_half((unsigned short)(t0[0] & 0xffffu))),
+                             __half2float(__ushort_as_half((unsigned short)(t0[0] >> 16))),
+                             __half2float(__ushort_as_half((unsigned short)(b0[0] & 0xffffu))),
+                             __half2float(__ushort_as_half((unsigned short)(b0[0] >> 16))));
+              v1 = vol_pool4(__half2float(__ushort_as_half((unsigned short)(t0[1] & 0xffffu))),
+                             __half2float(__ushort_as_half((unsigned short)(t0[1] >> 16))),
+                             __half2float(__ushort_as_half((unsigned short)(b0[1] & 0xffffu))),
+                             __half2float(__ushort_as_half((unsigned short)(b0[1] >> 16))));
+              s2[y * Wl[2] + x] = (_Float16)v0;
+              s2[y * Wl[2] + x + 1] = (_Float16)v1;
+            }
+            const unsigned pk = (unsigned)__half_as_ushort(__float2half(v0)) |
+                                ((unsigned)__half_as_ushort(__float2half(v1)) << 16);
+            __builtin_amdgcn_raw_buffer_store_b32(pk, r2, s < n2 ? s * 2 : (int)kOob, 0, 0);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < QPW; ++k) {
+          const long qp = qp0 + k;
+          const bool qok = qp < nq;
+          const __amdgpu_buffer_rsrc_t r3 = __builtin_amdgcn_make_buffer_rsrc(
+              a.lvl[3] + (qok ? qp : 0) * slice[3], (short)0, qok ? n3 * 2 : 0, kBufFlags);
+          const _Float16* s2 = s2q + k * Hl[2] * Wl[2];
+          const int s = lane;
           int y, x;
           if (tiled) {
             const int t = s >> 6, r = s & 63;
-            y = (t / TC[2]) * 8 + (r >> 3);
-            x = (t % TC[2]) * 8 + (r & 7);
+            y = (t / TC[3]) * 8 + (r >> 3);
+            x = (t % TC[3]) * 8 + (r & 7);
           } else {
-            y = s / Wl[2];
-            x = s % Wl[2];
+            y = s / Wl[3];
+            x = s % Wl[3];
           }
           float v = 0.0f;
-          if (s < n2 && y < Hl[2]) {
-            const unsigned t0 = top[k][i], b0 = bot[k][i];
-            v = vol_pool4(__half2float(__ushort_as_half((unsigned short)(t0 & 0xffffu))),
-                          __half2float(__ushort_as_half((unsigned short)(t0 >> 16))),
-                          __half2float(__ushort_as_half((unsigned short)(b0 & 0xffffu))),
-                          __half2float(__ushort_as_half((unsigned short)(b0 >> 16))));
-            s2[y * Wl[2] + x] = (_Float16)v;
+          if (s < n3 && y < Hl[3]) {
+            const _Float16* r0 = s2 + (2 * y) * Wl[2] + 2 * x;
+            v = vol_pool4((float)r0[0], (float)r0[1], (float)r0[Wl[2]], (float)r0[Wl[2] + 1]);
           }
-          __builtin_amdgcn_raw_buffer_store_b16((short)__half_as_ushort(__float2half(v)), r2,
-                                                s < n2 ? s * 2 : (int)kOob, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b16((short)__half_as_ushort(__float2half(v)), r3,
+                                                s < n3 ? s * 2 : (int)kOob, 0, 0);
         }
+        __builtin_amdgcn_wave_barrier();   // s2 is rewritten by the next step's level 2
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int k = 0; k < QPW; ++k) {
-        const long qp = qp0 + k;
-        const bool qok = qp < nq;
-        const __amdgpu_buffer_rsrc_t r3 = __builtin_amdgcn_make_buffer_rsrc(
-            a.lvl[3] + (qok ? qp : 0) * slice[3], (short)0, qok ? n3 * 2 : 0, kBufFlags);
-        const _Float16* s2 = s2q + k * Hl[2] * Wl[2];
-        const int s = lane;
-        int y, x;
-        if (tiled) {
-          const int t = s >> 6, r = s & 63;
-          y = (t / TC[3]) * 8 + (r >> 3);
-          x = (t % TC[3]) * 8 + (r & 7);
-        } else {
-          y = s / Wl[3];
-          x = s % Wl[3];
-        }
-        float v = 0.0f;
-        if (s < n3 && y < Hl[3]) {
-          const _Float16* r0 = s2 + (2 * y) * Wl[2] + 2 * x;
-          v = vol_pool4((float)r0[0], (float)r0[1], (float)r0[Wl[2]], (float)r0[Wl[2] + 1]);
-        }
-        __builtin_amdgcn_raw_buffer_store_b16((short)__half_as_ushort(__float2half(v)), r3,
-                                              s < n3 ? s * 2 : (int)kOob, 0, 0);
-      }
-      __builtin_amdgcn_wave_barrier();   // s2 is rewritten by the next step's level 2
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
+    };
+    if (n2 <= 2 * 128) run(std::integral_constant<int, 2>{});
+    else run(std::integral_constant<int, 4>{});
     return;
   }
   _Float16* s2 = reinterpret_cast<_Float16*>(lds) + (long)wave * Hl[2] * Wl[2];

@@ -36,5 +36,5 @@ for rep in range(3):
     torch.cuda.synchronize()
     ms = s.elapsed_time(e)
     print("variant %s rep %d: %.2f ms, %.2f GB written, %.0f GB/s" % (
-        "v" + os.environ.get("DROID_VOL_VARIANT", "3"), rep, ms, bytes_ / 1e9, bytes_ / ms / 1e6), flush=True)
+        "v" + os.environ.get("DROID_VOL_VARIANT", "4"), rep, ms, bytes_ / 1e9, bytes_ / ms / 1e6), flush=True)
     del lv

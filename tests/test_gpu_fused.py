@@ -307,9 +307,11 @@ def test_gru_global_context(E, H, W):
     assert torch.equal(out, droid_backends.gru_global_f16(h, w, b))
 
 
-@pytest.mark.parametrize("E,H,W", [(3, 8, 32), (2, 48, 64), (2, 4, 128)])
+@pytest.mark.parametrize("E,H,W", [(3, 8, 32), (2, 48, 64), (2, 4, 128), (3, 4, 32), (5, 12, 32)])
 def test_flow_encoder0(E, H, W):
-    """relu(conv7x7(motn.half()) + b) (droid_net.py:88-90 under autocast) vs torch fp32."""
+    """relu(conv7x7(motn.half()) + b) (droid_net.py:88-90 under autocast) vs torch fp32.
+    H*W % 256 == 0 runs the 256-pixel / 16-wave tile, the (3, 4, 32) and (5, 12, 32)
+    shapes the 128-pixel / 8-wave one."""
     import droid_backends
     from droid_mi355x.fused import pack_flow_enc0
     g = torch.Generator(device=DEV).manual_seed(24)
