@@ -20,6 +20,13 @@
 // forbid fusing them into v_fma_mix / v_fma_f16 (hipcc contracts by default).
 #pragma clang fp contract(off)
 
+// cache policy of the volume window loads (buffer-op aux bits) in the fused and
+// the reference-layout cooperative lookups (A/B builds: 2 = nt; each
+// wave-instruction there reads whole 128-B tiles, so no line is re-read later)
+#ifndef DROID_VOL_LOAD_AUX
+#define DROID_VOL_LOAD_AUX 2
+#endif
+
 namespace droid {
 
 template <typename T> struct Acc;
@@ -420,8 +427,8 @@ __global__ void __launch_bounds__(256) corr_lookup_coop_kernel(LookupLvlArgs a) 
     const int cm = TILED ? 64 : 8;
     const unsigned o0 = (yok && ok0) ? pbase + (unsigned)(rb + cm * c0) * 2u : kOob;
     const unsigned o1 = (yok && ok1) ? pbase + (unsigned)(rb + cm * (c0 + 1)) * 2u : kOob;
-    raw[r][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o0, 0, 0));
-    raw[r][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, 0));
+    raw[r][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o0, 0, DROID_VOL_LOAD_AUX));
+    raw[r][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, DROID_VOL_LOAD_AUX));
   }
   __half* const st = stage[wave];
 #pragma unroll
@@ -994,8 +1001,8 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
         const int cs = tiled ? 64 : 8;
         const unsigned o0 = (yok && ok0) ? pbase + (unsigned)(re + cs * c0) * 2u : kCeOob;
         const unsigned o1 = (yok && ok1) ? pbase + (unsigned)(re + cs * (c0 + 1)) * 2u : kCeOob;
-        raw[sl][j][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o0, 0, 0));
-        raw[sl][j][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, 0));
+        raw[sl][j][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o0, 0, DROID_VOL_LOAD_AUX));
+        raw[sl][j][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, DROID_VOL_LOAD_AUX));
       }
     } else if constexpr (!FAST) {
       const __half* base = vol + (vol_row(t) * (long)HW + (t % tpe) * kCeTP + px) * slice;
@@ -1077,8 +1084,8 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
       const int cs = tiled ? 64 : 8;
       const unsigned o0 = (yok && ok0) ? pbase + (unsigned)(re + cs * c0) * 2u : kCeOob;
       const unsigned o1 = (yok && ok1) ? pbase + (unsigned)(re + cs * (c0 + 1)) * 2u : kCeOob;
-      raw[sl][g][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o0, 0, 0));
-      raw[sl][g][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, 0));
+      raw[sl][g][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o0, 0, DROID_VOL_LOAD_AUX));
+      raw[sl][g][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o1, 0, DROID_VOL_LOAD_AUX));
     }
   };
   // bilinear windows of slot sl's tile -> As: lane (pp, jr) forms output row jr

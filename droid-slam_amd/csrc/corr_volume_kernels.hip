@@ -334,6 +334,16 @@ constexpr int kVol2Stores = 8;  // per wave and patch: 4 (level 0) + 2 (level 1)
 __device__ __forceinline__ int vol2_ty(int b, int c) { return 4 * (b >> 1) + 2 * (c >> 3) + ((c >> 1) & 1); }
 __device__ __forceinline__ int vol2_tx(int b, int c) { return 4 * (b & 1) + 2 * ((c >> 2) & 1) + (c & 1); }
 
+// cache policy of the level-0 / level-1 tile stores (buffer-op aux bits; A/B
+// builds: 2 = nt, streamed past the caches - the volume is read back only by
+// the next update()'s lookups, long after it has left L2 and the Infinity Cache)
+#ifndef DROID_VOL_STORE_AUX
+#define DROID_VOL_STORE_AUX 2
+#endif
+// the same for the pooling pass's level-1 loads and level-2/3 stores (A/B)
+#ifndef DROID_POOL_AUX
+#define DROID_POOL_AUX 2
+#endif
 typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
@@ -520,7 +530,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
       const u32x4_t val = *reinterpret_cast<const u32x4_t*>(s0 + q * kVol2S0 + ((seg ^ (q & 7)) << 3));
       const long off = a.tiled ? ((long)qg * TR[0] * (Wl[0] / 8) + py * (Wl[0] / 8) + px) * 64 + seg * 8
                                : (long)qg * HW + (long)(ty0 + seg) * W + tx0;
-      __builtin_amdgcn_raw_buffer_store_b128(val, ro[0], qg < qlim0 ? (int)(off * 2) : (int)kOob, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(val, ro[0], qg < qlim0 ? (int)(off * 2) : (int)kOob, 0, DROID_VOL_STORE_AUX);
     }
     // level 1: 32 q x 4 rows x 8 B (the patch's 4x4 level-1 block)
 #pragma unroll
@@ -564,7 +574,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
         const u32x4_t val = flush ? *reinterpret_cast<const u32x4_t*>(s0 + q * kVol2S0 + ((seg ^ (q & 7)) << 3))
                                   : u32x4_t{0u, 0u, 0u, 0u};
         const long off = ((long)qg * TR[1] * (Wl[1] / 8) + gy * (Wl[1] / 8) + gx) * 64 + seg * 8;
-        __builtin_amdgcn_raw_buffer_store_b128(val, ro[1], (flush && qg < qlim) ? (int)(off * 2) : (int)kOob, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(val, ro[1], (flush && qg < qlim) ? (int)(off * 2) : (int)kOob, 0,
+                                               DROID_VOL_STORE_AUX);
       }
       if (flush) {
 #pragma unroll
@@ -909,8 +920,8 @@ __global__ void __launch_bounds__(256) corr_volume_pool23_kernel(VolArgs a) {
             const bool ok = s < n2 && y < Hl[2];
             const unsigned ot = ok ? (unsigned)vol_elem(tiled, TC[1], Wl[1], 2 * y, 2 * x) * 2u : kOob;
             const unsigned ob = ok ? (unsigned)vol_elem(tiled, TC[1], Wl[1], 2 * y + 1, 2 * x) * 2u : kOob;
-            top[k][i] = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(r1, (int)ot, 0, 0));
-            bot[k][i] = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(r1, (int)ob, 0, 0));
+            top[k][i] = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(r1, (int)ot, 0, DROID_POOL_AUX));
+            bot[k][i] = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(r1, (int)ob, 0, DROID_POOL_AUX));
           }
         }
 #pragma unroll
@@ -948,7 +959,7 @@ __global__ void __launch_bounds__(256) corr_volume_pool23_kernel(VolArgs a) {
             }
             const unsigned pk = (unsigned)__half_as_ushort(__float2half(v0)) |
                                 ((unsigned)__half_as_ushort(__float2half(v1)) << 16);
-            __builtin_amdgcn_raw_buffer_store_b32(pk, r2, s < n2 ? s * 2 : (int)kOob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(pk, r2, s < n2 ? s * 2 : (int)kOob, 0, DROID_POOL_AUX);
           }
         }
         __builtin_amdgcn_wave_barrier();
@@ -976,7 +987,7 @@ __global__ void __launch_bounds__(256) corr_volume_pool23_kernel(VolArgs a) {
             v = vol_pool4((float)r0[0], (float)r0[1], (float)r0[Wl[2]], (float)r0[Wl[2] + 1]);
           }
           __builtin_amdgcn_raw_buffer_store_b16((short)__half_as_ushort(__float2half(v)), r3,
-                                                s < n3 ? s * 2 : (int)kOob, 0, 0);
+                                                s < n3 ? s * 2 : (int)kOob, 0, DROID_POOL_AUX);
         }
         __builtin_amdgcn_wave_barrier();   // s2 is rewritten by the next step's level 2
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
