@@ -51,6 +51,7 @@
 #endif
 
 namespace droid {
+typedef unsigned u32x4nt __attribute__((ext_vector_type(4)));  // non-temporal 16-B stores
 
 
 enum ConvEpi : int { EPI_ACT = 0, EPI_GRU_ZR = 1, EPI_GRU_Q = 2, EPI_HEAD = 3, EPI_GLO = 4, EPI_DWHEAD = 5,
@@ -962,6 +963,16 @@ __device__ __forceinline__ half8 gru_blend_f16(half8 z, half8 h, half8 q) {
   return a + b;
 }
 
+// DROID_BAND_A_NT (A/B builds): the band kernel's input bands by non-temporal LDS-DMA
+#ifndef DROID_BAND_A_NT
+#define DROID_BAND_A_NT 0
+#endif
+// DROID_EPI_NT (A/B builds): the band epilogue's output rows as non-temporal
+// stores (the maps are 0.8-1.6 GB at C3, far past L2 and the Infinity Cache)
+#ifndef DROID_EPI_NT
+#define DROID_EPI_NT 0
+#endif
+
 // The band epilogue around a caller-supplied pass 1: stage1(bl, act) writes
 // act(acc + column bias) of the caller's accumulators into the fp16 staging
 // tile smem[TMX][TN + 8] (bl = the tile's column biases in LDS, act = the
@@ -1182,7 +1193,10 @@ __device__ __forceinline__ void band_epilogue_core(const ConvArgs& a, _Float16* 
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int q = 0; q < RB; ++q) *reinterpret_cast<half8*>(dst0 + (q0 + q) * dstep) = outv[q];
+    for (int q = 0; q < RB; ++q) {
+      if constexpr (DROID_EPI_NT) __builtin_nontemporal_store(outv[q], reinterpret_cast<half8*>(dst0 + (q0 + q) * dstep));
+      else *reinterpret_cast<half8*>(dst0 + (q0 + q) * dstep) = outv[q];
+    }
   }
 }
 
@@ -1363,7 +1377,8 @@ conv_band_kernel(ConvArgs a) {
     for (int q = 0; q < BP::MAX_NHI; ++q) {
       if (q < nhi) {
         const unsigned off = (okc && hpix[q] >= 0) ? (unsigned)((hpix[q] * src.cstride + c) * 2) : kOob;
-        dma16(rs, dst + (wave_u + NW * q) * 1024, off);
+        if constexpr (DROID_BAND_A_NT) dma16_nt(rs, dst + (wave_u + NW * q) * 1024, off);
+        else dma16(rs, dst + (wave_u + NW * q) * 1024, off);
       }
     }
   };
@@ -2154,6 +2169,10 @@ static int launch_wino_kernel(const ConvArgs& a, long nwg, hipStream_t stream) {
 // 32w .. 32w+31 in registers (32 VGPRs), so the LDS holds only the ring and two
 // workgroups share a CU.  The per-column sums stay in registers and the mean
 // is a plain store - no atomics, deterministic.
+// DROID_GLO_NT (A/B builds): the hidden-state stream by non-temporal LDS-DMA
+#ifndef DROID_GLO_NT
+#define DROID_GLO_NT 0
+#endif
 constexpr int kGloTP = 64;
 constexpr int kGloRing = 5;  // 80 KB: two workgroups fill a CU's 160 KB LDS
 constexpr int kGloLds = kGloRing * 2 * kGloTP * 128;  // the tile ring (bytes)
@@ -2193,7 +2212,8 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
     for (int i = 0; i < 4; ++i) {
       const int q = wave_u + 4 * i, c = q & 1, pr = (q >> 1) * 8;
       const unsigned off = (unsigned)(((t * kGloTP + pr + lrow) * 128 + c * 64 + lpiece * 8) * 2);
-      dma16(rs, Al_a + (t % kGloRing) * 16384 + c * 8192 + pr * 128, off);
+      if constexpr (DROID_GLO_NT) dma16_nt(rs, Al_a + (t % kGloRing) * 16384 + c * 8192 + pr * 128, off);
+      else dma16(rs, Al_a + (t % kGloRing) * 16384 + c * 8192 + pr * 128, off);
     }
   };
   // the MFMA multiplies weights x pixels: lane (fr, fq) of block (i, j) holds
@@ -2396,7 +2416,9 @@ __global__ void __launch_bounds__(4 * TP) flow_enc0_kernel(const float* __restri
     const long pix0 = e * HW + (t - e * tpe) * TP;
     for (int idx = tid; idx < TP * 16; idx += NT) {
       const int r = idx >> 4, q = idx & 15;
-      *reinterpret_cast<uint4*>(out + (pix0 + r) * 128 + q * 8) = *reinterpret_cast<const uint4*>(&Os[r * kFeOS + q * 8]);
+      const uint4 ov = *reinterpret_cast<const uint4*>(&Os[r * kFeOS + q * 8]);
+      if constexpr (DROID_EPI_NT) __builtin_nontemporal_store(__builtin_bit_cast(u32x4nt, ov), reinterpret_cast<u32x4nt*>(out + (pix0 + r) * 128 + q * 8));
+      else *reinterpret_cast<uint4*>(out + (pix0 + r) * 128 + q * 8) = ov;
     }
   }
 }

@@ -26,8 +26,14 @@
 #ifndef DROID_VOL_LOAD_AUX
 #define DROID_VOL_LOAD_AUX 2
 #endif
+// DROID_CE0_OUT_NT (A/B builds): the fused lookup's 128-channel output rows as
+// non-temporal stores (0.8 GB at C3, past the caches)
+#ifndef DROID_CE0_OUT_NT
+#define DROID_CE0_OUT_NT 0
+#endif
 
 namespace droid {
+typedef unsigned u32x4nt __attribute__((ext_vector_type(4)));  // non-temporal 16-B stores
 
 template <typename T> struct Acc;
 template <> struct Acc<__half> {
@@ -1241,7 +1247,9 @@ __global__ void __launch_bounds__(512) corr_ce0_kernel(CorrCe0Args a) {
     const long pix0 = (t / tpe) * (long)HW + (t % tpe) * kCeTP;
     for (int idx = tid; idx < kCeTP * 16; idx += 512) {
       const int r = idx >> 4, q = idx & 15;
-      *reinterpret_cast<uint4*>(a.out + (pix0 + r) * 128 + q * 8) = *reinterpret_cast<const uint4*>(&Os[r * kCeOS + q * 8]);
+      const uint4 ov = *reinterpret_cast<const uint4*>(&Os[r * kCeOS + q * 8]);
+      if constexpr (DROID_CE0_OUT_NT) __builtin_nontemporal_store(__builtin_bit_cast(u32x4nt, ov), reinterpret_cast<u32x4nt*>(a.out + (pix0 + r) * 128 + q * 8));
+      else *reinterpret_cast<uint4*>(a.out + (pix0 + r) * 128 + q * 8) = ov;
     }
   };
 

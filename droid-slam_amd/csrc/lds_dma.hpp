@@ -43,6 +43,16 @@ __device__ __forceinline__ void dma16(rsrc_t rs, unsigned lds, unsigned voff) {
                : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(r)
                : "memory", "m0");
 }
+// the same with the non-temporal policy (nt): for streams that one workgroup
+// reads once, past L2 and the Infinity Cache
+__device__ __forceinline__ void dma16_nt(rsrc_t rs, unsigned lds, unsigned voff) {
+  const rsrc_t r = {__builtin_amdgcn_readfirstlane(rs.x), __builtin_amdgcn_readfirstlane(rs.y),
+                    __builtin_amdgcn_readfirstlane(rs.z), __builtin_amdgcn_readfirstlane(rs.w)};
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
 #pragma clang diagnostic pop
 
 }  // namespace droid
