@@ -51,10 +51,12 @@ LOOKUP_KERNEL = "corr_pyramid_f16_r3_kernel"
 # ConvGRU convz|convr|convq 3x3 448->128 + w 1x1 128->128, delta/weight 3x3
 # 128->128 + 3x3 128->2 each, GraphAgg conv1 3x3 128->128 (droid_net.py:59-143,
 # gru.py:19-32); per unique source frame-pixel: GraphAgg conv2 3x3 128->128,
-# eta 3x3 128->1, upmask 1x1 128->576.
+# eta 3x3 128->1.
 CONV_FLOPS_PER_EDGE_PIXEL = 2 * (196 * 128 + 128 * 128 * 9 + 4 * 128 * 49 + 128 * 64 * 9 + 3 * 448 * 128 * 9
                                  + 128 * 128 + 2 * (128 * 128 * 9 + 128 * 2 * 9) + 128 * 128 * 9)
-CONV_FLOPS_PER_FRAME_PIXEL = 2 * (128 * 128 * 9 + 128 * 9 + 128 * 576)
+# (GraphAgg's upmask, 1x1 128->576, is not counted: the reference's update()
+# discards it, factor_graph.py:209, and the fused operator never computes it)
+CONV_FLOPS_PER_FRAME_PIXEL = 2 * (128 * 128 * 9 + 128 * 9)
 # factored gates: 3 x 128 inp channels move from per-edge to per-source-frame pixels
 GATE_INP_FLOPS_PER_PIXEL = 2 * 3 * 128 * 128 * 9
 # HBM-bound stages per update (fused lookup path): lookup 3,059,712 B/edge (§8d fused row),
@@ -117,8 +119,12 @@ def build_state(args, rank, world, device):
     corr_impl = "alt" if args.lowmem else args.corr if not args.reference_op else "volume"
     graph = FactorGraph(video, net, device=device, corr_impl=corr_impl)
     graph.comm = comm
+    if args.reference_api:
+        graph.tiled_volume = False   # the reference's own row-major volume layout
     with torch.no_grad():
         graph.add_factors(ii_l, jj_l)
+        if args.reference_api:
+            graph.corr = ReferenceApiCorr(graph.corr)
         if args.config == "C2":
             # the frontend's state: edges older than the window stored inactive
             # (droid_frontend.py:42,106) - update(use_inactive=True) then optimises
@@ -127,6 +133,46 @@ def build_state(args, rank, world, device):
             graph.rm_factors(graph.ii < 7, store=True)
     torch.cuda.synchronize(device)
     return video, graph, (ii, jj), len(graph._ii)
+
+
+class ReferenceApiCorr:
+    """The reference's CorrBlock.__call__ verbatim in structure
+    (/root/reference/droid_slam/modules/corr.py:40-50, restated): coords
+    permuted to (B*N, 2, H, W), then per level one
+    droid_backends.corr_index_forward on the reference-layout volume
+    (E, H, W, H2/2^i, W2/2^i) at coords / 2^i, and a torch.cat of the four
+    49-channel results - what a maintainer gets by swapping only the
+    droid_backends extension under the reference's own modules/corr.py.
+    HIP events bracket each whole call (4 launches + the cat) on torch's
+    current stream, the stream the C ABI launches on."""
+
+    def __init__(self, block):
+        self.block = block
+        self.corr_pyramid = block.reference_pyramid()   # row-major (untiled) levels
+        self.num_levels, self.radius = block.num_levels, block.radius
+        self.events, self.active = [], False
+
+    def __call__(self, coords):
+        import droid_backends
+        if self.active:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+        out_pyramid = []
+        batch, num, ht, wd, _ = coords.shape
+        coords = coords.permute(0, 1, 4, 2, 3)
+        coords = coords.contiguous().view(batch * num, 2, ht, wd)
+        for i in range(self.num_levels):
+            corr, = droid_backends.corr_index_forward(self.corr_pyramid[i], coords / 2 ** i, self.radius)
+            out_pyramid.append(corr.view(batch, num, -1, ht, wd))
+        out = torch.cat(out_pyramid, dim=2)
+        if self.active:
+            e.record()
+            self.events.append((s, e))
+        return out
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        return float(np.mean([s.elapsed_time(e) for s, e in self.events])) if self.events else None
 
 
 class KernelTimer:
@@ -276,17 +322,27 @@ def cpu_baseline(graph, video, args):
             "wall_s": round(time.time() - t_all, 1)}
 
 
+def lib_sha16():
+    """sha256 (16 hex digits) of the libdroid_hip.so this process loaded."""
+    import hashlib
+    from droid_backends import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def load_traffic(name, e_local, kernel):
     """HBM bytes per launch from a committed PMC pass (profiles/pmc_<name>.json,
     FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) of this
-    launch's edge count and of the kernel named; None when no such measurement
-    exists (e.g. the pass predates the current kernel)."""
+    launch's edge count and of the kernel named, measured on the very library
+    this process loaded (the record's lib_sha16); None when no such measurement
+    exists (a pass on an older build says nothing about the current kernel)."""
     p = os.path.join(ROOT, "profiles", "pmc_%s.json" % name)
     if os.path.exists(p):
         try:
             with open(p) as f:
                 d = json.load(f)
-            if d.get("edges") == e_local and kernel in (d.get("kernel") or ""):
+            if (d.get("edges") == e_local and kernel in (d.get("kernel") or "")
+                    and d.get("lib_sha16") == lib_sha16()):
                 return d.get("traffic_bytes_per_launch")
         except Exception:
             return None
@@ -349,7 +405,13 @@ def main():
                     help="the reference's update() structure (NCHW state, materialised lookup) with the MI355X "
                          "UpdateModule drop-in (ReferenceLayoutUpdateModule): what the reference's own "
                          "factor_graph.py gets from swapping the module only")
+    ap.add_argument("--reference-api", action="store_true",
+                    help="the literal drop-in: --reference-layout with the reference's own CorrBlock.__call__ "
+                         "(modules/corr.py:40-50: 4 x droid_backends.corr_index_forward on the row-major volume "
+                         "+ torch.cat) instead of the one-launch tiled lookup")
     args = ap.parse_args()
+    if args.reference_api:
+        args.reference_layout = True
     if args.reference_layout:
         args.reference_op = True
     if args.config == "C4" and args.frames == 256:
@@ -397,7 +459,9 @@ def main():
     tiled_ref = graph.corr is not None and getattr(graph.corr, "tiled", False)
     LOOKUP_FN[0] = (("corr_pyramid_lookup_tiled" if tiled_ref else "corr_pyramid_lookup") if args.reference_op else
                     "corr_alt_ce0" if args.corr == "pyramid" or args.lowmem else "corr_lookup_ce0")
-    lookup = KernelTimer(droid_backends, LOOKUP_FN[0])
+    if args.reference_api:
+        LOOKUP_FN[0] = "corr_index_forward"
+    lookup = graph.corr if args.reference_api else KernelTimer(droid_backends, LOOKUP_FN[0])
     zr = zrp = None
     if not args.reference_op or args.reference_layout:
         zr = KernelTimer(droid_backends, "conv_nhwc_f16", when=lambda *a, **k: k.get("epi") == droid_backends.EPI_GRU_ZR)
@@ -457,18 +521,22 @@ def main():
         ms = 1000.0 * elapsed / args.steps
         bytes_per_launch = (LOOKUP_BYTES_PER_EDGE if args.reference_op else LOOKUP_CE0_BYTES_PER_EDGE) * e_local
         achieved = bytes_per_launch / (lookup_ms * 1e-3) / 1e9 if lookup_ms else None
-        coop = os.environ.get("DROID_LOOKUP_COOP") != "0" and (args.ht // 8) * (args.wd // 8) % 64 == 0
+        coop = (args.ht // 8) * (args.wd // 8) % 64 == 0   # the cooperative lookup's shape rule (corr_kernels.hip)
         ref_lookup = (("corr_lookup_coop_kernel<true> (cooperative 4-level lookup, NCHW out, 8x8-tiled volume pool)"
                        if coop else "corr_lookup_lvl_kernel<false, true> (4-level lookup, NCHW out, 8x8-tiled volume pool)")
                       if LOOKUP_FN[0] == "corr_pyramid_lookup_tiled" else
-                      "corr_pyramid_f16_r3_kernel<NCHW> (4-level lookup)" if os.environ.get("DROID_LOOKUP_V1") == "1"
+                      "corr_lookup_coop_kernel<false> (4-level lookup, NCHW out)" if coop
                       else "corr_lookup_lvl_kernel<false> (4-level lookup, NCHW out)")
+        if args.reference_api:
+            ref_lookup = ("CorrBlock.__call__ of modules/corr.py:40-50: 4 x corr_index_fwd_kernel<__half> "
+                          "(droid_corr_index_forward, one level each, row-major volume) + torch.cat, per call")
         lookup_roof = {"kernel": (ref_lookup if args.reference_op else
                                   "corr_ce0_kernel (4-level lookup fused with corr_encoder[0] 1x1 196->128)"),
                        "bound": "hbm",
                        "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                        "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
-                       "traffic": (load_traffic("corr_lookup_nchw", e_local, "corr_lookup_coop_kernel")
+                       "traffic": (None if args.reference_api else
+                                   load_traffic("corr_lookup_nchw", e_local, "corr_lookup_coop_kernel")
                                    if args.reference_op else load_traffic("corr_lookup", e_local, "corr_ce0_kernel<true>")),
                        "launch_ms": lookup_ms,
                        "algorithmic_bytes_per_launch": bytes_per_launch}
@@ -512,11 +580,16 @@ def main():
                                     "C2": "C2 frontend window (use_inactive=True)"}[args.config]
                                    + (": update_lowmem(steps=1, itrs=2), on-demand corr" if args.lowmem else
                                       ": update(itrs=2), %s corr" % args.corr)
-                                   + (", reference update() layout + MI355X UpdateModule drop-in" if args.reference_layout
+                                   + (", reference update() layout + the reference's CorrBlock.__call__ over "
+                                      "droid_backends.corr_index_forward + MI355X UpdateModule drop-in"
+                                      if args.reference_api else
+                                      ", reference update() layout + MI355X UpdateModule drop-in" if args.reference_layout
                                       else ", reference-structured torch UpdateModule" if args.reference_op else ""),
                        "keyframes": args.frames,
                        "edges": len(ii), "image": [args.ht, args.wd], "fmap": [args.ht // 8, args.wd // 8],
-                       "parallelism": "edge-sharded x%d (RCCL all-reduce of reduced camera system)" % world},
+                       "parallelism": ("edge-sharded x%d (%s all-reduce of the reduced camera system)"
+                                       % (world, "RCCL" if dist.get_backend() == "nccl" else dist.get_backend())
+                                       if dist_on else "single GPU (no process group)")},
             "roofline": roofline,
             "state_finite": finite,
         }

@@ -122,12 +122,14 @@ __global__ void __launch_bounds__(256) ba_zero_kernel(uint4* __restrict__ p, lon
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) p[i] = uint4{0u, 0u, 0u, 0u};
 }
 
+// Every region it is given is a 16-B aligned multiple of 16 B by the plan's
+// workspace layout (ba_plan.cpp aligns each section); anything else is a
+// layout bug and is rejected - there is no runtime-memset fallback, so no
+// memset node can enter a captured solve.
 static int ba_zero(void* p, size_t bytes, hipStream_t stream) {
   if (bytes == 0) return kOk;
-  if ((reinterpret_cast<uintptr_t>(p) & 15u) || (bytes & 15u)) {
-    DROID_HIP_CHECK(hipMemsetAsync(p, 0, bytes, stream));
-    return kOk;
-  }
+  if ((reinterpret_cast<uintptr_t>(p) & 15u) || (bytes & 15u))
+    return fail(kInvalidArgument, "ba: workspace region not 16-B aligned (layout bug)");
   const long n16 = (long)(bytes / 16);
   const long grid = std::min<long>((n16 + 255) / 256, 1024);
   ba_zero_kernel<<<dim3((unsigned)grid), 256, 0, stream>>>(static_cast<uint4*>(p), n16);
@@ -722,7 +724,7 @@ struct CholDev {
   double* ybuf; // [nbc*64]
   double* x;    // [n] (permuted order)
   float* dx;    // [n]
-  int inject;   // test hook (DROID_CHOL_FAULT_INJECT=1): raise the abort at once, as a timeout would
+  int inject;   // test hook (droid_chol_set_fault_inject): raise the abort at once, as a timeout would
   long long* prof;  // profiling builds: s_memrealtime per (task, phase < 8), or null
 };
 
@@ -850,6 +852,16 @@ __device__ bool poll_ge(int* w, int target, int* abort_w, int* flag) {
     }
     __builtin_amdgcn_s_sleep(2);
   }
+}
+
+// A broken invariant of the dataflow state (a sync counter not zeroed before
+// the launch, a task record outside the plan): status bits 1 (the solve is
+// skipped, as after a timeout) and 2 (kFlagState, reported as such by the
+// host), and the abort word so every worker drains.
+constexpr int kFlagState = 4;
+__device__ __forceinline__ void state_fault(int* abort_w, int* flag) {
+  __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  atomicOr(flag, 2 | kFlagState);
 }
 
 // wave-uniform lane -> every lane (two v_readlane_b32, no LDS round trip)
@@ -1039,6 +1051,20 @@ __device__ __forceinline__ void tall_solve(double* T, const double* Lt, const do
 #define DROID_CHOL_PANEL4 0
 #endif
 
+// every tile a task record names lies in the plan's slot map (wave-uniform)
+__device__ __forceinline__ bool task_record_ok(const CholDev& d, int type, int i, int j, int k) {
+  if (type < kPotrf || type > kBupd) return false;
+  if (i < 0 || i >= d.nbr || j < 0 || j >= d.nbc || k < 0 || k >= d.nbc) return false;
+  auto live = [&](int r, int c) { return __builtin_amdgcn_readfirstlane(d.slot[r * d.nbc + c]) >= 0; };
+  switch (type) {
+    case kPotrf: return live(k, k);
+    case kTrsm: return live(i, k) && live(k, k);
+    case kUpdate: return live(i, j) && live(i, k) && live(j, k);
+    case kBsolve: return i < d.nbc && live(i, i);
+    default: return live(i, j);
+  }
+}
+
 __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* T0 = sm;
@@ -1068,16 +1094,30 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
     atomicOr(d.flag, 2);
   }
 
-  for (;;) {
+  for (bool first = true;; first = false) {
     if (tid == 0) shi[0] = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const int tk = __builtin_amdgcn_readfirstlane(shi[0]);
+    // Entry invariant (kFlagState): the sync area was zeroed before this
+    // launch.  A launch hands out exactly ntasks + gridDim.x tickets when no
+    // worker aborts, so a workgroup's first ticket lies below that unless the
+    // counter kept a previous launch's value.
+    if (tk < 0 || (first && tk >= d.ntasks + (int)gridDim.x)) {
+      if (tid == 0) state_fault(abort_w, d.flag);
+      break;
+    }
     if (tk >= d.ntasks) break;
     const int* tsk = d.tasks + kTaskInts * tk;
     const int type = __builtin_amdgcn_readfirstlane(tsk[0]), i = __builtin_amdgcn_readfirstlane(tsk[1]);
     const int j = __builtin_amdgcn_readfirstlane(tsk[2]), k = __builtin_amdgcn_readfirstlane(tsk[3]);
     const int ta = __builtin_amdgcn_readfirstlane(tsk[4]), tb = __builtin_amdgcn_readfirstlane(tsk[5]);
     CH_STAMP(0);
+    // Task-record invariant: every index the task addresses is inside the plan
+    // (a corrupted record would otherwise turn into an out-of-range tile access).
+    if (!task_record_ok(d, type, i, j, k)) {
+      if (tid == 0) state_fault(abort_w, d.flag);
+      break;
+    }
     if (tid == 0) {
       bool ok = true;
       switch (type) {
@@ -1095,6 +1135,12 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           const int s = SL(i, j), si = SL(i, k), sj = SL(j, k);
           ok = poll_ge(&ver[s], ta, abort_w, d.flag) && poll_ge(&ver[si], d.fin[si], abort_w, d.flag) &&
                poll_ge(&ver[sj], d.fin[sj], abort_w, d.flag);
+          // the updates of a tile are applied in sequence by this chain alone, so
+          // its counter reads exactly `ta` here; more means a stale counter
+          if (ok && __hip_atomic_load(&ver[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ta) {
+            state_fault(abort_w, d.flag);
+            ok = false;
+          }
           break;
         }
         case kBsolve: {
@@ -1493,6 +1539,8 @@ static BaDev make_dev(BaPlan& p, char* ws) {
 
 static int num_cus() { return device_cu_count(); }
 static long long* g_chol_prof = nullptr;
+enum { kInjectOff = 0, kInjectAll = 1, kInjectOnce = 2, kInjectStale = 3 };
+static int g_chol_inject = kInjectOff;
 
 static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_t stream) {
   const int* I = reinterpret_cast<const int*>(ws + p.off_ints);
@@ -1509,16 +1557,11 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_
   c.ybuf = reinterpret_cast<double*>(ws + p.off_ybuf);
   c.x = reinterpret_cast<double*>(ws + p.off_x);
   c.dx = dx;
-  // test hook: "1" aborts every solve; "once<tag>" only the first solve after
-  // the tag changes (a timeout in one GN iteration of a multi-iteration call)
-  const char* inj = getenv("DROID_CHOL_FAULT_INJECT");
-  c.inject = 0;
-  if (inj && strncmp(inj, "once", 4) == 0) {
-    static std::string last_tag;
-    if (last_tag != inj) { c.inject = 1; last_tag = inj; }
-  } else if (inj && atoi(inj) != 0) {
-    c.inject = 1;
-  }
+  // test hook (droid_chol_set_fault_inject): a timeout in every solve, in the
+  // next solve only, or the next solve launched on a stale sync area
+  const int inj = g_chol_inject;
+  if (inj == kInjectOnce || inj == kInjectStale) g_chol_inject = kInjectOff;
+  c.inject = (inj == kInjectAll || inj == kInjectOnce) ? 1 : 0;
   c.prof = g_chol_prof;
   static bool attr = false;
   if (!attr) {
@@ -1526,12 +1569,13 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kCholLds));
     attr = true;
   }
-  if (int st = ba_zero(c.sync, p.sync_bytes, stream)) return st;
+  if (inj != kInjectStale)
+    if (int st = ba_zero(c.sync, p.sync_bytes, stream)) return st;
   // one worker per two CUs: the same makespan at C3 (2.38 vs 2.41 ms for
   // BA(itrs=2)) and 10 % less at C5 (11.6 vs 12.9 ms) than one per CU - fewer
   // workers polling the hand-off counters (profiles/r02/chol_grid_r02dn.txt)
   int grid = std::min(p.cs.ntasks, std::max(1, num_cus() / 2));
-  if (const char* g = getenv("DROID_CHOL_GRID")) grid = std::max(1, std::min(p.cs.ntasks, atoi(g)));  // A/B runs
+  if (const int g = ab_knob("DROID_CHOL_GRID", 0)) grid = std::max(1, std::min(p.cs.ntasks, g));  // A/B runs
   chol_dataflow_kernel<<<grid, 256, kCholLds, stream>>>(c);
   DROID_LAUNCH_CHECK();
   return kOk;
@@ -1542,6 +1586,16 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_
 using namespace droid;
 
 extern "C" {
+
+// Test hook for the dataflow solve's failure handling: 0 off, 1 every solve
+// aborts as on a dependency-wait timeout (status bit 1), 2 only the next solve
+// does, 3 the next solve is launched without zeroing its sync area (the
+// kernel's entry check must report it: status bits 1 and 2).  Process-wide.
+int droid_chol_set_fault_inject(int mode) {
+  if (mode < kInjectOff || mode > kInjectStale) return fail(kInvalidArgument, "chol_set_fault_inject: mode 0..3");
+  g_chol_inject = mode;
+  return kOk;
+}
 
 // Profiling builds (make prof): per Cholesky task, 8 int64 s_memrealtime
 // stamps (100 MHz): start, dependencies met, [potrf: last update applied,
@@ -1562,7 +1616,7 @@ int droid_ba_plan_upload(void* plan, void* workspace, hipStream_t stream) {
   DROID_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(workspace) + p->off_ints, p->ints.data(),
                                  p->ints.size() * sizeof(int), hipMemcpyHostToDevice, stream));
   // the status word reads "no failure" until a solve runs
-  DROID_HIP_CHECK(hipMemsetAsync(static_cast<char*>(workspace) + p->off_flag, 0, 64, stream));
+  if (int st = ba_zero(static_cast<char*>(workspace) + p->off_flag, 64, stream)) return st;
   p->uploaded = true;
   p->uploaded_to = workspace;
   return kOk;

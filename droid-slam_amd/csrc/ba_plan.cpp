@@ -505,29 +505,31 @@ static double chol_makespan(int n, int P, const std::vector<int>& perm, const st
   return std::max(cs.cp, cs.work / kWorkers);
 }
 
+// forced pose order for new plans (droid_ba_set_order): -1 = chosen by the
+// plan (default), 0 identity, 1 rcm, 2 mindeg, 3 nd (A/B runs and tests)
+static int g_force_order = -1;
+
 static void choose_order(BaPlan& p, const std::vector<std::pair<int, int>>& pairs) {
   const int P = p.P, n = p.n;
   std::vector<int> ident(P);
   for (int a = 0; a < P; ++a) ident[a] = a;
   p.perm = ident;
   p.order_kind = 0;
-  const char* force = getenv("DROID_BA_ORDER");  // identity | rcm | mindeg | nd (A/B and tests)
-  if (P <= 32 && !force) return;                  // a handful of tiles: nothing to gain
+  const int force = g_force_order;
+  if (P <= 32 && force < 0) return;                  // a handful of tiles: nothing to gain
   std::vector<std::vector<int>> adj(P);
   for (auto& pr : pairs) { adj[pr.first].push_back(pr.second); adj[pr.second].push_back(pr.first); }
   auto make = [&](int kind) {
     return kind == 1 ? order_rcm(P, adj) : kind == 2 ? order_mindeg(P, adj) : order_nd(P, adj);
   };
-  if (force) {
-    const std::string f(force);
-    const int kind = f == "rcm" ? 1 : f == "mindeg" ? 2 : f == "nd" ? 3 : 0;
-    if (kind) { p.perm = make(kind); p.order_kind = kind; }
+  if (force >= 0) {
+    if (force) { p.perm = make(force); p.order_kind = force; }
     return;
   }
   // the task graph (the critical path) is built only for orders whose tile
   // update count is within 4x of the fewest: a fill-heavy order's graph is
   // large (~1M tasks for the identity at C5) and never the fastest
-  const bool verbose = getenv("DROID_BA_PLAN_VERBOSE") != nullptr;
+  const bool verbose = ab_knob("DROID_BA_PLAN_VERBOSE", 0) != 0;
   std::vector<std::vector<int>> perms(4);
   std::vector<long> upd(4);
   perms[0] = ident;
@@ -609,7 +611,7 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, co
   // edges) BA(itrs=2) 0.209 ms at 2 splits vs 0.242 at 6 (the old 512-workgroup
   // target) and 0.281 at 12; C3 is fastest unsplit (2.41 vs 2.52 ms at 2)
   p.nsplit = std::max(1, std::min(std::max(1, HW / 256), (192 + std::max(E, 1) - 1) / std::max(E, 1)));
-  if (const char* f = getenv("DROID_BA_NSPLIT")) p.nsplit = std::max(1, std::min(std::max(1, HW / 64), atoi(f)));
+  if (const int f = ab_knob("DROID_BA_NSPLIT", 0)) p.nsplit = std::max(1, std::min(std::max(1, HW / 64), f));
   const int rounds = ceil_div(HW, 256);
   p.group_per_wave = std::max(1, std::min(rounds, (int)((long)p.K * rounds / 1024)));
   p.nchunk = ceil_div(rounds, p.group_per_wave);
@@ -886,6 +888,17 @@ int droid_chol_plan_structure(const void* plan, int* slot, int* fin, int* ycnt, 
 }
 
 void droid_ba_plan_destroy(void* plan) { delete static_cast<BaPlan*>(plan); }
+
+// Pose order of the plans created from now on: -1 = chosen per plan by the
+// expected dataflow makespan (default), 0 identity, 1 reverse Cuthill-McKee,
+// 2 minimum degree, 3 nested dissection.  Returns the previous setting, or -2
+// for a mode outside -1..3.  Process-wide (tests and A/B runs).
+int droid_ba_set_order(int kind) {
+  if (kind < -1 || kind > 3) return -2;
+  const int prev = g_force_order;
+  g_force_order = kind;
+  return prev;
+}
 
 size_t droid_ba_plan_workspace_bytes(const void* plan) {
   return plan ? static_cast<const BaPlan*>(plan)->total : 0;

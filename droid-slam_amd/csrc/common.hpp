@@ -39,6 +39,26 @@ int fail(int code, const std::string& msg);
                            std::string("kernel launch failed: ") + hipGetErrorString(_e)); \
   } while (0)
 
+// ---------------------------------------------------------------------------
+// A/B builds.  The product library (make) takes every kernel choice from its
+// arguments and compiled defaults - nothing from the environment - and ships
+// only the kernels the defaults run.  `make ab` (lib/ab/libdroid_hip.so,
+// -DDROID_AB=1) adds the measured-and-dropped variants and the experiment
+// knobs (env DROID_*) that select them, for A/B runs and bitwise cross-checks.
+// ---------------------------------------------------------------------------
+#ifndef DROID_AB
+#define DROID_AB 0
+#endif
+inline int ab_knob(const char* name, int dflt) {
+#if DROID_AB
+  const char* e = getenv(name);
+  return (e && e[0]) ? atoi(e) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
+}
+
 constexpr int kWave = 64;
 constexpr float kMinDepth = 0.25f;  // droid_kernels.cu:26
 

@@ -1537,10 +1537,7 @@ conv_band_kernel(ConvArgs a) {
 
 // DROID_CONV_ILV=0 selects the compiler-scheduled stage body (A/B runs)
 static bool band_interleaved() {
-  static const bool on = [] {
-    const char* e = getenv("DROID_CONV_ILV");
-    return !(e && e[0] == '0');
-  }();
+  static const bool on = ab_knob("DROID_CONV_ILV", 1) != 0;
   return on;
 }
 
@@ -1569,14 +1566,12 @@ static int launch_band_kernel(const ConvArgs& a, long nwg, int lds, hipStream_t 
   return kOk;
 }
 
+#if DROID_AB
 // DROID_CONV_NW4=1: the z|r gates (256x256, per-frame term) on the 4-wave tile
 // (A/B; measured 8.41 ms vs 7.4 for the 8-wave tile: one wave per SIMD leaves
 // the compiler-scheduled loop's LDS waits unhidden - it needs a hand schedule)
 static bool band_nw4() {
-  static const bool on = [] {
-    const char* e = getenv("DROID_CONV_NW4");
-    return e && e[0] == '1';
-  }();
+  static const bool on = ab_knob("DROID_CONV_NW4", 0) == 1;
   return on;
 }
 
@@ -1597,6 +1592,7 @@ static int launch_band_nw4(const ConvArgs& a0, hipStream_t stream) {
   DROID_LAUNCH_CHECK();
   return kOk;
 }
+#endif
 
 template <int TMX, int TN, bool DWHEAD = false>
 static int launch_band(const ConvArgs& a0, hipStream_t stream) {
@@ -1849,10 +1845,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 // DROID_CONV_BAND2=0 / 1: none / every shape it takes (A/B runs), read at load;
 // droid_conv_set_tile changes it per call (tests compare both tiles in one process).
 static int& band2_mode() {
-  static int mode = [] {
-    const char* e = getenv("DROID_CONV_BAND2");
-    return e ? atoi(e) : -1;
-  }();
+  static int mode = ab_knob("DROID_CONV_BAND2", -1);
   return mode;
 }
 static bool band2_for(int epi, long px) {
@@ -1883,281 +1876,9 @@ static int launch_band2_kernel(const ConvArgs& a0, hipStream_t stream) {
   return kOk;
 }
 
-// ---------------------------------------------------------------------------
-// Winograd band kernel (3x3, CHUNKED, W == 64): the 3x3 conv as F(2,3) along x.
-// For an output pixel pair (x, x+1) = (2P, 2P+1) of image row y and kernel row
-// ky, with d_t = in[y + ky - 1][2P + t] (t = -1..2) and g_t = w[ky][t + 1]:
-//   u0 = d_-1 - d_1   u1 = d_0 + d_1   u2 = d_1 - d_0   u3 = d_0 - d_2
-//   v0 = g_-1         v1 = (g_-1 + g_0 + g_1) / 2   v2 = (g_-1 - g_0 + g_1) / 2   v3 = g_1
-//   M_k = sum over (ky, ci) of u_k v_k (four GEMMs, M = pairs, N = Cout, K = 3 Cin)
-//   out(2P) = M0 + M1 + M2,   out(2P+1) = M1 - M2 - M3
-// 12 multiplies per pixel pair and input channel where the direct conv does
-// 18: two thirds of the MFMA work.  u_k is formed on packed fp16 (one rounding
-// of the exact sum, v_pk_add_f16), v_k is pre-transformed on the host
-// (pack_conv_wino) from the fp16 weights and rounded once; the accumulation
-// and the output transform are fp32.  Extra error: one fp16 rounding of u_k
-// and v_k, i.e. one more fp16 ulp of each operand, the class of error the
-// reference's autocast (cuDNN picks Winograd kernels for fp16 3x3 convs too)
-// already carries; parity tests bound it against the fp32 conv.
-//
-// Tile: 256 pixels (4 image rows) x 128 output channels on 8 waves; wave (wm,
-// wn) owns image row wm and channels wn*64 .. +63: 32 pixel pairs x 64 channels
-// for each of the four M_k (128 accumulators).  Pairs are interleaved so that
-// lane fr of pair fragment f holds pair 2 fr + f = pixels 4 fr + 2f, +1: the
-// band is stored in LDS by x mod 4 ("e0" x = 4fr, "o0" 4fr+1, "e1" 4fr+2, "o1"
-// 4fr+3 - four contiguous 16-row blocks per image row, conflict-free
-// ds_read_b128 as in the band kernel) and the two shifted inputs of the
-// transform are one DPP lane shift each: d_-1 of fragment 0 is o1 of lane fr-1
-// (row_shr:1, zero at x = -1), d_2 of fragment 1 is e0 of lane fr+1 (row_shl:1,
-// zero at x = 64); every other d_t is an unshifted read.  Per K-step of 32
-// channels a wave issues 4 + 16 ds_read_b128 (band, transformed weights), 8
-// DPP moves and 32 v_pk_add_f16 for 32 MFMAs.
-// LDS (144 KB): the 6-row band of one (64-channel chunk, 32-channel K half),
-// double buffered (2 x 24 KB, LDS-DMA as in the band kernel, issued three
-// stages ahead), and the transformed weights of one stage = (chunk, K half,
-// ky): [4 comps][128 channels][32] fp16 = 32 KB, triple buffered (issued two
-// stages ahead: a stage is half the band kernel's MFMA time, one stage of lead
-// left the DMA latency exposed - 7.9 vs 7.45 ms for z|r); all rows are 64 B
-// with the 16-B slot XOR-ed by kWinoG[(row & 15) >> 2] (conflict-free for the
-// ds_read_b128 lane groups of a 16-row fragment).
-// Global transformed weights: wt[stage][comp][Cout][32], stage = (chunk*2 + hk)*3 + ky.
-// Measured (C3, 2048 edges of 48x64, scripts/wino_bench.py, profiles/r03/
-// wino_r03bg.txt): z|r 7.90 ms vs 7.41 for the direct 256x256 band tile, q 4.28
-// vs 4.12, 128->128 1.75 vs 1.64 - slower despite a third less MFMA work
-// (SQ_VALU_MFMA_BUSY 6.04e9 vs 9.06e9).  The loop is bound by the SIMD's issue
-// slots, not the MFMA pipe: SQ_ACTIVE_INST_ANY 3.02e9 vs 1.65e9 - per 32 MFMAs
-// a wave issues 20 ds_read_b128, 40 VALU (the transform) and 5 LDS-DMAs (~60-185
-// issue cycles each, MI355X_MICROARCH.md), against 24 reads, ~6 VALU and 4.7
-// DMAs per 64 MFMAs in the direct tile (its 256 x 128 tile, bound by 4
-// accumulator sets in 128 VGPRs, moves twice the weight bytes per MFMA).
-// Issuing the DMAs after the stage's first MFMAs, and prefetching the weights
-// two stages ahead instead of one, measured the same; the first build's slot
-// swizzle (a wrong kWinoG constant: 1.13e9 bank-conflict cycles) cost 0.3 ms.
-// Opt-in (DROID_CONV_WINO=1 in droid_mi355x.fused); parity: tests/test_gpu_wino.py.
-constexpr int kWinoTM = 256, kWinoTN = 128;
-constexpr int kWinoBand = 6 * 64 * 64;         // one band buffer: 6 rows x 64 px x 32 channels (bytes)
-constexpr int kWinoWst = 4 * kWinoTN * 64;     // one weight stage buffer (bytes)
-constexpr int kWinoNW = 3;                     // weight stage buffers (two stages in flight)
-constexpr int kWinoLds = 2 * kWinoBand + kWinoNW * kWinoWst;
-static_assert(kWinoLds <= kLdsMax, "wino LDS");
-
-__device__ __forceinline__ int wino_g(int q) { return (0x78 >> (2 * q)) & 3; }   // {0, 2, 3, 1}[q]
-
-typedef int int4v_t __attribute__((ext_vector_type(4)));
-// lane shift within each 16-lane row; lanes whose source leaves the row keep `old`
-template <int CTRL>
-__device__ __forceinline__ half8 dpp_half8(half8 old, half8 src) {
-  const int4v_t o = __builtin_bit_cast(int4v_t, old), s = __builtin_bit_cast(int4v_t, src);
-  int4v_t r;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) r[k] = __builtin_amdgcn_update_dpp(o[k], s[k], CTRL, 0xF, 0xF, false);
-  return __builtin_bit_cast(half8, r);
-}
-constexpr int kDppRowShl1 = 0x101, kDppRowShr1 = 0x111;
-
-__device__ __forceinline__ void wait_vmcnt_wino(int n) {
-  switch (n) {   // wave-uniform; the counts the stage pipeline produces
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-template <int EPI>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_wino_kernel(ConvArgs a) {
-  extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
-  char* lds = reinterpret_cast<char*>(smem);
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int HW = a.H * 64;
-  const long wgid = xcd_work_id(a.m_tiles * a.n_tiles);
-  const long mt = wgid / a.n_tiles;
-  const int nt = (int)(wgid - mt * a.n_tiles);
-  const long m0 = mt * kWinoTM;
-  const int n0 = nt * kWinoTN;
-  const int y0 = (int)((m0 % HW) >> 6);
-  const long band0 = m0 - 64;
-  char* Hl = lds;                      // [2][6 rows][64 px][64 B]
-  char* Bl = lds + 2 * kWinoBand;      // [3][4 comps][128 ch][64 B]
-  const unsigned Hl_a = lds_addr(Hl), Bl_a = lds_addr(Bl);
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  // column tid's bias (+ per-image bias), loaded before any DMA (the counted
-  // vmcnt waits below count DMAs only)
-  float bcol = 0.f;
-  if (tid < kWinoTN) {
-    const int co = n0 + tid;
-    if (a.bias) bcol = a.bias[co];
-    if (a.bbias) bcol += a.bbias[(long)(m0 / HW) * a.Cout + co];
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  // 64-B LDS rows (band and weights alike): 16-B slot kq of a row whose index
-  // within its 16-row fragment is r16 is stored at kq ^ kWinoG[r16 >> 2]
-  // ---- band DMA, stage group b = (chunk b >> 1, K half b & 1): instruction q
-  // of this wave fills LDS rows 16 (wave + 8q) .. + 15; lane l writes row
-  // r = 16 (wave + 8q) + (l >> 2), slot l & 3 = channel piece (l & 3) ^ kWinoG[l >> 4]
-  // of pixel (ry, x): r = 64 ry + 16 (x & 3) + (x >> 2)
-  const int lpiece = (lane & 3) ^ wino_g(lane >> 4);
-  int hpix[3];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const int r = (wave + 8 * q) * 16 + (lane >> 2);
-    const int ry = r >> 6, rem = r & 63;
-    const int x = ((rem & 15) << 2) | (rem >> 4);
-    const int y = y0 - 1 + ry;
-    hpix[q] = (y >= 0 && y < a.H) ? ry * 64 + x : -1;
-  }
-  auto issue_band = [&](int bg) {
-    const int chunk = bg >> 1;
-    int s = 0;
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-      if (q + 1 < a.nsrc && chunk >= a.chunk_end[q]) s = q + 1;
-    const int cstart = s ? a.chunk_end[s - 1] : 0;
-    const ConvSrc src = a.src[s];
-    const int c = (chunk - cstart) * BK + (bg & 1) * 32 + lpiece * 8;
-    const bool okc = c < src.C;
-    const rsrc_t rs = make_rsrc(src.ptr + band0 * src.cstride, 6 * 64 * src.cstride * 2);
-    const unsigned dst = Hl_a + (bg & 1) * kWinoBand;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const unsigned off = (okc && hpix[q] >= 0) ? (unsigned)((hpix[q] * src.cstride + c) * 2) : kOob;
-      dma16(rs, dst + (wave_u + 8 * q) * 1024, off);
-    }
-  };
-  // ---- weight DMA: instruction q fills 1-KB block wb = wave + 8q = rows 16 wb ..
-  // + 15 (comp wb >> 3, channels 16 (wb & 7) ..); lane l: channel row l >> 2,
-  // slot l & 3 = logical K piece lpiece
-  const long wst_bytes = (long)4 * a.Cout * 64;   // one global stage
-  const rsrc_t rsw = make_rsrc(a.wp, (unsigned)(wst_bytes * a.nstage));
-  unsigned woff[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int wb = wave + 8 * q;
-    const int comp = wb >> 3, ch = (wb & 7) * 16 + (lane >> 2);
-    woff[q] = (unsigned)((((long)comp * a.Cout + n0 + ch) * 32 + lpiece * 8) * 2);
-  }
-  auto issue_w = [&](int st) {
-    const unsigned dst = Bl_a + (st % kWinoNW) * kWinoWst;
-    const unsigned sb = (unsigned)(st * wst_bytes);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dma16(rsw, dst + (wave_u + 8 * q) * 1024, woff[q] + sb);
-  };
-
-  // ---- fragment addresses (lane fr reads row fr of a 16-row fragment, slot kq4)
-  const int fr = lane & 15, kq4 = lane >> 4;
-  const int rsl = fr * 64 + ((kq4 ^ wino_g(fr >> 2)) << 4);
-  const int abase = wm * 4096 + rsl;
-  const int bbase = wn * 4096 + rsl;
-
-  floatx4 acc[4][2][4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[k][f][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  // stage s = (band group bg = s / 3 = (chunk, K half), kernel row ty = s % 3)
-  // = weight stage s of the global layout
-  const int nb = 2 * a.cpt;
-  const int nst = a.nstage;   // 3 * nb
-  issue_band(0);
-  issue_w(0);
-  if (nst > 1) issue_w(1);
-  const half8 zero8 = {};
-  int s = 0;
-  int wbuf = 0;   // s % kWinoNW
-  for (int bg = 0; bg < nb; ++bg) {
-    const char* Hb = Hl + (bg & 1) * kWinoBand;
-#pragma unroll
-    for (int ty = 0; ty < 3; ++ty, ++s) {
-      // DMA instructions of this wave issued after W(s): W(s+1) (4, issued one
-      // stage ago or in the prologue) and the bands issued at stages s-1 and
-      // s-2 (3 each, at stages 3b' issuing band b'+1)
-      const int nafter = (s + 1 < nst ? 4 : 0) + ((s >= 1 && (s - 1) % 3 == 0 && (s - 1) / 3 + 1 < nb) ? 3 : 0) +
-                         ((s >= 2 && (s - 2) % 3 == 0 && (s - 2) / 3 + 1 < nb) ? 3 : 0);
-      wait_vmcnt_wino(nafter);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      // W(s+2) into the buffer stage s-1 used; band bg+1 into the buffer band bg-1
-      // used (issuing them after this stage's first MFMAs instead measured the same)
-      if (s + 2 < nst) {
-        const unsigned dst = Bl_a + (wbuf == 0 ? 2 : wbuf - 1) * kWinoWst;
-        const unsigned sb = (unsigned)((s + 2) * wst_bytes);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) dma16(rsw, dst + (wave_u + 8 * q) * 1024, woff[q] + sb);
-      }
-      if (ty == 0 && bg + 1 < nb) issue_band(bg + 1);
-      const char* Ar = Hb + abase + ty * 4096;
-      const half8 e0 = *reinterpret_cast<const half8*>(Ar);
-      const half8 o0 = *reinterpret_cast<const half8*>(Ar + 1024);
-      const half8 e1 = *reinterpret_cast<const half8*>(Ar + 2048);
-      const half8 o1 = *reinterpret_cast<const half8*>(Ar + 3072);
-      const char* Bb = Bl + wbuf * kWinoWst + bbase;
-      // fragment 0: (d_-1, d_0, d_1, d_2) = (o1[fr-1], e0, o0, e1); fragment 1: (o0, e1, o1, e0[fr+1])
-      const half8 dm = dpp_half8<kDppRowShr1>(zero8, o1);
-      const half8 dp = dpp_half8<kDppRowShl1>(zero8, e0);
-      half8 u[4][2];
-      u[0][0] = dm - o0;  u[0][1] = o0 - o1;
-      u[1][0] = e0 + o0;  u[1][1] = e1 + o1;
-      u[2][0] = o0 - e0;  u[2][1] = o1 - e1;
-      u[3][0] = e0 - e1;  u[3][1] = e1 - dp;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        half8 bf[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8*>(Bb + k * 8192 + j * 1024);
-#pragma unroll
-        for (int f = 0; f < 2; ++f)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[k][f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], u[k][f], acc[k][f][j], 0, 0, 0);
-      }
-      wbuf = wbuf == 2 ? 0 : wbuf + 1;
-    }
-  }
-  (void)issue_w;
-  // output transform + pass 1: lane (fr, fq) of (f, j) holds channels wn*64 + 16 j
-  // + 4 fq .. + 3 of pair 2 fr + f = tile pixels 64 wm + 4 fr + 2 f, + 1
-  constexpr int ER = kWinoTN + 8;
-  const int fq = lane >> 4;
-  band_epilogue_core<kWinoTM, kWinoTN, 512, EPI, false>(
-      a, smem, m0, n0, tid, bcol, nullptr, [&](const float* bl, auto act) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = wn * 64 + j * 16 + fq * 4;
-          const floatx4 bv = *reinterpret_cast<const floatx4*>(bl + c);
-#pragma unroll
-          for (int f = 0; f < 2; ++f) {
-            half4_t o0, o1;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const float m0v = acc[0][f][j][k], m1v = acc[1][f][j][k], m2v = acc[2][f][j][k], m3v = acc[3][f][j][k];
-              o0[k] = (_Float16)act(((m0v + m1v) + m2v) + bv[k]);
-              o1[k] = (_Float16)act(((m1v - m2v) - m3v) + bv[k]);
-            }
-            const int px = wm * 64 + 4 * fr + 2 * f;
-            *reinterpret_cast<half4_t*>(&smem[px * ER + c]) = o0;
-            *reinterpret_cast<half4_t*>(&smem[(px + 1) * ER + c]) = o1;
-          }
-        }
-      });
-}
-
-template <int EPI>
-static int launch_wino_kernel(const ConvArgs& a, long nwg, hipStream_t stream) {
-  static bool attr = false;
-  if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wino_kernel<EPI>),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-    attr = true;
-  }
-  conv_wino_kernel<EPI><<<dim3((unsigned)nwg), 512, kWinoLds, stream>>>(a);
-  return kOk;
-}
+#if DROID_AB
+#include "ab/conv_wino_ab.inc"
+#endif
 
 // ---------------------------------------------------------------------------
 // ConvGRU global context (modules/gru.py:19-32, the glo branch):
@@ -2487,18 +2208,12 @@ __global__ void __launch_bounds__(256) eta_damping_kernel(const __half* __restri
 using namespace droid;
 
 static int band_version() {
-  static const int v = [] {
-    const char* e = getenv("DROID_CONV_BAND");
-    return e ? atoi(e) : 1;
-  }();
+  static const int v = ab_knob("DROID_CONV_BAND", 1);
   return v;
 }
 
 static bool rows_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("DROID_CONV_ROWS");
-    return !(e && atoi(e) == 0);
-  }();
+  static const bool on = ab_knob("DROID_CONV_ROWS", 1) != 0;
   return on;
 }
 
@@ -2583,10 +2298,7 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
   // 3x3 (and larger) convs over wide-enough outputs take the LDS-halo kernel;
   // DROID_CONV_HALO=0 / 4 / 8 (default) selects none / 4-wave / 8-wave tiles;
   // DROID_CONV_ROWS=0 disables the row-band variant.
-  static const int halo_nw = [] {
-    const char* e = getenv("DROID_CONV_HALO");
-    return e ? atoi(e) : 8;
-  }();
+  static const int halo_nw = ab_knob("DROID_CONV_HALO", 8);
   const bool halo_ok = !a.im2col && ks > 1 && Cout % 128 == 0 && (ks >> 1) * (W + 1) <= kHaloMax &&
                        epi != EPI_GLO && epi != EPI_HEAD;
   // LDS-DMA band kernel (3x3, whole-row tiles); DROID_CONV_BAND=0 disables it
@@ -2596,6 +2308,9 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
                        (epi != EPI_GRU_ZR || gru_ch % 128 == 0);
   int ns_, nh_;
   if (wt) {  // Winograd tile (droid_conv_wino_f16): W == 64, whole 4-row tiles, 128-channel N tiles
+#if !DROID_AB
+    return fail(kUnsupported, "conv_wino_f16: the Winograd tile ships in the A/B build only (make ab)");
+#else
     if (a.im2col || ks != 3 || W != 64 || H % 4 || Cout % kWinoTN ||
         !(epi == EPI_ACT ? a.stage_out != 0 : (pre && (epi == EPI_GRU_ZR || epi == EPI_GRU_Q))) ||
         (epi == EPI_GRU_ZR && gru_ch % kWinoTN))
@@ -2614,6 +2329,7 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
     if (st != kOk) return st;
     DROID_LAUNCH_CHECK();
     return kOk;
+#endif
   }
   // two-workgroups-per-CU tile: W == 64, 128-channel N tiles
   if (band_ok && band2_shape(epi, B, H, W, Cout, gru_ch)) {
@@ -2622,9 +2338,11 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
     return launch_band2_kernel<EPI_ACT>(a, stream);
   }
   if (pre) {  // the per-source term exists on the band tiles only
+#if DROID_AB
     if (band_ok && epi == EPI_GRU_ZR && Cout == 256 && 256 % W == 0 && (H * W) % 256 == 0 && band_nw4() &&
         band_fits<256, 256, 4>(W, &ns_, &nh_))
       return launch_band_nw4<256, 256>(a, stream);
+#endif
     if (band_ok && epi == EPI_GRU_ZR && Cout == 256 && 256 % W == 0 && (H * W) % 256 == 0 &&
         band_fits<256, 256>(W, &ns_, &nh_))
       return launch_band<256, 256>(a, stream);
@@ -2667,7 +2385,7 @@ int droid_conv_set_tile(int mode) {
 // Which kernel droid_conv_gru_pre_f16 runs for a ConvGRU gate conv (epi 1: z|r,
 // Cout 256; epi 2: q, Cout 128) over B images of H x W under the current tile
 // policy: 1 = conv_band2_kernel, 0 = the 8-wave band tile (<256,256> for z|r,
-// <384,128> for q), 2 = the opt-in 4-wave z|r tile (DROID_CONV_NW4=1), -1 = no
+// <384,128> for q), 2 = the 4-wave z|r tile (A/B build, DROID_CONV_NW4=1), -1 = no
 // band tile for the shape.
 int droid_conv_gate_tile(int epi, int B, int H, int W) {
   if ((epi != EPI_GRU_ZR && epi != EPI_GRU_Q) || B < 0 || H <= 0 || W <= 0) return -1;
@@ -2675,7 +2393,9 @@ int droid_conv_gate_tile(int epi, int B, int H, int W) {
   const int Cout = epi == EPI_GRU_ZR ? 256 : 128;
   if (band2_shape(epi, B, H, W, Cout, 128)) return 1;
   int ns_, nh_;
+#if DROID_AB
   if (epi == EPI_GRU_ZR && band_nw4() && (H * W) % 256 == 0 && band_fits<256, 256, 4>(W, &ns_, &nh_)) return 2;
+#endif
   if (epi == EPI_GRU_ZR) return ((H * W) % 256 == 0 && band_fits<256, 256>(W, &ns_, &nh_)) ? 0 : -1;
   return ((H * W) % 384 == 0 && band_fits<384, 128>(W, &ns_, &nh_)) ? 0 : -1;
 }
@@ -2896,10 +2616,7 @@ int droid_flow_enc0_f16(const float* motn, const void* w, const float* bias, voi
     attr = true;
   }
   // DROID_FE_TP=128: the 128-pixel tile on a shape that allows 256 (A/B runs)
-  static const int tp_env = [] {
-    const char* e = getenv("DROID_FE_TP");
-    return e ? atoi(e) : 256;
-  }();
+  static const int tp_env = ab_knob("DROID_FE_TP", 256);
   if (tp_env == 256 && (H * W) % 256 == 0 && fe_lds_bytes(W, 256) <= kLdsMax) {
     const long ntiles = (long)E * H * W / 256;
     const long grid = std::min<long>(ntiles, device_cu_count());

@@ -10,8 +10,11 @@
 // gathered from a 51 GB volume whose 16-B window rows make the lookup
 // DRAM-burst bound.
 //
-// corr_alt_ce0_kernel: persistent, one 8-wave workgroup per CU, software
-// pipelined over "stages" = (8x8-pixel query tile of one edge, pyramid level):
+// The product kernel is corr_alt2_kernel (two 4-wave workgroups per CU, its
+// design note below).  It refines the round-2 kernel described here,
+// corr_alt_ce0_kernel (now in ab/, the A/B build only; bitwise-equal outputs):
+// persistent, one 8-wave workgroup per CU, software pipelined over "stages" =
+// (8x8-pixel query tile of one edge, pyramid level):
 //   * the union of the tile's 64 windows at that level (their bounding box,
 //     clipped to the map) reaches LDS by LDS-DMA (NHWC rows are contiguous, one
 //     16-B piece per lane, XOR-swizzled slots) ONE STAGE AHEAD, into the other
@@ -207,352 +210,9 @@ __device__ __forceinline__ void alt_box_mfma(const char* lds, int box, _Float16*
   }
 }
 
-__global__ void __launch_bounds__(512) corr_alt_ce0_kernel(AltArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  _Float16* Cs = reinterpret_cast<_Float16*>(lds + kAltC);
-  int* pix = reinterpret_cast<int*>(lds + kAltPix);
-  int* grp = reinterpret_cast<int*>(lds + kAltGrp);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int H = a.H, W = a.W, HW = H * W;
-  const int tcols = W / 8, tpe = (H / 8) * tcols;
-  const unsigned lds_a = lds_addr(lds);
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-
-  // XCD-aware order: the workgroups of one XCD (blockIdx % 8) walk adjacent tiles
-  const int G = gridDim.x;
-  const int b0 = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  if (b0 >= a.ntiles) return;
-
-  // corr_encoder[0] B fragments of this wave's 16 output channels: per level,
-  // K = 49 real columns padded to 64 (2 K-steps of 32)
-  half8 wl[4][2];
-#pragma unroll
-  for (int l = 0; l < 4; ++l)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      half8 v;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int k = 32 * s + 8 * fq + i;
-        v[i] = k < 49 ? (_Float16)a.w[(wave * 16 + fr) * 224 + 49 * l + k] : (_Float16)0.f;
-      }
-      wl[l][s] = v;
-    }
-  const float bias = a.bias[wave * 16 + fr];
-
-  // tile geometry (32-bit: the launcher checks ntiles < 2^31).  Edge and frame
-  // indices are wave-uniform scalar loads (lgkmcnt), so no vmcnt wait - which
-  // would also drain the in-flight box DMA - is ever needed for them.
-  struct Tile { int e, ty0, tx0, f1, f2; };
-  auto tile_of = [&](int t) {
-    Tile r;
-    const int slot = t / tpe;   // the walk's edge slot; the tile inside the edge is the same either way
-    r.e = __builtin_amdgcn_readfirstlane(a.order ? a.order[slot] : slot);
-    const int tt = t - slot * tpe;
-    r.ty0 = (tt / tcols) * 8;
-    r.tx0 = (tt - (tt / tcols) * tcols) * 8;
-    // plain loads: the compiler waits for them at their first use (the next
-    // tile's box DMA, three stages later), not here as the scalar-load asm did
-    r.f1 = (DROID_ALT_ABL & 64) ? 0 : a.f1[r.e];
-    r.f2 = (DROID_ALT_ABL & 64) ? 0 : a.f2[r.e];
-    return r;
-  };
-  // coordinates of a tile's 64 pixels -> LDS slot by LDS-DMA (lanes 0..31 of wave 0, 16 B = 2 px each)
-  auto coords_dma = [&](const Tile& T, int slot) {
-    if (wave_u == 0) {
-      const int e = T.e, ty0 = T.ty0, tx0 = T.tx0;
-      const rsrc_t rs = make_rsrc(a.coords + (long)e * HW * 2, (unsigned)(HW * 8));
-      // slot pixel p <- image pixel (ty0 + alt_py(p), tx0 + alt_px(p)); pairs (p, p+1) share a row piece.
-      // Only lanes 0..31 may run the DMA: every active lane writes its 16 B at LDS base + 16 lane,
-      // and lanes 32..63 would land on the next 512 B (the other slot / the level boxes).
-      const int p = 2 * (lane & 31);
-      if (lane < 32)
-        dma16(rs, lds_a + kAltCoord + slot * 512, (unsigned)((((ty0 + alt_py(p)) * W + tx0 + alt_px(p)) * 2) * 4));
-    }
-  };
-  // a tile's 64 query feature rows (16 KB) -> box 1 + kAltF1 by LDS-DMA, once per
-  // workgroup (each wave then reads the fragments it needs from LDS): 2 x 1 KB per wave
-  auto f1_dma = [&](const Tile& T) {
-    const rsrc_t rs = make_rsrc(a.pyr[0] + (long)__builtin_amdgcn_readfirstlane(T.f1) * HW * 128, (unsigned)(HW * 256));
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int ins = wave_u + 8 * k;
-      const int p = ins * 4 + (lane >> 4);
-      const int piece = (lane & 15) ^ (p & 15);
-      const unsigned off = (unsigned)((((T.ty0 + alt_py(p)) * W + T.tx0 + alt_px(p)) * 128 + piece * 8) * 2);
-      dma16(rs, lds_a + kAltBox1 + kAltF1 + ins * 1024, off);
-    }
-  };
-  auto read_f1 = [&](half8 (&af)[4][4]) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int row = q * 16 + fr, piece = ks * 4 + fq;
-        af[q][ks] = *reinterpret_cast<const half8*>(lds + kAltBox1 + kAltF1 + row * 256 + ((piece ^ (row & 15)) << 4));
-      }
-  };
-  auto stage_fits = [&](int slot, int l) {
-    const int* lv = reinterpret_cast<const int*>(lds + kAltLvl) + slot * 16 + 4 * l;
-    return lv[2] * lv[3] <= alt_cap(l);
-  };
-  // Stages run the levels coarse to fine (3, 2, 1, 0): the largest box (level
-  // 0) is prefetched during level 1's compute, and the next tile's first box
-  // (level 3, tiny) is what competes with this tile's last level and the next
-  // query features for the vector memory pipe.  Stage s uses box buffer s & 1.
-  auto stage_dma = [&](const Tile& T, int slot, int l, int buf) {   // the whole-tile box of (T, l)
-    const int* lv = reinterpret_cast<const int*>(lds + kAltLvl) + slot * 16 + 4 * l;
-    alt_box_dma(a, l, T.f2, lv[0], lv[1], lv[2], lv[3], lds_a + (buf ? kAltBox1 : kAltBox0), wave_u, lane);
-  };
-
-  // ---- prologue: tile b0's coordinates and boxes, its level-0 box in flight ----
-  int t = b0;
-  int slot = 0;
-  Tile cur = tile_of(t);
-  coords_dma(cur, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (wave_u == 0)
-    alt_tile_boxes(a, reinterpret_cast<const float*>(lds + kAltCoord), reinterpret_cast<int*>(lds + kAltLvl), lane);
-  __syncthreads();
-  if (stage_fits(0, 3)) stage_dma(cur, 0, 3, 0);
-  f1_dma(cur);
-  half8 af[4][4];
-  floatx4 acc[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  // a finished tile's 64 output rows, staged at box 1 + 0 (bias + ReLU applied)
-  auto store_out = [&](int oe, int oty0, int otx0) {
-    const _Float16* Os = reinterpret_cast<const _Float16*>(lds + kAltBox1);
-    for (int idx = tid; idx < 64 * 16 * !(DROID_ALT_ABL & 16); idx += 512) {
-      const int p = idx >> 4, pc = idx & 15;
-      const long m = ((long)oe * H + oty0 + alt_py(p)) * W + otx0 + alt_px(p);
-      *reinterpret_cast<uint4*>(a.out + m * 128 + pc * 8) = *reinterpret_cast<const uint4*>(&Os[p * kAltOS + pc * 8]);
-    }
-  };
-  bool has_out = false;          // the previous tile's rows wait in the staging area
-  int pe = 0, pty0 = 0, ptx0 = 0;
-  int stage = 0;   // profiling stamps only
-  (void)stage;
-  for (;;) {
-    const int tn_ = t + G;                  // the tile after this one
-    const bool more = tn_ < a.ntiles;
-    const Tile nxt = more ? tile_of(tn_) : cur;
-    const int e = cur.e, ty0 = cur.ty0, tx0 = cur.tx0, f2 = cur.f2;
-    const float* cxy = reinterpret_cast<const float*>(lds + kAltCoord + slot * 512);
-    const int* lvb = reinterpret_cast<const int*>(lds + kAltLvl) + slot * 16;
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {   // unrolled: the level's weight fragments stay static register operands
-      const int l = 3 - st;
-      const int Hl = a.Hl[l], Wl = a.Wl[l];
-      const unsigned box = (st & 1) ? kAltBox1 : kAltBox0;
-      ALT_STAMP(0, ALT_NOW());
-      // (a) this stage's box (and the next tile's coordinates) have landed
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      ALT_STAMP(1, ALT_NOW());
-      if (st == 0) {
-        // the query features (DMA'd during the previous tile's last stage) -> registers,
-        // and the previous tile's output rows (staged in box 1) -> HBM; every wave is
-        // done reading both before box 1 is refilled below.  The stores go out here,
-        // not at the end of the previous tile, so that stage-start vmcnt(0) waits only
-        // retire them a stage later instead of waiting for their write latency.
-        read_f1(af);
-        if (has_out) store_out(pe, pty0, ptx0);
-        __syncthreads();
-      }
-      const bool fits = (DROID_ALT_ABL & 128) || lvb[4 * l + 2] * lvb[4 * l + 3] <= alt_cap(l);
-      _Float16* As = reinterpret_cast<_Float16*>(lds + ((st & 1) ? kAltBox1 + kAltA1 : kAltBox0));
-      ALT_STAMP(7, (long long)(lvb[4 * l + 2] * lvb[4 * l + 3]) * 2 + (fits ? 0 : 1));
-      // (b) the next stage's box -> the other buffer, in flight during this stage
-      if (DROID_ALT_ABL & 8) {
-      } else if (st < 3) {
-        if (stage_fits(slot, l - 1)) stage_dma(cur, slot, l - 1, (st + 1) & 1);
-      } else if (more) {
-        if (stage_fits(slot ^ 1, 3)) stage_dma(nxt, slot ^ 1, 3, 0);
-      }
-      if (st == 0 && more) coords_dma(nxt, slot ^ 1);
-      ALT_CSTAMP(3);
-      // (c) C = F1 x box^T
-      if (fits) {
-        if (!(DROID_ALT_ABL & 1)) alt_box_mfma(lds, box, Cs, af, min(lvb[4 * l + 2] * lvb[4 * l + 3], alt_cap(l)), 15, -1, wave_u, fr, fq);
-        ALT_CSTAMP(4);
-        if (tid < 64) { pix[3 * tid] = lvb[4 * l]; pix[3 * tid + 1] = lvb[4 * l + 1]; pix[3 * tid + 2] = lvb[4 * l + 2]; }
-        ALT_CSTAMP(5);
-      } else {
-        // slow path: groups = per quadrant its box if it fits, else its 16 pixels' own windows
-        // slow path: groups = per half (quadrants 2h, 2h+1) its box if it fits, else
-        // per quadrant its box if it fits, else its 16 pixels' own windows
-        if (wave_u == 0) {
-          const float scl = 1.0f / (float)(1 << l);
-          const int ox = alt_floor(cxy[2 * lane] * scl) - 3, oy = alt_floor(cxy[2 * lane + 1] * scl) - 3;
-          int qx0 = ox, qx1 = ox + 7, qy0 = oy, qy1 = oy + 7;
-#pragma unroll
-          for (int m = 1; m < 16; m <<= 1) {
-            qx0 = min(qx0, __shfl_xor(qx0, m)); qx1 = max(qx1, __shfl_xor(qx1, m));
-            qy0 = min(qy0, __shfl_xor(qy0, m)); qy1 = max(qy1, __shfl_xor(qy1, m));
-          }
-          int hx0 = min(qx0, __shfl_xor(qx0, 16)), hx1 = max(qx1, __shfl_xor(qx1, 16));
-          int hy0 = min(qy0, __shfl_xor(qy0, 16)), hy1 = max(qy1, __shfl_xor(qy1, 16));
-          const int hn = alt_clip(hx0, hx1, hy0, hy1, Wl, Hl);
-          const int qn = alt_clip(qx0, qx1, qy0, qy1, Wl, Hl);
-          int px0 = ox, px1 = ox + 7, py0 = oy, py1 = oy + 7;
-          const int pn = alt_clip(px0, px1, py0, py1, Wl, Hl);
-          const bool hfit = hn <= alt_cap(l), qfit = qn <= alt_cap(l);
-          pix[3 * lane] = hfit ? hx0 : qfit ? qx0 : px0;
-          pix[3 * lane + 1] = hfit ? hy0 : qfit ? qy0 : py0;
-          pix[3 * lane + 2] = hfit ? hx1 - hx0 + 1 : qfit ? qx1 - qx0 + 1 : px1 - px0 + 1;
-          const unsigned long long hb = __ballot(hfit), qb = __ballot(qfit);
-          const int q = lane >> 4, h = lane >> 5;
-          auto qcnt = [&](int qq) { return ((qb >> (16 * qq)) & 1ull) ? 1 : 16; };
-          auto hcnt = [&](int hh) { return ((hb >> (32 * hh)) & 1ull) ? 1 : qcnt(2 * hh) + qcnt(2 * hh + 1); };
-          const int hbase = h ? hcnt(0) : 0;
-          const int qbase = hbase + ((q & 1) ? qcnt(q - 1) : 0);
-          if (hfit) {
-            if ((lane & 31) == 0) {
-              int* g = grp + 4 + 6 * hbase;
-              g[0] = hx0; g[1] = hy0; g[2] = hn ? hx1 - hx0 + 1 : 0; g[3] = hn ? hy1 - hy0 + 1 : 0;
-              g[4] = 3 << (2 * h); g[5] = -1;
-            }
-          } else if (qfit) {
-            if ((lane & 15) == 0) {
-              int* g = grp + 4 + 6 * qbase;
-              g[0] = qx0; g[1] = qy0; g[2] = qn ? qx1 - qx0 + 1 : 0; g[3] = qn ? qy1 - qy0 + 1 : 0;
-              g[4] = 1 << q; g[5] = -1;
-            }
-          } else {
-            int* g = grp + 4 + 6 * (qbase + (lane & 15));
-            g[0] = px0; g[1] = py0; g[2] = pn ? px1 - px0 + 1 : 0; g[3] = pn ? py1 - py0 + 1 : 0;
-            g[4] = 1 << q; g[5] = lane;
-          }
-          if (lane == 0) grp[0] = hcnt(0) + hcnt(1);
-        }
-        __syncthreads();
-        const int ng = grp[0];
-        for (int gi = 0; gi < ng; ++gi) {
-          const int* g = grp + 4 + 6 * gi;
-          alt_box_dma(a, l, f2, g[0], g[1], g[2], g[3], lds_a + box, wave_u, lane);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();
-          alt_box_mfma(lds, box, Cs, af, g[2] * g[3], g[4], g[5], wave_u, fr, fq);
-          __syncthreads();  // box free for the next group
-        }
-      }
-      ALT_STAMP(2, ALT_NOW());
-      __syncthreads();
-      // box 1 (this stage's box) is free past the output staging: the next tile's
-      // query features land there during the bilinear, the encoder and the stores
-      if (st == 3 && more) f1_dma(nxt);
-      ALT_LSTAMP(3);
-      // (d) bilinear windows (volume-lookup arithmetic): thread (px, x offset) -> 7 outputs
-      // The reference rounds every product and sum of halves through float
-      // (at::Half); float carries >= 2*11+2 bits, so that equals the native
-      // half op (corr_kernels.hip): _Float16 arithmetic, no contraction.
-      if (tid < 64 * 7 && !(DROID_ALT_ABL & 2)) {
-        const int p = tid / 7, ac = tid - p * 7;
-        const float scl = 1.0f / (float)(1 << l);
-        const float x0 = cxy[2 * p] * scl, y0 = cxy[2 * p + 1] * scl;
-        const float fx0 = floorf(x0), fy0 = floorf(y0);
-        const float dx = x0 - fx0, dy = y0 - fy0;
-        const int xi0 = alt_floor(x0), yi0 = alt_floor(y0);
-        // float product, then half (rnd16 keeps hipcc from one-rounding v_fma_mixlo)
-        const _Float16 w11 = (_Float16)rnd16(dx * dy);
-        const _Float16 w10 = (_Float16)rnd16(dx * (1.0f - dy));
-        const _Float16 w01 = (_Float16)rnd16((1.0f - dx) * dy);
-        const _Float16 w00 = (_Float16)rnd16((1.0f - dx) * (1.0f - dy));
-        const int gx0 = pix[3 * p], gy0 = pix[3 * p + 1], gbw = pix[3 * p + 2];
-        const int xa = xi0 - 3 + ac;
-        const bool va = xa >= 0 && xa < Wl, vb = xa + 1 >= 0 && xa + 1 < Wl;
-        const _Float16* crow = Cs + p * kAltCS;
-        const _Float16 z = (_Float16)0.f;
-        // all 16 taps are read unconditionally (an invalid tap reads element 0 and
-        // is replaced by zero) so that the reads issue back to back under one wait
-        // instead of one LDS round trip per window row
-        _Float16 ca[8], cb[8];
-        int mk[8];
-#pragma unroll
-        for (int j = 0; j <= 7; ++j) {
-          const int y = yi0 - 3 + j;
-          const bool vy = y >= 0 && y < Hl;
-          const int o = (xa - gx0) + (y - gy0) * gbw;
-          mk[j] = (vy && va) | ((vy && vb) << 1);
-          ca[j] = crow[(mk[j] & 1) ? o : 0];
-          cb[j] = crow[(mk[j] & 2) ? o + 1 : 0];
-        }
-        // (the scheduler would otherwise interleave a wait after every pair of reads)
-        asm volatile("" : "+v"(ca[0]), "+v"(ca[1]), "+v"(ca[2]), "+v"(ca[3]), "+v"(ca[4]), "+v"(ca[5]),
-                     "+v"(ca[6]), "+v"(ca[7]), "+v"(cb[0]), "+v"(cb[1]), "+v"(cb[2]), "+v"(cb[3]), "+v"(cb[4]),
-                     "+v"(cb[5]), "+v"(cb[6]), "+v"(cb[7]));
-#pragma unroll
-        for (int j = 0; j <= 7; ++j) {
-          ca[j] = (mk[j] & 1) ? ca[j] : z;
-          cb[j] = (mk[j] & 2) ? cb[j] : z;
-        }
-        _Float16* arow = As + p * kAltAS + ac * 7;
-#pragma unroll
-        for (int j = 1; j <= 7; ++j) {
-          _Float16 s = z + ca[j - 1] * w00;
-          s = s + ca[j] * w01;
-          s = s + cb[j - 1] * w10;
-          s = s + cb[j] * w11;
-          arow[j - 1] = s;
-        }
-      }
-      if (wave_u == 7 && !(DROID_ALT_ABL & 256)) {
-        // the idle wave zeroes the lookup tile's K padding (columns 49..63): the
-        // tile shares its buffer with box data.  Row = lane; 2 + 4 + 8 + 16 B.
-        char* row = reinterpret_cast<char*>(As + lane * kAltAS);
-        *reinterpret_cast<_Float16*>(row + 98) = (_Float16)0.f;
-        *reinterpret_cast<unsigned*>(row + 100) = 0u;
-        *reinterpret_cast<uint2*>(row + 104) = make_uint2(0u, 0u);
-        *reinterpret_cast<uint4*>(row + 112) = make_uint4(0u, 0u, 0u, 0u);
-      }
-      ALT_LSTAMP(4);
-      if ((st == 1 || st == 2) && more && wave_u == 7 && !(DROID_ALT_ABL & 32)) {
-        // the next tile's level boxes, on the wave the bilinear leaves idle (its
-        // coordinates, DMA'd during the first stage, landed at stage 1's wait):
-        // levels 3, 2 now (level 3 is prefetched at stage 3), levels 1, 0 next stage
-        alt_tile_boxes(a, reinterpret_cast<const float*>(lds + kAltCoord + (slot ^ 1) * 512),
-                       reinterpret_cast<int*>(lds + kAltLvl) + (slot ^ 1) * 16, lane, st == 1 ? 2 : 0,
-                       st == 1 ? 4 : 2);
-      }
-      __syncthreads();
-      ALT_LSTAMP(5);
-      // (e) this level's slice of corr_encoder[0]: 64 px x 16 co per wave, K = 64
-#pragma unroll
-      for (int s = 0; s < 2 * !(DROID_ALT_ABL & 4); ++s) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const half8 x = *reinterpret_cast<const half8*>(&As[(q * 16 + fr) * kAltAS + s * 32 + fq * 8]);
-          acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, wl[l][s], acc[q], 0, 0, 0);
-        }
-      }
-      if (st == 3) {
-        // (f) bias, ReLU -> staging in this stage's box buffer (box 1: its MFMA is done) -> rows
-        _Float16* Os = reinterpret_cast<_Float16*>(lds + kAltBox1);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            Os[(q * 16 + fq * 4 + k) * kAltOS + wave * 16 + fr] = (_Float16)fmaxf(acc[q][k] + bias, 0.f);
-          acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
-        }
-        __syncthreads();
-        if (!more) store_out(e, ty0, tx0);   // the last tile: nothing follows to defer to
-      }
-      ALT_STAMP(6, ALT_NOW());
-      ++stage;
-    }
-    if (!more) break;
-    has_out = true;
-    pe = e; pty0 = ty0; ptx0 = tx0;
-    t = tn_;
-    cur = nxt;
-    slot ^= 1;
-  }
-}
+#if DROID_AB
+#include "ab/corr_alt_v1_ab.inc"
+#endif
 
 
 // ===========================================================================
@@ -1219,16 +879,15 @@ using namespace droid;
 
 static long long* g_alt_prof = nullptr;
 static int& alt_chunk_edges() {
-  static int v = [] {
-    const char* e = getenv("DROID_ALT_CHUNK");
-    return e ? std::max(0, atoi(e)) : 0;
-  }();
+  static int v = std::max(0, ab_knob("DROID_ALT_CHUNK", 0));
   return v;
 }
+// 2 = corr_alt2_kernel (the product kernel); the A/B build adds 1 (the round-2
+// one-workgroup-per-CU kernel) and 3 (corr_alt2_kernel<V3>)
 static int& alt_variant() {
   static int v = [] {
-    const char* e = getenv("DROID_ALT_VARIANT");
-    return (e && e[0] == '1') ? 1 : (e && e[0] == '3') ? 3 : 2;
+    const int e = ab_knob("DROID_ALT_VARIANT", 2);
+    return (e == 1 || e == 3) ? e : 2;
   }();
   return v;
 }
@@ -1292,48 +951,59 @@ int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int*
   const long chunk = (long)alt_chunk_edges() * (H / 8) * (W / 8);
   a.chunk = (chunk > 0 && 8 * chunk + a.ntiles < 0x7fffffffL) ? (int)chunk : 0;
   if (a.ntiles == 0) return kOk;
-  static bool attr = false;
-  if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt_ce0_kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, kAltLds));
-    attr = true;
-  }
+#if DROID_AB
   if (alt_variant() == 1) {
+    static bool attr = false;
+    if (!attr) {
+      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt_ce0_kernel),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kAltLds));
+      attr = true;
+    }
     const long grid = std::min<long>(a.ntiles, device_cu_count());
     corr_alt_ce0_kernel<<<dim3((unsigned)grid), 512, kAltLds, stream>>>(a);
-  } else {
-    static bool attr2 = false;
-    if (!attr2) {
-      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<false>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
-      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<true>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
-      attr2 = true;
-    }
-    static const int per_cu = [] {
-      const char* e = getenv("DROID_ALT2_WG_PER_CU");   // timing experiments: 1 = one workgroup per CU
-      return (e && e[0] == '1') ? 1 : 2;
-    }();
-    const long grid = std::min<long>(a.ntiles, (long)per_cu * device_cu_count());
-    if (alt_variant() == 3) corr_alt2_kernel<true><<<dim3((unsigned)grid), 256, kB2Lds, stream>>>(a);
-    else corr_alt2_kernel<false><<<dim3((unsigned)grid), 256, kB2Lds, stream>>>(a);
+    DROID_LAUNCH_CHECK();
+    return kOk;
   }
+#endif
+  static bool attr2 = false;
+  if (!attr2) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<false>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
+#if DROID_AB
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<true>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
+#endif
+    attr2 = true;
+  }
+  // two workgroups per CU (A/B: DROID_ALT2_WG_PER_CU=1 for one)
+  static const int per_cu = ab_knob("DROID_ALT2_WG_PER_CU", 2) == 1 ? 1 : 2;
+  const long grid = std::min<long>(a.ntiles, (long)per_cu * device_cu_count());
+#if DROID_AB
+  if (alt_variant() == 3) {
+    corr_alt2_kernel<true><<<dim3((unsigned)grid), 256, kB2Lds, stream>>>(a);
+    DROID_LAUNCH_CHECK();
+    return kOk;
+  }
+#endif
+  corr_alt2_kernel<false><<<dim3((unsigned)grid), 256, kB2Lds, stream>>>(a);
   DROID_LAUNCH_CHECK();
   return kOk;
 }
 
-// A/B hook: 1 = the one-workgroup-per-CU kernel, 2 = corr_alt2_kernel (default),
-// 3 = corr_alt2_kernel<V3> (env DROID_ALT_VARIANT sets the initial value)
-// A/B hook: corr_alt2_kernel's XCD chunk in edges (0 = the plain interleaved
-// walk; env DROID_ALT_CHUNK sets the initial value, default 8)
+// A/B hook: corr_alt2_kernel's XCD chunk in edges (0, the default = the plain
+// interleaved walk; in the A/B build env DROID_ALT_CHUNK sets the initial value)
 int droid_alt_set_chunk(int edges) {
   if (edges < 0) return fail(kInvalidArgument, "alt_set_chunk: edges >= 0");
   alt_chunk_edges() = edges;
   return kOk;
 }
 
+// A/B hook: 2 = corr_alt2_kernel (the product kernel); 1 = the one-workgroup-
+// per-CU kernel and 3 = corr_alt2_kernel<V3> exist in the A/B build only
+// (there env DROID_ALT_VARIANT sets the initial value)
 int droid_alt_set_variant(int v) {
   if (v < 1 || v > 3) return fail(kInvalidArgument, "alt_set_variant: 1, 2 or 3");
+  if (!DROID_AB && v != 2) return fail(kUnsupported, "alt_set_variant: variants 1 and 3 ship in the A/B build only (make ab)");
   alt_variant() = v;
   return kOk;
 }

@@ -623,23 +623,20 @@ altcorr_bwd_kernel(const float* __restrict__ fmap1, const float* __restrict__ fm
 // ===========================================================================
 using namespace droid;
 
-// DROID_LOOKUP_V1=1: the round-3 lookup kernels for the reference-layout paths (A/B runs)
+// A/B build, DROID_LOOKUP_V1=1: the round-3 one-launch kernel
+// (corr_pyramid_f16_r3_kernel, NCHW out) for the reference-layout lookups; the
+// product library takes corr_lookup_lvl / corr_lookup_coop there (the r3 kernel
+// stays the channels-last fallback, droid_corr_pyramid_lookup_nhwc)
 static bool lookup_lvl_on() {
-  static const bool on = [] {
-    const char* e = getenv("DROID_LOOKUP_V1");
-    return !(e && e[0] == '1');
-  }();
+  static const bool on = ab_knob("DROID_LOOKUP_V1", 0) != 1;
   return on;
 }
 
 // the cooperative NCHW lookup (corr_lookup_coop_kernel) for the 4-level
-// reference lookups; DROID_LOOKUP_COOP=0 / droid_lookup_set_coop(0) for the
-// per-thread kernel (A/B and the bitwise test)
+// reference lookups; droid_lookup_set_coop(0) (or DROID_LOOKUP_COOP=0 in the
+// A/B build) for the per-thread kernel (A/B and the bitwise test)
 static int& lookup_coop() {
-  static int v = [] {
-    const char* e = getenv("DROID_LOOKUP_COOP");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
+  static int v = ab_knob("DROID_LOOKUP_COOP", 1) == 0 ? 0 : 1;
   return v;
 }
 static bool coop_ok(int HW, const void* out, long maxslice) {

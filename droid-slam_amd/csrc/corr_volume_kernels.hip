@@ -8,24 +8,23 @@
 // level is written to HBM and read back by the next; at 2048 edges that is
 // 51 GB written + 70 GB re-read, plus the tile8 copy for the fused lookup.
 //
-// corr_volume_pyramid_kernel writes every level exactly once: a workgroup owns
-// 256 query pixels of one edge (8 waves x 32) and walks the target map in 8x8
-// patches (Z order, so each level-1 / level-2 tile of the 8x8-tiled layout is
-// completed by consecutive patches while its lines are in L2):
-//   * the patch's 64 target feature rows (16 KB) reach LDS by LDS-DMA, one
-//     patch ahead (double buffer), shared by the 8 waves;
-//   * a wave multiplies its 32 query rows (registers) by the patch on MFMA
-//     (v_mfma_f32_16x16x32_f16, fp32 accumulation), 4 N-blocks of 16 target
-//     pixels, each a 4x4 target sub-patch, and rounds to fp16 (V0);
-//   * the three pooling levels are formed in registers from the rounded
-//     values with the reference's arithmetic: a 2x2 window's four fp16 values
-//     summed in float in (h, w) order, times 1/4, rounded - across lanes
-//     (xor 1 / 4 for level 1, 2 / 8 for level 2) and across the 4 N-blocks
-//     (level 3);
-//   * V0 and the pooled values go through a per-wave LDS staging area to
-//     coalesced stores: 128 B per query pixel and patch for level 0 (one 8x8
-//     tile, or 8 row pieces of the reference layout), 4 x 8 B, 2 x 4 B, 2 B for
-//     levels 1..3.
+// Here every level is written exactly once and never re-read by the build
+// itself, in two launches (the design history - the round-3 one-pass kernel
+// and two other variants, all writing the same bytes - is in ab/, built only
+// by `make ab`):
+//   * corr_volume_pyramid2_kernel: a workgroup owns 256 query pixels of one
+//     edge and walks the target map in 8x8 patches (Z order); each patch's 64
+//     target feature rows (16 KB) reach LDS by LDS-DMA one patch ahead; the
+//     level-0 values are an MFMA GEMM (v_mfma_f32_16x16x32_f16, fp32
+//     accumulation) with the patch's target rows as A, so a lane's four
+//     accumulators are a 2x2 target window, rounded to fp16; level 1 is pooled
+//     in the lane with the reference's arithmetic (the window's four fp16
+//     values summed in float in (h, w) order, / 4, rounded) and, in the tiled
+//     layout, held in registers until the 2x2 patch group completes one
+//     level-1 tile; levels 0 and 1 leave as whole 128-B tiles (non-temporal
+//     stores: the volume is read by a later kernel, never by this one);
+//   * corr_volume_pool23_kernel: levels 2 and 3 pooled from the stored level 1
+//     in storage order, one 128-B line per wave-instruction.
 // Query features come from the frames' NHWC level-0 feature maps (the
 // AltCorrBlock pyramid level 0, i.e. fmap / 4) indexed per edge, so no
 // per-edge feature copy exists either.
@@ -70,232 +69,6 @@ __device__ __forceinline__ float vol_pool4(float a, float b, float c, float d) {
   return rnd16(s / 4.0f);
 }
 
-__global__ void __launch_bounds__(512) corr_volume_pyramid_kernel(VolArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  const int H = a.H, W = a.W, HW = H * W;
-  const int e = __builtin_amdgcn_readfirstlane((int)(blockIdx.x / a.qblocks));
-  const int qb = (int)(blockIdx.x % a.qblocks);
-  const int fa = __builtin_amdgcn_readfirstlane(a.f1[e]);
-  const int fb = __builtin_amdgcn_readfirstlane(a.f2[e]);
-  const unsigned lds_a = lds_addr(lds);
-  char* stage = lds + kVolStage + wave * kVolStageWave;
-  _Float16* s0 = reinterpret_cast<_Float16*>(stage);                   // [32][64]
-  _Float16* s1 = s0 + 32 * 64;                                         // [32][16]
-  _Float16* s2 = s1 + 32 * 16;                                         // [32][4]
-  _Float16* s3 = s2 + 32 * 4;                                          // [32]
-
-  // this wave's 32 query rows: A fragments for 2 row blocks x 4 K-steps
-  const int q0 = qb * kVolQ + wave * 32;
-  half8 af[2][4];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int q = min(q0 + 16 * r + fr, HW - 1);
-    const __half* row = a.f + ((long)fa * HW + q) * 128;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) af[r][ks] = *reinterpret_cast<const half8*>(row + ks * 32 + fq * 8);
-  }
-
-  const rsrc_t rsb = make_rsrc(a.f + (long)fb * HW * 128, (unsigned)(HW * 256));
-  const int pcols = W / 8, npatch = (H / 8) * pcols;
-  // Z order over 2x2 patch groups (a level-1 tile = 2x2 patches)
-  auto patch_yx = [&](int p, int& py, int& px) {
-    const int gcols = (pcols + 1) / 2;
-    const int g = p >> 2, k = p & 3;
-    int gy = g / gcols, gx = g - gy * gcols;
-    py = 2 * gy + (k >> 1);
-    px = 2 * gx + (k & 1);
-  };
-  // patches in Z order may fall off an odd edge of the grid: skip those slots
-  const int gslots = ((H / 8 + 1) / 2) * ((pcols + 1) / 2) * 4;
-  auto patch_dma = [&](int p, int buf) {
-    int py, px;
-    patch_yx(p, py, px);
-    // 16 x 1 KB: wave w issues rows 4w..4w+3 and 32+4w..; row = 16 b + c
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int ins = wave_u + 8 * k;
-      const int row = ins * 4 + (lane >> 4);
-      const int b = row >> 4, c = row & 15;
-      const int t = (8 * py + vol_ty(b, c)) * W + 8 * px + vol_tx(b, c);
-      const int piece = (lane & 15) ^ (row & 15);
-      dma16(rsb, lds_a + kVolB + buf * 16384 + ins * 1024, (unsigned)((t * 128 + piece * 8) * 2));
-    }
-  };
-  auto valid = [&](int p) {
-    int py, px;
-    patch_yx(p, py, px);
-    return py < H / 8 && px < pcols;
-  };
-  int first = 0;
-  while (first < gslots && !valid(first)) ++first;
-  if (first < gslots) patch_dma(first, 0);
-  int buf = 0;
-  // level geometry
-  int Hl[4], Wl[4], TR[4];
-#pragma unroll
-  for (int l = 0; l < 4; ++l) {
-    Hl[l] = H >> l;
-    Wl[l] = W >> l;
-    TR[l] = (Hl[l] + 7) / 8;  // tile rows (tiled layout)
-  }
-  for (int p = first; p < gslots;) {
-    int nxt = p + 1;
-    while (nxt < gslots && !valid(nxt)) ++nxt;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();   // patch p landed in buf; every wave done with buf ^ 1
-    if (nxt < gslots) patch_dma(nxt, buf ^ 1);
-    int py, px;
-    patch_yx(p, py, px);
-    const int ty0 = 8 * py, tx0 = 8 * px;
-
-    // V0 for 32 query rows x 64 target pixels: D[target col][query row] per N-block
-    float v[2][4][4];   // [row block][N-block][i]: query row 16 r + 4 fq + i, target col fr
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      half8 bf[4];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int row = b * 16 + fr, piece = ks * 4 + fq;
-        bf[ks] = *reinterpret_cast<const half8*>(lds + kVolB + buf * 16384 + row * 256 + ((piece ^ (row & 15)) << 4));
-      }
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[r][ks], bf[ks], c, 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[r][b][i] = rnd16(c[i]);
-      }
-    }
-    // level 0 -> staging [q][tile-row-major 8x8]
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          s0[(16 * r + 4 * fq + i) * 64 + vol_ty(b, fr) * 8 + vol_tx(b, fr)] = (_Float16)v[r][b][i];
-    // level 1: 2x2 windows of each 4x4 sub-patch (cols c, c^1, c^4, c^5 with c's row / col even)
-    float u[2][4][4];
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float x00 = v[r][b][i];
-          const float x01 = __shfl_xor(x00, 1), x10 = __shfl_xor(x00, 4), x11 = __shfl_xor(x00, 5);
-          u[r][b][i] = vol_pool4(x00, x01, x10, x11);   // valid on lanes whose col has even row and col
-        }
-    const bool l1lane = (fr & 5) == 0;
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (l1lane)   // level-1 pixel (2 (b>>1) + (fr>>3), 2 (b&1) + ((fr>>1)&1)) of the 4x4 level-1 patch
-            s1[(16 * r + 4 * fq + i) * 16 + (2 * (b >> 1) + (fr >> 3)) * 4 + 2 * (b & 1) + ((fr >> 1) & 1)] =
-                (_Float16)u[r][b][i];
-    // level 2: 2x2 of the level-1 values at cols 0, 2, 8, 10 of each N-block; level 3: the 4 N-blocks
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float w2[4];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const float y00 = u[r][b][i];
-          w2[b] = vol_pool4(y00, __shfl_xor(y00, 2), __shfl_xor(y00, 8), __shfl_xor(y00, 10));
-        }
-        if (fr == 0) {
-          const int q = 16 * r + 4 * fq + i;
-#pragma unroll
-          for (int b = 0; b < 4; ++b) s2[q * 4 + b] = (_Float16)w2[b];   // (b>>1, b&1) of the 2x2 level-2 patch
-          s3[q] = (_Float16)vol_pool4(w2[0], w2[1], w2[2], w2[3]);
-        }
-      }
-    // stores (the staging area is this wave's own: a wave barrier suffices)
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const long E0 = (long)e * HW;
-    // level 0: 32 q x 128 B, 8 lanes per query pixel
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int q = 8 * k + (lane >> 3), seg = lane & 7;   // seg = tile row
-      const int qg = q0 + q;
-      const uint4 val = *reinterpret_cast<const uint4*>(s0 + q * 64 + seg * 8);
-      if (qg < HW) {
-        long off;
-        if (a.tiled) off = ((E0 + qg) * TR[0] * (Wl[0] / 8) + py * (Wl[0] / 8) + px) * 64 + seg * 8;
-        else off = (E0 + qg) * (long)HW + (long)(ty0 + seg) * W + tx0;
-        *reinterpret_cast<uint4*>(a.lvl[0] + off) = val;
-      }
-    }
-    // level 1: 32 q x 4 rows x 8 B (the patch's 4x4 level-1 block)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int q = 16 * k + (lane >> 2), rr = lane & 3;
-      const int qg = q0 + q;
-      const uint2 val = *reinterpret_cast<const uint2*>(s1 + q * 16 + rr * 4);
-      const int y = ty0 / 2 + rr, x = tx0 / 2;
-      if (qg < HW) {
-        long off;
-        if (a.tiled) off = ((E0 + qg) * TR[1] * (Wl[1] / 8) + (y >> 3) * (Wl[1] / 8) + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7);
-        else off = (E0 + qg) * (long)(Hl[1] * Wl[1]) + (long)y * Wl[1] + x;
-        *reinterpret_cast<uint2*>(a.lvl[1] + off) = val;
-      }
-    }
-    // level 2: 32 q x 2 rows x 4 B; level 3: 32 q x 2 B
-    {
-      const int q = lane >> 1, rr = lane & 1;
-      const int qg = q0 + q;
-      const unsigned val = *reinterpret_cast<const unsigned*>(s2 + q * 4 + rr * 2);
-      const int y = ty0 / 4 + rr, x = tx0 / 4;
-      if (qg < HW) {
-        long off;
-        if (a.tiled) off = ((E0 + qg) * TR[2] * (Wl[2] / 8) + (y >> 3) * (Wl[2] / 8) + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7);
-        else off = (E0 + qg) * (long)(Hl[2] * Wl[2]) + (long)y * Wl[2] + x;
-        *reinterpret_cast<unsigned*>(a.lvl[2] + off) = val;
-      }
-    }
-    if (lane < 32) {
-      const int qg = q0 + lane;
-      const int y = ty0 / 8, x = tx0 / 8;
-      if (qg < HW) {
-        long off;
-        if (a.tiled) off = ((E0 + qg) * TR[3] * (Wl[3] / 8) + (y >> 3) * (Wl[3] / 8) + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7);
-        else off = (E0 + qg) * (long)(Hl[3] * Wl[3]) + (long)y * Wl[3] + x;
-        a.lvl[3][off] = *reinterpret_cast<const __half*>(s3 + lane);
-      }
-    }
-    buf ^= 1;
-    p = nxt;
-  }
-  // tiled layout: rows of the last tile row past H_l are zero (levels whose height is not a multiple of 8)
-  if (a.tiled) {
-#pragma unroll
-    for (int l = 1; l < 4; ++l) {
-      const int pad = TR[l] * 8 - Hl[l];
-      if (pad == 0) continue;
-      const int tcols = Wl[l] / 8;
-      // per query pixel: tcols tiles x pad rows x 16 B
-      const int pieces = tcols * pad;
-      for (int idx = lane; idx < 32 * pieces; idx += 64) {
-        const int q = idx / pieces, k = idx - q * pieces;
-        const int tc = k / pad, rr = Hl[l] - (TR[l] - 1) * 8 + (k - tc * pad);
-        const int qg = q0 + q;
-        if (qg < HW) {
-          const long off = (((long)e * HW + qg) * TR[l] * tcols + (TR[l] - 1) * tcols + tc) * 64 + rr * 8;
-          *reinterpret_cast<uint4*>(a.lvl[l] + off) = uint4{0u, 0u, 0u, 0u};
-        }
-      }
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Round 4: corr_volume_pyramid2_kernel, the same pyramid with the MFMA operands
@@ -627,225 +400,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
   }
 }
 
-// ---------------------------------------------------------------------------
-// corr_volume_pyramid3_kernel (round 4): corr_volume_pyramid2_kernel with
-//   * a 3-deep ring of patch buffers, the target rows of patch p + 2 issued at
-//     patch p (two patches of compute to cover the DMA latency instead of one);
-//   * level 0 stored straight from the accumulators: the lanes fq and fq ^ 1
-//     hold horizontally adjacent 2x2 windows of one query, so one exchange
-//     (lanes l ^ 16) leaves each with 8 contiguous bytes of one tile row (the
-//     even lane row y, the odd lane row y + 1 of its 4x4 sub-patch) - 8 stores
-//     of 8 B per patch and wave, no level-0 staging in LDS (60.8 KB per
-//     workgroup: two per CU);
-//   * every DMA and store issued unconditionally (out-of-range offsets), so the
-//     counts behind the hand-off wait are fixed: before patch p the wave waits
-//     for all but the stores of p - 2 and p - 1 and the DMA of p + 1.
-// Same arithmetic, the same values in the same order: bitwise the v1 / v2 pyramid.
-// ---------------------------------------------------------------------------
-constexpr int kVol3Ring = 3;
-constexpr int kVol3StageWave = 32 * kVol2S1 * 2 + 32 * 4 * 2 + 32 * 2;
-constexpr int kVol3Lds = kVol3Ring * 16384 + 8 * kVol3StageWave;
-static_assert(2 * kVol3Lds <= 160 * 1024, "corr_volume_pyramid3: two workgroups per CU");
-constexpr int kVol3Stores = 12;  // per wave and patch: 8 (level 0) + 2 (level 1) + 1 + 1
-
-__device__ __forceinline__ void vol3_wait(int n) {
-  switch (n) {  // wave-uniform; the counts the ring produces
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 26: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) corr_volume_pyramid3_kernel(VolArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  const int H = a.H, W = a.W, HW = H * W;
-  const int e = __builtin_amdgcn_readfirstlane((int)(blockIdx.x / a.qblocks));
-  const int qb = (int)(blockIdx.x % a.qblocks);
-  const int fa = __builtin_amdgcn_readfirstlane(a.f1[e]);
-  const int fb = __builtin_amdgcn_readfirstlane(a.f2[e]);
-  const unsigned lds_a = lds_addr(lds);
-  char* stage = lds + kVol3Ring * 16384 + wave * kVol3StageWave;
-  _Float16* s1 = reinterpret_cast<_Float16*>(stage);                   // [32][kVol2S1]
-  _Float16* s2 = s1 + 32 * kVol2S1;                                    // [32][4]
-  _Float16* s3 = s2 + 32 * 4;                                          // [32]
-
-  const int q0 = qb * kVolQ + wave * 32;
-  half8 qf[2][4];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int q = min(q0 + 16 * r + fr, HW - 1);
-    const __half* row = a.f + ((long)fa * HW + q) * 128;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) qf[r][ks] = *reinterpret_cast<const half8*>(row + ks * 32 + fq * 8);
-  }
-  int Hl[4], Wl[4], TR[4];
-  long slice[4];
-#pragma unroll
-  for (int l = 0; l < 4; ++l) {
-    Hl[l] = H >> l;
-    Wl[l] = W >> l;
-    TR[l] = (Hl[l] + 7) / 8;
-    slice[l] = a.tiled ? (long)TR[l] * (Wl[l] / 8) * 64 : (long)Hl[l] * Wl[l];
-  }
-  __amdgpu_buffer_rsrc_t ro[4];
-#pragma unroll
-  for (int l = 0; l < 4; ++l)
-    ro[l] = __builtin_amdgcn_make_buffer_rsrc(a.lvl[l] + (long)e * HW * slice[l], (short)0,
-                                              (int)(HW * slice[l] * 2), kBufFlags);
-  const rsrc_t rsb = make_rsrc(a.f + (long)fb * HW * 128, (unsigned)(HW * 256));
-  const int pcols = W / 8;
-  auto patch_yx = [&](int p, int& py, int& px) {
-    const int gcols = (pcols + 1) / 2;
-    const int g = p >> 2, k = p & 3;
-    int gy = g / gcols, gx = g - gy * gcols;
-    py = 2 * gy + (k >> 1);
-    px = 2 * gx + (k & 1);
-  };
-  const int gslots = ((H / 8 + 1) / 2) * ((pcols + 1) / 2) * 4;
-  auto valid = [&](int p) {
-    int py, px;
-    patch_yx(p, py, px);
-    return p < gslots && py < H / 8 && px < pcols;
-  };
-  auto next_valid = [&](int p) {
-    int q = p + 1;
-    while (q < gslots && !valid(q)) ++q;
-    return q;
-  };
-  // patch p's 64 target rows into ring slot `slot`; p >= gslots: the same two
-  // instructions with out-of-range offsets (fixed DMA count per patch)
-  auto patch_dma = [&](int p, int slot) {
-    int py = 0, px = 0;
-    const bool ok = p < gslots;
-    if (ok) patch_yx(p, py, px);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int ins = wave_u + 8 * k;
-      const int row = ins * 4 + (lane >> 4);
-      const int b = row >> 4, c = row & 15;
-      const int t = (8 * py + vol2_ty(b, c)) * W + 8 * px + vol2_tx(b, c);
-      const int piece = (lane & 15) ^ (row & 15);
-      dma16(rsb, lds_a + slot * 16384 + ins * 1024, ok ? (unsigned)((t * 128 + piece * 8) * 2) : kOob);
-    }
-  };
-  int p = 0;
-  while (p < gslots && !valid(p)) ++p;
-  int p1 = next_valid(p);
-  patch_dma(p, 0);
-  patch_dma(p1, 1);
-  int slot = 0, iter = 0;
-  for (; p < gslots; ++iter) {
-    const int p2 = next_valid(p1);
-    vol3_wait(iter == 0 ? 2 : iter == 1 ? 14 : 26);
-    __syncthreads();   // patch p landed in its slot; every wave done with patch p - 1's slot
-    patch_dma(p2, slot == 0 ? 2 : slot - 1);
-    int py, px;
-    patch_yx(p, py, px);
-    const int ty0 = 8 * py, tx0 = 8 * px;
-    const int qlim = (a.ablate & 1) ? 0 : HW;
-    float u[2][4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      half8 tf[4];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int row = b * 16 + fr, piece = ks * 4 + fq;
-        tf[ks] = *reinterpret_cast<const half8*>(lds + slot * 16384 + row * 256 + ((piece ^ (row & 15)) << 4));
-      }
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(tf[ks], qf[r][ks], c, 0, 0, 0);
-        float v[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = rnd16(c[i]);
-        const int q = 16 * r + fr, qg = q0 + q;
-        // level 0: rows y, y + 1 of the lane's 2x2 window; trade one pair with lane ^ 16
-        const unsigned top = pack2h(v[0], v[1]), bot = pack2h(v[2], v[3]);
-        const bool odd = fq & 1;
-        const unsigned got = (unsigned)__shfl_xor((int)(odd ? top : bot), 16);
-        const u32x2_t val = odd ? u32x2_t{got, bot} : u32x2_t{top, got};
-        const int y = 4 * (b >> 1) + 2 * (fq >> 1) + (odd ? 1 : 0), x = 4 * (b & 1);
-        const long off = a.tiled ? ((long)qg * TR[0] * (Wl[0] / 8) + py * (Wl[0] / 8) + px) * 64 + y * 8 + x
-                                 : (long)qg * HW + (long)(ty0 + y) * W + tx0 + x;
-        __builtin_amdgcn_raw_buffer_store_b64(val, ro[0], qg < qlim ? (int)(off * 2) : (int)kOob, 0, 0);
-        u[r][b] = vol_pool4(v[0], v[1], v[2], v[3]);
-        s1[q * kVol2S1 + (2 * (b >> 1) + (fq >> 1)) * 4 + 2 * (b & 1) + (fq & 1)] = (_Float16)u[r][b];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      float w2[4];
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-        w2[b] = vol_pool4(u[r][b], __shfl_xor(u[r][b], 16), __shfl_xor(u[r][b], 32), __shfl_xor(u[r][b], 48));
-      if (fq == 0) {
-        const int q = 16 * r + fr;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) s2[q * 4 + b] = (_Float16)w2[b];
-        s3[q] = (_Float16)vol_pool4(w2[0], w2[1], w2[2], w2[3]);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int q = 16 * k + (lane >> 2), rr = lane & 3;
-      const int qg = q0 + q;
-      const u32x2_t val = *reinterpret_cast<const u32x2_t*>(s1 + q * kVol2S1 + rr * 4);
-      const int y = ty0 / 2 + rr, x = tx0 / 2;
-      const long off = a.tiled ? ((long)qg * TR[1] * (Wl[1] / 8) + (y >> 3) * (Wl[1] / 8) + (x >> 3)) * 64 +
-                                     (y & 7) * 8 + (x & 7)
-                               : (long)qg * (Hl[1] * Wl[1]) + (long)y * Wl[1] + x;
-      __builtin_amdgcn_raw_buffer_store_b64(val, ro[1], qg < qlim ? (int)(off * 2) : (int)kOob, 0, 0);
-    }
-    {
-      const int q = lane >> 1, rr = lane & 1;
-      const int qg = q0 + q;
-      const unsigned val = *reinterpret_cast<const unsigned*>(s2 + q * 4 + rr * 2);
-      const int y = ty0 / 4 + rr, x = tx0 / 4;
-      const long off = a.tiled ? ((long)qg * TR[2] * (Wl[2] / 8) + (y >> 3) * (Wl[2] / 8) + (x >> 3)) * 64 +
-                                     (y & 7) * 8 + (x & 7)
-                               : (long)qg * (Hl[2] * Wl[2]) + (long)y * Wl[2] + x;
-      __builtin_amdgcn_raw_buffer_store_b32(val, ro[2], qg < qlim ? (int)(off * 2) : (int)kOob, 0, 0);
-    }
-    {
-      const int qg = q0 + (lane & 31);
-      const int y = ty0 / 8, x = tx0 / 8;
-      const long off = a.tiled ? ((long)qg * TR[3] * (Wl[3] / 8) + (y >> 3) * (Wl[3] / 8) + (x >> 3)) * 64 +
-                                     (y & 7) * 8 + (x & 7)
-                               : (long)qg * (Hl[3] * Wl[3]) + (long)y * Wl[3] + x;
-      const short val = (short)__half_as_ushort(*reinterpret_cast<const __half*>(s3 + (lane & 31)));
-      __builtin_amdgcn_raw_buffer_store_b16(val, ro[3], (lane < 32 && qg < qlim) ? (int)(off * 2) : (int)kOob, 0, 0);
-    }
-    slot = slot == 2 ? 0 : slot + 1;
-    p = p1;
-    p1 = p2;
-  }
-  if (a.tiled) {
-#pragma unroll
-    for (int l = 1; l < 4; ++l) {
-      const int pad = TR[l] * 8 - Hl[l];
-      if (pad == 0) continue;
-      const int tcols = Wl[l] / 8;
-      const int pieces = tcols * pad;
-      for (int idx = lane; idx < 32 * pieces; idx += 64) {
-        const int q = idx / pieces, k = idx - q * pieces;
-        const int tc = k / pad, rr = Hl[l] - (TR[l] - 1) * 8 + (k - tc * pad);
-        const int qg = q0 + q;
-        if (qg < HW) {
-          const long off = (((long)e * HW + qg) * TR[l] * tcols + (TR[l] - 1) * tcols + tc) * 64 + rr * 8;
-          *reinterpret_cast<uint4*>(a.lvl[l] + off) = uint4{0u, 0u, 0u, 0u};
-        }
-      }
-    }
-  }
-}
+#if DROID_AB
+#include "ab/corr_volume_ab.inc"
+#endif
 
 // ---------------------------------------------------------------------------
 // corr_volume_pool23_kernel (round 4, variant 4): levels 2 and 3 of every
@@ -1081,22 +638,21 @@ int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, i
   a.W = W;
   a.tiled = tiled ? 1 : 0;
   a.qblocks = ceil_div(H * W, kVolQ);
-  if (const char* ab = getenv("DROID_VOL_ABLATE")) a.ablate = atoi(ab);   // timing experiments only
+  a.ablate = ab_knob("DROID_VOL_ABLATE", 0);   // timing experiments (A/B build only)
   const long grid = (long)E * a.qblocks;
   if (grid == 0) return kOk;
   if (grid > 0x7fffffffL) return fail(kUnsupported, "corr_volume_pyramid: too many edges");
-  // DROID_VOL_VARIANT (A/B runs; DROID_VOL_V1=1 = variant 1): 1 the round-3 kernel,
-  // 2 corr_volume_pyramid2_kernel<0> (every level per patch), 3 the ring variant,
-  // 4 (default) corr_volume_pyramid2_kernel<1 / 2> + corr_volume_pool23_kernel.
-  // C3, 2048 edges, identical bytes (hash64): v1 33.3 ms, v2 19.9-23.2, v3 23.6,
-  // v4 15.6-16.1 (profiles/r04/vol_v*.txt, r04g_vol_v*.txt)
-  static const int variant = [] {
-    const char* e = getenv("DROID_VOL_VARIANT");
-    const char* e1 = getenv("DROID_VOL_V1");
-    return e ? atoi(e) : (e1 && e1[0] == '1') ? 1 : 4;
-  }();
+  // The product kernel is variant 4: corr_volume_pyramid2_kernel<1 / 2> writes
+  // levels 0 and 1, corr_volume_pool23_kernel pools levels 2 and 3 from the
+  // stored level 1.  The A/B build keeps DROID_VOL_VARIANT 1 (the round-3
+  // kernel), 2 (corr_volume_pyramid2_kernel<0>, every level per patch) and 3
+  // (the ring variant).  C3, 2048 edges, identical bytes (hash64): v1 33.3 ms,
+  // v2 19.9-23.2, v3 23.6, v4 15.6-16.1 then 12.0-12.8 with non-temporal
+  // stores (profiles/r04/vol_v*.txt, r04g_vol_v*.txt, r04x_vol_store_aux.txt)
+  static const int variant = ab_knob("DROID_VOL_VARIANT", 4);
   if ((long)H * W * H * W * 2 >= 0x7fffffffL && variant != 1)
     return fail(kUnsupported, "corr_volume_pyramid: an edge's level-0 volume must stay below 2 GB");
+#if DROID_AB
   if (variant == 3) {
     static bool attr3 = false;
     if (!attr3) {
@@ -1105,7 +661,10 @@ int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, i
       attr3 = true;
     }
     corr_volume_pyramid3_kernel<<<dim3((unsigned)grid), 512, kVol3Lds, stream>>>(a);
-  } else if (variant == 1) {
+    DROID_LAUNCH_CHECK();
+    return kOk;
+  }
+  if (variant == 1) {
     static bool attr = false;
     if (!attr) {
       DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid_kernel),
@@ -1113,32 +672,39 @@ int droid_corr_volume_pyramid(const void* fmaps, const int* f1, const int* f2, i
       attr = true;
     }
     corr_volume_pyramid_kernel<<<dim3((unsigned)grid), 512, kVolLds, stream>>>(a);
-  } else {
-    static bool attr2 = false;
-    if (!attr2) {
+    DROID_LAUNCH_CHECK();
+    return kOk;
+  }
+  if (variant == 2) {
+    static bool attr0 = false;
+    if (!attr0) {
       DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel<0>),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, kVol2Lds));
-      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel<1>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kVol2Lds));
-      DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel<2>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kVol2Lds));
-      attr2 = true;
+      attr0 = true;
     }
-    if (variant == 4) {
-      if (tiled) corr_volume_pyramid2_kernel<1><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
-      else corr_volume_pyramid2_kernel<2><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
-      DROID_LAUNCH_CHECK();
-      VolArgs b = a;
-      const long nq = (long)E * H * W;
-      b.qblocks = (int)nq;   // the pooling pass reads its (edge, pixel) count from qblocks
-      const long g2 = std::min<long>((nq + 3) / 4, 16L * device_cu_count());
-      if (g2 > 0x7fffffffL || nq > 0x7fffffffL) return fail(kUnsupported, "corr_volume_pyramid: too many pixels");
-      const int lds2 = 2 * 4 * (H / 4) * (W / 4) * 2;   // two query pixels' level 2 per wave
-      corr_volume_pool23_kernel<<<dim3((unsigned)g2), 256, lds2, stream>>>(b);
-    } else {
-      corr_volume_pyramid2_kernel<0><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
-    }
+    corr_volume_pyramid2_kernel<0><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
+    DROID_LAUNCH_CHECK();
+    return kOk;
   }
+#endif
+  static bool attr2 = false;
+  if (!attr2) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel<1>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kVol2Lds));
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_volume_pyramid2_kernel<2>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kVol2Lds));
+    attr2 = true;
+  }
+  if (tiled) corr_volume_pyramid2_kernel<1><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
+  else corr_volume_pyramid2_kernel<2><<<dim3((unsigned)grid), 512, kVol2Lds, stream>>>(a);
+  DROID_LAUNCH_CHECK();
+  VolArgs b = a;
+  const long nq = (long)E * H * W;
+  b.qblocks = (int)nq;   // the pooling pass reads its (edge, pixel) count from qblocks
+  const long g2 = std::min<long>((nq + 3) / 4, 16L * device_cu_count());
+  if (g2 > 0x7fffffffL || nq > 0x7fffffffL) return fail(kUnsupported, "corr_volume_pyramid: too many pixels");
+  const int lds2 = 2 * 4 * (H / 4) * (W / 4) * 2;   // two query pixels' level 2 per wave
+  corr_volume_pool23_kernel<<<dim3((unsigned)g2), 256, lds2, stream>>>(b);
   DROID_LAUNCH_CHECK();
   return kOk;
 }

@@ -198,9 +198,11 @@ depth_filter_kernel(const float* __restrict__ poses, const float* __restrict__ d
       const float d01 = D[(v0 + 0) * W + u0 + 1];
       const float d10 = D[(v0 + 1) * W + u0 + 0];
       const float d11 = D[(v0 + 1) * W + u0 + 1];
-      const float idj = 1.0f / dj;
-      if (fabsf(idj - 1.0f / d00) < t || fabsf(idj - 1.0f / d01) < t ||
-          fabsf(idj - 1.0f / d10) < t || fabsf(idj - 1.0f / d11) < t)
+      // the reference's test is in double (droid_kernels.cu:768-772: 1.0 / dj
+      // with a double literal), so a count at the threshold flips the same way
+      const double idj = 1.0 / (double)dj, td = (double)t;
+      if (fabs(idj - 1.0 / (double)d00) < td || fabs(idj - 1.0 / (double)d01) < td ||
+          fabs(idj - 1.0 / (double)d10) < td || fabs(idj - 1.0 / (double)d11) < td)
         count += 1.0f;
     }
   }

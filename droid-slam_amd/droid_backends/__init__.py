@@ -280,6 +280,34 @@ def corr_alt_ce0(pyramid, f1, f2, coords, w, bias, out=None, order=None):
     return out
 
 
+BA_ORDERS = ("identity", "rcm", "mindeg", "nd")
+
+
+def ba_set_order(order):
+    """Pose order of the BA plans built from now on (droid_ba_set_order):
+    None = chosen per plan (default) or one of BA_ORDERS.  Returns the previous
+    setting (None or a name).  Cached plans keep their order."""
+    prev = lib.droid_ba_set_order(-1 if order is None else BA_ORDERS.index(order))
+    if prev == -2:
+        raise RuntimeError("ba_set_order: order must be None or one of %s" % (BA_ORDERS,))
+    return None if prev < 0 else BA_ORDERS[prev]
+
+
+# the library's build (droid_build_info): the A/B build carries the dropped
+# kernel variants and reads the DROID_* experiment knobs; the product does not
+AB_BUILD = bool(lib.droid_build_info() & 1)
+
+CHOL_INJECT_OFF, CHOL_INJECT_ALL, CHOL_INJECT_ONCE, CHOL_INJECT_STALE = 0, 1, 2, 3
+
+
+def chol_set_fault_inject(mode):
+    """Test hook (droid_chol_set_fault_inject): CHOL_INJECT_ALL makes every
+    dataflow solve abort as on a dependency-wait timeout, CHOL_INJECT_ONCE only
+    the next one, CHOL_INJECT_STALE launches the next solve on a sync area that
+    was not zeroed (the kernel's entry check reports it)."""
+    check(lib.droid_chol_set_fault_inject(int(mode)), "chol_set_fault_inject")
+
+
 def alt_set_variant(v):
     """A/B hook (droid_alt_set_variant): 1 = corr_alt_ce0_kernel, 2 = corr_alt2_kernel, 3 = corr_alt2_kernel<V3>."""
     check(lib.droid_alt_set_variant(int(v)), "alt_set_variant")
@@ -402,11 +430,13 @@ def conv_gru_pre_f16(sources, wp, cout, bias, bbias, epi, pre, pre_idx, pre_coff
 
 
 def wino_supported(H, W, cout):
-    """Whether the update operator takes the Winograd tile: opted in with
-    DROID_CONV_WINO=1 (it measures slower than the direct band tile on MI355X,
+    """Whether the update operator takes the Winograd tile: only with the A/B
+    library (make ab; DROID_HIP_LIB) and opted in with DROID_CONV_WINO=1 (it
+    measures slower than the direct band tile on MI355X,
     csrc/conv_kernels.hip: conv_wino_kernel) and a shape droid_conv_wino_f16
     accepts (W == 64, whole 4-row tiles, 128-channel output tiles)."""
-    return W == 64 and H % 4 == 0 and cout % 128 == 0 and os.environ.get("DROID_CONV_WINO", "0") == "1"
+    return (AB_BUILD and W == 64 and H % 4 == 0 and cout % 128 == 0
+            and os.environ.get("DROID_CONV_WINO", "0") == "1")
 
 
 def conv_wino_f16(sources, wt, cout, bias=None, bbias=None, act=0, epi=EPI_ACT, out=None, out_coff=0,
@@ -910,7 +940,12 @@ class BaPlan:
         if evt is None:
             return
         evt.synchronize()
-        if (int(self._status[0]) | int(self._status[1])) & 2:
+        st = int(self._status[0]) | int(self._status[1])
+        if st & 4:
+            raise RuntimeError("ba: the dataflow Cholesky found its state corrupt (a sync counter not zeroed "
+                               "before the launch, or a task record outside the plan) in %s; that Gauss-Newton "
+                               "step left poses and disparities unchanged" % self.name)
+        if st & 2:
             raise RuntimeError("ba: the dataflow Cholesky timed out (dependency wait exceeded) in %s; that "
                                "Gauss-Newton step left poses and disparities unchanged" % self.name)
 
@@ -1018,6 +1053,8 @@ def dense_spd_solve(A, b, lm=0.0, ep=0.0):
             check(lib.droid_chol_set_system(h, _ptr(ws), _ptr(A), n, _ptr(b), _stream(A)), "chol set_system")
             check(lib.droid_chol_solve(h, _ptr(ws), float(lm), float(ep), _ptr(dx), _stream(A)), "chol solve")
         flag = int(ws[foff.value:foff.value + 4].view(torch.int32).item())
+        if flag & 4:
+            raise RuntimeError("dense_spd_solve: the dataflow Cholesky found its state corrupt")
         if flag & 2:
             raise RuntimeError("dense_spd_solve: the dataflow Cholesky timed out")
         return dx, bool(flag & 1)

@@ -22,6 +22,7 @@ _sz = ctypes.c_size_t
 
 _SIGS = {
     "droid_last_error": ([], ctypes.c_char_p),
+    "droid_build_info": ([], ctypes.c_int),
     "droid_abi_version": ([], _i),
     "droid_device_count": ([], _i),
     "droid_corr_index_forward": ([_i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p], _i),
@@ -63,6 +64,7 @@ _SIGS = {
     "droid_projective_transform": ([_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p], _i),
     "droid_frame_distance": ([_p, _p, _p, _p, _p, _i, _i, _i, _f, _p, _p], _i),
     "droid_chol_set_profile": ([_p], _i),
+    "droid_chol_set_fault_inject": ([_i], _i),
     "droid_instance_norm_workspace": ([_i, _i, _i], _sz),
     "droid_instance_norm_act_f16": ([_p, _p, _p, _i, _i, _i, _i, _f, _p, _sz, _p], _i),
     "droid_proximity_workspace": ([_i, _i, _i], _sz),
@@ -78,6 +80,7 @@ _SIGS = {
     "droid_ba_plan_clear_status": ([_p, _p, _p], _i),
     "droid_ba_plan_destroy": ([_p], None),
     "droid_ba_plan_workspace_bytes": ([_p], _sz),
+    "droid_ba_set_order": ([_i], _i),
     "droid_ba_plan_info": ([_p, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),
                             ctypes.POINTER(_i)], _i),
     "droid_ba_plan_kx": ([_p, _p], _i),

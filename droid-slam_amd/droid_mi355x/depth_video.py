@@ -221,8 +221,9 @@ def ba_sharded(poses, disps, intrinsics, disps_sens, target, weight, eta, ii_hos
             ev[1].record()
             timing.append(ev + (flat.numel() * flat.element_size(),))
         plan.solve_system(lm, ep, dx)
-        # the status words agreed before the step is applied (status values are
-        # 0..3 per word, so MAX keeps the timeout bit, value >= 2, of any rank):
+        # the status words agreed before the step is applied (a word is 0, 1, or
+        # one of 2, 3, 6, 7 when bit 1 - timeout or corrupt state - is set, so
+        # MAX keeps the skip bit of any rank):
         # a rank whose dataflow solve timed out makes EVERY rank skip this step's
         # back-substitution and retraction, so the replicated poses stay equal
         dist.all_reduce(status, op=dist.ReduceOp.MAX, group=group)

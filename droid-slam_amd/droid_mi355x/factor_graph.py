@@ -10,6 +10,7 @@ features come out of the fused reprojection kernel; the correlation lookup
 is one kernel for all levels; BA runs fully on the GPU.
 """
 import os
+import warnings
 import sys
 
 import numpy as np
@@ -126,14 +127,20 @@ class FactorGraph:
         # CorrBlock(tiled=...): the volume pool in 8x8 tiles for every operator - the
         # fused lookup reads it, and so does CorrBlock.__call__ (the reference
         # operators' NCHW lookup, droid_corr_pyramid_lookup_tiled); the layout is
-        # internal to the block (DROID_TILED_VOLUME=0: reference row-major layout)
-        self.tiled_volume = os.environ.get("DROID_TILED_VOLUME", "1") != "0"
+        # internal to the block (set False before add_factors for the reference
+        # row-major layout)
+        self.tiled_volume = True
+        # the on-demand lookup's tile walk grouped by target frame (measured
+        # within +-3 % of edge order, so off; see _alt_order)
+        self.alt_order_by_target = False
         self._version = 0          # bumped by every edge edit
         self._ba_tw = None         # (key, BA target rows, BA weight rows), see _ba_inputs
         # HIP-graph replay of update() per edge set (fused operator, one device,
         # frontend-sized graphs where host issue and launch gaps dominate):
         # DROID_UPDATE_GRAPHS=1 enables it (off by default; see _update_graphed)
         self.graphs = os.environ.get("DROID_UPDATE_GRAPHS", "0") == "1"
+        # a failed capture falls back to eager with one warning; strict re-raises (tests)
+        self.graph_strict = os.environ.get("DROID_GRAPH_STRICT", "0") == "1"
         self._graph = None         # captured update: dict(key, graph, plan, state, keep)
         self._graph_warm = None    # key of the last eager call (the capture follows it)
         self._cap_stream = None
@@ -453,13 +460,18 @@ class FactorGraph:
                     static[name].copy_(getattr(self, name))
                 if rec is not None:
                     rec.remove()
-        except Exception:
+        except Exception as exc:
             if rec is not None:
                 rec.remove()
-            # capture unsupported here (an upload, a plan build, an op that syncs): stay eager
+            # capture unsupported here (an upload, a plan build, an op that syncs): stay
+            # eager, and say so once - or re-raise when capture safety is under test
             main.wait_stream(cs)
             self.net, self.target, self.weight = saved
             self.graphs = False
+            if self.graph_strict:
+                raise
+            warnings.warn("FactorGraph: HIP-graph capture of update() failed (%s: %s); update() runs eagerly "
+                          "from now on" % (type(exc).__name__, exc), RuntimeWarning, stacklevel=3)
             self._update(*args)
             return
         main.wait_stream(cs)
@@ -643,12 +655,12 @@ class FactorGraph:
         return PendingAltLookup(self._alt_pyr[1], f1, f2, coords1, order=self._alt_order(f2h))
 
     def _alt_order(self, f2h):
-        """the on-demand lookup's tile walk, opt-in (DROID_ALT_ORDER=1): edges
+        """the on-demand lookup's tile walk, opt-in (alt_order_by_target): edges
         grouped by target frame (stable sort), so the tiles that read one frame's
         pyramid rows run together.  Measured at C3 (profiles/r04/r04n_alt_time.txt):
         within +-3 % of edge order for every XCD chunk size - the kernel is bound
         by its per-tile phases, not by L2 misses - so edge order is the default."""
-        if os.environ.get("DROID_ALT_ORDER", "0") != "1":
+        if not self.alt_order_by_target:
             return None
         return self._dev("alt_order", np.argsort(f2h, kind="stable").astype(np.int32))
 

@@ -449,11 +449,16 @@ class ReferenceLayoutUpdateModule(torch.nn.Module):
         edge's rows are compared with the first edge of its source frame (a
         read of inp, once per (inp, ii) pair - the caller's tensors are the same
         objects across the updates of an edge set); when any edge differs, the
-        per-edge gates run."""
-        key = (id(inp), _version_of(inp), id(ii), _version_of(ii), num_unique)
+        per-edge gates run.  The pair is recognised by identity and version
+        counter; inference tensors (torch.inference_mode) have no version
+        counter, so for them identity alone decides: an inference-mode caller
+        that refills the same inp or ii tensor in place between calls must pass
+        a new tensor instead (the reference's graph gathers a new inp per edge
+        edit, factor_graph.py:118, so its calls never do)."""
+        key = (id(inp), _version_of(inp), id(ii), _version_of(ii), num_unique,
+               inp.data_ptr(), tuple(inp.shape), ii.data_ptr(), tuple(ii.shape))
         c = getattr(self, "_frames", None)
-        if (c is not None and c[0] == key and c[1] is inp and c[2] is ii and key[1] is not None
-                and key[3] is not None):
+        if c is not None and c[0] == key and c[1] is inp and c[2] is ii:
             return c[3]
         E = inp_cl.shape[0]
         first = torch.full((num_unique,), E, dtype=torch.int64, device=inp_cl.device)

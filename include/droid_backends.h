@@ -34,6 +34,10 @@ extern "C" {
 const char* droid_last_error(void);
 int droid_abi_version(void);
 int droid_device_count(void);
+/* bit 0: the A/B build (`make ab`: dropped kernel variants + DROID_* experiment
+ * knobs), bit 1: the profiling build (`make prof`); 0 for the product library,
+ * which takes no kernel choice from the environment */
+int droid_build_info(void);
 
 /* ---- correlation -------------------------------------------------------- */
 
@@ -110,6 +114,12 @@ int droid_conv_set_tile(int mode);
 int droid_conv_gate_tile(int epi, int B, int H, int W);
 /* profiling builds only (make prof): Cholesky task timeline, 8 int64 per task */
 int droid_chol_set_profile(void* buf);
+/* Test hook for the dataflow solve's failure handling (no reference
+ * counterpart): 0 off, 1 every solve aborts as on a dependency-wait timeout
+ * (status bit 1), 2 only the next solve does, 3 the next solve is launched
+ * without zeroing its sync area (status bits 1 and 2 from the kernel's entry
+ * check).  Process-wide. */
+int droid_chol_set_fault_inject(int mode);
 
 /* CorrBlock pyramid construction (modules/corr.py:24-38,63-71) for E edges in
  * one pass: fmaps (NF,H,W,128) fp16 = frame features / 4 in NHWC (the
@@ -393,6 +403,12 @@ int droid_ba_plan_create_sharded(const int64_t* ii_host, const int64_t* jj_host,
                                  int motion_only, int own_lo, int own_hi, void** plan_out);
 void droid_ba_plan_destroy(void* plan);
 size_t droid_ba_plan_workspace_bytes(const void* plan);
+/* Pose order of the plans created from now on (no reference counterpart:
+ * Eigen's SimplicialLLT picks its own AMD ordering, droid_kernels.cu:1192):
+ * -1 = chosen per plan by the expected dataflow makespan (default),
+ * 0 identity, 1 reverse Cuthill-McKee, 2 minimum degree, 3 nested dissection.
+ * Returns the previous setting, -2 for a mode outside -1..3. */
+int droid_ba_set_order(int kind);
 /* nb_max = largest Schur Gram tile count (16 variables) of any depth frame */
 int droid_ba_plan_info(const void* plan, int* K, int* P, int* nblocks, int* nb_max);
 int droid_ba_plan_kx(const void* plan, int64_t* kx_host);
@@ -413,7 +429,9 @@ int droid_ba_plan_system_region(const void* plan, size_t* offset, size_t* bytes)
  * = the OR of the earlier solves' since droid_ba_run started or the caller
  * cleared them (sticky); bit 0 = a factorisation was not SPD (dx = 0, as the
  * reference), bit 1 = a dataflow solve timed out (that solve left poses and
- * disparities unchanged; the caller must report an error) */
+ * disparities unchanged; the caller must report an error), bit 2 (with bit 1)
+ * = the dataflow solve found its state corrupt: a sync counter not zeroed
+ * before the launch or a task record outside the plan (also skipped) */
 int droid_ba_plan_flag_offset(const void* plan, size_t* offset);
 /* zero both status words, stream-ordered (start of a staged build/solve BA call) */
 int droid_ba_plan_clear_status(void* plan, void* workspace, hipStream_t stream);

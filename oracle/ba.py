@@ -17,6 +17,8 @@ dx = 0 if the factorisation fails, disps updated for every frame of kx.
 Sparse-vs-dense: Eigen's SimplicialLLT (AMD ordering) and a dense Cholesky are
 the same exact factorisation up to fp64 roundoff.
 """
+import os
+
 import numpy as np
 
 from .se3 import adj_se3, act_se3, rel_se3, retr_se3
@@ -25,16 +27,30 @@ MIN_DEPTH = 0.25
 ALPHA = 0.05
 
 
+def _threads():
+    """worker threads for the per-chunk linearisation (numpy releases the GIL
+    in its array kernels): the CPU quota of this process, at most 16."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def linearize(poses, disps, intrinsics, targets, weights, ii, jj, chunk=64):
     """Per-edge Hessian blocks and per-pixel Schur terms (droid_kernels.cu:176-424).
 
-    Returns Hs (4,E,6,6), vs (2,E,6), Eii/Eij (E,6,HW), Cii/bz (E,HW).
+    Returns Hs (4,E,6,6), vs (2,E,6), Eii/Eij (E,6,HW), Cii/bz (E,HW).  Edge
+    chunks are independent and linearised on worker threads; the results are
+    the same arrays as a serial pass.
     """
     E = len(ii)
     if E > chunk:
-        parts = [_linearize(poses, disps, intrinsics, targets[s:s + chunk], weights[s:s + chunk],
-                            np.asarray(ii)[s:s + chunk], np.asarray(jj)[s:s + chunk])
-                 for s in range(0, E, chunk)]
+        from concurrent.futures import ThreadPoolExecutor
+        job = lambda s: _linearize(poses, disps, intrinsics, targets[s:s + chunk], weights[s:s + chunk],
+                                   np.asarray(ii)[s:s + chunk], np.asarray(jj)[s:s + chunk])
+        with ThreadPoolExecutor(_threads()) as ex:
+            parts = list(ex.map(job, range(0, E, chunk)))
         return (np.concatenate([p[0] for p in parts], axis=1), np.concatenate([p[1] for p in parts], axis=1),
                 *[np.concatenate([p[k] for p in parts], axis=0) for k in range(2, 6)])
     return _linearize(poses, disps, intrinsics, targets, weights, ii, jj)

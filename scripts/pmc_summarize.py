@@ -15,6 +15,8 @@ import sys
 
 src, dst = sys.argv[1], sys.argv[2]
 E = 2048
+# the library the passes measured (bench.py reports a record only for this build)
+LIB_SHA16 = open(os.path.join(src, "lib_sha16.txt")).read().strip()
 
 
 KNAME = {}
@@ -58,7 +60,9 @@ for key, name, algo in (("zr", "conv_zr", 2 * 256 * 320 * 9 * 3072 * E), ("looku
                         ("alt", "corr_alt", ALT * E)):
     fb = kf * min(fetch[key])
     wb = kw * min(write[key])
-    d = {"edges": E, "kernel": KNAME.get(key), "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+    if key not in fetch or key not in write:
+        continue
+    d = {"edges": E, "kernel": KNAME.get(key), "lib_sha16": LIB_SHA16, "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
          "traffic_bytes_per_launch": fb + wb, "raw_fetch": fetch[key], "raw_write": write[key],
          "calibration": res["calibration"],
          "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; units calibrated on a "

@@ -5,7 +5,13 @@ every rank) on a C5-shaped problem (2048 KF / ~16k edges), every
 rank on cuda:0.  Writes <out>.rank<R>.npz: poses, disps, dx and the [lo, hi)
 frames whose depths this rank owns.
 
-usage: python -m torch.distributed.run --nproc-per-node 2 tests/sharded_ba_worker.py <out prefix> <H> <W>
+With a 4th argument "inject", rank 0 alone makes its dataflow solves abort
+(droid_chol_set_fault_inject): first in every GN iteration of one call, then
+in the first iteration of a second call.  The status words are all-reduced
+before each step is applied, so every rank must skip the same steps and raise;
+the npz then also holds each call's poses / disps and whether it raised.
+
+usage: python -m torch.distributed.run --nproc-per-node 2 tests/sharded_ba_worker.py <out prefix> <H> <W> [inject]
 """
 import os
 import sys
@@ -22,6 +28,7 @@ import torch  # noqa: E402
 
 def main():
     out, H, W = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    inject = len(sys.argv) > 4 and sys.argv[4] == "inject"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     dev = torch.device("cuda", 0)
@@ -42,6 +49,26 @@ def main():
     d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     poses, disps = d(prob["poses"]), d(prob["disps"])
     comm = dict(group=None, own=own)
+    if inject:
+        import droid_backends
+        rec = {}
+        for call, mode in (("all", droid_backends.CHOL_INJECT_ALL), ("once", droid_backends.CHOL_INJECT_ONCE)):
+            droid_backends.chol_set_fault_inject(mode if rank == 0 else droid_backends.CHOL_INJECT_OFF)
+            ba_sharded(poses, disps, d(prob["intrinsics"]), d(prob["disps_sens"]), d(prob["targets"][sel]),
+                       d(prob["weights"][sel]), d(eta_l), ii_l, jj_l, t0, t1, 2, 1e-5, 1e-2, False, comm)
+            droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_OFF)
+            try:
+                comm["_last_plan"].check_status()
+                raised = False
+            except RuntimeError as e:
+                raised = "timed out" in str(e)
+            rec[call + "_poses"] = poses.cpu().numpy()
+            rec[call + "_disps"] = disps.cpu().numpy()
+            rec[call + "_raised"] = np.asarray(raised)
+        np.savez("%s.rank%d.npz" % (out, rank), own=np.asarray(own), **rec)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     dx, dz = ba_sharded(poses, disps, d(prob["intrinsics"]), d(prob["disps_sens"]), d(prob["targets"][sel]),
                         d(prob["weights"][sel]), d(eta_l), ii_l, jj_l, t0, t1, 2, 1e-5, 1e-2, False, comm)
     torch.cuda.synchronize()

@@ -30,6 +30,46 @@ def test_library_exports_header():
         assert callable(getattr(droid_backends, name))
 
 
+def test_product_library_takes_no_kernel_choice_from_env(monkeypatch):
+    """the product library is not the A/B build, ships only
+    the default kernels (the dropped variants answer 'unsupported') and reads
+    no DROID_* experiment knob; the A/B library (make ab) exports the same
+    entry points and reports its build."""
+    import ctypes as ct
+    from droid_backends import _lib
+    assert _lib.lib.droid_build_info() == 0
+    assert _lib.lib.droid_alt_set_variant(1) == 2 and _lib.lib.droid_alt_set_variant(3) == 2   # kUnsupported
+    assert _lib.lib.droid_alt_set_variant(2) == 0
+    # an order forced through the ABI, not the environment: DROID_BA_ORDER is ignored
+    monkeypatch.setenv("DROID_BA_ORDER", "rcm")
+    from droid_mi355x import synthetic
+    ii, jj = synthetic.c3_edges(num_kf=64, num_edges=512, rng=np.random.default_rng(5))
+    st, h = _plan(ii, jj, N=64, t0=1, t1=64)
+    assert st == 0
+    kind, nwide, ntasks = ct.c_int(), ct.c_int(), ct.c_int()
+    perm = np.zeros(63, np.int32)
+    assert _lib.lib.droid_ba_plan_order(h, ct.byref(kind), perm.ctypes.data_as(ct.c_void_p), ct.byref(nwide),
+                                        ct.byref(ntasks)) == 0
+    _lib.lib.droid_ba_plan_destroy(h)
+    assert kind.value == 0   # the plan's own choice on this dense-at-tile-level graph: identity
+    prev = _lib.lib.droid_ba_set_order(1)
+    try:
+        st, h = _plan(ii, jj, N=64, t0=1, t1=64)
+        assert st == 0
+        assert _lib.lib.droid_ba_plan_order(h, ct.byref(kind), perm.ctypes.data_as(ct.c_void_p), ct.byref(nwide),
+                                            ct.byref(ntasks)) == 0
+        _lib.lib.droid_ba_plan_destroy(h)
+        assert kind.value == 1
+    finally:
+        _lib.lib.droid_ba_set_order(prev)
+    ab = os.path.join(ROOT, "droid-slam_amd", "lib", "ab", "libdroid_hip.so")
+    if os.path.exists(ab):
+        lab = ct.CDLL(ab)
+        assert lab.droid_build_info() & 1
+        for s in _header_symbols():
+            assert hasattr(lab, s), s
+
+
 def _plan(ii, jj, N=6, H=4, W=6, t0=1, t1=5, eta_rows=None, motion_only=0, own=(0, 2 ** 31 - 1)):
     from droid_backends._lib import lib
     ii = np.ascontiguousarray(ii, dtype=np.int64)

@@ -272,12 +272,12 @@ def test_nested_dissection_order_solves():
     _check_solves(st, _spd_with_blocks(P, pairs, rng), st["perm"], rng)
 
 
-def test_nested_dissection_disconnected_graph_solves(monkeypatch):
+def test_nested_dissection_disconnected_graph_solves(ba_order):
     """Forced nested dissection on a pose graph in three pieces (two lapping
     trajectories and a run of poses without edges): every pose is ordered once
     and the task list still solves the reduced system."""
     from droid_mi355x import synthetic
-    monkeypatch.setenv("DROID_BA_ORDER", "nd")
+    ba_order("nd")
     a_i, a_j = synthetic.c5_edges(num_kf=160, lap=40)
     b_i, b_j = synthetic.c5_edges(num_kf=120, lap=30)
     ii = np.concatenate([a_i, b_i + 200])
@@ -307,8 +307,8 @@ def test_c5_plan_is_tile_sparse():
 
 
 @pytest.mark.parametrize("order", ["rcm", "mindeg", "nd"])
-def test_forced_orders_solve(order, monkeypatch):
-    monkeypatch.setenv("DROID_BA_ORDER", order)
+def test_forced_orders_solve(order, ba_order):
+    ba_order(order)
     ii, jj, N, t0, t1 = _graph("C2")
     st = ba_plan(ii, jj, N, t0, t1)
     assert st["kind"] == {"rcm": 1, "mindeg": 2, "nd": 3}[order]

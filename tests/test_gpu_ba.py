@@ -102,14 +102,14 @@ def test_ba_stereo_c4_full_graph():
 
 
 @pytest.mark.parametrize("order", ["rcm", "mindeg", "nd"])
-def test_ba_forced_pose_orders(order, monkeypatch):
+def test_ba_forced_pose_orders(order, ba_order):
     """Every pose order the plan can choose solves the same step: with a
     forced reverse Cuthill-McKee, minimum degree or nested dissection order
     (the factor's tile structure and Cholesky task graph change) a C3-graph BA
     and a lapping-trajectory BA (where the plan picks nested dissection on its
     own) stay within 1e-4 of the oracle."""
     import droid_backends
-    monkeypatch.setenv("DROID_BA_ORDER", order)
+    ba_order(order)
     droid_backends._PLAN_CACHE.clear()   # plans are cached per edge set, not per order
     try:
         got, ref = run_both(synthetic.ba_problem("C3", H=16, W=24), iterations=2, lm=1e-5, ep=1e-2)

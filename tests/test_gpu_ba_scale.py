@@ -8,8 +8,11 @@ north star's bar):
   §8d) on one device: fill-reducing pose order + tile-sparse dataflow
   Cholesky on the 12282-variable reduced system;
 * the same BA edge-sharded over 2 ranks (gloo, both on cuda:0): per-rank
-  Schur terms, all-reduce of the input tiles, identical solves.
-The C5 tests use 16x24 depth maps: the graph, not the image, is what C5
+  Schur terms, all-reduce of the input tiles, identical solves; and over 4
+  ranks (middle-rank partitions) at the config's 48x64 depth maps;
+* the failure handling: timeouts and a stale sync area, single-device and
+  agreed across ranks.
+Most C5 tests use 16x24 depth maps: the graph, not the image, is what C5
 scales, and the fp64 oracle then finishes in well under a minute."""
 import os
 import socket
@@ -103,15 +106,8 @@ def _free_port():
 @pytest.mark.timeout(300)
 def test_ba_c5_sharded_two_ranks(c5, tmp_path):
     prob, ref = c5
-    env = dict(os.environ, PYTHONUNBUFFERED="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
-        env.pop(k, None)
     out = str(tmp_path / "c5")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                        os.path.join(HERE, "sharded_ba_worker.py"), out, str(C5_HW[0]), str(C5_HW[1])],
-                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=280)
-    assert r.returncode == 0, r.stdout.decode(errors="replace")[-3000:]
+    _torchrun(2, [out, C5_HW[0], C5_HW[1]], 280)
     covered = np.zeros(2048, bool)
     edges = 0
     for rank in range(2):
@@ -125,37 +121,135 @@ def test_ba_c5_sharded_two_ranks(c5, tmp_path):
     assert covered.all() and edges == len(prob["ii"])
 
 
-def test_chol_timeout_is_reported_and_state_untouched(monkeypatch):
+def test_chol_timeout_is_reported_and_state_untouched():
     """The dataflow solve's safety net (bounded spins -> abort, flag bit 1):
     forced here with the test hook, ba() must raise and leave poses/disps as
     they were (the abort used to corrupt them silently)."""
     import droid_backends
     prob = synthetic.ba_problem("C3", H=16, W=24)
     poses, disps = dev(prob["poses"]), dev(prob["disps"])
-    monkeypatch.setenv("DROID_CHOL_FAULT_INJECT", "1")
-    with pytest.raises(RuntimeError, match="timed out"):
-        droid_backends.ba(poses, disps, dev(prob["intrinsics"]), dev(prob["disps_sens"]), dev(prob["targets"]),
-                          dev(prob["weights"]), dev(prob["eta"]), dev(prob["ii"]), dev(prob["jj"]), prob["t0"],
-                          prob["t1"], 1, 1e-4, 0.1, False)
+    droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_ALL)
+    try:
+        with pytest.raises(RuntimeError, match="timed out"):
+            droid_backends.ba(poses, disps, dev(prob["intrinsics"]), dev(prob["disps_sens"]), dev(prob["targets"]),
+                              dev(prob["weights"]), dev(prob["eta"]), dev(prob["ii"]), dev(prob["jj"]), prob["t0"],
+                              prob["t1"], 1, 1e-4, 0.1, False)
+    finally:
+        droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_OFF)
     np.testing.assert_array_equal(host(poses), prob["poses"])
     np.testing.assert_array_equal(host(disps), prob["disps"])
-    monkeypatch.delenv("DROID_CHOL_FAULT_INJECT")
     got = _gpu_ba(prob, 1, 1e-4, 0.1)          # and the next solve on the same plan is clean
     assert np.isfinite(got["dx"]).all()
 
 
-def test_chol_timeout_in_first_gn_iteration_is_still_reported(monkeypatch):
+def test_chol_timeout_in_first_gn_iteration_is_still_reported():
     """the status word used to be cleared by every solve, so a
     timeout in GN iteration 1 of ba(iterations=2) vanished when iteration 2
     succeeded.  The sticky word keeps it: ba() raises."""
     import droid_backends
     prob = synthetic.ba_problem("C3", H=16, W=24, seed=7)
     poses, disps = dev(prob["poses"]), dev(prob["disps"])
-    monkeypatch.setenv("DROID_CHOL_FAULT_INJECT", "once-first-iteration")
-    with pytest.raises(RuntimeError, match="timed out"):
-        droid_backends.ba(poses, disps, dev(prob["intrinsics"]), dev(prob["disps_sens"]), dev(prob["targets"]),
-                          dev(prob["weights"]), dev(prob["eta"]), dev(prob["ii"]), dev(prob["jj"]), prob["t0"],
-                          prob["t1"], 2, 1e-4, 0.1, False)
-    monkeypatch.delenv("DROID_CHOL_FAULT_INJECT")
+    droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_ONCE)
+    try:
+        with pytest.raises(RuntimeError, match="timed out"):
+            droid_backends.ba(poses, disps, dev(prob["intrinsics"]), dev(prob["disps_sens"]), dev(prob["targets"]),
+                              dev(prob["weights"]), dev(prob["eta"]), dev(prob["ii"]), dev(prob["jj"]), prob["t0"],
+                              prob["t1"], 2, 1e-4, 0.1, False)
+    finally:
+        droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_OFF)
     got = _gpu_ba(prob, 2, 1e-4, 0.1)          # the next call on the same plan starts clean
     assert np.isfinite(got["dx"]).all()
+
+
+def test_chol_stale_sync_area_is_detected():
+    """the dataflow kernel checks its entry state.  A solve
+    launched on a sync area that was not zeroed (the previous launch's ticket
+    and version counters) must report status bit 2 and change nothing, not run
+    tasks against stale hand-off counters; the solve after it is clean."""
+    import droid_backends
+    prob = synthetic.ba_problem("C3", H=16, W=24, seed=11)
+    ref1 = _gpu_ba(prob, 1, 1e-4, 0.1)          # a clean solve leaves the counters at their final values
+    poses, disps = dev(prob["poses"]), dev(prob["disps"])
+    droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_STALE)
+    try:
+        with pytest.raises(RuntimeError, match="state corrupt"):
+            droid_backends.ba(poses, disps, dev(prob["intrinsics"]), dev(prob["disps_sens"]), dev(prob["targets"]),
+                              dev(prob["weights"]), dev(prob["eta"]), dev(prob["ii"]), dev(prob["jj"]), prob["t0"],
+                              prob["t1"], 1, 1e-4, 0.1, False)
+    finally:
+        droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_OFF)
+    np.testing.assert_array_equal(host(poses), prob["poses"])
+    np.testing.assert_array_equal(host(disps), prob["disps"])
+    got = _gpu_ba(prob, 1, 1e-4, 0.1)
+    for k in ("dx", "poses", "disps"):
+        np.testing.assert_array_equal(got[k], ref1[k], err_msg=k)   # bitwise: the BA is deterministic
+
+
+def _torchrun(nproc, args, timeout):
+    env = dict(os.environ, PYTHONUNBUFFERED="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(HERE, "sharded_ba_worker.py")] + [str(a) for a in args],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=timeout)
+    assert r.returncode == 0, r.stdout.decode(errors="replace")[-3000:]
+
+
+@pytest.mark.timeout(300)
+def test_ba_sharded_fault_on_one_rank_is_agreed(tmp_path):
+    """the sharded BA all-reduces (MAX) the status words before each
+    step is applied.  Rank 0 alone aborts its solves; both ranks must skip the
+    same steps (poses and disparities bitwise equal across ranks, and unchanged
+    when every step aborted) and both must raise."""
+    prob = synthetic.ba_problem("C5", H=C5_HW[0], W=C5_HW[1])
+    out = str(tmp_path / "inj")
+    _torchrun(2, [out, C5_HW[0], C5_HW[1], "inject"], 280)
+    d = [np.load(out + ".rank%d.npz" % r) for r in range(2)]
+    for r in range(2):
+        assert bool(d[r]["all_raised"]) and bool(d[r]["once_raised"]), "rank %d did not raise" % r
+        # every GN step of the first call was skipped on every rank: nothing moved
+        np.testing.assert_array_equal(d[r]["all_poses"], prob["poses"])
+        np.testing.assert_array_equal(d[r]["all_disps"], prob["disps"])
+    # the second call skipped its first step everywhere and applied the second
+    # (identical all-reduced system -> identical solve on both ranks)
+    np.testing.assert_array_equal(d[0]["once_poses"], d[1]["once_poses"])
+    assert np.abs(d[0]["once_poses"] - prob["poses"]).max() > 0
+
+
+@pytest.mark.timeout(480)
+def test_ba_sharded_four_ranks_full_resolution(tmp_path):
+    """the edge-sharded C5 BA at the config's 48x64 depth
+    maps over 4 ranks (two middle ranks with both neighbours), every rank on
+    cuda:0 over gloo, against the fp64 oracle at 1e-4.  The oracle runs while
+    the ranks do."""
+    prob = synthetic.ba_problem("C5", H=48, W=64)
+    out = str(tmp_path / "c5full")
+    env = dict(os.environ, PYTHONUNBUFFERED="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    proc = subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+                             "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                             os.path.join(HERE, "sharded_ba_worker.py"), out, "48", "64"],
+                            env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    try:
+        ref = oba.ba(**{k: prob[k] for k in KEYS}, iterations=2, lm=1e-5, ep=1e-2, motion_only=False)
+        log, _ = proc.communicate(timeout=300)
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+            proc.communicate()
+    assert proc.returncode == 0, log.decode(errors="replace")[-3000:]
+    covered = np.zeros(2048, bool)
+    edges = 0
+    for rank in range(4):
+        d = np.load(out + ".rank%d.npz" % rank)
+        lo, hi = (int(x) for x in d["own"])
+        assert (0 < lo and hi < 2048) == (rank in (1, 2))
+        edges += int(d["edges"])
+        np.testing.assert_allclose(d["dx"], ref["dx"], atol=TOL, rtol=0)
+        np.testing.assert_allclose(d["poses"], ref["poses"], atol=TOL, rtol=0)
+        np.testing.assert_allclose(d["disps"][lo:hi], ref["disps"][lo:hi], atol=TOL, rtol=0)
+        covered[lo:hi] = True
+    assert covered.all() and edges == len(prob["ii"])
+    assert np.abs(ref["dx"]).max() > 1e-4

@@ -24,12 +24,12 @@ def _ref(xs, w, bias=None, bb=None):
 
 @pytest.mark.parametrize("B,H,splits,cout,act", [(3, 8, [128], 128, 1), (2, 4, [128, 96, 64], 256, 0),
                                                   (1, 48, [128], 384, 0), (2, 12, [64, 8], 128, 1)])
-def test_wino_act_matches_fp32_conv(B, H, splits, cout, act):
+def test_wino_act_matches_fp32_conv(B, H, splits, cout, act, ab_backends):
     """EPI_ACT (bias, optional ReLU) at W = 64: partial channel chunks (96, 8),
     several sources, one-tile images (H = 4), several output tiles; the error
     bound is the fp16 class (an fp16 ulp of each transformed operand + the fp16
     output rounding) and within 3x of the direct conv's own error."""
-    import droid_backends
+    droid_backends = ab_backends   # the Winograd tile ships in the A/B build only
     from droid_mi355x.fused import pack_conv, pack_conv_wino
     W = 64
     g = torch.Generator(device=DEV).manual_seed(31 + H)
@@ -56,10 +56,10 @@ def test_wino_act_matches_fp32_conv(B, H, splits, cout, act):
     assert abs((out.float() - ref).mean().item()) < 1e-4
 
 
-def test_wino_image_edges_and_zero_rows():
+def test_wino_image_edges_and_zero_rows(ab_backends):
     """x = -1 / x = 64 neighbours and the rows above / below each image are zero:
     a delta input at every edge position reproduces the clipped kernel exactly."""
-    import droid_backends
+    droid_backends = ab_backends   # the Winograd tile ships in the A/B build only
     from droid_mi355x.fused import pack_conv_wino
     B, H, W, C = 2, 8, 64, 64
     x = torch.zeros((B, H, W, C), dtype=torch.float16, device=DEV)
@@ -78,11 +78,11 @@ def test_wino_image_edges_and_zero_rows():
 
 
 @pytest.mark.parametrize("B,H", [(3, 8), (2, 48)])
-def test_wino_gru_pre_epilogues(B, H):
+def test_wino_gru_pre_epilogues(B, H, ab_backends):
     """z|r and q gates with the per-source-frame term (EPI_GRU_ZR / EPI_GRU_Q on
     the Winograd tile) vs torch fp32 over the full 448-channel input, at the
     bounds of the direct band kernel's own test (test_gpu_fused.py::test_conv_gru_pre_epilogues)."""
-    import droid_backends
+    droid_backends = ab_backends   # the Winograd tile ships in the A/B build only
     from droid_backends import EPI_GRU_Q, EPI_GRU_ZR
     from droid_mi355x.fused import pack_conv_wino
     W = 64
@@ -118,9 +118,9 @@ def test_wino_gru_pre_epilogues(B, H):
     np.testing.assert_allclose(host(hn.float()), host(ref), atol=4e-3)
 
 
-def test_wino_rejects_unsupported_shape():
+def test_wino_rejects_unsupported_shape(ab_backends):
     """W != 64 -> DROID_UNSUPPORTED raised (the caller runs the direct conv)."""
-    import droid_backends
+    droid_backends = ab_backends   # the Winograd tile ships in the A/B build only
     from droid_mi355x.fused import pack_conv_wino
     x = torch.zeros((1, 8, 32, 128), dtype=torch.float16, device=DEV)
     out = torch.empty_like(x)

@@ -366,13 +366,14 @@ def test_corr_alt_ce0_matches_volume_path(noise, H, W, E):
 
 @pytest.mark.parametrize("noise,H,W,E,far", [(1.5, 16, 24, 6, 0.0), (40.0, 16, 24, 6, 0.0), (1.5, 48, 64, 300, 0.0),
                                              (8.0, 48, 64, 300, 0.0), (4.0, 48, 64, 200, 0.1), (0.3, 32, 64, 64, 0.0)])
-def test_corr_alt2_bitwise_equals_alt1(noise, H, W, E, far):
+def test_corr_alt2_bitwise_equals_alt1(noise, H, W, E, far, ab_backends):
     """corr_alt2_kernel (two 4-wave workgroups per CU, C in place, merged
     level-3/2/1 stage, group fallbacks) computes every value with the same
     operations in the same order as corr_alt_ce0_kernel: outputs bitwise equal.
     far: fraction of pixels thrown 30-200 px off the map (windows partly or
     wholly outside, boxes over the region -> half / quadrant / pixel groups)."""
-    import droid_backends
+    import droid_backends as product
+    droid_backends = ab_backends   # corr_alt_ce0_kernel (variant 1) ships in the A/B build only
     from droid_mi355x.corr import AltCorrBlock
     rng = np.random.default_rng(41)
     NF = 8
@@ -399,21 +400,23 @@ def test_corr_alt2_bitwise_equals_alt1(noise, H, W, E, far):
         out = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
     finally:
         droid_backends.alt_set_variant(2)
+    prod = product.corr_alt_ce0(pyr, f1, f2, c, w224, b)   # the product library's corr_alt2_kernel
     torch.cuda.synchronize()
     diff = (out.float() - ref.float()).abs()
     assert torch.equal(out, ref), (float(diff.max()), int((diff > 0).sum()))
+    assert torch.equal(prod, out)
 
 
 @pytest.mark.parametrize("noise,H,W,E,far", [(1.5, 16, 24, 6, 0.0), (40.0, 16, 24, 6, 0.0), (1.5, 48, 64, 300, 0.0),
                                              (4.0, 48, 64, 200, 0.1), (0.3, 32, 64, 64, 0.0)])
-def test_corr_alt2_v3_matches_v2(noise, H, W, E, far):
+def test_corr_alt2_v3_matches_v2(noise, H, W, E, far, ab_backends):
     """corr_alt2_kernel<V3> (box blocks split over the waves, transposed C
     MFMA, lookup tile in the k = 8 iy + ix order with the encoder weights
     permuted to match): the C values and the bilinear windows are the V2 values;
     only corr_encoder[0]'s fp32 summation order differs (a permuted K), so the
     fp16 outputs agree to a few ulps and are mostly identical; every fallback
     (incoherent, off-map coordinates) included."""
-    import droid_backends
+    droid_backends = ab_backends   # corr_alt2_kernel<V3> ships in the A/B build only
     from droid_mi355x.corr import AltCorrBlock
     rng = np.random.default_rng(43)
     NF = 8
@@ -450,7 +453,7 @@ def test_corr_alt2_v3_matches_v2(noise, H, W, E, far):
     assert float((diff == 0).float().mean()) > 0.9
 
 
-def test_corr_alt_ordered_walk_is_bitwise_the_same():
+def test_corr_alt_ordered_walk_is_bitwise_the_same(ab_backends):
     """droid_corr_alt_ce0_ordered: walking the tiles in an edge permutation
     (edges grouped by target frame, FactorGraph._alt_order) changes only which
     workgroup computes a tile - the outputs are the same bytes in the same
@@ -474,11 +477,12 @@ def test_corr_alt_ordered_walk_is_bitwise_the_same():
     f1, f2 = torch.as_tensor(ii, device=DEV), torch.as_tensor(jj, device=DEV)
     order = torch.as_tensor(np.argsort(jj, kind="stable").astype(np.int32), device=DEV)
     try:
-        for v in (2, 3):
-            droid_backends.alt_set_variant(v)
-            ref = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
-            out = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b, order=order)
+        for bk, v in ((droid_backends, 2), (ab_backends, 3)):   # V3: the A/B build only
+            bk.alt_set_variant(v)
+            ref = bk.corr_alt_ce0(pyr, f1, f2, c, w224, b)
+            out = bk.corr_alt_ce0(pyr, f1, f2, c, w224, b, order=order)
             torch.cuda.synchronize()
+            bk.alt_set_variant(2)
             assert torch.equal(out, ref), v
         # the XCD chunking of the walk (droid_alt_set_chunk): interleaved, one
         # edge, a chunk that does not divide the 40 edges, more than all of them
@@ -883,7 +887,10 @@ def test_reference_layout_module_under_inference_mode():
         ni, ip, co, fl = net.clone(), inp.clone(), corr.clone(), flow.clone()
         assert ni.is_inference()
         b1 = d(ni, ip, co, fl, ii, jj)
+        checked = d._frames
         b2 = d(b1[0], ip, co, fl, ii, jj)
+        # the per-frame content check ran once for this (inp, ii) pair
+        assert d._frames is checked
         # the per-frame gate term on an inference inp_frames tensor
         f = FusedUpdateModule(m)
         nhwc = lambda t: t[0].permute(0, 2, 3, 1).contiguous()

@@ -389,6 +389,7 @@ def test_update_graph_replay_matches_eager():
         video = _c2_video(48, 64, seed=57)
         g = FactorGraph(video, FusedUpdateModule(m), device="cuda")
         g.graphs = graphs
+        g.graph_strict = True
         with torch.no_grad():
             g.add_factors(ii, jj)
             for _ in range(4):
