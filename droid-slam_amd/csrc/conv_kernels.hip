@@ -39,6 +39,7 @@
 #include "common.hpp"
 #include "lds_dma.hpp"
 #include <algorithm>
+#include <type_traits>
 
 #ifndef DROID_CONV_PROFILE
 #define DROID_CONV_PROFILE 0
@@ -1068,8 +1069,10 @@ __device__ __forceinline__ void band_epilogue_core(const ConvArgs& a, _Float16* 
   const long mrow = m0 + r0;
   const bool rhalf = epi == EPI_GRU_ZR && c >= a.gru_ch;
   // pass (2) in batches of RB rounds (the 4-wave tile has 32 rounds per thread:
-  // all of them in flight would need 3 x 128 VGPRs)
-  constexpr int RB = RND > (NT >= 512 ? 16 : 8) ? (NT >= 512 ? 16 : 8) : RND;
+  // all of them in flight would need 3 x 128 VGPRs; with its accumulators in
+  // the AGPR file its VGPRs are free here, so it takes batches of 16)
+  constexpr int RBMAX = (NT >= 512 || TN == 256) ? 16 : 8;
+  constexpr int RB = RND > RBMAX ? RBMAX : RND;
   static_assert(RND % RB == 0, "band epilogue: whole batches");
   half8 hpre[kPreH ? RB : 1], zpre[EB == EPI_GRU_Q ? RB : 1], ppre[kPre ? RB : 1];
   // the per-frame term's pieces (pixel m of image b -> pixel of its source
@@ -1298,6 +1301,21 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
   }
 }
 
+// acc += a x b (v_mfma_f32_16x16x32_f16) with the accumulator pinned in the
+// AGPR file ("+a"): the 4-wave tile's 256 accumulators per lane fill the AGPRs
+// exactly, and with the builtin the register allocator moved some of them to
+// VGPRs and back (v_accvgpr_read / write in every stage and ~512 at each chunk's
+// back edge).  Hazards the compiler no longer pads (cdna_hip_programming.md
+// §5.7 item 2): operands come from ds_read (LDS loads, counted by hipcc's
+// lgkmcnt waits, no VALU wait states); consecutive MFMAs on the same
+// accumulator take it whole as C (0 states); the accumulators' zero fill is
+// separated from the first MFMA by the stage prologue; and mfma_acc_drain()
+// pads the 12 states an 8-pass MFMA's D needs before any other reader.
+__device__ __forceinline__ void mfma_acc(floatx4& acc, const half8& a, const half8& b) {
+  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_acc_drain() { asm volatile("s_nop 7\n\ts_nop 4" ::: "memory"); }
+
 // one MFMA then one LDS read, R times (sched_group_barrier sequence)
 template <int R>
 struct MfmaReadPairs {
@@ -1448,6 +1466,97 @@ conv_band_kernel(ConvArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tid == 0) prof[2] = (long long)__builtin_amdgcn_s_memtime();
   }
+  if constexpr (NW == 4) {
+    // One wave per SIMD: nothing else on the SIMD hides this wave's LDS
+    // latency, so each stage is software pipelined in program order (every
+    // group fenced by sched_barrier), the tap t a compile-time constant (a
+    // generic lambda per tap: the nine stages of a chunk exceed the unroller's
+    // budget).  The stage's first four K-half-0 A fragments were read before
+    // its barrier (same band, t > 0), so after the barrier the B fragments are
+    // the only reads outstanding, and half 0 runs column by column over A_0..A_3
+    // (B_j, then B_j+1, ...: the first four MFMAs need B_0 alone while the other
+    // B reads - the four waves' reads land in one burst after the barrier -
+    // still arrive), then over A_4..A_7 (read behind B); half 1's fragments are
+    // read under half 0's MFMAs, the next stage's first four A fragments under
+    // half 1's.  Every accumulator still sees the same products in the same
+    // order: bitwise the sums of the 8-wave tile.
+    half8 apf[4];
+    for (int ch = 0; ch < nch; ++ch) {
+      const char* Hb = Hl + (ch & 1) * hbytes;
+      auto stage = [&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        constexpr int ty = t / 3 - 1, tx = t % 3 - 1;
+        const int st = ch * 9 + t;
+        if (!(DROID_CONV_ABLATE & 4) || st == 0) wait_vmcnt((t == 1 && ch + 1 < nch) ? nhi : 0);
+        if (!(DROID_CONV_ABLATE & 1)) __builtin_amdgcn_s_barrier();
+        const char* Bb = Bl + (st & 1) * TN * 128;
+        auto ald = [&](int hk, int i, int tyy, int txx) {
+          return *reinterpret_cast<const half8*>(Hb + abase[i % NPAR][txx + 1][hk] + tyy * rowb + (i / NPAR) * 8192);
+        };
+        auto bld = [&](int hk, int j) { return *reinterpret_cast<const half8*>(Bb + bbase[hk] + j * 2048); };
+        half8 a0[FM], a1[FM], b0[FN], b1[FN];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b0[j] = bld(0, j);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a0[i] = t == 0 ? ald(0, i, ty, tx) : apf[i];
+#pragma unroll
+        for (int i = 4; i < FM; ++i) a0[i] = ald(0, i, ty, tx);
+        __builtin_amdgcn_sched_barrier(0);
+        // half 0: columns over A_0..A_3, then over A_4..A_7; half 1's 16
+        // fragments read one per 4 MFMAs; the next stage's DMA issued once the
+        // first MFMAs are under way
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+#pragma unroll
+            for (int ii = 0; ii < 4; ++ii) {
+              const int i = 4 * ih + ii;
+              mfma_acc(acc[i][j], a0[i], b0[j]);
+              const int m = (ih * FN + j) * 4 + ii;
+              if (m % 4 == 3) {
+                const int r = m / 4;   // 0 .. 15
+                if (r < FN) b1[r] = bld(1, r);
+                else a1[r - FN] = ald(1, r - FN, ty, tx);
+              }
+              __builtin_amdgcn_sched_barrier(0);
+              if (m == 1 && (!(DROID_CONV_ABLATE & 2) || st == 0)) {
+                if (st + 1 < nst) issue_b(st + 1);
+                if (t == 0 && ch + 1 < nch) issue_halo(ch + 1);
+                __builtin_amdgcn_sched_barrier(0);
+              }
+            }
+          }
+        }
+        // half 1; the next stage's first four half-0 A fragments (same band,
+        // t < 8) read one per 16 MFMAs
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            mfma_acc(acc[i][j], a1[i], b1[j]);
+            if constexpr (t < 8) {
+              if (j == 3 && i % 2 == 1) {
+                constexpr int tn = t + 1;
+                apf[i / 2] = ald(0, i / 2, tn / 3 - 1, tn % 3 - 1);
+              }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      };
+      stage(std::integral_constant<int, 0>{});
+      stage(std::integral_constant<int, 1>{});
+      stage(std::integral_constant<int, 2>{});
+      stage(std::integral_constant<int, 3>{});
+      stage(std::integral_constant<int, 4>{});
+      stage(std::integral_constant<int, 5>{});
+      stage(std::integral_constant<int, 6>{});
+      stage(std::integral_constant<int, 7>{});
+      stage(std::integral_constant<int, 8>{});
+    }
+  } else {
   int st = 0;
   for (int ch = 0; ch < nch; ++ch) {
     const char* Hb = Hl + (ch & 1) * hbytes;
@@ -1518,6 +1627,8 @@ conv_band_kernel(ConvArgs a) {
       }
     }
   }
+  }   // NW == 4
+  if constexpr (NW == 4) mfma_acc_drain();
   if (prof && tid == 0) prof[3] = (long long)__builtin_amdgcn_s_memtime();
   if constexpr (DWHEAD) {
     static_assert(TMX == 256 && TN == 256 && NW == 8, "dw/head fusion runs on the 8-wave 256x256 tile");
@@ -1566,13 +1677,16 @@ static int launch_band_kernel(const ConvArgs& a, long nwg, int lds, hipStream_t 
   return kOk;
 }
 
+static int& band2_mode();
 #if DROID_AB
-// DROID_CONV_NW4=1: the z|r gates (256x256, per-frame term) on the 4-wave tile
-// (A/B; measured 8.41 ms vs 7.4 for the 8-wave tile: one wave per SIMD leaves
-// the compiler-scheduled loop's LDS waits unhidden - it needs a hand schedule)
+// A/B build: the z|r gates (256x256, per-frame term) on the 4-wave tile, tile
+// policy 2 (droid_conv_set_tile) or DROID_CONV_NW4=1.  Measured (round 5,
+// profiles/r05/): 7.85 vs 7.45 ms for the 8-wave tile at C3 - a single wave
+// per SIMD pays every ds_read_b128's issue (~18 clk, scripts/probe/
+// mfma_1wave.hip) on its own MFMA stream: 2818 vs 2564 clk per stage.
 static bool band_nw4() {
-  static const bool on = ab_knob("DROID_CONV_NW4", 0) == 1;
-  return on;
+  static const bool env = ab_knob("DROID_CONV_NW4", 0) == 1;
+  return env || band2_mode() == 2;
 }
 
 template <int TMX, int TN>
@@ -1586,11 +1700,16 @@ static int launch_band_nw4(const ConvArgs& a0, hipStream_t stream) {
   const int lds = main_b > epi_b ? main_b : epi_b;
   if (lds > kLdsMax) return fail(kUnsupported, "conv band: LDS");
   const long nwg = a.m_tiles * a.n_tiles;
-  // (the interleaved stage body spills on this tile: 61 VGPRs, AGPRs used as spill space in the loop)
   const int st = launch_band_kernel<TMX, TN, false, false, EPI_GRU_ZRP, 4>(a, nwg, lds, stream);
   if (st != kOk) return st;
   DROID_LAUNCH_CHECK();
   return kOk;
+}
+#else
+static bool band_nw4() { return false; }
+template <int TMX, int TN>
+static int launch_band_nw4(const ConvArgs&, hipStream_t) {
+  return fail(kUnsupported, "conv band: the 4-wave z|r tile ships in the A/B build only (make ab)");
 }
 #endif
 
@@ -1850,7 +1969,7 @@ static int& band2_mode() {
 }
 static bool band2_for(int epi, long px) {
   const int mode = band2_mode();
-  return mode == 1 || (mode < 0 && (epi == EPI_ACT || epi == EPI_GRU_Q || px / 256 <= 8L * device_cu_count()));
+  return mode == 1 || ((mode < 0 || mode == 2) && (epi == EPI_ACT || epi == EPI_GRU_Q || px / 256 <= 8L * device_cu_count()));
 }
 // a band-eligible 3x3 conv of this shape runs on the two-workgroup tile
 static bool band2_shape(int epi, int B, int H, int W, int Cout, int gru_ch) {
@@ -2338,11 +2457,9 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
     return launch_band2_kernel<EPI_ACT>(a, stream);
   }
   if (pre) {  // the per-source term exists on the band tiles only
-#if DROID_AB
     if (band_ok && epi == EPI_GRU_ZR && Cout == 256 && 256 % W == 0 && (H * W) % 256 == 0 && band_nw4() &&
         band_fits<256, 256, 4>(W, &ns_, &nh_))
       return launch_band_nw4<256, 256>(a, stream);
-#endif
     if (band_ok && epi == EPI_GRU_ZR && Cout == 256 && 256 % W == 0 && (H * W) % 256 == 0 &&
         band_fits<256, 256>(W, &ns_, &nh_))
       return launch_band<256, 256>(a, stream);
@@ -2373,10 +2490,11 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
 // Tile policy of the W == 64 3x3 convs: -1 = default (plain convs and small
 // gate-conv grids on the two-workgroups-per-CU tile, C3-sized gate convs on the
 // 8-wave band tiles), 0 = 8-wave band tiles only, 1 = the two-workgroup tile
-// wherever it applies.  Returns the previous policy.  Process-wide, not
-// thread-safe by design (tests and A/B runs).
+// wherever it applies, 2 (A/B build only) = the default with the factored z|r
+// gates of the 8-wave-tile grids on the 4-wave 256x256 tile.  Returns the previous policy.
+// Process-wide, not thread-safe by design (tests and A/B runs).
 int droid_conv_set_tile(int mode) {
-  if (mode < -1 || mode > 1) return -2;
+  if (mode < -1 || mode > (DROID_AB ? 2 : 1)) return -2;
   const int prev = band2_mode();
   band2_mode() = mode;
   return prev;
@@ -2393,9 +2511,7 @@ int droid_conv_gate_tile(int epi, int B, int H, int W) {
   const int Cout = epi == EPI_GRU_ZR ? 256 : 128;
   if (band2_shape(epi, B, H, W, Cout, 128)) return 1;
   int ns_, nh_;
-#if DROID_AB
   if (epi == EPI_GRU_ZR && band_nw4() && (H * W) % 256 == 0 && band_fits<256, 256, 4>(W, &ns_, &nh_)) return 2;
-#endif
   if (epi == EPI_GRU_ZR) return ((H * W) % 256 == 0 && band_fits<256, 256>(W, &ns_, &nh_)) ? 0 : -1;
   return ((H * W) % 384 == 0 && band_fits<384, 128>(W, &ns_, &nh_)) ? 0 : -1;
 }

@@ -55,6 +55,8 @@ elif which in ("zrp", "qp"):   # 8 edges per source frame, as in the C3 graph
                                                   0 if which == "zrp" else 256, h=net, **kw)
 else:
     run = lambda: droid_backends.conv_nhwc_f16(srcs, wp, cout, 3, bias=bias, act=1, out=out)
+if os.environ.get("TL_TILE"):   # tile policy (droid_conv_set_tile): 0 8-wave, 2 the 4-wave z|r tile
+    droid_backends.conv_set_tile(int(os.environ["TL_TILE"]))
 for _ in range(3):
     run()
 torch.cuda.synchronize()
