@@ -1218,7 +1218,8 @@ __device__ __forceinline__ void band_epilogue_core(const ConvArgs& a, _Float16* 
 //       the caller.
 template <int FM, int FN, int WM = 4, bool CONTIG = false>
 __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
-                                                int wm, int wn, int lane, int tid, float bcol) {
+                                                int wm, int wn, int lane, int tid, float bcol,
+                                                long long* prof = nullptr) {
   constexpr int TMX = 256, TS = 264, YS = 37, NT = 512;
   const int W = a.W, H = a.H, HW = H * W;
   const int R = TMX / W;
@@ -1226,9 +1227,26 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
   const int y0 = (int)((m0 % HW) / W);
   const int fr = lane & 15, fq = lane >> 4;
   _Float16* T = smem;             // [256][TS]
-  _Float16* Bh = smem + TMX * TS; // [48][TS]
-  float* const bl = reinterpret_cast<float*>(smem + TMX * TS + 48 * TS);  // [256] column biases
+  // head weights [48][256] fp16, unpadded 512-B rows with the 16-B piece p of
+  // row r stored at slot p ^ (r & 15) (the 16 rows of a B fragment read one
+  // piece each: 16 distinct 16-B slots of one 256-B span, conflict-free)
+  _Float16* Bh = smem + TMX * TS;
+  float* const bl = reinterpret_cast<float*>(smem + TMX * TS + 48 * 256);  // [256] column biases
   __syncthreads();  // main-loop LDS reads are done
+  {
+    // the head weights (24 KB) by LDS-DMA now, so they land during pass 1 and
+    // take no VGPRs (loaded after pass 1 they cost ~4k of the epilogue's 16k
+    // clk, profiles/r05/r05k_*): instruction q of wave w fills rows
+    // 2 (w + 8 q) .. + 1, lane l the slot l & 31 of row 2 (w + 8 q) + (l >> 5)
+    static_assert(48 * 32 == 3 * NT, "dwhead: three 16-B weight pieces per thread");
+    const rsrc_t rs = make_rsrc(a.hw, 48 * 256 * 2);
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int ins = wv + 8 * q, row = 2 * ins + (l >> 5), piece = (l & 31) ^ (row & 15);
+      dma16(rs, lds_addr(Bh) + ins * 1024, (unsigned)((row * 256 + piece * 8) * 2));
+    }
+  }
   if (tid < 256) bl[tid] = bcol;
   __syncthreads();
   // lane (fr, fq) of fragment (i, j): pixels frag_row(i) + 4 fq .. + 3 of channel 16 j + fr
@@ -1242,11 +1260,9 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
                         pack_f16x2(fmaxf(acc[i][j][0] + bv, 0.f), fmaxf(acc[i][j][1] + bv, 0.f)),
                         pack_f16x2(fmaxf(acc[i][j][2] + bv, 0.f), fmaxf(acc[i][j][3] + bv, 0.f)));
   }
-  for (int idx = tid; idx < 48 * 32; idx += NT) {
-    const int r = idx >> 5, p = idx & 31;
-    *reinterpret_cast<uint4*>(&Bh[r * TS + p * 8]) = *reinterpret_cast<const uint4*>(a.hw + r * 256 + p * 8);
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's head-weight DMAs landed
   __syncthreads();
+  if (prof && tid == 0) prof[6] = (long long)__builtin_amdgcn_s_memtime();  // pass 1 + head weights in LDS
   // (2) wave w: pixel fragments 2w, 2w+1; all 3 tap-channel fragments; K = 256
   const int wave = tid >> 6;
   floatx4 y[2][3];
@@ -1261,12 +1277,16 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
     for (int f = 0; f < 2; ++f)
       af[f] = *reinterpret_cast<const half8*>(&T[((2 * wave + f) * 16 + fr) * TS + s * 32 + fq * 8]);
 #pragma unroll
-    for (int n = 0; n < 3; ++n) bf[n] = *reinterpret_cast<const half8*>(&Bh[(n * 16 + fr) * TS + s * 32 + fq * 8]);
+    for (int n = 0; n < 3; ++n) {
+      const int row = n * 16 + fr;
+      bf[n] = *reinterpret_cast<const half8*>(&Bh[row * 256 + (((4 * s + fq) ^ (row & 15)) << 3)]);
+    }
 #pragma unroll
     for (int f = 0; f < 2; ++f)
 #pragma unroll
       for (int n = 0; n < 3; ++n) y[f][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[f], bf[n], y[f][n], 0, 0, 0);
   }
+  if (prof && tid == 0) prof[7] = (long long)__builtin_amdgcn_s_memtime();  // wave 0's head GEMM issued
   __syncthreads();  // T and Bh reads done: Y overwrites them
   float* Y = reinterpret_cast<float*>(smem);  // [256][YS]
 #pragma unroll
@@ -1279,6 +1299,7 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
         if (col < 36) Y[((2 * wave + f) * 16 + fq * 4 + k) * YS + col] = y[f][n][k];
       }
   __syncthreads();
+  if (prof && tid == 0) prof[8] = (long long)__builtin_amdgcn_s_memtime();  // Y in LDS
   // (3) output rows y0-1 .. y0+R
   for (int idx = tid; idx < (R + 2) * W * 4; idx += NT) {
     const int c = idx & 3, px = idx >> 2;
@@ -1632,7 +1653,7 @@ conv_band_kernel(ConvArgs a) {
   if (prof && tid == 0) prof[3] = (long long)__builtin_amdgcn_s_memtime();
   if constexpr (DWHEAD) {
     static_assert(TMX == 256 && TN == 256 && NW == 8, "dw/head fusion runs on the 8-wave 256x256 tile");
-    dwhead_epilogue<FM, FN>(a, acc, smem, m0, wm, wn, lane, tid, bcol);
+    dwhead_epilogue<FM, FN>(a, acc, smem, m0, wm, wn, lane, tid, bcol, prof);
   } else {
     band_epilogue<TMX, TN, FM, FN, BP::WM, false, BP::NT, EPI>(a, acc, smem, m0, n0, wm, wn, lane, tid, bcol, prof);
   }
@@ -1721,7 +1742,7 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
   a.m_tiles = (long)a.B * a.H * a.W / TMX;
   const int main_b = 2 * TN * 128 + 2 * a.nhi * 8 * 1024;
   // EPI_DWHEAD keeps the head weights [48][264] beside the hidden-map tile
-  const int epi_b = TMX * (TN + 8) * 2 + TN * 4 + (DWHEAD ? 48 * 264 * 2 : 0);
+  const int epi_b = TMX * (TN + 8) * 2 + TN * 4 + (DWHEAD ? 48 * 256 * 2 : 0);
   const int lds = main_b > epi_b ? main_b : epi_b;
   if (lds > kLdsMax) return fail(kUnsupported, "conv band: LDS");
   const long nwg = a.m_tiles * a.n_tiles;

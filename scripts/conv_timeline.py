@@ -92,7 +92,12 @@ for name, v in (("prologue", pro), ("main loop", loop), ("epilogue issue", epi),
 stages = (cin // 64 if cin % 64 == 0 else cin // 64 + 1) * 9
 tn = 256 if cout == 256 else 128
 floor = 64 * (tile // 64) * (tn // 32)   # 2 waves/SIMD x 2*FM*FN MFMAs x 16 clk
-if (p[:, 6] > 0).all():   # band_epilogue sub-phases (wave 0) and the last wave's drain
+if which == "dwh" and (p[:, 6] > 0).all():   # dwhead_epilogue sub-phases
+    for name, v in (("  pass 1 + head weights", p[:, 6] - p[:, 3]), ("  head GEMM (wave 0)", p[:, 7] - p[:, 6]),
+                    ("  GEMM barrier + Y stores", p[:, 8] - p[:, 7]), ("  tap sums + atomics", p[:, 4] - p[:, 8]),
+                    ("last wave drained after wave 0", p[:, 9] - p[:, 5])):
+        print("  %-30s median %8.0f clk  p90 %8.0f" % (name, np.median(v), np.percentile(v, 90)))
+elif (p[:, 6] > 0).all():   # band_epilogue sub-phases (wave 0) and the last wave's drain
     for name, v in (("  pass 1 (acc -> LDS)", p[:, 6] - p[:, 3]), ("  pass-2 load issue", p[:, 7] - p[:, 6]),
                     ("  staging barrier", p[:, 8] - p[:, 7]), ("  pass 2 + stores", p[:, 4] - p[:, 8]),
                     ("last wave drained after wave 0", p[:, 9] - p[:, 5])):
