@@ -290,6 +290,15 @@ __device__ __forceinline__ void b2_box_dma(const AltArgs& a, int l, int f2, int 
 // the box.  Since every wave reads every block, the C values (packed fp16, 2
 // VGPRs per block) are written only after a barrier.
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+// Round 5, TR (the product layout): the MFMA runs transposed (query pixels as
+// rows - the same products and fp16 rounding, so C is bitwise the same), a lane
+// holds 4 consecutive pixels of one tap and stores them as ONE 8-B word per block
+// (a ds_write_b16 costs the LDS transfer of a ds_write_b32: four of them per
+// block were the C phase's write cost), and C(p, t) sits at byte
+// (2 p + 8 t) & 127 of tap row t: the 16 taps of a block, one per lane of a
+// 16-lane store group, land on 16 different 8-B slots (unrotated, all 16 on one
+// bank pair).  The bilinear reads apply the same rotation (b2_caddr).
+template <bool TR>
 __device__ __forceinline__ void b2_corr(char* lds, int T, int qmask, const half8 (&af)[4], int wave_u, int fr,
                                         int fq) {
   constexpr int NB = kB2Rows / 16;
@@ -306,7 +315,9 @@ __device__ __forceinline__ void b2_corr(char* lds, int T, int qmask, const half8
           bf[ks] = *reinterpret_cast<const half8*>(lds + (b * 16 + fr) * 256 + (((ks * 4 + fq) ^ fr) << 4));
         floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[ks], af[ks], c, 0, 0, 0);
+        for (int ks = 0; ks < 4; ++ks)
+          c = TR ? __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks], bf[ks], c, 0, 0, 0)
+                 : __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[ks], af[ks], c, 0, 0, 0);
         cv[b][0] = half2_t{(_Float16)c[0], (_Float16)c[1]};
         cv[b][1] = half2_t{(_Float16)c[2], (_Float16)c[3]};
       }
@@ -318,14 +329,37 @@ __device__ __forceinline__ void b2_corr(char* lds, int T, int qmask, const half8
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       if (b < nb) {
-        // lane (fr, fq): C[tap b*16 + 4 fq + k][pixel q*16 + fr]
-        char* base = lds + (b * 16 + 4 * fq) * 256 + (q * 16 + fr) * 2;
-        *reinterpret_cast<_Float16*>(base) = cv[b][0][0];
-        *reinterpret_cast<_Float16*>(base + 256) = cv[b][0][1];
-        *reinterpret_cast<_Float16*>(base + 512) = cv[b][1][0];
-        *reinterpret_cast<_Float16*>(base + 768) = cv[b][1][1];
+        if (TR) {
+          // lane (fr, fq): C[pixel q*16 + 4 fq + k][tap b*16 + fr], k < 4
+          typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+          const u32x2_t v = {__builtin_bit_cast(unsigned, cv[b][0]), __builtin_bit_cast(unsigned, cv[b][1])};
+          *reinterpret_cast<u32x2_t*>(lds + (b * 16 + fr) * 256 + ((32 * q + 8 * fq + 8 * fr) & 127)) = v;
+        } else {
+          // lane (fr, fq): C[tap b*16 + 4 fq + k][pixel q*16 + fr]
+          char* base = lds + (b * 16 + 4 * fq) * 256 + (q * 16 + fr) * 2;
+          *reinterpret_cast<_Float16*>(base) = cv[b][0][0];
+          *reinterpret_cast<_Float16*>(base + 256) = cv[b][0][1];
+          *reinterpret_cast<_Float16*>(base + 512) = cv[b][1][0];
+          *reinterpret_cast<_Float16*>(base + 768) = cv[b][1][1];
+        }
       }
     }
+  }
+}
+
+// The 8 window-row taps tr + i (i < 8) of pixel p as 4 packed pairs: C(p, t) at
+// byte 256 t + 2 p (unrotated) or 256 t + ((2 p + 8 t) & 127) (TR); a row
+// outside the map (ok false) reads past the allocation, i.e. zeros.
+template <bool TR>
+__device__ __forceinline__ void b2_crow(const char* lds, int tr, bool ok, int p, unsigned (&pe)[4]) {
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  const unsigned rb = ok ? (unsigned)(tr * 256) : kB2Zero;
+  const unsigned u = (unsigned)(2 * p + 8 * tr);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const unsigned a0 = TR ? rb + (unsigned)(2 * q) * 256u + ((u + 16u * q) & 127u) : rb + 2 * p + (2 * q) * 256;
+    const unsigned a1 = TR ? rb + (unsigned)(2 * q + 1) * 256u + ((u + 16u * q + 8u) & 127u) : rb + 2 * p + (2 * q + 1) * 256;
+    pe[q] = __builtin_bit_cast(unsigned, h2_t{b2_ldh(lds, a0), b2_ldh(lds, a1)});
   }
 }
 
@@ -376,6 +410,7 @@ __device__ __forceinline__ void b2_corr3(char* lds, int T, int qmask, const half
 // volume-lookup at::Half arithmetic in corr_alt_ce0_kernel's order.  Both
 // rows' 32 taps are read before any arithmetic (one LDS round trip; wave 3's
 // second row is read and dropped).
+template <bool TR>
 __device__ __forceinline__ void b2_bilinear(char* lds, const float* cxy, int l, int Hl, int Wl, int bx0, int by0,
                                             int bw, int toff, int as, int qmask, int gpix, int wave_u, int lane) {
   const int p = lane;
@@ -405,9 +440,6 @@ __device__ __forceinline__ void b2_bilinear(char* lds, const float* cxy, int l, 
   const int lo = min(max(-xs, 0), 8), hi = max(min(Wl - xs, 8), 0);
   const unsigned cmask = hi > lo ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
   const bool any_partial = __builtin_amdgcn_ballot_w64(cmask != 0xffu) != 0;
-  auto rowbase = [&](int y) {
-    return (y >= 0 && y < Hl) ? (unsigned)((toff + (y - by0) * bw + xs - bx0) * 256 + 2 * p) : kB2Zero;
-  };
   // window rows (ya, ya + 1) of both output rows as packed tap pairs (2j, 2j + 1):
   // the arithmetic below runs two outputs per instruction (v_pk_mul / v_pk_add
   // _f16, each op rounded exactly as the scalar half op)
@@ -418,11 +450,8 @@ __device__ __forceinline__ void b2_bilinear(char* lds, const float* cxy, int l, 
     const int ya = yi0 - 3 + wave_u + 4 * r;
 #pragma unroll
     for (int ab = 0; ab < 2; ++ab) {
-      const unsigned base = rowbase(ya + ab);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        pe[r][ab][q] = __builtin_bit_cast(unsigned, h2_t{b2_ldh(lds, base + (2 * q) * 256),
-                                                         b2_ldh(lds, base + (2 * q + 1) * 256)});
+      const int y = ya + ab;
+      b2_crow<TR>(lds, toff + (y - by0) * bw + xs - bx0, y >= 0 && y < Hl, p, pe[r][ab]);
     }
   }
   if (any_partial) {   // columns outside the map read zeros
@@ -464,6 +493,7 @@ __device__ __forceinline__ void b2_bilinear(char* lds, const float* cxy, int l, 
 // ds_write_b16.  Every piece of every pixel in qmask is written (wave 3 writes
 // the zero row 7), so the encoder needs no padding mask.  Same arithmetic as
 // b2_bilinear, value for value.
+template <bool TR>
 __device__ __forceinline__ void b2_bilinear3(char* lds, const float* cxy, int l, int Hl, int Wl, int bx0, int by0,
                                              int bw, int toff, int as, int qmask, int gpix, int wave_u, int lane) {
   const int p = lane;
@@ -490,9 +520,6 @@ __device__ __forceinline__ void b2_bilinear3(char* lds, const float* cxy, int l,
   const int lo = min(max(-xs, 0), 8), hi = max(min(Wl - xs, 8), 0);
   const unsigned cmask = hi > lo ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
   const bool any_partial = __builtin_amdgcn_ballot_w64(cmask != 0xffu) != 0;
-  auto rowbase = [&](int y) {
-    return (y >= 0 && y < Hl) ? (unsigned)((toff + (y - by0) * bw + xs - bx0) * 256 + 2 * p) : kB2Zero;
-  };
   typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
   const int nr = wave_u == 3 ? 1 : 2;
   unsigned pe[2][2][4];
@@ -501,11 +528,8 @@ __device__ __forceinline__ void b2_bilinear3(char* lds, const float* cxy, int l,
     const int ya = yi0 - 3 + wave_u + 4 * r;
 #pragma unroll
     for (int ab = 0; ab < 2; ++ab) {
-      const unsigned base = rowbase(ya + ab);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        pe[r][ab][q] = __builtin_bit_cast(unsigned, h2_t{b2_ldh(lds, base + (2 * q) * 256),
-                                                         b2_ldh(lds, base + (2 * q + 1) * 256)});
+      const int y = ya + ab;
+      b2_crow<TR>(lds, toff + (y - by0) * bw + xs - bx0, y >= 0 && y < Hl, p, pe[r][ab]);
     }
   }
   if (any_partial) {
@@ -615,8 +639,21 @@ __device__ __forceinline__ void b2_plan_groups(const AltArgs& a, const float* cx
   if (lane == 0) grp[0] = hcnt(0) + hcnt(1);
 }
 
-template <bool V3>
+// corr_alt2_kernel variants (CV bits): kCvSplit - the C phase with the box
+// blocks split over the waves (all four M-blocks' query rows per wave, b2_corr3);
+// kCvRowK - the lookup tile in the k = 8 iy + ix order (b2_bilinear3: one 16-B
+// store per window row) with corr_encoder[0]'s weights permuted to match;
+// kCvTrans - the transposed C MFMA with rotated 8-B C stores (b2_corr<true>).
+// V2 = 0, V3 = kCvSplit | kCvRowK, the round-5 product = kCvRowK | kCvTrans.
+constexpr int kCvSplit = 1, kCvRowK = 2, kCvTrans = 8;
+constexpr int kAltProdCV = kCvRowK | kCvTrans;
+template <int CV>
 __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
+  constexpr bool V3 = (CV & kCvSplit) != 0;        // C split over the waves
+  constexpr bool RK = (CV & kCvRowK) != 0;         // k = 8 iy + ix lookup tile
+  constexpr bool TR = (CV & kCvTrans) != 0;        // transposed, rotated C
+  static_assert(!(V3 && TR), "the split C phase writes the unrotated layout");
+  static_assert(!V3 || RK, "the split C phase ships with the row-K tile only (V3)");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int* grp = reinterpret_cast<int*>(lds + kB2Grp);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -659,8 +696,8 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
           const int k = 32 * s + 8 * fq + i;
           // V3 lookup-tile order k = 8 iy + ix <-> the reference channel 7 ix + iy
           const int iy = k >> 3, ix = k & 7;
-          const bool ok = V3 ? (ix < 7 && iy < 7) : k < 49;
-          const int ch = V3 ? 7 * ix + iy : k;
+          const bool ok = RK ? (ix < 7 && iy < 7) : k < 49;
+          const int ch = RK ? 7 * ix + iy : k;
           v[i] = ok ? (_Float16)a.w[(wave * 32 + 16 * n + fr) * 224 + 49 * l + ch] : (_Float16)0.f;
         }
         wl[l][n][s] = v;
@@ -724,10 +761,10 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
   };
   auto encode = [&](int L, int as, int qmask) {
     switch (L) {
-      case 3: b2_encode<3, V3>(lds, as, qmask, wl, acc, fq, eoff); break;
-      case 2: b2_encode<2, V3>(lds, as, qmask, wl, acc, fq, eoff); break;
-      case 1: b2_encode<1, V3>(lds, as, qmask, wl, acc, fq, eoff); break;
-      default: b2_encode<0, V3>(lds, as, qmask, wl, acc, fq, eoff); break;
+      case 3: b2_encode<3, RK>(lds, as, qmask, wl, acc, fq, eoff); break;
+      case 2: b2_encode<2, RK>(lds, as, qmask, wl, acc, fq, eoff); break;
+      case 1: b2_encode<1, RK>(lds, as, qmask, wl, acc, fq, eoff); break;
+      default: b2_encode<0, RK>(lds, as, qmask, wl, acc, fq, eoff); break;
     }
   };
   // level L of tile T: its tile box if it fits the region, else the fallback groups
@@ -752,11 +789,11 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
       wait_bar();
       if (L == 0) B2_STAMP(9);
       if (V3) b2_corr3(lds, gw * gh, qmask, af, wave_u, fr, fq);
-      else b2_corr(lds, gw * gh, qmask, af[0], wave_u, fr, fq);
+      else b2_corr<TR>(lds, gw * gh, qmask, af[0], wave_u, fr, fq);
       if (L == 0) B2_STAMP(10);
       __syncthreads();
-      if (V3) b2_bilinear3(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, 0, qmask, gpix, wave_u, lane);
-      else b2_bilinear(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, 0, qmask, gpix, wave_u, lane);
+      if (RK) b2_bilinear3<TR>(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, 0, qmask, gpix, wave_u, lane);
+      else b2_bilinear<TR>(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, 0, qmask, gpix, wave_u, lane);
       if (side && gi == ng - 1 && wave_u == 3 && more)   // the next tile's boxes, on the wave with one window row
         alt_tile_boxes(a, reinterpret_cast<const float*>(lds + kB2Coord + nslot * 512),
                        reinterpret_cast<int*>(lds + kB2Lvl) + nslot * 16, lane);
@@ -806,27 +843,27 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
       wait_bar();
       B2_STAMP(2);
       if (V3) b2_corr3(lds, T321, 15, af, wave_u, fr, fq);
-      else b2_corr(lds, T321, 15, af[0], wave_u, fr, fq);
+      else b2_corr<TR>(lds, T321, 15, af[0], wave_u, fr, fq);
       B2_STAMP(3);
       __syncthreads();
       B2_STAMP(4);
       for (int i = 0; i < 3; ++i) {
         const int L = 3 - i;
-        if (V3)
-          b2_bilinear3(lds, cxy, L, a.Hl[L], a.Wl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
+        if (RK)
+          b2_bilinear3<TR>(lds, cxy, L, a.Hl[L], a.Wl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
                        __builtin_amdgcn_readfirstlane(lv[4 * L + 1]), __builtin_amdgcn_readfirstlane(lv[4 * L + 2]),
                        toffs[i], i, 15, -1, wave_u, lane);
         else
-          b2_bilinear(lds, cxy, L, a.Hl[L], a.Wl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
+          b2_bilinear<TR>(lds, cxy, L, a.Hl[L], a.Wl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
                       __builtin_amdgcn_readfirstlane(lv[4 * L + 1]), __builtin_amdgcn_readfirstlane(lv[4 * L + 2]),
                       toffs[i], i, 15, -1, wave_u, lane);
       }
       B2_STAMP(5);
       __syncthreads();
       B2_STAMP(6);
-      b2_encode<3, V3>(lds, 0, 15, wl, acc, fq, eoff);
-      b2_encode<2, V3>(lds, 1, 15, wl, acc, fq, eoff);
-      b2_encode<1, V3>(lds, 2, 15, wl, acc, fq, eoff);
+      b2_encode<3, RK>(lds, 0, 15, wl, acc, fq, eoff);
+      b2_encode<2, RK>(lds, 1, 15, wl, acc, fq, eoff);
+      b2_encode<1, RK>(lds, 2, 15, wl, acc, fq, eoff);
       __syncthreads();
       B2_STAMP(7);
     } else {
@@ -891,6 +928,17 @@ static int& alt_variant() {
   }();
   return v;
 }
+
+#if DROID_AB
+// the A/B build's corr_alt2_kernel variant for alt variant 2 (DROID_ALT2_CV: 0, 2, 8, 10)
+static int& alt2_cv() {
+  static int v = [] {
+    const int e = ab_knob("DROID_ALT2_CV", kAltProdCV);
+    return (e == 0 || e == kCvRowK || e == kCvTrans) ? e : kAltProdCV;
+  }();
+  return v;
+}
+#endif
 
 extern "C" {
 
@@ -967,10 +1015,16 @@ int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int*
 #endif
   static bool attr2 = false;
   if (!attr2) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<false>),
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<kAltProdCV>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
 #if DROID_AB
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<true>),
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<kCvSplit | kCvRowK>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<0>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<kCvRowK>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<kCvTrans>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
 #endif
     attr2 = true;
@@ -979,13 +1033,22 @@ int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int*
   static const int per_cu = ab_knob("DROID_ALT2_WG_PER_CU", 2) == 1 ? 1 : 2;
   const long grid = std::min<long>(a.ntiles, (long)per_cu * device_cu_count());
 #if DROID_AB
-  if (alt_variant() == 3) {
-    corr_alt2_kernel<true><<<dim3((unsigned)grid), 256, kB2Lds, stream>>>(a);
+  // variant 3 = V3; variant 2 runs DROID_ALT2_CV's kernel (0 = the round-4
+  // V2, 2 = row-K only, 8 = transposed C only, 10 = the product)
+  const int cv = alt_variant() == 3 ? (kCvSplit | kCvRowK) : alt2_cv();
+  if (cv != kAltProdCV) {
+    const dim3 g((unsigned)grid);
+    switch (cv) {
+      case kCvSplit | kCvRowK: corr_alt2_kernel<kCvSplit | kCvRowK><<<g, 256, kB2Lds, stream>>>(a); break;
+      case 0: corr_alt2_kernel<0><<<g, 256, kB2Lds, stream>>>(a); break;
+      case kCvRowK: corr_alt2_kernel<kCvRowK><<<g, 256, kB2Lds, stream>>>(a); break;
+      default: corr_alt2_kernel<kCvTrans><<<g, 256, kB2Lds, stream>>>(a); break;
+    }
     DROID_LAUNCH_CHECK();
     return kOk;
   }
 #endif
-  corr_alt2_kernel<false><<<dim3((unsigned)grid), 256, kB2Lds, stream>>>(a);
+  corr_alt2_kernel<kAltProdCV><<<dim3((unsigned)grid), 256, kB2Lds, stream>>>(a);
   DROID_LAUNCH_CHECK();
   return kOk;
 }
@@ -998,13 +1061,21 @@ int droid_alt_set_chunk(int edges) {
   return kOk;
 }
 
-// A/B hook: 2 = corr_alt2_kernel (the product kernel); 1 = the one-workgroup-
-// per-CU kernel and 3 = corr_alt2_kernel<V3> exist in the A/B build only
-// (there env DROID_ALT_VARIANT sets the initial value)
+// A/B hook: 2 = corr_alt2_kernel (the product kernel); in the A/B build only:
+// 1 = the one-workgroup-per-CU kernel, 3 = corr_alt2_kernel<V3>, and the
+// round-5 pieces apart - 4 = the round-4 V2 (CV 0), 5 = row-K lookup tile only
+// (CV 2), 6 = transposed C only (CV 8); env DROID_ALT_VARIANT / DROID_ALT2_CV
+// set the initial values there
 int droid_alt_set_variant(int v) {
-  if (v < 1 || v > 3) return fail(kInvalidArgument, "alt_set_variant: 1, 2 or 3");
-  if (!DROID_AB && v != 2) return fail(kUnsupported, "alt_set_variant: variants 1 and 3 ship in the A/B build only (make ab)");
+  if (v < 1 || v > 6) return fail(kInvalidArgument, "alt_set_variant: 1 .. 6");
+  if (!DROID_AB && v != 2) return fail(kUnsupported, "alt_set_variant: variants other than 2 ship in the A/B build only (make ab)");
+#if DROID_AB
+  static const int cvs[7] = {0, 0, kAltProdCV, 0, 0, kCvRowK, kCvTrans};
+  alt2_cv() = v == 2 || v >= 4 ? cvs[v] : alt2_cv();
+  alt_variant() = v >= 4 ? 2 : v;
+#else
   alt_variant() = v;
+#endif
   return kOk;
 }
 

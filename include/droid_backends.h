@@ -90,10 +90,13 @@ int droid_conv_set_profile(void* buf);
  * done / lookup barrier / stage end, then box taps * 2 + slow-path flag)
  * (scripts/alt_timeline.py). */
 int droid_alt_set_profile(void* buf);
-/* A/B hook for the on-demand lookup: 1 = corr_alt_ce0_kernel (one 8-wave
- * workgroup per CU), 2 = corr_alt2_kernel (two 4-wave workgroups per CU, the
- * default; env DROID_ALT_VARIANT=1 selects 1 at load).  Outputs are bitwise
- * equal; tests compare the two. */
+/* A/B hook for the on-demand lookup: 2 = corr_alt2_kernel (two 4-wave
+ * workgroups per CU, the product).  The A/B build (make ab) adds 1 =
+ * corr_alt_ce0_kernel (one 8-wave workgroup per CU), 3 = the V3 C split, 4 =
+ * the round-4 corr_alt2_kernel, 5 / 6 = its row-K lookup tile / transposed C
+ * alone.  1, 4 and 6 are bitwise equal; 2, 3 and 5 are bitwise equal and
+ * differ from the first set by corr_encoder[0]'s K order only (a few ulps);
+ * the other values return kUnsupported in the product library. */
 int droid_alt_set_variant(int v);
 /* Tuning hook: edges per XCD chunk of corr_alt2_kernel's tile walk (0 = interleaved, the default). */
 int droid_alt_set_chunk(int edges);

@@ -30,15 +30,23 @@ def timed(**kw):
 
 
 outs = {}
-for variant in (1, 2, 3):   # droid_alt_set_variant: the one-workgroup kernel, corr_alt2_kernel, <V3>
+# droid_alt_set_variant: 2 = the product; the A/B build (DROID_HIP_LIB=.../lib/ab/libdroid_hip.so)
+# adds 1 = the one-workgroup kernel, 4 = the round-4 corr_alt2_kernel, 6 = its transposed C
+# alone, 5 = its row-K lookup tile alone, 3 = V3
+variants = (1, 4, 6, 5, 3, 2) if droid_backends.AB_BUILD else (2,)
+for variant in variants:
     droid_backends.alt_set_variant(variant)
     outs[variant], med, mn = timed()
     print("%s variant %d: median %.3f ms (min %.3f)" % (os.environ.get("DROID_HIP_LIB", "default"), variant, med, mn))
-print("C3 outputs bitwise equal (1, 2):", bool(torch.equal(outs[1], outs[2])))
-d = (outs[3].float() - outs[2].float()).abs()
-print("V3 vs V2: max diff %.3g of scale %.3g, identical fraction %.4f" % (float(d.max()), float(outs[2].float().abs().max()),
-                                                                     float((d == 0).float().mean())))
+if droid_backends.AB_BUILD:
+    print("C3 outputs bitwise equal (1, 4, 6):", bool(torch.equal(outs[1], outs[4]) and torch.equal(outs[1], outs[6])))
+    print("C3 outputs bitwise equal (2, 3, 5):", bool(torch.equal(outs[2], outs[3]) and torch.equal(outs[2], outs[5])))
+    d = (outs[2].float() - outs[4].float()).abs()
+    print("product vs round-4 V2: max diff %.3g of scale %.3g, identical fraction %.4f" % (
+        float(d.max()), float(outs[4].float().abs().max()), float((d == 0).float().mean())))
 droid_backends.alt_set_variant(2)
+if "--quick" in sys.argv:   # the variants only (PMC passes: scripts/pmc_alt.sh)
+    sys.exit(0)
 order = torch.argsort(f2.long(), stable=True).to(torch.int32)
 for chunk in (0, 1, 2, 4, 8, 16, 32):
     droid_backends.alt_set_chunk(chunk)

@@ -367,13 +367,15 @@ def test_corr_alt_ce0_matches_volume_path(noise, H, W, E):
 @pytest.mark.parametrize("noise,H,W,E,far", [(1.5, 16, 24, 6, 0.0), (40.0, 16, 24, 6, 0.0), (1.5, 48, 64, 300, 0.0),
                                              (8.0, 48, 64, 300, 0.0), (4.0, 48, 64, 200, 0.1), (0.3, 32, 64, 64, 0.0)])
 def test_corr_alt2_bitwise_equals_alt1(noise, H, W, E, far, ab_backends):
-    """corr_alt2_kernel (two 4-wave workgroups per CU, C in place, merged
-    level-3/2/1 stage, group fallbacks) computes every value with the same
-    operations in the same order as corr_alt_ce0_kernel: outputs bitwise equal.
-    far: fraction of pixels thrown 30-200 px off the map (windows partly or
-    wholly outside, boxes over the region -> half / quadrant / pixel groups)."""
-    import droid_backends as product
-    droid_backends = ab_backends   # corr_alt_ce0_kernel (variant 1) ships in the A/B build only
+    """The round-4 corr_alt2_kernel (two 4-wave workgroups per CU, C in place,
+    merged level-3/2/1 stage, group fallbacks; A/B variant 4) and its round-5
+    transposed, rotated C layout alone (variant 6) compute every value with the
+    same operations in the same order as corr_alt_ce0_kernel: outputs bitwise
+    equal.  The product (transposed C + row-K lookup tile) is checked against
+    them in test_corr_alt2_v3_matches_v2.  far: fraction of pixels thrown
+    30-200 px off the map (windows partly or wholly outside, boxes over the
+    region -> half / quadrant / pixel groups)."""
+    droid_backends = ab_backends   # variants 1, 4 and 6 ship in the A/B build only
     from droid_mi355x.corr import AltCorrBlock
     rng = np.random.default_rng(41)
     NF = 8
@@ -396,27 +398,32 @@ def test_corr_alt2_bitwise_equals_alt1(noise, H, W, E, far, ab_backends):
     try:
         droid_backends.alt_set_variant(1)
         ref = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
-        droid_backends.alt_set_variant(2)
+        droid_backends.alt_set_variant(4)
         out = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
+        droid_backends.alt_set_variant(6)
+        out6 = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
     finally:
         droid_backends.alt_set_variant(2)
-    prod = product.corr_alt_ce0(pyr, f1, f2, c, w224, b)   # the product library's corr_alt2_kernel
     torch.cuda.synchronize()
     diff = (out.float() - ref.float()).abs()
     assert torch.equal(out, ref), (float(diff.max()), int((diff > 0).sum()))
-    assert torch.equal(prod, out)
+    assert torch.equal(out6, ref)
 
 
 @pytest.mark.parametrize("noise,H,W,E,far", [(1.5, 16, 24, 6, 0.0), (40.0, 16, 24, 6, 0.0), (1.5, 48, 64, 300, 0.0),
                                              (4.0, 48, 64, 200, 0.1), (0.3, 32, 64, 64, 0.0)])
 def test_corr_alt2_v3_matches_v2(noise, H, W, E, far, ab_backends):
-    """corr_alt2_kernel<V3> (box blocks split over the waves, transposed C
-    MFMA, lookup tile in the k = 8 iy + ix order with the encoder weights
-    permuted to match): the C values and the bilinear windows are the V2 values;
-    only corr_encoder[0]'s fp32 summation order differs (a permuted K), so the
-    fp16 outputs agree to a few ulps and are mostly identical; every fallback
+    """The product corr_alt2_kernel (round 5: transposed C MFMA with rotated
+    8-B C stores, lookup tile in the k = 8 iy + ix order with the encoder
+    weights permuted to match) and the A/B kernels that share its lookup-tile
+    order - V3 (box blocks split over the waves) and the row-K tile alone
+    (variant 5) - are bitwise equal to each other: their C values and bilinear
+    windows are the round-4 V2 values (variant 4), and only corr_encoder[0]'s
+    fp32 summation order differs from V2 (a permuted K), so against V2 the fp16
+    outputs agree to a few ulps and are mostly identical; every fallback
     (incoherent, off-map coordinates) included."""
-    droid_backends = ab_backends   # corr_alt2_kernel<V3> ships in the A/B build only
+    import droid_backends as product
+    droid_backends = ab_backends   # variants 3, 4 and 5 ship in the A/B build only
     from droid_mi355x.corr import AltCorrBlock
     rng = np.random.default_rng(43)
     NF = 8
@@ -437,15 +444,20 @@ def test_corr_alt2_v3_matches_v2(noise, H, W, E, far, ab_backends):
     b = torch.randn(128, generator=g, device=DEV) * 0.1
     f1, f2 = torch.as_tensor(ii, device=DEV), torch.as_tensor(jj, device=DEV)
     try:
-        droid_backends.alt_set_variant(2)
+        droid_backends.alt_set_variant(4)
         ref = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
         droid_backends.alt_set_variant(3)
         out = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
         out2 = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
+        droid_backends.alt_set_variant(5)
+        out5 = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
     finally:
         droid_backends.alt_set_variant(2)
+    prod = product.corr_alt_ce0(pyr, f1, f2, c, w224, b)   # the product library's corr_alt2_kernel
     torch.cuda.synchronize()
     assert torch.equal(out, out2)                      # deterministic
+    assert torch.equal(out5, out)
+    assert torch.equal(prod, out)
     assert bool(torch.isfinite(out.float()).all())
     scale = float(ref.float().abs().max())
     diff = (out.float() - ref.float()).abs()
