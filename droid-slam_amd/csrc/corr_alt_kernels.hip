@@ -290,34 +290,74 @@ __device__ __forceinline__ void b2_box_dma(const AltArgs& a, int l, int f2, int 
 // the box.  Since every wave reads every block, the C values (packed fp16, 2
 // VGPRs per block) are written only after a barrier.
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
-// Round 5, TR (the product layout): the MFMA runs transposed (query pixels as
-// rows - the same products and fp16 rounding, so C is bitwise the same), a lane
-// holds 4 consecutive pixels of one tap and stores them as ONE 8-B word per block
-// (a ds_write_b16 costs the LDS transfer of a ds_write_b32: four of them per
-// block were the C phase's write cost), and C(p, t) sits at byte
-// (2 p + 8 t) & 127 of tap row t: the 16 taps of a block, one per lane of a
-// 16-lane store group, land on 16 different 8-B slots (unrotated, all 16 on one
-// bank pair).  The bilinear reads apply the same rotation (b2_caddr).
-template <bool TR>
-__device__ __forceinline__ void b2_corr(char* lds, int T, int qmask, const half8 (&af)[4], int wave_u, int fr,
-                                        int fq) {
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+// Round 5, PM (the product layout): C pixel-major - C(p, t) at byte p S + 2 t
+// of the region, S = the stage's per-pixel stride (b2_cstride: the T taps
+// rounded up to whole 16-tap blocks, S = 8 mod 16) - instead of in place over the box rows (C(p, t) at 256 t + 2 p).  A
+// lane's 4 consecutive taps of one pixel are then ONE aligned 8-B store per
+// block (conflict-free: S / 4 = 2 mod 4 spreads the 16 lanes of a store group
+// over all 32 banks) instead of four 2-B stores, and a window row - 8
+// consecutive taps of one pixel - comes back as 5 aligned dwords (b2_crow)
+// instead of 8 2-B reads that the compiler had to pack pairwise, with an LDS
+// round trip per pair.  The lookup tiles move to their own area (b2_lk) past
+// the C region.  Same products, same fp16 rounding: C is bitwise the same.
+constexpr int kB2Lk = 160 * 256;   // PM: lookup tiles, 3 slots x 64 px x 128 B
+static_assert(kB2Lk >= 64 * (32 * ((kB2Rows + 15) / 16) + 8) && kB2Lk + 3 * 64 * 128 <= kB2Rows * 256, "PM C region and lookup tiles");
+// S covers whole 16-tap blocks (b2_corr stores every tap of its last block)
+__device__ __forceinline__ int b2_cstride(int T) { return 32 * ((T + 15) >> 4) + 8; }
+template <bool PM>
+__device__ __forceinline__ unsigned b2_lk(int as, int p) {
+  return PM ? (unsigned)(kB2Lk + (as * 64 + p) * 128) : (unsigned)((as * 64 + p) * 256 + 128);
+}
+template <bool PM, typename Post>
+__device__ __forceinline__ void b2_corr(char* lds, int T, int S, int qmask, const half8 (&af)[4], int wave_u, int fr,
+                                        int fq, Post post) {
   constexpr int NB = kB2Rows / 16;
   const bool on = (qmask >> wave_u) & 1;
   const int nb = (T + 15) >> 4;
   half2_t cv[NB][2];
-  if (on) {
+  auto ldb = [&](int b, half8 (&bf)[4]) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      bf[ks] = *reinterpret_cast<const half8*>(lds + (b * 16 + fr) * 256 + (((ks * 4 + fq) ^ fr) << 4));
+  };
+  if (on && PM) {
+    // software-pipelined (round 5): block b + 1's box fragments are loaded
+    // before block b's MFMAs and block b - 1's fp16 conversion is deferred into
+    // block b, so the LDS latency and the MFMA result latency overlap work
+    // instead of serialising every block (rows past nb are loaded and dropped)
+    half8 bb[2][4];   // ping-pong by block parity (a compile-time index: no copies)
+    floatx4 cp = floatx4{0.f, 0.f, 0.f, 0.f};
+    ldb(0, bb[0]);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (b < nb) {
+        if (b + 1 < NB) ldb(b + 1, bb[(b + 1) & 1]);
+        floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bb[b & 1][ks], af[ks], c, 0, 0, 0);
+        if (b > 0) {
+          cv[b - 1][0] = half2_t{(_Float16)cp[0], (_Float16)cp[1]};
+          cv[b - 1][1] = half2_t{(_Float16)cp[2], (_Float16)cp[3]};
+        }
+        cp = c;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if (b == nb - 1) {
+        cv[b][0] = half2_t{(_Float16)cp[0], (_Float16)cp[1]};
+        cv[b][1] = half2_t{(_Float16)cp[2], (_Float16)cp[3]};
+      }
+  } else if (on) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       if (b < nb) {
         half8 bf[4];
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          bf[ks] = *reinterpret_cast<const half8*>(lds + (b * 16 + fr) * 256 + (((ks * 4 + fq) ^ fr) << 4));
+        ldb(b, bf);
         floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          c = TR ? __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks], bf[ks], c, 0, 0, 0)
-                 : __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[ks], af[ks], c, 0, 0, 0);
+        for (int ks = 0; ks < 4; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[ks], af[ks], c, 0, 0, 0);
         cv[b][0] = half2_t{(_Float16)c[0], (_Float16)c[1]};
         cv[b][1] = half2_t{(_Float16)c[2], (_Float16)c[3]};
       }
@@ -329,13 +369,11 @@ __device__ __forceinline__ void b2_corr(char* lds, int T, int qmask, const half8
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       if (b < nb) {
-        if (TR) {
-          // lane (fr, fq): C[pixel q*16 + 4 fq + k][tap b*16 + fr], k < 4
-          typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+        // lane (fr, fq): C[tap b*16 + 4 fq + k][pixel q*16 + fr]
+        if (PM) {
           const u32x2_t v = {__builtin_bit_cast(unsigned, cv[b][0]), __builtin_bit_cast(unsigned, cv[b][1])};
-          *reinterpret_cast<u32x2_t*>(lds + (b * 16 + fr) * 256 + ((32 * q + 8 * fq + 8 * fr) & 127)) = v;
+          *reinterpret_cast<u32x2_t*>(lds + (q * 16 + fr) * S + 2 * (b * 16 + 4 * fq)) = v;
         } else {
-          // lane (fr, fq): C[tap b*16 + 4 fq + k][pixel q*16 + fr]
           char* base = lds + (b * 16 + 4 * fq) * 256 + (q * 16 + fr) * 2;
           *reinterpret_cast<_Float16*>(base) = cv[b][0][0];
           *reinterpret_cast<_Float16*>(base + 256) = cv[b][0][1];
@@ -345,21 +383,46 @@ __device__ __forceinline__ void b2_corr(char* lds, int T, int qmask, const half8
       }
     }
   }
+  post();   // PM: the bilinear's per-pixel window table (b2_win_table), in the dead box past C
 }
 
-// The 8 window-row taps tr + i (i < 8) of pixel p as 4 packed pairs: C(p, t) at
-// byte 256 t + 2 p (unrotated) or 256 t + ((2 p + 8 t) & 127) (TR); a row
-// outside the map (ok false) reads past the allocation, i.e. zeros.
-template <bool TR>
-__device__ __forceinline__ void b2_crow(const char* lds, int tr, bool ok, int p, unsigned (&pe)[4]) {
-  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
-  const unsigned rb = ok ? (unsigned)(tr * 256) : kB2Zero;
-  const unsigned u = (unsigned)(2 * p + 8 * tr);
+// The 8 window-row taps tr + i (i < 8) of pixel p of the 4 window rows a thread
+// needs (rows (r, ab): output row r, its upper / lower tap row) as 4 packed
+// pairs (2q, 2q + 1); a row outside the map (ok false) reads past the
+// allocation, i.e. zeros.  PM: 5 aligned dwords over each row's 16 bytes - all
+// 20 loads issued before the first funnel shift, one LDS round trip for the
+// four rows - then a shift by 0 or 16 bits.
+template <bool PM>
+__device__ __forceinline__ void b2_crows(const char* lds, const int (&tr)[2][2], const bool (&ok)[2][2], int p, int S,
+                                         unsigned (&pe)[2][2][4]) {
+  if (PM) {
+    unsigned d[2][2][5], sh[2][2];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const unsigned a0 = TR ? rb + (unsigned)(2 * q) * 256u + ((u + 16u * q) & 127u) : rb + 2 * p + (2 * q) * 256;
-    const unsigned a1 = TR ? rb + (unsigned)(2 * q + 1) * 256u + ((u + 16u * q + 8u) & 127u) : rb + 2 * p + (2 * q + 1) * 256;
-    pe[q] = __builtin_bit_cast(unsigned, h2_t{b2_ldh(lds, a0), b2_ldh(lds, a1)});
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int ab = 0; ab < 2; ++ab) {
+        const unsigned rb = ok[r][ab] ? (unsigned)(p * S + 2 * tr[r][ab]) : kB2Zero;
+        sh[r][ab] = (rb & 2u) * 8u;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) d[r][ab][i] = *reinterpret_cast<const unsigned*>(lds + (rb & ~3u) + 4 * i);
+      }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int ab = 0; ab < 2; ++ab)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pe[r][ab][q] = __builtin_amdgcn_alignbit(d[r][ab][q + 1], d[r][ab][q], sh[r][ab]);
+  } else {
+    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int ab = 0; ab < 2; ++ab) {
+        const unsigned rb = ok[r][ab] ? (unsigned)(tr[r][ab] * 256 + 2 * p) : kB2Zero;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          pe[r][ab][q] = __builtin_bit_cast(unsigned, h2_t{b2_ldh(lds, rb + (2 * q) * 256), b2_ldh(lds, rb + (2 * q + 1) * 256)});
+      }
   }
 }
 
@@ -410,12 +473,12 @@ __device__ __forceinline__ void b2_corr3(char* lds, int T, int qmask, const half
 // volume-lookup at::Half arithmetic in corr_alt_ce0_kernel's order.  Both
 // rows' 32 taps are read before any arithmetic (one LDS round trip; wave 3's
 // second row is read and dropped).
-template <bool TR>
+template <bool PM>
 __device__ __forceinline__ void b2_bilinear(char* lds, const float* cxy, int l, int Hl, int Wl, int bx0, int by0,
-                                            int bw, int toff, int as, int qmask, int gpix, int wave_u, int lane) {
+                                            int bw, int toff, int S, int as, int qmask, int gpix, int wave_u, int lane) {
   const int p = lane;
   if (!((qmask >> (p >> 4)) & 1)) return;
-  char* arow = lds + (as * 64 + p) * 256 + 128;
+  char* arow = lds + b2_lk<PM>(as, p);
   const int sw = p & 7;
   const int nr = wave_u == 3 ? 1 : 2;
   const _Float16 z = (_Float16)0.f;
@@ -445,15 +508,19 @@ __device__ __forceinline__ void b2_bilinear(char* lds, const float* cxy, int l, 
   // _f16, each op rounded exactly as the scalar half op)
   typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
   unsigned pe[2][2][4];
+  int tr[2][2];
+  bool okr[2][2];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int ya = yi0 - 3 + wave_u + 4 * r;
 #pragma unroll
     for (int ab = 0; ab < 2; ++ab) {
       const int y = ya + ab;
-      b2_crow<TR>(lds, toff + (y - by0) * bw + xs - bx0, y >= 0 && y < Hl, p, pe[r][ab]);
+      tr[r][ab] = toff + (y - by0) * bw + xs - bx0;
+      okr[r][ab] = y >= 0 && y < Hl;
     }
   }
+  b2_crows<PM>(lds, tr, okr, p, S, pe);
   if (any_partial) {   // columns outside the map read zeros
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -493,12 +560,12 @@ __device__ __forceinline__ void b2_bilinear(char* lds, const float* cxy, int l, 
 // ds_write_b16.  Every piece of every pixel in qmask is written (wave 3 writes
 // the zero row 7), so the encoder needs no padding mask.  Same arithmetic as
 // b2_bilinear, value for value.
-template <bool TR>
+template <bool PM>
 __device__ __forceinline__ void b2_bilinear3(char* lds, const float* cxy, int l, int Hl, int Wl, int bx0, int by0,
-                                             int bw, int toff, int as, int qmask, int gpix, int wave_u, int lane) {
+                                             int bw, int toff, int S, int as, int qmask, int gpix, int wave_u, int lane) {
   const int p = lane;
   if (!((qmask >> (p >> 4)) & 1)) return;
-  char* arow = lds + (as * 64 + p) * 256 + 128;
+  char* arow = lds + b2_lk<PM>(as, p);
   const int sw = p & 7;
   auto put_row = [&](int iy, uint4 v) { *reinterpret_cast<uint4*>(arow + ((iy ^ sw) << 4)) = v; };
   const uint4 zero4 = uint4{0u, 0u, 0u, 0u};
@@ -523,15 +590,19 @@ __device__ __forceinline__ void b2_bilinear3(char* lds, const float* cxy, int l,
   typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
   const int nr = wave_u == 3 ? 1 : 2;
   unsigned pe[2][2][4];
+  int tr[2][2];
+  bool okr[2][2];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int ya = yi0 - 3 + wave_u + 4 * r;
 #pragma unroll
     for (int ab = 0; ab < 2; ++ab) {
       const int y = ya + ab;
-      b2_crow<TR>(lds, toff + (y - by0) * bw + xs - bx0, y >= 0 && y < Hl, p, pe[r][ab]);
+      tr[r][ab] = toff + (y - by0) * bw + xs - bx0;
+      okr[r][ab] = y >= 0 && y < Hl;
     }
   }
+  b2_crows<PM>(lds, tr, okr, p, S, pe);
   if (any_partial) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -569,9 +640,126 @@ __device__ __forceinline__ void b2_bilinear3(char* lds, const float* cxy, int l,
   }
 }
 
+// Round 5, the product's bilinear (PM + row-K), in two halves so the merged
+// level-3/2/1 stage can issue the next level's C reads before this level's
+// lookup-tile stores (LDS stores the compiler cannot reorder loads across).
+// Thread = (wave w, pixel lane): ADJACENT output rows 2w, 2w + 1 (wave 3: row
+// 6 and the zero row 7), so 3 tap rows (15 aligned dwords) instead of 4 per
+// thread.  The arithmetic is b2_bilinear3's, value for value.
+struct B2Bl {
+  unsigned d[3][5];
+  unsigned bits;   // column mask (bits 0..7) | 16-bit shift of tap row j (bit 8 + j)
+};
+// the pixel's window origin and bilinear weights at level l (fp32 -> fp16 as
+// the volume lookup's at::Half arithmetic), computed ONCE per pixel and level
+// into a 16-B LDS entry - {xs (24 bits) | column mask << 24, yi0, w00 | w01 << 16,
+// w10 | w11 << 16} - instead of by every wave in every bilinear pass (the
+// bilinear phase is VALU-issue bound)
+constexpr int kB2Win = 256 * 256;   // PM: [4 levels][64 px] uint4, past the lookup tiles
+static_assert(kB2Win >= kB2Lk + 3 * 64 * 128 && kB2Win + 4 * 64 * 16 <= kB2Rows * 256, "PM window table");
+__device__ __forceinline__ void b2_win_table(char* lds, const float* cxy, int l, int Wl, int p) {
+  const float scl = 1.0f / (float)(1 << l);
+  const float x0 = cxy[2 * p] * scl, y0 = cxy[2 * p + 1] * scl;
+  const float fx0 = floorf(x0), fy0 = floorf(y0);
+  const float dx = x0 - fx0, dy = y0 - fy0;
+  const int xs = alt_floor(x0) - 3;
+  const int lo = min(max(-xs, 0), 8), hi = max(min(Wl - xs, 8), 0);
+  const unsigned cmask = hi > lo ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  const h2_t wa = {(_Float16)rnd16((1.0f - dx) * (1.0f - dy)), (_Float16)rnd16((1.0f - dx) * dy)};   // w00, w01
+  const h2_t wb = {(_Float16)rnd16(dx * (1.0f - dy)), (_Float16)rnd16(dx * dy)};                      // w10, w11
+  *reinterpret_cast<uint4*>(lds + kB2Win + (l * 64 + p) * 16) =
+      uint4{((unsigned)xs & 0xffffffu) | (cmask << 24), (unsigned)alt_floor(y0), __builtin_bit_cast(unsigned, wa),
+            __builtin_bit_cast(unsigned, wb)};
+}
+__device__ __forceinline__ B2Bl b2_bl_prep(const char* lds, int l, int Hl, int bx0, int by0, int bw, int toff, int S,
+                                           int qmask, int wave_u, int lane) {
+  B2Bl st;
+  const int p = lane;
+  const bool on = (qmask >> (p >> 4)) & 1;
+  const uint4 e = *reinterpret_cast<const uint4*>(lds + kB2Win + (l * 64 + p) * 16);
+  const int xs = (int)(e.x << 8) >> 8, yi0 = (int)e.y;
+  st.bits = e.x >> 24;
+  const int nrow = wave_u == 3 ? 2 : 3;   // wave 3: tap rows 6, 7 (output row 6 only)
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (j >= nrow) break;
+    const int y = yi0 - 3 + 2 * wave_u + j;
+    const unsigned rb = (on && y >= 0 && y < Hl) ? (unsigned)(p * S + 2 * (toff + (y - by0) * bw + xs - bx0)) : kB2Zero;
+    st.bits |= (rb & 2u) << (7 + j);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) st.d[j][i] = *reinterpret_cast<const unsigned*>(lds + (rb & ~3u) + 4 * i);
+  }
+  return st;
+}
+__device__ __forceinline__ void b2_bl_fin(char* lds, const B2Bl& st, int l, int as, int qmask, int gpix, int wave_u,
+                                          int lane) {
+  const int p = lane;
+  if (!((qmask >> (p >> 4)) & 1)) return;
+  char* arow = lds + b2_lk<true>(as, p);
+  const int sw = p & 7;
+  auto put_row = [&](int iy, uint4 v) { *reinterpret_cast<uint4*>(arow + ((iy ^ sw) << 4)) = v; };
+  const uint4 zero4 = uint4{0u, 0u, 0u, 0u};
+  if (gpix >= 0 && gpix != p) {   // a single-pixel group: the M-block's other rows are zero
+    put_row(2 * wave_u, zero4);
+    put_row(2 * wave_u + 1, zero4);
+    return;
+  }
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  const int nrow = wave_u == 3 ? 2 : 3;
+  unsigned pe[3][4];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (j >= nrow) break;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pe[j][q] = __builtin_amdgcn_alignbit(st.d[j][q + 1], st.d[j][q], ((st.bits >> (8 + j)) & 1u) * 16u);
+  }
+  const unsigned cmask = st.bits & 0xffu;
+  if (__builtin_amdgcn_ballot_w64(cmask != 0xffu) != 0) {   // columns outside the map read zeros
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned m = (((cmask >> (2 * q)) & 1) ? 0xffffu : 0u) | (((cmask >> (2 * q + 1)) & 1) ? 0xffff0000u : 0u);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        if (j >= nrow) break;
+        pe[j][q] &= m;
+      }
+    }
+  }
+  const _Float16 z = (_Float16)0.f;
+  // the weights as two named scalars: hipcc (ROCm 7.2) miscompiles
+  // __builtin_bit_cast of an ext_vector element (v[i], v.y) to element 0
+  const unsigned* we = reinterpret_cast<const unsigned*>(lds + kB2Win + (l * 64 + p) * 16 + 8);
+  const unsigned we0 = we[0], we1 = we[1];
+  const h2_t wa = __builtin_bit_cast(h2_t, we0), wb = __builtin_bit_cast(h2_t, we1);
+  const h2_t W00 = {wa[0], wa[0]}, W01 = {wa[1], wa[1]}, W10 = {wb[0], wb[0]}, W11 = {wb[1], wb[1]}, Z2 = {z, z};
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (r == 1 && wave_u == 3) {   // window row 7 does not exist - its piece is zero
+      put_row(7, zero4);
+      break;
+    }
+    unsigned o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // outputs 2q, 2q + 1 (output 7 is the zero pad)
+      const h2_t ae = __builtin_bit_cast(h2_t, pe[r][q]), be = __builtin_bit_cast(h2_t, pe[r + 1][q]);
+      const unsigned an = q < 3 ? pe[r][q + 1] : 0u, bn = q < 3 ? pe[r + 1][q + 1] : 0u;
+      const h2_t ao = __builtin_bit_cast(h2_t, __builtin_amdgcn_alignbit(an, pe[r][q], 16));
+      const h2_t bo = __builtin_bit_cast(h2_t, __builtin_amdgcn_alignbit(bn, pe[r + 1][q], 16));
+      h2_t v = Z2 + ae * W00;
+      v = v + be * W01;
+      v = v + ao * W10;
+      v = v + bo * W11;
+      o[q] = __builtin_bit_cast(unsigned, v);
+    }
+    o[3] &= 0xffffu;
+    put_row(2 * wave_u + r, uint4{o[0], o[1], o[2], o[3]});
+  }
+}
+
 // corr_encoder[0] slice of level L for the M-blocks in qmask from lookup tile slot `as`;
 // acc[q][n] = out^T: lane (fr, fq) holds out[pixel q*16 + fr][co 32 w + 16 n + 4 fq + k]
-template <int L, bool V3 = false>
+template <int L, bool V3, bool PM>
 __device__ __forceinline__ void b2_encode(const char* lds, int as, int qmask, const half8 (&wl)[4][2][2],
                                           floatx4 (&acc)[4][2], int fq, const int (&eoff)[2]) {
 #pragma unroll
@@ -579,7 +767,7 @@ __device__ __forceinline__ void b2_encode(const char* lds, int as, int qmask, co
     if (!((qmask >> q) & 1)) continue;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      half8 x = *reinterpret_cast<const half8*>(lds + (as * 64 + q * 16) * 256 + eoff[s]);
+      half8 x = *reinterpret_cast<const half8*>(lds + b2_lk<PM>(as, q * 16) - (PM ? 0 : 128) + eoff[s]);
       if (!V3 && s == 1) {   // columns 49..63 (lanes fq 2: k 48..55, fq 3: k 56..63) are padding
         uint4 u = __builtin_bit_cast(uint4, x);
         u.x &= fq == 3 ? 0u : fq == 2 ? 0xffffu : 0xffffffffu;
@@ -643,16 +831,17 @@ __device__ __forceinline__ void b2_plan_groups(const AltArgs& a, const float* cx
 // blocks split over the waves (all four M-blocks' query rows per wave, b2_corr3);
 // kCvRowK - the lookup tile in the k = 8 iy + ix order (b2_bilinear3: one 16-B
 // store per window row) with corr_encoder[0]'s weights permuted to match;
-// kCvTrans - the transposed C MFMA with rotated 8-B C stores (b2_corr<true>).
-// V2 = 0, V3 = kCvSplit | kCvRowK, the round-5 product = kCvRowK | kCvTrans.
-constexpr int kCvSplit = 1, kCvRowK = 2, kCvTrans = 8;
-constexpr int kAltProdCV = kCvRowK | kCvTrans;
+// kCvPm - C pixel-major with 8-B C stores and dword window-row reads, the
+// lookup tiles in their own area (b2_corr<true>, b2_crow<true>, b2_lk<true>).
+// V2 = 0, V3 = kCvSplit | kCvRowK, the round-5 product = kCvRowK | kCvPm.
+constexpr int kCvSplit = 1, kCvRowK = 2, kCvPm = 4;
+constexpr int kAltProdCV = kCvRowK | kCvPm;
 template <int CV>
 __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
   constexpr bool V3 = (CV & kCvSplit) != 0;        // C split over the waves
   constexpr bool RK = (CV & kCvRowK) != 0;         // k = 8 iy + ix lookup tile
-  constexpr bool TR = (CV & kCvTrans) != 0;        // transposed, rotated C
-  static_assert(!(V3 && TR), "the split C phase writes the unrotated layout");
+  constexpr bool PM = (CV & kCvPm) != 0;           // pixel-major C, lookup tiles apart
+  static_assert(!(V3 && PM), "the split C phase writes the tap-major layout");
   static_assert(!V3 || RK, "the split C phase ships with the row-K tile only (V3)");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int* grp = reinterpret_cast<int*>(lds + kB2Grp);
@@ -705,7 +894,7 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
   if (tid < 128) reinterpret_cast<float*>(lds + kB2Bias)[tid] = a.bias[tid];   // read at the output staging
   int eoff[2];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) eoff[s] = fr * 256 + 128 + (((s * 4 + fq) ^ (fr & 7)) << 4);
+  for (int s = 0; s < 2; ++s) eoff[s] = (PM ? fr * 128 : fr * 256 + 128) + (((s * 4 + fq) ^ (fr & 7)) << 4);
 
   struct Tile { int e, ty0, tx0, f1, f2; };
   auto tile_of = [&](int t) {
@@ -761,10 +950,10 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
   };
   auto encode = [&](int L, int as, int qmask) {
     switch (L) {
-      case 3: b2_encode<3, RK>(lds, as, qmask, wl, acc, fq, eoff); break;
-      case 2: b2_encode<2, RK>(lds, as, qmask, wl, acc, fq, eoff); break;
-      case 1: b2_encode<1, RK>(lds, as, qmask, wl, acc, fq, eoff); break;
-      default: b2_encode<0, RK>(lds, as, qmask, wl, acc, fq, eoff); break;
+      case 3: b2_encode<3, RK, PM>(lds, as, qmask, wl, acc, fq, eoff); break;
+      case 2: b2_encode<2, RK, PM>(lds, as, qmask, wl, acc, fq, eoff); break;
+      case 1: b2_encode<1, RK, PM>(lds, as, qmask, wl, acc, fq, eoff); break;
+      default: b2_encode<0, RK, PM>(lds, as, qmask, wl, acc, fq, eoff); break;
     }
   };
   // level L of tile T: its tile box if it fits the region, else the fallback groups
@@ -789,11 +978,19 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
       wait_bar();
       if (L == 0) B2_STAMP(9);
       if (V3) b2_corr3(lds, gw * gh, qmask, af, wave_u, fr, fq);
-      else b2_corr<TR>(lds, gw * gh, qmask, af[0], wave_u, fr, fq);
+      else b2_corr<PM>(lds, gw * gh, b2_cstride(gw * gh), qmask, af[0], wave_u, fr, fq, [&] {
+          if (RK && PM && wave_u == 0) b2_win_table(lds, cxy, L, Wl, lane);   // this group's level
+        });
       if (L == 0) B2_STAMP(10);
       __syncthreads();
-      if (RK) b2_bilinear3<TR>(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, 0, qmask, gpix, wave_u, lane);
-      else b2_bilinear<TR>(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, 0, qmask, gpix, wave_u, lane);
+      if (RK && PM) {
+        const B2Bl bl = b2_bl_prep(lds, L, Hl, gx0, gy0, gw, 0, b2_cstride(gw * gh), qmask, wave_u, lane);
+        b2_bl_fin(lds, bl, L, 0, qmask, gpix, wave_u, lane);
+      } else if (RK) {
+        b2_bilinear3<PM>(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, b2_cstride(gw * gh), 0, qmask, gpix, wave_u, lane);
+      } else {
+        b2_bilinear<PM>(lds, cxy, L, Hl, Wl, gx0, gy0, gw, 0, b2_cstride(gw * gh), 0, qmask, gpix, wave_u, lane);
+      }
       if (side && gi == ng - 1 && wave_u == 3 && more)   // the next tile's boxes, on the wave with one window row
         alt_tile_boxes(a, reinterpret_cast<const float*>(lds + kB2Coord + nslot * 512),
                        reinterpret_cast<int*>(lds + kB2Lvl) + nslot * 16, lane);
@@ -843,27 +1040,44 @@ __global__ void __launch_bounds__(256, 2) corr_alt2_kernel(AltArgs a) {
       wait_bar();
       B2_STAMP(2);
       if (V3) b2_corr3(lds, T321, 15, af, wave_u, fr, fq);
-      else b2_corr<TR>(lds, T321, 15, af[0], wave_u, fr, fq);
+      else b2_corr<PM>(lds, T321, b2_cstride(T321), 15, af[0], wave_u, fr, fq, [&] {
+          if (RK && PM && wave_u >= 1)   // levels 1, 2, 3
+            b2_win_table(lds, cxy, wave_u, wave_u == 1 ? a.Wl[1] : wave_u == 2 ? a.Wl[2] : a.Wl[3], lane);
+        });
       B2_STAMP(3);
       __syncthreads();
       B2_STAMP(4);
-      for (int i = 0; i < 3; ++i) {
-        const int L = 3 - i;
-        if (RK)
-          b2_bilinear3<TR>(lds, cxy, L, a.Hl[L], a.Wl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
-                       __builtin_amdgcn_readfirstlane(lv[4 * L + 1]), __builtin_amdgcn_readfirstlane(lv[4 * L + 2]),
-                       toffs[i], i, 15, -1, wave_u, lane);
-        else
-          b2_bilinear<TR>(lds, cxy, L, a.Hl[L], a.Wl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
-                      __builtin_amdgcn_readfirstlane(lv[4 * L + 1]), __builtin_amdgcn_readfirstlane(lv[4 * L + 2]),
-                      toffs[i], i, 15, -1, wave_u, lane);
+      if (RK && PM) {   // levels 3, 2, 1 pipelined: level i + 1's C reads before level i's stores
+        auto prep = [&](int L, int i) {
+          return b2_bl_prep(lds, L, a.Hl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
+                            __builtin_amdgcn_readfirstlane(lv[4 * L + 1]), __builtin_amdgcn_readfirstlane(lv[4 * L + 2]),
+                            toffs[i], b2_cstride(T321), 15, wave_u, lane);
+        };
+        const B2Bl s3 = prep(3, 0);
+        const B2Bl s2 = prep(2, 1);
+        b2_bl_fin(lds, s3, 3, 0, 15, -1, wave_u, lane);
+        const B2Bl s1 = prep(1, 2);
+        b2_bl_fin(lds, s2, 2, 1, 15, -1, wave_u, lane);
+        b2_bl_fin(lds, s1, 1, 2, 15, -1, wave_u, lane);
+      } else {
+        for (int i = 0; i < 3; ++i) {
+          const int L = 3 - i;
+          if (RK)
+            b2_bilinear3<PM>(lds, cxy, L, a.Hl[L], a.Wl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
+                         __builtin_amdgcn_readfirstlane(lv[4 * L + 1]), __builtin_amdgcn_readfirstlane(lv[4 * L + 2]),
+                         toffs[i], b2_cstride(T321), i, 15, -1, wave_u, lane);
+          else
+            b2_bilinear<PM>(lds, cxy, L, a.Hl[L], a.Wl[L], __builtin_amdgcn_readfirstlane(lv[4 * L]),
+                        __builtin_amdgcn_readfirstlane(lv[4 * L + 1]), __builtin_amdgcn_readfirstlane(lv[4 * L + 2]),
+                        toffs[i], b2_cstride(T321), i, 15, -1, wave_u, lane);
+        }
       }
       B2_STAMP(5);
       __syncthreads();
       B2_STAMP(6);
-      b2_encode<3, RK>(lds, 0, 15, wl, acc, fq, eoff);
-      b2_encode<2, RK>(lds, 1, 15, wl, acc, fq, eoff);
-      b2_encode<1, RK>(lds, 2, 15, wl, acc, fq, eoff);
+      b2_encode<3, RK, PM>(lds, 0, 15, wl, acc, fq, eoff);
+      b2_encode<2, RK, PM>(lds, 1, 15, wl, acc, fq, eoff);
+      b2_encode<1, RK, PM>(lds, 2, 15, wl, acc, fq, eoff);
       __syncthreads();
       B2_STAMP(7);
     } else {
@@ -930,11 +1144,11 @@ static int& alt_variant() {
 }
 
 #if DROID_AB
-// the A/B build's corr_alt2_kernel variant for alt variant 2 (DROID_ALT2_CV: 0, 2, 8, 10)
+// the A/B build's corr_alt2_kernel variant for alt variant 2 (DROID_ALT2_CV: 0, 2, 4, 6)
 static int& alt2_cv() {
   static int v = [] {
     const int e = ab_knob("DROID_ALT2_CV", kAltProdCV);
-    return (e == 0 || e == kCvRowK || e == kCvTrans) ? e : kAltProdCV;
+    return (e == 0 || e == kCvRowK || e == kCvPm) ? e : kAltProdCV;
   }();
   return v;
 }
@@ -1024,7 +1238,7 @@ int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int*
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
     DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<kCvRowK>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<kCvTrans>),
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_alt2_kernel<kCvPm>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds));
 #endif
     attr2 = true;
@@ -1034,7 +1248,7 @@ int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int*
   const long grid = std::min<long>(a.ntiles, (long)per_cu * device_cu_count());
 #if DROID_AB
   // variant 3 = V3; variant 2 runs DROID_ALT2_CV's kernel (0 = the round-4
-  // V2, 2 = row-K only, 8 = transposed C only, 10 = the product)
+  // V2, 2 = row-K only, 4 = pixel-major C only, 6 = the product)
   const int cv = alt_variant() == 3 ? (kCvSplit | kCvRowK) : alt2_cv();
   if (cv != kAltProdCV) {
     const dim3 g((unsigned)grid);
@@ -1042,7 +1256,7 @@ int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int*
       case kCvSplit | kCvRowK: corr_alt2_kernel<kCvSplit | kCvRowK><<<g, 256, kB2Lds, stream>>>(a); break;
       case 0: corr_alt2_kernel<0><<<g, 256, kB2Lds, stream>>>(a); break;
       case kCvRowK: corr_alt2_kernel<kCvRowK><<<g, 256, kB2Lds, stream>>>(a); break;
-      default: corr_alt2_kernel<kCvTrans><<<g, 256, kB2Lds, stream>>>(a); break;
+      default: corr_alt2_kernel<kCvPm><<<g, 256, kB2Lds, stream>>>(a); break;
     }
     DROID_LAUNCH_CHECK();
     return kOk;
@@ -1064,13 +1278,13 @@ int droid_alt_set_chunk(int edges) {
 // A/B hook: 2 = corr_alt2_kernel (the product kernel); in the A/B build only:
 // 1 = the one-workgroup-per-CU kernel, 3 = corr_alt2_kernel<V3>, and the
 // round-5 pieces apart - 4 = the round-4 V2 (CV 0), 5 = row-K lookup tile only
-// (CV 2), 6 = transposed C only (CV 8); env DROID_ALT_VARIANT / DROID_ALT2_CV
+// (CV 2), 6 = pixel-major C only (CV 4); env DROID_ALT_VARIANT / DROID_ALT2_CV
 // set the initial values there
 int droid_alt_set_variant(int v) {
   if (v < 1 || v > 6) return fail(kInvalidArgument, "alt_set_variant: 1 .. 6");
   if (!DROID_AB && v != 2) return fail(kUnsupported, "alt_set_variant: variants other than 2 ship in the A/B build only (make ab)");
 #if DROID_AB
-  static const int cvs[7] = {0, 0, kAltProdCV, 0, 0, kCvRowK, kCvTrans};
+  static const int cvs[7] = {0, 0, kAltProdCV, 0, 0, kCvRowK, kCvPm};
   alt2_cv() = v == 2 || v >= 4 ? cvs[v] : alt2_cv();
   alt_variant() = v >= 4 ? 2 : v;
 #else

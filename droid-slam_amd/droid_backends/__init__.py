@@ -311,7 +311,7 @@ def chol_set_fault_inject(mode):
 def alt_set_variant(v):
     """A/B hook (droid_alt_set_variant): 2 = corr_alt2_kernel (the product); the A/B
     build adds 1 = corr_alt_ce0_kernel, 3 = corr_alt2_kernel<V3>, 4 = the round-4 V2,
-    5 = V2 with the row-K lookup tile, 6 = V2 with the transposed rotated C."""
+    5 = V2 with the row-K lookup tile, 6 = V2 with the pixel-major C layout."""
     check(lib.droid_alt_set_variant(int(v)), "alt_set_variant")
 
 

@@ -93,7 +93,7 @@ int droid_alt_set_profile(void* buf);
 /* A/B hook for the on-demand lookup: 2 = corr_alt2_kernel (two 4-wave
  * workgroups per CU, the product).  The A/B build (make ab) adds 1 =
  * corr_alt_ce0_kernel (one 8-wave workgroup per CU), 3 = the V3 C split, 4 =
- * the round-4 corr_alt2_kernel, 5 / 6 = its row-K lookup tile / transposed C
+ * the round-4 corr_alt2_kernel, 5 / 6 = its row-K lookup tile / pixel-major C
  * alone.  1, 4 and 6 are bitwise equal; 2, 3 and 5 are bitwise equal and
  * differ from the first set by corr_encoder[0]'s K order only (a few ulps);
  * the other values return kUnsupported in the product library. */

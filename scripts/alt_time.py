@@ -31,7 +31,7 @@ def timed(**kw):
 
 outs = {}
 # droid_alt_set_variant: 2 = the product; the A/B build (DROID_HIP_LIB=.../lib/ab/libdroid_hip.so)
-# adds 1 = the one-workgroup kernel, 4 = the round-4 corr_alt2_kernel, 6 = its transposed C
+# adds 1 = the one-workgroup kernel, 4 = the round-4 corr_alt2_kernel, 6 = its pixel-major C
 # alone, 5 = its row-K lookup tile alone, 3 = V3
 variants = (1, 4, 6, 5, 3, 2) if droid_backends.AB_BUILD else (2,)
 for variant in variants:

@@ -369,9 +369,9 @@ def test_corr_alt_ce0_matches_volume_path(noise, H, W, E):
 def test_corr_alt2_bitwise_equals_alt1(noise, H, W, E, far, ab_backends):
     """The round-4 corr_alt2_kernel (two 4-wave workgroups per CU, C in place,
     merged level-3/2/1 stage, group fallbacks; A/B variant 4) and its round-5
-    transposed, rotated C layout alone (variant 6) compute every value with the
-    same operations in the same order as corr_alt_ce0_kernel: outputs bitwise
-    equal.  The product (transposed C + row-K lookup tile) is checked against
+    pixel-major C layout alone (variant 6) compute every value with the same
+    operations in the same order as corr_alt_ce0_kernel: outputs bitwise
+    equal.  The product (pixel-major C + row-K lookup tile) is checked against
     them in test_corr_alt2_v3_matches_v2.  far: fraction of pixels thrown
     30-200 px off the map (windows partly or wholly outside, boxes over the
     region -> half / quadrant / pixel groups)."""
@@ -413,8 +413,8 @@ def test_corr_alt2_bitwise_equals_alt1(noise, H, W, E, far, ab_backends):
 @pytest.mark.parametrize("noise,H,W,E,far", [(1.5, 16, 24, 6, 0.0), (40.0, 16, 24, 6, 0.0), (1.5, 48, 64, 300, 0.0),
                                              (4.0, 48, 64, 200, 0.1), (0.3, 32, 64, 64, 0.0)])
 def test_corr_alt2_v3_matches_v2(noise, H, W, E, far, ab_backends):
-    """The product corr_alt2_kernel (round 5: transposed C MFMA with rotated
-    8-B C stores, lookup tile in the k = 8 iy + ix order with the encoder
+    """The product corr_alt2_kernel (round 5: C pixel-major with 8-B C
+    stores and dword window-row reads, lookup tile in the k = 8 iy + ix order with the encoder
     weights permuted to match) and the A/B kernels that share its lookup-tile
     order - V3 (box blocks split over the waves) and the row-K tile alone
     (variant 5) - are bitwise equal to each other: their C values and bilinear
