@@ -323,12 +323,14 @@ def test_flow_encoder0(E, H, W):
     np.testing.assert_allclose(host(out.float()), host(ref), atol=2e-3 * max(1.0, float(ref.abs().max())), rtol=2e-3)
 
 
-@pytest.mark.parametrize("noise,H,W,E", [(1.5, 16, 24, 6), (40.0, 16, 24, 6), (1.5, 48, 64, 300), (8.0, 48, 64, 300)])
+@pytest.mark.parametrize("noise,H,W,E", [(1.5, 16, 24, 6), (40.0, 16, 24, 6), (1.5, 48, 64, 300), (8.0, 48, 64, 300),
+                                         (40.0, 48, 64, 48)])
 def test_corr_alt_ce0_matches_volume_path(noise, H, W, E):
     """On-demand correlation (feature pyramid, MFMA) + corr_encoder[0] == the
     volume lookup + corr_encoder[0] up to fp16 rounding of the pooled levels
     (modules/corr.py: CorrBlock vs AltCorrBlock semantics).  Coherent windows /
-    incoherent (half, quadrant and pixel fallbacks); at 48x64 with 300 edges
+    incoherent (half, quadrant and pixel fallbacks; at 48x64 with noise 40 for
+    the product's pixel-major C and window table on every fallback path); at 48x64 with 300 edges
     every workgroup walks many tiles (the cross-tile pipeline)."""
     import droid_backends
     from droid_mi355x.corr import AltCorrBlock, CorrBlock
