@@ -10,8 +10,8 @@
 // gathered from a 51 GB volume whose 16-B window rows make the lookup
 // DRAM-burst bound.
 //
-// The product kernel is corr_alt2_kernel (two 4-wave workgroups per CU, its
-// design note below).  It refines the round-2 kernel described here,
+// The product kernel is corr_alt2_kernel<kAltProdCV> (two 4-wave workgroups
+// per CU, its design note below; round 5: C pixel-major, row-K lookup tile).  It refines the round-2 kernel described here,
 // corr_alt_ce0_kernel (now in ab/, the A/B build only; bitwise-equal outputs):
 // persistent, one 8-wave workgroup per CU, software pipelined over "stages" =
 // (8x8-pixel query tile of one edge, pyramid level):
@@ -240,6 +240,12 @@ __device__ __forceinline__ void alt_box_mfma(const char* lds, int box, _Float16*
 // so the pass adds exactly 0 to them).  Every value is computed by the same
 // operations in the same order as corr_alt_ce0_kernel: the outputs are
 // bitwise equal (tests/test_gpu_fused.py).
+// The layout above is the round-4 kernel's (A/B variant 4).  The round-5
+// product (kCvRowK | kCvPm, see kAltProdCV) keeps the box rows but stores C
+// pixel-major past the box's use - C(p, t) at byte p S + 2 t (b2_cstride) -
+// puts the lookup tiles in a dense 128-B-per-pixel area from kB2Lk (k = 8 iy +
+// ix order, one 16-B store per window row) and the per-pixel window table at
+// kB2Win; see the notes at b2_corr and b2_bl_prep and DESIGN.md §3.
 // ===========================================================================
 constexpr int kB2Rows = 304;
 constexpr int kB2Coord = kB2Rows * 256;       // [2 slots][64 px] float2
