@@ -552,12 +552,12 @@ def main():
         else:
             roofline, lookup_roof = lookup_roof, None
         if args.lowmem or args.corr == "pyramid":
-            lookup_roof["kernel"] = ("corr_alt_ce0_kernel (on-demand 4-level correlation windows on MFMA from the "
+            lookup_roof["kernel"] = ("corr_alt2_kernel (on-demand 4-level correlation windows on MFMA from the "
                                      "feature pyramid, fused with corr_encoder[0] 1x1 196->128)")
             lookup_roof["algorithmic_bytes_per_launch"] = ALT_BYTES_PER_EDGE * e_local
             lookup_roof["achieved"] = ALT_BYTES_PER_EDGE * e_local / (lookup_ms * 1e-3) / 1e9 if lookup_ms else None
             lookup_roof["frac"] = lookup_roof["achieved"] / PEAK_HBM_GBS if lookup_ms else None
-            lookup_roof["traffic"] = load_traffic("corr_alt", e_local, "corr_alt_ce0_kernel")
+            lookup_roof["traffic"] = load_traffic("corr_alt", e_local, "corr_alt2_kernel")
         result = {
             "metric": ("factor_graph.update_lowmem() steps/sec at 256 KF x 2k edges, 384x512" if args.lowmem else "factor_graph.update() iters/sec at 256 KF x 2k edges, 384x512" if args.config == "C3"
                        else "factor_graph.update() iters/sec, C5 %d KF x %d edges, 384x512" % (args.frames, len(ii))
