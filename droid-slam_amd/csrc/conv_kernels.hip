@@ -2284,6 +2284,209 @@ __global__ void __launch_bounds__(4 * TP) flow_enc0_kernel(const float* __restri
   }
 }
 
+// Round 5: the same conv with the weights resident in VGPRs - the product's
+// 256-pixel tile (flow_enc0_kernel<256>, above, stays in the A/B build as
+// droid_fe_set_variant(0)).  There every one of the 16 waves re-reads its half
+// of the weights (64 channels x K 224, 28 KB) from LDS for every tile, ~700 KB
+// of LDS reads per 256-pixel tile with the A fragments for 896 MFMAs.  Here 8
+// waves, wave (wm, wn) = 128 pixels x 32 channels (WN = 4), hold their 14 B
+// fragments (56 VGPRs, loaded once per workgroup straight from the ABI
+// layout), so a tile's LDS traffic is the A fragments and the output staging.
+// C3: 0.440-0.444 vs 0.490-0.498 ms (profiles/r05/r05ac_fe_ab.txt); WN = 2
+// (64 x 64 per wave, half the A reads) needs 254 VGPRs and measured 0.484.  The
+// K order, the operands and the epilogue are those of flow_enc0_kernel: the
+// outputs are bitwise the same (test_flow_encoder0_resident_weights_bitwise).
+template <int TP, int WN>
+__global__ void __launch_bounds__(512) flow_enc0_rw_kernel(const float* __restrict__ motn,
+                                                           const __half* __restrict__ w,
+                                                           const float* __restrict__ bias, __half* __restrict__ out,
+                                                           int H, int W, long ntiles) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 smem_fe[];
+  // WN channel waves x WM pixel waves: wave (wm, wn) = TP / WM pixels (FP fragments) x 128 / WN channels (NJ)
+  constexpr int NT = 512, WM = 8 / WN, FP = TP / (16 * WM), NJ = 128 / (16 * WN), CW = 128 / WN;
+  static_assert(WM * WN == 8 && FP * 16 * WM == TP && NJ >= 1, "flow_enc0_rw: wave grid");
+  const int RB = TP / W + 6, PW = W + 8;
+  _Float16* In = smem_fe;                    // [RB][PW][4]
+  _Float16* Os = In + RB * PW * 4;           // [TP][kFeOS]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int HW = H * W, tpe = HW / TP;
+  const int wm = wave / WN, wn = wave % WN, fr = lane & 15, fq = lane >> 4;
+  // B fragment (ks, j): channel wn*64 + 16 j + fr, kernel row ks, taps 2 fq and
+  // 2 fq + 1 (4 channels each; the row's eighth tap is zero)
+  half8 wf[7][NJ];
+#pragma unroll
+  for (int ks = 0; ks < 7; ++ks)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const __half* wr = w + (wn * CW + j * 16 + fr) * kFeK + (ks * 7 + 2 * fq) * 8;
+      const uint2 lo = *reinterpret_cast<const uint2*>(wr);
+      const uint2 hi = fq < 3 ? *reinterpret_cast<const uint2*>(wr + 8) : make_uint2(0, 0);
+      wf[ks][j] = __builtin_bit_cast(half8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+    }
+  for (int idx = tid; idx < RB * PW; idx += NT)
+    *reinterpret_cast<uint2*>(&In[idx * 4]) = make_uint2(0, 0);  // padding columns stay zero
+  const int nin = (RB * W + NT - 1) / NT;  // <= 2 for TP = 256, W <= 128
+  float v[2][4];
+  auto load_in = [&](long t) {
+    const long e = t / tpe;
+    const int y0 = (int)(t - e * tpe) * (TP / W);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + NT * u;
+      const int ry = idx / W, x = idx - ry * W, y = y0 - 3 + ry;
+      const bool ok = u < nin && ry < RB && t < ntiles && y >= 0 && y < H;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[u][c] = ok ? motn[(e * 4 + c) * HW + (long)y * W + x] : 0.f;
+    }
+  };
+  auto store_in = [&]() {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + NT * u;
+      const int ry = idx / W, x = idx - ry * W;
+      if (u < nin && ry < RB) {
+        half4_t h;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) h[c] = (_Float16)v[u][c];
+        *reinterpret_cast<half4_t*>(&In[(ry * PW + x + 3) * 4]) = h;
+      }
+    }
+  };
+  floatx4 bj[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) bj[j] = *reinterpret_cast<const floatx4*>(bias + wn * CW + j * 16 + fq * 4);
+  int pyx[FP];  // band slot of the lane's pixel in fragment f, at tap (-3,-3)
+#pragma unroll
+  for (int f = 0; f < FP; ++f) {
+    const int p = wm * 16 * FP + f * 16 + fr;
+    pyx[f] = (p / W) * PW + (p % W);
+  }
+  long t = blockIdx.x;
+  load_in(t);
+  __syncthreads();
+  for (; t < ntiles; t += gridDim.x) {
+    store_in();
+    __syncthreads();
+    load_in(t + gridDim.x);
+    floatx4 acc[FP][NJ];
+#pragma unroll
+    for (int f = 0; f < FP; ++f)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[f][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 7; ++ks) {
+      half8 af[FP];
+#pragma unroll
+      for (int f = 0; f < FP; ++f) {
+        const uint2* src = reinterpret_cast<const uint2*>(&In[(pyx[f] + ks * PW + 2 * fq) * 4]);
+        const uint2 lo = src[0], hi = src[1];
+        af[f] = __builtin_bit_cast(half8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+#pragma unroll
+      for (int f = 0; f < FP; ++f)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][j], af[f], acc[f][j], 0, 0, 0);
+      // one kernel row's A fragments live at a time (hoisting all seven rows'
+      // loads ahead of the MFMAs spilled the resident weights)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int f = 0; f < FP; ++f)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        half4_t o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = (_Float16)fmaxf(acc[f][j][k] + bj[j][k], 0.f);
+        *reinterpret_cast<half4_t*>(&Os[(wm * 16 * FP + f * 16 + fr) * kFeOS + wn * CW + j * 16 + fq * 4]) = o;
+      }
+    __syncthreads();
+    const long e = t / tpe;
+    const long pix0 = e * HW + (t - e * tpe) * TP;
+    for (int idx = tid; idx < TP * 16; idx += NT) {
+      const int r = idx >> 4, q = idx & 15;
+      const uint4 ov = *reinterpret_cast<const uint4*>(&Os[r * kFeOS + q * 8]);
+      *reinterpret_cast<uint4*>(out + (pix0 + r) * 128 + q * 8) = ov;
+    }
+  }
+}
+
+constexpr int kFeRwWN = 4;   // channel waves of flow_enc0_rw_kernel (2: 254 VGPRs and slower)
+__host__ __device__ constexpr int fe_rw_lds_bytes(int W, int TP) {
+  return (TP / W + 6) * (W + 8) * 8 + TP * kFeOS * 2;
+}
+template <int WN>
+static int launch_fe_rw(const float* motn, const void* w, const float* bias, void* out, int H, int W, long ntiles,
+                         long grid, hipStream_t stream) {
+  static bool attr = false;  // one per instantiation
+  if (!attr) {
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&flow_enc0_rw_kernel<256, WN>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    attr = true;
+  }
+  flow_enc0_rw_kernel<256, WN><<<dim3((unsigned)grid), 512, fe_rw_lds_bytes(W, 256), stream>>>(
+      motn, (const __half*)w, bias, (__half*)out, H, W, ntiles);
+  return kOk;
+}
+
+// GraphAgg's eta head (droid_net.py:48-50: a 3x3 conv 128 -> 1 on the
+// aggregated map; the conv_nhwc_f16 entry with Cout == 1 at W == 64).  The
+// generic 128 x 16 tile spends 18 barrier-separated K stages on one output
+// channel (0.17 ms per update at C3, latency-bound).  Here the conv is the 1x1
+// projection onto the nine taps, Y(q, t) = w_t . x(q) (MFMA, K = 128, N = 16 with
+// taps 9..15 zero), over the band of rows y0 - 1 .. y0 + R of one frame, loaded
+// straight from global memory into the A fragments; then each output pixel
+// sums its nine shifted taps from LDS (zero outside the image) and adds the
+// bias.  One pass over the input (+2/R for the halo rows), fp32 sums, one fp16
+// rounding - as the generic tile, in another order.
+constexpr int kEtaR = 4, kEtaYS = 17;
+__global__ void __launch_bounds__(256) eta_conv_kernel(const __half* __restrict__ x, int cstride,
+                                                       const __half* __restrict__ wp, const float* __restrict__ bias,
+                                                       __half* __restrict__ out, int out_cstride, int out_coff, int H) {
+  constexpr int W = 64, NF = (kEtaR + 2) * W / 16;   // band fragments of 16 pixels (24)
+  __shared__ float Ys[(kEtaR + 2) * W * kEtaYS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int bands = H / kEtaR;
+  const int b = blockIdx.x / bands, y0 = (blockIdx.x - b * bands) * kEtaR;
+  // B fragment s: tap fr (zero past 8) x channels 32 s + 8 fq .. + 7 (packed
+  // weights: [chunk][tap][64], pack_conv)
+  half8 wf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    wf[s] = fr < 9 ? *reinterpret_cast<const half8*>(wp + ((s >> 1) * 9 + fr) * 64 + (s & 1) * 32 + 8 * fq)
+                   : half8{};
+#pragma unroll
+  for (int i = 0; i < NF / 4; ++i) {
+    const int fgi = wave + 4 * i;
+    const int bp = fgi * 16 + fr;               // band pixel of the lane's A row
+    const int y = y0 - 1 + bp / W;
+    const bool ok = y >= 0 && y < H;
+    const __half* src = x + ((long)(b * H + (ok ? y : 0)) * W + (bp % W)) * cstride + 8 * fq;
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const half8 af = ok ? *reinterpret_cast<const half8*>(src + 32 * s) : half8{};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, wf[s], acc, 0, 0, 0);
+    }
+    // D: column fr = tap, rows 4 fq .. + 3 = the fragment's pixels
+    if (fr < 9) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) Ys[(fgi * 16 + 4 * fq + k) * kEtaYS + fr] = acc[k];
+    }
+  }
+  __syncthreads();
+  const int r = tid / W, xx = tid - r * W;     // output pixel (row y0 + r)
+  float sum = 0.f;
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int xs = xx + dx;
+      if (xs >= 0 && xs < W) sum += Ys[((r + 1 + dy) * W + xs) * kEtaYS + (dy + 1) * 3 + dx + 1];
+    }
+  if (bias) sum += bias[0];
+  out[((long)(b * H + y0 + r) * W + xx) * out_cstride + out_coff] = (__half)sum;
+}
+
 // The delta / weight heads' finish (droid_net.py:128-132 + factor_graph.py:
 // 209-211) in one pass over the fused head output: head (E,HW,4) f32 = the raw
 // 3x3 head sums [du, dv, wu, wv] (droid_conv_dw_head_f16), b [4]:
@@ -2435,6 +2638,16 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
     return fail(kInvalidArgument, "conv_nhwc_f16: out32 is null");
   if (a.stage_out && out && (reinterpret_cast<uintptr_t>(out) & 15)) a.stage_out = 0;
   if (B == 0) return kOk;
+  // the one-output-channel 3x3 conv (GraphAgg's eta head) at W == 64
+  if (!wt && ks == 3 && Cout == 1 && nsrc == 1 && C[0] == 128 && epi == EPI_ACT && act == 0 && !bbias && W == 64 &&
+      H % kEtaR == 0 && (cstride[0] % 8) == 0) {
+    const long nwg = (long)B * (H / kEtaR);
+    if (nwg > 0x7fffffffL) return fail(kUnsupported, "conv_nhwc_f16: problem too large");
+    eta_conv_kernel<<<dim3((unsigned)nwg), 256, 0, stream>>>((const __half*)srcs[0], cstride[0], (const __half*)wp,
+                                                            bias, (__half*)out, out_cstride, out_coff, H);
+    DROID_LAUNCH_CHECK();
+    return kOk;
+  }
   // 3x3 (and larger) convs over wide-enough outputs take the LDS-halo kernel;
   // DROID_CONV_HALO=0 / 4 / 8 (default) selects none / 4-wave / 8-wave tiles;
   // DROID_CONV_ROWS=0 disables the row-band variant.
@@ -2737,6 +2950,20 @@ int droid_glo_gates_f32(const float* part, int splits, const float* w, const flo
 // flow_encoder[0] (flow_enc0_kernel): motn (E,4,H,W) f32, w [128][416] fp16
 // (column t*8 + c = weight[co][c][t/7][t%7] for t < 49, c < 4; else zero), bias
 // [128] f32 -> out (E,H,W,128) fp16 = relu(conv7x7(motn) + bias).
+#if DROID_AB
+// A/B build only: the 256-pixel flow_enc0 tile, 1 = flow_enc0_rw_kernel (the
+// product's, weights in VGPRs), 0 = flow_enc0_kernel<256> (weights in LDS)
+static int& fe_variant() {
+  static int v = ab_knob("DROID_FE_VARIANT", 1);
+  return v;
+}
+int droid_fe_set_variant(int v) {
+  const int prev = fe_variant();
+  fe_variant() = v ? 1 : 0;
+  return prev;
+}
+#endif
+
 int droid_flow_enc0_f16(const float* motn, const void* w, const float* bias, void* out, int E, int H, int W,
                         hipStream_t stream) {
   if (E < 0 || H <= 0 || W <= 0 || !motn || !w || !bias || !out || (reinterpret_cast<uintptr_t>(bias) & 15))
@@ -2748,17 +2975,24 @@ int droid_flow_enc0_f16(const float* motn, const void* w, const float* bias, voi
   if (!attr) {
     DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&flow_enc0_kernel<128>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+#if DROID_AB
     DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&flow_enc0_kernel<256>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+#endif
     attr = true;
   }
   // DROID_FE_TP=128: the 128-pixel tile on a shape that allows 256 (A/B runs)
   static const int tp_env = ab_knob("DROID_FE_TP", 256);
-  if (tp_env == 256 && (H * W) % 256 == 0 && fe_lds_bytes(W, 256) <= kLdsMax) {
+  if (tp_env == 256 && (H * W) % 256 == 0 && fe_rw_lds_bytes(W, 256) <= kLdsMax) {
     const long ntiles = (long)E * H * W / 256;
     const long grid = std::min<long>(ntiles, device_cu_count());
-    flow_enc0_kernel<256><<<dim3((unsigned)grid), 1024, fe_lds_bytes(W, 256), stream>>>(
-        motn, (const __half*)w, bias, (__half*)out, H, W, ntiles);
+#if DROID_AB
+    if (fe_variant() == 0)   // the round-4 tile: 16 waves, weights in LDS
+      flow_enc0_kernel<256><<<dim3((unsigned)grid), 1024, fe_lds_bytes(W, 256), stream>>>(
+          motn, (const __half*)w, bias, (__half*)out, H, W, ntiles);
+    else
+#endif
+      launch_fe_rw<kFeRwWN>(motn, w, bias, out, H, W, ntiles, grid, stream);
   } else {
     const long ntiles = (long)E * H * W / 128;
     const long grid = std::min<long>(ntiles, device_cu_count());

@@ -150,6 +150,30 @@ def test_conv64_matches_fp32_conv(B, H, splits):
     np.testing.assert_allclose(host(out.float()), host(ref), atol=4e-3, rtol=1e-3)
 
 
+@pytest.mark.parametrize("B,H,cstride,off,bias", [(3, 8, 128, 0, True), (2, 48, 136, 8, True), (5, 4, 128, 0, False),
+                                                  (256, 48, 128, 0, True)])
+def test_eta_conv_matches_fp32_conv(B, H, cstride, off, bias):
+    """GraphAgg's eta head shape (3x3 128 -> 1, droid_net.py:48-50; eta_conv_kernel,
+    the conv_nhwc_f16 path for Cout == 1 at W = 64) vs the fp32 conv of the same
+    fp16 operands: image-edge taps zero, a strided / offset source, no bias, the
+    C3 frame count; the fp16 output rounding is the only error."""
+    import droid_backends
+    from droid_mi355x.fused import pack_conv
+    W = 64
+    g = torch.Generator(device=DEV).manual_seed(B + H)
+    xb = torch.randn((B, H, W, cstride), generator=g, device=DEV).half()
+    x = xb[..., off:off + 128]
+    w = torch.randn((1, 128, 3, 3), generator=g, device=DEV) / 34.0
+    b = torch.randn(1, generator=g, device=DEV) if bias else None
+    out = torch.full((B, H, W, 1), float("nan"), dtype=torch.float16, device=DEV)
+    droid_backends.conv_nhwc_f16([(xb, off, 128)], pack_conv(w, [128]), 1, 3, bias=b, out=out)
+    ref = _ref([x], w, b)
+    err = (out.float() - ref).abs()
+    assert float(err.max()) <= 2e-3 * max(1.0, float(ref.abs().max())), float(err.max())
+    assert torch.equal(out, droid_backends.conv_nhwc_f16([(xb, off, 128)], pack_conv(w, [128]), 1, 3, bias=b,
+                                                         out=torch.empty_like(out)))
+
+
 def test_corr_lookup_ce0_cooperative_gather_deterministic():
     """The fused lookup's cooperative gather (csrc/corr_kernels.hip, DROID_CE0_COOP)
     parks each pixel's coordinates in LDS between its issue and bilinear steps:

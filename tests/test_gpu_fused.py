@@ -310,8 +310,8 @@ def test_gru_global_context(E, H, W):
 @pytest.mark.parametrize("E,H,W", [(3, 8, 32), (2, 48, 64), (2, 4, 128), (3, 4, 32), (5, 12, 32)])
 def test_flow_encoder0(E, H, W):
     """relu(conv7x7(motn.half()) + b) (droid_net.py:88-90 under autocast) vs torch fp32.
-    H*W % 256 == 0 runs the 256-pixel / 16-wave tile, the (3, 4, 32) and (5, 12, 32)
-    shapes the 128-pixel / 8-wave one."""
+    H*W % 256 == 0 runs the 256-pixel tile (flow_enc0_rw_kernel, weights in VGPRs),
+    the (3, 4, 32) and (5, 12, 32) shapes the 128-pixel / 8-wave one."""
     import droid_backends
     from droid_mi355x.fused import pack_flow_enc0
     g = torch.Generator(device=DEV).manual_seed(24)
@@ -321,6 +321,31 @@ def test_flow_encoder0(E, H, W):
     out = droid_backends.flow_enc0_f16(motn, pack_flow_enc0(w), b)
     ref = F.relu(F.conv2d(motn.half().float(), w.half().float(), b, padding=3)).permute(0, 2, 3, 1)
     np.testing.assert_allclose(host(out.float()), host(ref), atol=2e-3 * max(1.0, float(ref.abs().max())), rtol=2e-3)
+
+
+@pytest.mark.parametrize("E,H,W", [(3, 8, 32), (2, 48, 64), (2, 4, 128), (3, 16, 16), (300, 48, 64)])
+def test_flow_encoder0_resident_weights_bitwise(E, H, W, ab_backends):
+    """flow_enc0_rw_kernel (the product's 256-pixel tile: 8 waves, weights in
+    VGPRs) multiplies the same operands in the same K order as the round-4
+    flow_enc0_kernel (16 waves, weights in LDS; A/B build, droid_fe_set_variant(0)):
+    bitwise the same outputs, including a persistent walk over many tiles."""
+    import ctypes
+    import droid_backends
+    from droid_mi355x.fused import pack_flow_enc0
+    g = torch.Generator(device=DEV).manual_seed(25 + W)
+    motn = (8 * torch.randn((E, 4, H, W), generator=g, device=DEV)).clamp(-64, 64)
+    wp = pack_flow_enc0(torch.randn((128, 4, 7, 7), generator=g, device=DEV) / 14.0)
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    out = droid_backends.flow_enc0_f16(motn, wp, b)
+    set_v = ab_backends.lib.droid_fe_set_variant
+    set_v.argtypes, set_v.restype = [ctypes.c_int], ctypes.c_int
+    prev = set_v(0)
+    try:
+        ref = ab_backends.flow_enc0_f16(motn, wp, b)
+    finally:
+        set_v(prev)
+    assert torch.equal(out, ref)
+    assert torch.equal(out, ab_backends.flow_enc0_f16(motn, wp, b))
 
 
 @pytest.mark.parametrize("noise,H,W,E", [(1.5, 16, 24, 6), (40.0, 16, 24, 6), (1.5, 48, 64, 300), (8.0, 48, 64, 300),
