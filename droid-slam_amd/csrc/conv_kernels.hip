@@ -1351,7 +1351,7 @@ struct MfmaReadPairs<0> {
   static __device__ __forceinline__ void emit() {}
 };
 
-template <int TMX, int TN, bool DWHEAD, bool ILV, int EPI, int NW = 8>
+template <int TMX, int TN, bool DWHEAD, bool ILV, int EPI, int NW = 8, bool PAIR = false>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 ? 1 : 2, NW == 4 ? 1 : 2)))
 conv_band_kernel(ConvArgs a) {
   using BP = Band<TMX, TN, NW>;
@@ -1372,8 +1372,8 @@ conv_band_kernel(ConvArgs a) {
   const long band0 = m0 - W;  // pixel index of the band's first (halo) row
   const int nslot = a.nslot, nhi = a.nhi;
   const int hbytes = nhi * NW * 1024;  // one band buffer
-  char* Bl = lds;                     // [2][TN][128 B]
-  char* Hl = lds + 2 * TN * 128;      // [2][nhi * 64 slots][128 B]
+  char* Bl = lds;                     // [2][TN][128 B]  (PAIR: [2][2 taps][TN][128 B])
+  char* Hl = lds + (PAIR ? 4 : 2) * TN * 128;      // [2][nhi * 64 slots][128 B]
 
   // ---- DMA lane geometry: instruction q of this wave covers 8 LDS rows of
   // 128 B; lane l writes row 8*(wave + 8q) + (l >> 3), 16-B slot l & 7, which
@@ -1473,8 +1473,23 @@ conv_band_kernel(ConvArgs a) {
     prof[0] = (long long)hwid | ((long long)(xcc & 15) << 32);
     prof[1] = (long long)__builtin_amdgcn_s_memtime();
   }
+  // PAIR: the weights of two-tap stage (ch, u) - taps 2u and 2u + 1 (u = 4: tap
+  // 8 alone) - into tap blocks 0 / 1 of the double buffer of stage position sp
+  auto issue_pair = [&](int ch, int u, int sp) {
+    const unsigned dst = Bl_a + (sp & 1) * 2 * TN * 128;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int tap = 2 * u + k;
+      if (tap < 9) {
+#pragma unroll
+        for (int q = 0; q < NBI; ++q)
+          dma16(rsb, dst + k * TN * 128 + (wave_u + NW * q) * 1024, boff[q] + (ch * 9 + tap) * BK * 2);
+      }
+    }
+  };
   issue_halo(0);
-  issue_b(0);
+  if constexpr (PAIR) issue_pair(0, 0, 0);
+  else issue_b(0);
   // column tid's bias (+ per-image bias), loaded now so the latency hides under
   // the main loop; the epilogue shares them through LDS
   float bcol = 0.f;
@@ -1576,6 +1591,56 @@ conv_band_kernel(ConvArgs a) {
       stage(std::integral_constant<int, 6>{});
       stage(std::integral_constant<int, 7>{});
       stage(std::integral_constant<int, 8>{});
+    }
+  } else if constexpr (PAIR) {
+    // Two-tap stages (the 64-channel 384-row tile, flow_encoder[2]): 5 barriers
+    // per chunk instead of 9, each over 2 x 24 MFMAs per wave (the one-tap
+    // stage's fixed costs - barrier, waits, DMA issue - were a third of its
+    // time); the double-buffered weights are two tap blocks per stage, which
+    // fills the LDS exactly (32 + 128 KB).  Same products in the same order per
+    // accumulator: bitwise the one-tap kernel.
+    static_assert(ILV && NW == 8 && TN == 64, "two-tap stages: the 64-channel interleaved tile");
+    auto tap_mfma = [&](const char* Hb, const char* Bb, int ty, int tx) {
+      __builtin_amdgcn_sched_barrier(0);
+      half8 af[2][FM], bf[2][FN];
+#pragma unroll
+      for (int hk = 0; hk < 2; ++hk) {
+        auto aptr = [&](int i) { return Hb + abase[i % NPAR][tx + 1][hk] + ty * rowb + (i / NPAR) * 8192; };
+        af[hk][0] = *reinterpret_cast<const half8*>(aptr(0));
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[hk][j] = *reinterpret_cast<const half8*>(Bb + bbase[hk] + j * 2048);
+#pragma unroll
+        for (int i = 1; i < FM; ++i) af[hk][i] = *reinterpret_cast<const half8*>(aptr(i));
+      }
+#pragma unroll
+      for (int hk = 0; hk < 2; ++hk)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[hk][j], af[hk][i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, FM + FN, 0);
+      MfmaReadPairs<FM + FN>::emit();
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * FM * FN - (FM + FN), 0);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    const int nsp = nch * 5;
+    int sp = 0;
+    for (int ch = 0; ch < nch; ++ch) {
+      const char* Hb = Hl + (ch & 1) * hbytes;
+#pragma unroll
+      for (int u = 0; u < 5; ++u, ++sp) {
+        // this stage's weights (and at u == 0 this chunk's band) must have
+        // landed; at u == 1 the next chunk's band (issued after them) may stay in flight
+        wait_vmcnt((u == 1 && ch + 1 < nch) ? nhi : 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (sp + 1 < nsp) issue_pair(u < 4 ? ch : ch + 1, u < 4 ? u + 1 : 0, sp + 1);
+        if (u == 0 && ch + 1 < nch) issue_halo(ch + 1);
+        const char* Bb = Bl + (sp & 1) * 2 * TN * 128;
+        tap_mfma(Hb, Bb, (2 * u) / 3 - 1, (2 * u) % 3 - 1);
+        if (u < 4) tap_mfma(Hb, Bb + TN * 128, (2 * u + 1) / 3 - 1, (2 * u + 1) % 3 - 1);
+      }
     }
   } else {
   int st = 0;
@@ -1686,16 +1751,24 @@ static bool band_fits(int W, int* nslot, int* nhi) {
   return true;
 }
 
-template <int TMX, int TN, bool DWHEAD, bool ILV, int EPI, int NW = 8>
+template <int TMX, int TN, bool DWHEAD, bool ILV, int EPI, int NW = 8, bool PAIR = false>
 static int launch_band_kernel(const ConvArgs& a, long nwg, int lds, hipStream_t stream) {
   static bool attr = false;  // one per instantiation
   if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN, DWHEAD, ILV, EPI, NW>),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    DROID_HIP_CHECK(hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv_band_kernel<TMX, TN, DWHEAD, ILV, EPI, NW, PAIR>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     attr = true;
   }
-  conv_band_kernel<TMX, TN, DWHEAD, ILV, EPI, NW><<<dim3((unsigned)nwg), NW * 64, lds, stream>>>(a);
+  conv_band_kernel<TMX, TN, DWHEAD, ILV, EPI, NW, PAIR><<<dim3((unsigned)nwg), NW * 64, lds, stream>>>(a);
   return kOk;
+}
+
+// the 64-channel 384-row tile's two-tap stages (flow_encoder[2]); DROID_CONV_PAIR=0
+// (A/B build) keeps the one-tap stages
+static int& band_pair() {
+  static int on = ab_knob("DROID_CONV_PAIR", 1);
+  return on;
 }
 
 static int& band2_mode();
@@ -1765,7 +1838,17 @@ static int launch_band(const ConvArgs& a0, hipStream_t stream) {
         else if (epi == EPI_GRU_QP) st = launch_band_kernel<TMX, TN, false, true, EPI_GRU_QP>(a, nwg, lds, stream);
         else if (epi == EPI_GRU_ZR) st = launch_band_kernel<TMX, TN, false, true, EPI_GRU_ZR>(a, nwg, lds, stream);
         else if (epi == EPI_GRU_ZRP) st = launch_band_kernel<TMX, TN, false, true, EPI_GRU_ZRP>(a, nwg, lds, stream);
-        else st = launch_band_kernel<TMX, TN, false, true, EPI_ACT>(a, nwg, lds, stream);
+        else if constexpr (TN == 64) {
+          // two-tap stages when the doubled weight buffer still fits (W == 64: exactly)
+          const int main_p = 4 * TN * 128 + 2 * a.nhi * 8 * 1024;
+          if (band_pair() && main_p <= kLdsMax)
+            st = launch_band_kernel<TMX, TN, false, true, EPI_ACT, 8, true>(a, nwg, main_p > epi_b ? main_p : epi_b,
+                                                                           stream);
+          else
+            st = launch_band_kernel<TMX, TN, false, true, EPI_ACT>(a, nwg, lds, stream);
+        } else {
+          st = launch_band_kernel<TMX, TN, false, true, EPI_ACT>(a, nwg, lds, stream);
+        }
       }
     }
     if (!ilv) {
@@ -2733,6 +2816,16 @@ int droid_conv_set_tile(int mode) {
   band2_mode() = mode;
   return prev;
 }
+
+#if DROID_AB
+// A/B build only (not in include/droid_backends.h): the 64-channel band tile's
+// two-tap stages (1, the product's) or one-tap stages (0); returns the previous
+int droid_conv_set_pair(int on) {
+  const int prev = band_pair();
+  band_pair() = on ? 1 : 0;
+  return prev;
+}
+#endif
 
 // Which kernel droid_conv_gru_pre_f16 runs for a ConvGRU gate conv (epi 1: z|r,
 // Cout 256; epi 2: q, Cout 128) over B images of H x W under the current tile

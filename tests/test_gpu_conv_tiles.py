@@ -150,6 +150,35 @@ def test_conv64_matches_fp32_conv(B, H, splits):
     np.testing.assert_allclose(host(out.float()), host(ref), atol=4e-3, rtol=1e-3)
 
 
+@pytest.mark.parametrize("B,H,splits", [(3, 8, [128]), (2, 12, [96, 64]), (64, 48, [128]), (1, 24, [64])])
+def test_conv64_two_tap_stages_bitwise(B, H, splits, ab_backends):
+    """The 64-channel band tile's two-tap stages (the product's: 5 barriers per
+    chunk, two tap blocks of weights per stage) sum the same products in the same
+    order as its one-tap stages (A/B build, droid_conv_set_pair(0)): bitwise the
+    same outputs, single- and multi-source, partial chunks, one-chunk inputs."""
+    import ctypes
+    import droid_backends
+    from droid_mi355x.fused import pack_conv
+    W, cout = 64, 64
+    g = torch.Generator(device=DEV).manual_seed(7 + H)
+    xs = [torch.randn((B, H, W, c), generator=g, device=DEV).half() for c in splits]
+    cin = sum(splits)
+    w = torch.randn((cout, cin, 3, 3), generator=g, device=DEV) / (cin * 9) ** 0.5
+    bias = torch.randn(cout, generator=g, device=DEV)
+    srcs = [(x, 0, c) for x, c in zip(xs, splits)]
+    out = droid_backends.conv_nhwc_f16(srcs, pack_conv(w, splits), cout, 3, bias=bias, act=1,
+                                       out=torch.empty((B, H, W, cout), dtype=torch.float16, device=DEV))
+    set_pair = ab_backends.lib.droid_conv_set_pair
+    set_pair.argtypes, set_pair.restype = [ctypes.c_int], ctypes.c_int
+    prev = set_pair(0)
+    try:
+        one = ab_backends.conv_nhwc_f16(srcs, pack_conv(w, splits), cout, 3, bias=bias, act=1,
+                                        out=torch.empty_like(out))
+    finally:
+        set_pair(prev)
+    assert torch.equal(out, one)
+
+
 @pytest.mark.parametrize("B,H,cstride,off,bias", [(3, 8, 128, 0, True), (2, 48, 136, 8, True), (5, 4, 128, 0, False),
                                                   (256, 48, 128, 0, True)])
 def test_eta_conv_matches_fp32_conv(B, H, cstride, off, bias):
