@@ -31,7 +31,7 @@ def per_kernel(counter):
         name = r["Kernel_Name"]
         key = ("copy" if name.startswith("__amd_rocclr_copyBuffer") and len(out.get("copy", [])) < 3 else
                "zr" if ("conv_band_kernel<256, 256, false, false, 6>" in name or
-                        "conv_band_kernel<256, 256, false, false, 6, 8>" in name) else
+                        "conv_band_kernel<256, 256, false, false, 6, 8" in name) else
                "lookup" if ("corr_ce0_kernel" in name or "corr_pyramid_f16_r3_kernel" in name) else
                "lookup_nchw" if "corr_lookup_coop_kernel" in name else
                "alt" if ("corr_alt_ce0_kernel" in name or "corr_alt2_kernel" in name) else None)
