@@ -444,6 +444,14 @@ def main():
     args.force_dist = os.environ.get("DROID_BENCH_FORCE_DIST") == "1"
     dist_on = world > 1 or args.force_dist
     if dist_on:
+        if world == 1 and "RANK" not in os.environ:
+            # a forced one-rank group started without a launcher: a local rendezvous
+            import socket
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+            os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(port))
         backend = os.environ.get("DROID_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)

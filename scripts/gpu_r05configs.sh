@@ -12,9 +12,11 @@ run() {  # name, args...
   timeout -k 10 400 "$@" > $O/bench_$n.json 2> $O/bench_$n.err || { tail -20 $O/bench_$n.err; exit 1; }
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(d['value'], 3), round(d['ms_per_step'], 3))" $O/bench_$n.json $n
 }
+if [ "${CFG_SKIP_DONE:-0}" != 1 ]; then
 run C2 python -u bench.py --config C2 --no-cpu-baseline
 run C4 python -u bench.py --config C4 --no-cpu-baseline
 run lowmem python -u bench.py --lowmem --no-cpu-baseline
 run 2rank env DROID_BENCH_ONE_DEVICE=1 DROID_BENCH_BACKEND=gloo python -u bench.py --gpus 2 --no-cpu-baseline
+fi
 run rccl1 env DROID_BENCH_FORCE_DIST=1 python -u bench.py --no-cpu-baseline
 run C5 python -u bench.py --config C5 --steps 3 --warmup 1 --no-cpu-baseline
