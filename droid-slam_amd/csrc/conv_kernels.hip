@@ -2107,23 +2107,25 @@ static int launch_band2_kernel(const ConvArgs& a0, hipStream_t stream) {
 // ConvGRU global context (modules/gru.py:19-32, the glo branch):
 //   glo[e][co] = mean over the edge's pixels of sigmoid(w . h + b)[co] * h[co]
 // for a 1x1 128 -> 128 conv w on the hidden state h itself.  One workgroup per
-// edge streams its pixels in 64-pixel tiles by LDS-DMA through a ring of 4
-// tile buffers, four tiles in flight (one in flight left the kernel latency
-// bound at ~2.5 TB/s); wave w keeps the weight fragments of its output columns
-// 32w .. 32w+31 in registers (32 VGPRs), so the LDS holds only the ring and two
-// workgroups share a CU.  The per-column sums stay in registers and the mean
-// is a plain store - no atomics, deterministic.
+// edge streams its pixels in 64-pixel tiles by LDS-DMA through a ring of tile
+// buffers (kGloRingProd = 3: two tiles in flight per workgroup, three
+// workgroups per CU - round 5; the round-4 ring of 5 held four in flight with
+// two workgroups per CU); wave w keeps the weight fragments of its output
+// columns 32w .. 32w+31 in registers (32 VGPRs), so the LDS holds only the ring.
+// The per-column sums stay in registers and the mean is a plain store - no
+// atomics, deterministic.
 // DROID_GLO_NT (A/B builds): the hidden-state stream by non-temporal LDS-DMA
 #ifndef DROID_GLO_NT
 #define DROID_GLO_NT 0
 #endif
 constexpr int kGloTP = 64;
-constexpr int kGloRing = 5;  // 80 KB: two workgroups fill a CU's 160 KB LDS
-constexpr int kGloLds = kGloRing * 2 * kGloTP * 128;  // the tile ring (bytes)
+// the tile ring: kGloRing buffers of 16 KB (kGloRingProd below)
+constexpr int glo_lds(int ring) { return ring * 2 * kGloTP * 128; }
 
 // split: blockIdx.y of gridDim.y pixel ranges of the edge (whole 64-pixel tiles);
 // range y writes its share of the mean to glo + y * E * 128 (the caller adds
 // the ranges in order; one range = the plain mean)
+template <int kGloRing>
 __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__ h, const __half* __restrict__ w,
                                                       const float* __restrict__ bias, float* __restrict__ glo,
                                                       int HW) {
@@ -2960,14 +2962,43 @@ __global__ void __launch_bounds__(384) glo_gates_kernel(const float* __restrict_
   else out_q[(long)e * 128 + t - 256] = acc + b[t];
 }
 
-static int glo_set_attr() {
-  static bool attr = false;
+// Tile ring of gru_glo_kernel: 3 buffers (48 KB, three workgroups per CU) in the
+// product - 0.386 vs 0.426 ms for the round-4 ring of 5 (80 KB, two per CU) at
+// C3, bitwise the same sums (profiles/r05/r05al_glo_ab*.txt); the A/B build
+// keeps rings 5 and 2 (five per CU: 0.389 ms) behind droid_glo_set_ring.
+constexpr int kGloRingProd = 3;
+#if DROID_AB
+static int& glo_ring() {
+  static int r = ab_knob("DROID_GLO_RING", kGloRingProd);
+  return r;
+}
+int droid_glo_set_ring(int r) {
+  const int prev = glo_ring();
+  glo_ring() = (r == 2 || r == 3 || r == 5) ? r : kGloRingProd;
+  return prev;
+}
+#endif
+}  // extern "C"
+template <int R>
+static int launch_glo_ring(dim3 grid, const void* h, const void* w, const float* bias, float* out, int HW,
+                           hipStream_t stream) {
+  static bool attr = false;  // one per instantiation
   if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gru_glo_kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, kGloLds));
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gru_glo_kernel<R>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, glo_lds(R)));
     attr = true;
   }
+  gru_glo_kernel<R><<<grid, 256, glo_lds(R), stream>>>((const __half*)h, (const __half*)w, bias, out, HW);
   return kOk;
+}
+extern "C" {
+static int launch_glo(dim3 grid, const void* h, const void* w, const float* bias, float* out, int HW,
+                      hipStream_t stream) {
+#if DROID_AB
+  if (glo_ring() == 5) return launch_glo_ring<5>(grid, h, w, bias, out, HW, stream);
+  if (glo_ring() == 2) return launch_glo_ring<2>(grid, h, w, bias, out, HW, stream);
+#endif
+  return launch_glo_ring<kGloRingProd>(grid, h, w, bias, out, HW, stream);
 }
 
 int droid_gru_global_f16(const void* h, const void* w, const float* bias, float* glo, int E, int HW,
@@ -2977,8 +3008,7 @@ int droid_gru_global_f16(const void* h, const void* w, const float* bias, float*
       (reinterpret_cast<uintptr_t>(w) & 15) || (reinterpret_cast<uintptr_t>(bias) & 15))
     return fail(kUnsupported, "gru_global_f16: needs H*W % 64 == 0 and 16-B aligned operands");
   if (E == 0) return kOk;
-  { const int st = glo_set_attr(); if (st != kOk) return st; }
-  gru_glo_kernel<<<dim3(E, 1), 256, kGloLds, stream>>>((const __half*)h, (const __half*)w, bias, glo, HW);
+  { const int st = launch_glo(dim3(E, 1), h, w, bias, glo, HW, stream); if (st != kOk) return st; }
   DROID_LAUNCH_CHECK();
   return kOk;
 }
@@ -2994,8 +3024,7 @@ int droid_gru_global_split_f16(const void* h, const void* w, const float* bias, 
       (reinterpret_cast<uintptr_t>(w) & 15) || (reinterpret_cast<uintptr_t>(bias) & 15))
     return fail(kUnsupported, "gru_global_split_f16: needs H*W % 64 == 0, splits <= H*W/64, 16-B aligned operands");
   if (E == 0) return kOk;
-  { const int st = glo_set_attr(); if (st != kOk) return st; }
-  gru_glo_kernel<<<dim3(E, splits), 256, kGloLds, stream>>>((const __half*)h, (const __half*)w, bias, part, HW);
+  { const int st = launch_glo(dim3(E, splits), h, w, bias, part, HW, stream); if (st != kOk) return st; }
   DROID_LAUNCH_CHECK();
   return kOk;
 }

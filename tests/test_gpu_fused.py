@@ -307,6 +307,30 @@ def test_gru_global_context(E, H, W):
     assert torch.equal(out, droid_backends.gru_global_f16(h, w, b))
 
 
+@pytest.mark.parametrize("E,H,W", [(3, 8, 32), (2048, 48, 64), (5, 4, 16)])
+def test_gru_global_ring_depths_bitwise(E, H, W, ab_backends):
+    """gru_glo_kernel's tile ring (the product's 3 buffers, three workgroups per
+    CU) changes only how many tiles are in flight: bitwise the sums of the
+    round-4 ring of 5 and of a ring of 2 (A/B build, droid_glo_set_ring)."""
+    import ctypes
+    import droid_backends
+    g = torch.Generator(device=DEV).manual_seed(29)
+    h = torch.tanh(torch.randn((E, H, W, 128), generator=g, device=DEV)).half()
+    w = (torch.randn((128, 128), generator=g, device=DEV) / 11.3).half()
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    out = droid_backends.gru_global_f16(h, w, b)
+    set_ring = ab_backends.lib.droid_glo_set_ring
+    set_ring.argtypes, set_ring.restype = [ctypes.c_int], ctypes.c_int
+    prev = set_ring(5)
+    try:
+        r5 = ab_backends.gru_global_f16(h, w, b)
+        set_ring(2)
+        r2 = ab_backends.gru_global_f16(h, w, b)
+    finally:
+        set_ring(prev)
+    assert torch.equal(out, r5) and torch.equal(out, r2)
+
+
 @pytest.mark.parametrize("E,H,W", [(3, 8, 32), (2, 48, 64), (2, 4, 128), (3, 4, 32), (5, 12, 32)])
 def test_flow_encoder0(E, H, W):
     """relu(conv7x7(motn.half()) + b) (droid_net.py:88-90 under autocast) vs torch fp32.
