@@ -4,7 +4,7 @@
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$R" || exit 1
-O=gpurun_out/r05ak
+O=gpurun_out/${AB_OUT:-r05ak}
 mkdir -p $O
 for r in 1 2 3; do
   for v in new pre; do
