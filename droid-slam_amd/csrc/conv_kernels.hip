@@ -2125,7 +2125,12 @@ constexpr int glo_lds(int ring) { return ring * 2 * kGloTP * 128; }
 // split: blockIdx.y of gridDim.y pixel ranges of the edge (whole 64-pixel tiles);
 // range y writes its share of the mean to glo + y * E * 128 (the caller adds
 // the ranges in order; one range = the plain mean)
-template <int kGloRing>
+// PK (the product, kGloPkProd): sigmoid(y + b) * h on packed fp32 (v_pk_fma_f32
+// / v_pk_add_f32, two values per instruction; the exp argument as one fma of y
+// with the scaled bias) - the kernel is VALU-bound on this (2 transcendentals
+// per value); 0.3835 vs 0.4249 ms at C3 for the scalar form, which the A/B
+// build keeps (droid_glo_set_pk; profiles/r05/r05pk_glo_pk_ab.txt)
+template <int kGloRing, bool PK>
 __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__ h, const __half* __restrict__ w,
                                                       const float* __restrict__ bias, float* __restrict__ glo,
                                                       int HW) {
@@ -2169,6 +2174,15 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
 #pragma unroll
   for (int j = 0; j < 2; ++j) bj[j] = *reinterpret_cast<const floatx4*>(bias + wave * 32 + j * 16 + fq * 4);
   floatx4 colsum[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  f2_t nb[2][2], cs2[2][2];   // PK: -log2(e) b and the column sums, in pairs
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      nb[j][k] = f2_t{bj[j][2 * k], bj[j][2 * k + 1]} * f2_t{-1.4426950408889634f, -1.4426950408889634f};
+      cs2[j][k] = f2_t{0.f, 0.f};
+    }
   // the weight and bias loads land before the ring starts (the counted vmcnt
   // waits below assume only DMAs are outstanding)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2213,11 +2227,28 @@ __global__ void __launch_bounds__(256) gru_glo_kernel(const __half* __restrict__
         const int r = i * 16 + fr;
         const half4_t hv = *reinterpret_cast<const half4_t*>(
             At + c * 8192 + r * 128 + ((((kk >> 3) ^ (r & 7)) << 4) | ((kk & 7) << 1)));
+        if constexpr (PK) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)  // v_rcp_f32 sigmoid: no IEEE division
-          colsum[j][k] += sigmoid_fast(acc[i][j][k] + bj[j][k]) * (float)hv[k];
+          for (int k = 0; k < 2; ++k) {
+            const f2_t tt = __builtin_elementwise_fma(
+                f2_t{acc[i][j][2 * k], acc[i][j][2 * k + 1]},
+                f2_t{-1.4426950408889634f, -1.4426950408889634f}, nb[j][k]);
+            const f2_t den = f2_t{__builtin_amdgcn_exp2f(tt[0]), __builtin_amdgcn_exp2f(tt[1])} + f2_t{1.f, 1.f};
+            const f2_t sg = {__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+            cs2[j][k] = __builtin_elementwise_fma(sg, f2_t{(float)hv[2 * k], (float)hv[2 * k + 1]}, cs2[j][k]);
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)  // v_rcp_f32 sigmoid: no IEEE division
+            colsum[j][k] += sigmoid_fast(acc[i][j][k] + bj[j][k]) * (float)hv[k];
+        }
       }
     }
+  }
+  if constexpr (PK) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      colsum[j] = floatx4{cs2[j][0][0], cs2[j][0][1], cs2[j][1][0], cs2[j][1][1]};
   }
   // sum over the 16 pixel lanes (fr) of each channel quadruple
 #pragma unroll
@@ -2967,6 +2998,7 @@ __global__ void __launch_bounds__(384) glo_gates_kernel(const float* __restrict_
 // C3, bitwise the same sums (profiles/r05/r05al_glo_ab*.txt); the A/B build
 // keeps rings 5 and 2 (five per CU: 0.389 ms) behind droid_glo_set_ring.
 constexpr int kGloRingProd = 3;
+constexpr bool kGloPkProd = true;
 #if DROID_AB
 static int& glo_ring() {
   static int r = ab_knob("DROID_GLO_RING", kGloRingProd);
@@ -2977,24 +3009,40 @@ int droid_glo_set_ring(int r) {
   glo_ring() = (r == 2 || r == 3 || r == 5) ? r : kGloRingProd;
   return prev;
 }
+static int& glo_pk() {
+  static int v = ab_knob("DROID_GLO_PK", kGloPkProd ? 1 : 0);
+  return v;
+}
+// A/B: the packed-fp32 sigmoid sum of gru_glo_kernel (1, the product) or the
+// scalar one (0, round 5 until its last commits)
+int droid_glo_set_pk(int v) {
+  const int prev = glo_pk();
+  glo_pk() = v ? 1 : 0;
+  return prev;
+}
 #endif
 }  // extern "C"
-template <int R>
+template <int R, bool PK = kGloPkProd>
 static int launch_glo_ring(dim3 grid, const void* h, const void* w, const float* bias, float* out, int HW,
                            hipStream_t stream) {
   static bool attr = false;  // one per instantiation
   if (!attr) {
-    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gru_glo_kernel<R>),
+    DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gru_glo_kernel<R, PK>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, glo_lds(R)));
     attr = true;
   }
-  gru_glo_kernel<R><<<grid, 256, glo_lds(R), stream>>>((const __half*)h, (const __half*)w, bias, out, HW);
+  gru_glo_kernel<R, PK><<<grid, 256, glo_lds(R), stream>>>((const __half*)h, (const __half*)w, bias, out, HW);
   return kOk;
 }
 extern "C" {
 static int launch_glo(dim3 grid, const void* h, const void* w, const float* bias, float* out, int HW,
                       hipStream_t stream) {
 #if DROID_AB
+  if (glo_pk() != (kGloPkProd ? 1 : 0)) {
+    if (glo_ring() == 5) return launch_glo_ring<5, !kGloPkProd>(grid, h, w, bias, out, HW, stream);
+    if (glo_ring() == 2) return launch_glo_ring<2, !kGloPkProd>(grid, h, w, bias, out, HW, stream);
+    return launch_glo_ring<kGloRingProd, !kGloPkProd>(grid, h, w, bias, out, HW, stream);
+  }
   if (glo_ring() == 5) return launch_glo_ring<5>(grid, h, w, bias, out, HW, stream);
   if (glo_ring() == 2) return launch_glo_ring<2>(grid, h, w, bias, out, HW, stream);
 #endif

@@ -1017,3 +1017,32 @@ def test_conv1x1_nchw_matches_torch(E, C, H, W):
     droid_backends.conv_nhwc_f16([(nhwc, 0, nhwc.shape[-1])], pack_conv(wp, [nhwc.shape[-1]]), 128, 1, bias=b, act=1,
                                  out=cl)
     assert float((out.float() - cl.float()).abs().max()) < 2e-3
+
+
+@pytest.mark.parametrize("E,H,W", [(3, 8, 32), (2048, 48, 64), (96, 48, 64)])
+def test_gru_global_packed_sum_matches_scalar(E, H, W, ab_backends):
+    """gru_glo_kernel's sigmoid sum on packed fp32 (the product) vs the scalar
+    form the A/B build keeps (droid_glo_set_pk(0)): the same values up to fp32
+    rounding of the exp argument (one fma instead of an add and a multiply), and
+    both vs torch fp32."""
+    import ctypes
+    import droid_backends
+    g = torch.Generator(device=DEV).manual_seed(31)
+    h = torch.tanh(torch.randn((E, H, W, 128), generator=g, device=DEV)).half()
+    w = (torch.randn((128, 128), generator=g, device=DEV) / 11.3).half()
+    b = torch.randn(128, generator=g, device=DEV) * 0.1
+    out = droid_backends.gru_global_f16(h, w, b)
+    set_pk = ab_backends.lib.droid_glo_set_pk
+    set_pk.argtypes, set_pk.restype = [ctypes.c_int], ctypes.c_int
+    prev = set_pk(1)
+    try:
+        pk = ab_backends.gru_global_f16(h, w, b)
+        set_pk(0)
+        scalar = ab_backends.gru_global_f16(h, w, b)
+    finally:
+        set_pk(prev)
+    assert torch.equal(out, pk)
+    np.testing.assert_allclose(host(out), host(scalar), atol=1e-7, rtol=1e-5)
+    hf = h.float().view(E, H * W, 128)
+    ref = (torch.sigmoid(hf @ w.float().t() + b) * hf).mean(1)
+    np.testing.assert_allclose(host(out), host(ref), atol=1e-6, rtol=1e-4)
