@@ -5,7 +5,7 @@
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$R" || exit 1
-O=gpurun_out/r05cfg
+O=gpurun_out/${CFG_OUT:-r05cfg}
 mkdir -p $O
 run() {  # name, args...
   local n=$1; shift
