@@ -50,16 +50,29 @@ enum ContribKind : int {
   kSchurRhs = 3,    // -S_f(6*ra+r, wcol)
 };
 
-// tile tasks of the dataflow Cholesky, 8 ints each: {type, i, j, k, a, b, 0, 0}
-//   kPotrf  i=j=k, a=klast, b=below  factor (k,k) after applying its last update
-//                                    (k,k,klast) itself (klast -1: none);
-//                                    below: also solve tile (k+1,k)
-//   kTrsm   i, j=k=k                 tile (i,k) <- A_ik Linv_k^T
+// tile tasks of the dataflow Cholesky, 8 ints each: {type, i, j, k, a, b, c, 0}
+//   kPotrf  i=j=k, a=klast, b=below, factor (k,k) after applying its last update
+//           c=next+1, d=chained      (k,k,klast) itself (klast -1: none), store L_kk
+//                                    and its diagonal-block inverses; below: also
+//                                    solve tile (k+1,k); next: the ticket of
+//                                    potrf(k+1), which this task then runs itself
+//                                    (L(k+1,k) stays in LDS); chained: this ticket
+//                                    is that placeholder (skipped when handed out)
+//   kTrsm   i, j=k=k, a=seq, b=upd   tile (i,k) <- A_ik L_kk^-T (blocked forward
+//                                    substitution); upd: then also the update
+//                                    (i,k+1,k), the seq-th (and last) of (i,k+1)
 //   kUpdate i, j, k, a=seq           tile (i,j) -= L_ik L_jk^T, its seq-th update
-//   kBsolve i=j=k=c, a=fused         x_c = Linv_c^T y_c; fused: y_{c-1} -= L_{c,c-1}^T x_c
-//   kBupd   i=r, j=k=c, a=seq        y_c -= L_rc^T x_r, the seq-th update of y_c
-enum CholTaskType : int { kPotrf = 0, kTrsm = 1, kUpdate = 2, kBsolve = 3, kBupd = 4 };
+//   kBcol   i=j=k=c                  back solve of block c: x_c = L_cc^-T (y_c -
+//                                    sum_{r>c} L_rc^T x_r), the x_r taken as they
+//                                    are published, the parent's last
+enum CholTaskType : int { kPotrf = 0, kTrsm = 1, kUpdate = 2, kBcol = 3 };
 constexpr int kTaskInts = 8;
+
+// The dataflow solve's sync area (zeroed before every launch): ticket, abort
+// word, 2 spare ints, ver[nslots] | yver[nbc] | lkk[nbc], then (16-B aligned)
+// the x hand-off granules {double x, int tag, int 0}, 64 per block column.
+inline size_t chol_gran_off(int nslots, int nbc) { return ((size_t)(4 + nslots + 2 * nbc) * 4 + 15) & ~(size_t)15; }
+inline size_t chol_sync_bytes(int nslots, int nbc) { return chol_gran_off(nslots, nbc) + (size_t)nbc * 64 * 16; }
 
 struct Contrib {
   int kind, src, a0, a1;
@@ -68,7 +81,8 @@ struct Contrib {
 // Tile-sparse structure of one factorisation: nbc pivot tile columns, nbr tile
 // rows (the rhs is row n), slot[i*nbc+j] = storage slot of lower tile (i,j) or
 // -1; fin[s] = final version of slot s (its update count + 1); ycnt[c] = final
-// version of y_c (1 + number of back-solve updates it receives).
+// version of y_c (1: its forward-solved value; the back solve accumulates its
+// updates inside the kBcol task).
 struct CholStructure {
   int n = 0, nbc = 0, nbr = 0, nslots = 0, nslots_a = 0;
   std::vector<int> slot, fin, ycnt, tasks;

@@ -706,7 +706,7 @@ constexpr int kSc1 = 16;        // buffer-op aux bit: sc1
 constexpr unsigned kOobOff = 0x80000000u;
 constexpr unsigned kSpinLimit = 1u << 24;
 constexpr unsigned long long kSpinTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
-constexpr int kCholLds = (3 * 64 * LT + 256 + 4 * 272) * 8 + 16;
+constexpr int kCholLds = (3 * 64 * LT + 256 + 4 * 272) * 8 + 32;
 
 struct CholDev {
   double* M;          // factor tiles: slot s at M + kTile * s, row-major 64 x 64
@@ -715,30 +715,30 @@ struct CholDev {
   int ntasks;
   const int* slot;    // [nbr * nbc] tile -> slot, -1 = structural zero
   const int* fin;     // [nslots] final version per slot
-  const int* ycnt;    // [nbc] final version of y_c
   const int* outmap;  // [n] permuted variable -> dx index
   int nslots;
-  int* sync;    // [0] ticket [1] abort [4..] ver[nslots] | yver[nbc] | xdone[nbc] | lver[nbc]
+  int* sync;    // [0] ticket [1] abort [4..] ver[nslots] | yver[nbc] | lkk[nbc]  (ba.hpp chol_sync_bytes)
+  unsigned* gran;  // x hand-off granules {double x, tag, 0}, 64 per block column (inside the sync area)
   int* flag;    // bit 0: factorisation failed (dx = 0), bit 1: spin timeout
   double* linv; // [nbc][64][64]
   double* ybuf; // [nbc*64]
-  double* x;    // [n] (permuted order)
   float* dx;    // [n]
   int inject;   // test hook (droid_chol_set_fault_inject): raise the abort at once, as a timeout would
-  long long* prof;  // profiling builds: s_memrealtime per (task, phase < 8), or null
+  long long* prof;  // profiling builds: s_memrealtime per (task, stamp < 16), or null
 };
 
 #ifndef DROID_CONV_PROFILE
 #define DROID_CONV_PROFILE 0
 #endif
 #if DROID_CONV_PROFILE
-#define CH_STAMP(ph)                                                                          \
+#define CH_STAMPT(t, ph)                                                                      \
   do {                                                                                        \
-    if (d.prof && tid == 0) d.prof[(long)tk * 8 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+    if (d.prof && tid == 0) d.prof[(long)(t) * 16 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
-#define CH_STAMP(ph) do { } while (0)
+#define CH_STAMPT(t, ph) do { } while (0)
 #endif
+#define CH_STAMP(ph) CH_STAMPT(tk, ph)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mkrs(const void* p, size_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
@@ -943,6 +943,57 @@ __device__ __forceinline__ double rsqrt_f64_1(double x) {
   return y * fma(-0.5 * x * y, y, 1.5);
 }
 
+// Round 6 panel: the same 16-column factor as panel_factor, with every
+// cross-lane value on the column-to-column critical path taken by v_readlane:
+// lane r keeps its own running diagonal dg = A(r,r) - sum_m L(r,m)^2 (its own
+// x values only), so the next pivot is readlane(dg) right after this column's
+// scale; the next column's entry L(c+1,c) comes by one readlane pair too.
+// Only the columns two or more ahead get this column through the LDS
+// broadcast, which then has a full column step to land.  Per column the chain
+// is: scale -> fma(dg) -> readlane -> rsq + one Newton step -> scale.  Same
+// arithmetic as panel_factor (the diagonal's updates in the same order), one
+// Newton step in the rsqrt (~2^-46 relative).
+__device__ __forceinline__ void panel_factor2(double* T, double* dinv, int c0, int Bp, int lane, int* flag,
+                                              double* colbuf) {
+  double v[16], invs[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = T[lane * LT + c0 + q];
+  double dg = 0.0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) dg = (lane == c0 + q) ? v[q] : dg;
+  bool bad = false;
+  double piv = c0 < Bp ? bcast_lane(dg, c0) : 1.0;
+#pragma unroll
+  for (int jj = 0; jj < 16; ++jj) {
+    bad |= !(piv > 0.0 && piv < 1e300);
+    const double inv = rsqrt_f64_1(piv);
+    invs[jj] = inv;
+    const double x = v[jj] * inv;  // L(r, c0+jj); the diagonal lane gets sqrt(piv)
+    v[jj] = x;
+    if (jj < 15) {
+      dg = fma(-x, x, dg);
+      piv = c0 + jj + 1 < Bp ? bcast_lane(dg, c0 + jj + 1) : 1.0;   // wave-uniform condition
+      const double l1 = bcast_lane(x, c0 + jj + 1);
+      v[jj + 1] = fma(-x, l1, v[jj + 1]);
+      if (jj < 14) {
+        colbuf[lane] = x;
+        double lq[16];
+#pragma unroll
+        for (int q = jj + 2; q < 16; ++q) lq[q] = colbuf[c0 + q];
+#pragma unroll
+        for (int q = jj + 2; q < 16; ++q) v[q] = fma(-x, lq[q], v[q]);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) T[lane * LT + c0 + q] = v[q];
+  double mine = 0.0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) mine = (lane == q) ? invs[q] : mine;
+  if (lane < 16) dinv[c0 + lane] = mine;
+  if (bad && lane == 0) atomicOr(flag, 1);
+}
+
 // Round 4: the 16-wide panel in blocks of 4 columns.  The column-at-a-time
 // panel above pays per column an LDS broadcast round trip AND the pivot chain
 // (readlane -> rsqrt -> scale -> next diagonal -> readlane; ~270 clk per column,
@@ -1051,17 +1102,115 @@ __device__ __forceinline__ void tall_solve(double* T, const double* Lt, const do
 #define DROID_CHOL_PANEL4 0
 #endif
 
+// 16x16 block C(cr.., cc..) -= A(ar.., a0 + [0, 4 NK)) B(br.., b0 + [0, 4 NK))^T
+// on f64 MFMA, all operands in LDS tiles of row stride LT (one wave).
+template <int NK>
+__device__ __forceinline__ void blk_sub(double* C, int cr, int cc, const double* A, int ar, int a0,
+                                        const double* B, int br, int b0, int lane) {
+  const int fr = lane & 15, fk = lane >> 4;
+  dbl4 acc;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = C[(cr + 4 * q + fk) * LT + cc + fr];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk)
+    acc = mfma64(-A[(ar + fr) * LT + a0 + 4 * kk + fk], B[(br + fr) * LT + b0 + 4 * kk + fk], acc);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) C[(cr + 4 * q + fk) * LT + cc + fr] = acc[q];
+  asm volatile("" ::: "memory");
+}
+
+// one wave: rows [r0, r0 + nrows) (nrows a multiple of 16, <= 48) of stored
+// tile `s` (nr rows, nc columns real; zeros elsewhere) -> LDS tile B
+__device__ __forceinline__ void rows_load(__amdgpu_buffer_rsrc_t r, int s, int nr, int nc, double* B, int r0,
+                                          int nrows, int lane) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {   // two halves of at most 12 16-B pieces per lane in flight
+    dbl2 v[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q)
+      if (2 * (12 * h + q) < nrows) {
+        const int rr = r0 + 2 * (12 * h + q) + (lane >> 5), cc = (lane & 31) * 2;
+        v[q] = ld2(r, tile_off(s, rr, cc, nr, nc));
+      }
+#pragma unroll
+    for (int q = 0; q < 12; ++q)
+      if (2 * (12 * h + q) < nrows) {
+        const int rr = r0 + 2 * (12 * h + q) + (lane >> 5), cc = (lane & 31) * 2;
+        *reinterpret_cast<dbl2*>(&B[rr * LT + cc]) = v[q];
+      }
+  }
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ int wave_ld(int* w) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// poll_ge by a whole wave (every lane reads the same word; the wave decides on lane 0's value)
+__device__ bool wave_poll_ge(int* w, int target, int* abort_w, int* flag) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned s = 0;; ++s) {
+    if (wave_ld(w) >= target) return true;
+    if (wave_ld(abort_w)) return false;
+    if (s > kSpinLimit || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+      if ((threadIdx.x & 63) == 0) {
+        __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicOr(flag, 2);
+      }
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// x hand-off of the back solve: 16-B granules {x (2 dwords), tag, 0}, each
+// written whole by one sc1 store and polled with sc1 loads (the tag is the
+// flag: no separate counter, no second round trip).  Lanes < 16 of the wave
+// wait for granules g0 .. g0 + 15 and leave their x in dst[lane].
+__device__ bool gran_wait(__amdgpu_buffer_rsrc_t rg, unsigned g0, double* dst, int lane, int* abort_w, int* flag) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned s = 0;; ++s) {
+    u32x4 g = {0u, 0u, 1u, 0u};
+    if (lane < 16) g = __builtin_amdgcn_raw_buffer_load_b128(rg, (int)((g0 + lane) * 16), 0, kSc1);
+    if (__builtin_amdgcn_ballot_w64(g[2] == 0u) == 0) {
+      if (lane < 16) dst[lane] = __builtin_bit_cast(double, ((unsigned long long)g[1] << 32) | g[0]);
+      return true;
+    }
+    if (wave_ld(abort_w)) return false;
+    if (s > kSpinLimit || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+      if (lane == 0) {
+        __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicOr(flag, 2);
+      }
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");   // re-read the granules every pass
+  }
+}
+
+// out[j] = sum_t M[t][j] v[t] over the 64 rows of LDS tile M, j = lane: wave w
+// sums rows 16w..16w+15 into part[w][j] (the caller adds the four partials in
+// wave order after a barrier: a fixed reduction order)
+__device__ __forceinline__ void gemv_t_part(const double* M, const double* v, double* part, int wave, int lane) {
+  double s = 0.0;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) s = fma(M[(16 * wave + t) * LT + lane], v[16 * wave + t], s);
+  part[64 * wave + lane] = s;
+}
+
 // every tile a task record names lies in the plan's slot map (wave-uniform)
-__device__ __forceinline__ bool task_record_ok(const CholDev& d, int type, int i, int j, int k) {
-  if (type < kPotrf || type > kBupd) return false;
+__device__ __forceinline__ bool task_record_ok(const CholDev& d, int type, int i, int j, int k, int b) {
+  if (type < kPotrf || type > kBcol) return false;
   if (i < 0 || i >= d.nbr || j < 0 || j >= d.nbc || k < 0 || k >= d.nbc) return false;
-  auto live = [&](int r, int c) { return __builtin_amdgcn_readfirstlane(d.slot[r * d.nbc + c]) >= 0; };
+  auto live = [&](int r, int cc) {
+    return r < d.nbr && __builtin_amdgcn_readfirstlane(d.slot[r * d.nbc + cc]) >= 0;
+  };
   switch (type) {
-    case kPotrf: return live(k, k);
+    case kPotrf: return live(k, k) && (!b || live(k + 1, k));
     case kTrsm: return live(i, k) && live(k, k);
     case kUpdate: return live(i, j) && live(i, k) && live(j, k);
-    case kBsolve: return i < d.nbc && live(i, i);
-    default: return live(i, j);
+    default: return i < d.nbc && live(i, i);   // kBcol
   }
 }
 
@@ -1072,7 +1221,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
   double* T2 = sm + 2 * 64 * LT;
   double* vec = sm + 3 * 64 * LT;        // 256
   double* scr = vec + 256;               // [4][16][17]
-  int* shi = reinterpret_cast<int*>(scr + 4 * 272);
+  int* shi = reinterpret_cast<int*>(scr + 4 * 272);   // [8]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: wave-conditional code branches, never masks
   const int fr = lane & 15, fk = lane >> 4;
@@ -1081,18 +1230,23 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
   const __amdgpu_buffer_rsrc_t rM = mkrs(d.M, (size_t)d.nslots * kTile * 8);
   const __amdgpu_buffer_rsrc_t rL = mkrs(d.linv, (size_t)nbc * kTile * 8);
   const __amdgpu_buffer_rsrc_t rY = mkrs(d.ybuf, (size_t)nbc * 64 * 8);
-  const __amdgpu_buffer_rsrc_t rX = mkrs(d.x, (size_t)n * 8);
+  const __amdgpu_buffer_rsrc_t rG = mkrs(d.gran, (size_t)nbc * 64 * 16);
   int* ticket = d.sync;
   int* abort_w = d.sync + 1;
   int* ver = d.sync + 4;
   int* yver = ver + d.nslots;
-  int* xdone = yver + nbc;
-  int* lver = xdone + nbc;  // L_kk^-1 stored (published after the pivot tiles)
+  int* lkk = yver + nbc;    // L_kk and its D_p stored: potrf(k)'s waves 0 and 1 each add 1 after their stores
   auto SL = [&](int i, int j) { return d.slot[i * nbc + j]; };
   if (d.inject && blockIdx.x == 0 && tid == 0) {
     __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     atomicOr(d.flag, 2);
   }
+  // every wave's verdict on its own blocking waits -> shi[4 + wave]; all agree after a barrier
+  auto all_ok = [&](bool ok) {
+    if (lane == 0) shi[4 + wave] = ok ? 1 : 0;
+    __syncthreads();
+    return __builtin_amdgcn_readfirstlane(shi[4] & shi[5] & shi[6] & shi[7]) != 0;
+  };
 
   for (bool first = true;; first = false) {
     if (tid == 0) shi[0] = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1111,24 +1265,25 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
     const int type = __builtin_amdgcn_readfirstlane(tsk[0]), i = __builtin_amdgcn_readfirstlane(tsk[1]);
     const int j = __builtin_amdgcn_readfirstlane(tsk[2]), k = __builtin_amdgcn_readfirstlane(tsk[3]);
     const int ta = __builtin_amdgcn_readfirstlane(tsk[4]), tb = __builtin_amdgcn_readfirstlane(tsk[5]);
+    // a chained potrf(k) (record word 7) is run by the workgroup that factored
+    // column k-1, straight after it, with L(k,k-1) still in LDS: its ticket is a
+    // placeholder that keeps the ticket order topological
+    if (type == kPotrf && __builtin_amdgcn_readfirstlane(tsk[7]) != 0) continue;
     CH_STAMP(0);
     // Task-record invariant: every index the task addresses is inside the plan
     // (a corrupted record would otherwise turn into an out-of-range tile access).
-    if (!task_record_ok(d, type, i, j, k)) {
+    if (!task_record_ok(d, type, i, j, k, tb)) {
       if (tid == 0) state_fault(abort_w, d.flag);
       break;
     }
     if (tid == 0) {
       bool ok = true;
       switch (type) {
-        case kPotrf: {  // all updates of the tile but the last (applied here); L(k, klast) is awaited below
-          const int s = SL(k, k);
-          ok = poll_ge(&ver[s], ta >= 0 ? d.fin[s] - 2 : 0, abort_w, d.flag);
+        case kPotrf:    // awaited inside the branch (a chained successor awaits the same way)
           break;
-        }
         case kTrsm: {
           const int s = SL(i, k);
-          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&lver[k], 1, abort_w, d.flag);
+          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&lkk[k], 2, abort_w, d.flag);
           break;
         }
         case kUpdate: {
@@ -1143,14 +1298,8 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           }
           break;
         }
-        case kBsolve: {
-          ok = poll_ge(&lver[i], 1, abort_w, d.flag);   // y_i is awaited after the tile loads are issued
-          break;
-        }
-        default: {  // kBupd (r = i, c = j)
-          const int s = SL(i, j);
-          ok = poll_ge(&xdone[i], 1, abort_w, d.flag) && poll_ge(&ver[s], d.fin[s], abort_w, d.flag) &&
-               poll_ge(&yver[j], 1 + ta, abort_w, d.flag);
+        default: {  // kBcol: L_cc with its diagonal-block inverses, and the forward value of y_c
+          ok = poll_ge(&lkk[i], 2, abort_w, d.flag) && poll_ge(&yver[i], 1, abort_w, d.flag);
           break;
         }
       }
@@ -1161,146 +1310,216 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
     CH_STAMP(1);
 
     if (type == kPotrf) {
-      const int R0 = 64 * k, Bp = min(64, n - R0), Br = min(64, n + 1 - R0);
-      const int skk = SL(k, k);
-      dbl2 pre[8];
-      tile_issue(rM, skk, Br, Bp, pre);  // A(k,k) is final but for (k,k,klast): load while L(k,klast) is awaited
-      if (ta >= 0) {  // the tile's last update (k, k, klast): T0 -= L(k,klast) L(k,klast)^T
-        const int sl = SL(k, ta);
-        if (tid == 0) shi[3] = poll_ge(&ver[sl], d.fin[sl], abort_w, d.flag) ? 1 : 0;
+      // Round 6: the diagonal factor's 16-column panels (wave 0) run beside the
+      // rest of the tile's last update and the in-tile trailing updates (waves
+      // 1-3), and waves 1-3 load tile (k+1,k) as soon as it has its other
+      // updates; between two panels only the next block column's update (3
+      // blocks, 4 MFMAs each) sits on the chain.  After the panels wave 1 forms
+      // the diagonal-block inverses D_p while wave 0 stores L_kk; the workgroup
+      // solves tile (k+1,k) (tall_solve), publishes it, and - when the plan
+      // chains potrf(k+1) to this task - goes straight on to potrf(k+1) with
+      // L(k+1,k) still in LDS (no hand-off, no reload).  L_kk and the D_p are
+      // what the trsm tasks below and the back solve read.
+      double* tL = T1;   // L(k,klast) for the last update, then the D_p
+      double* tB = T2;   // tile (k+1,k)
+      double* dinv = vec + 128;
+      int kc = k, ka = ta, kb = tb, tcur = tk;
+      const int* rec = tsk;
+      bool haveL = false;   // L(k,klast) already in tL (chained from potrf(k-1))
+      bool alive = true;
+      for (;;) {
+        const int R0 = 64 * kc, Bp = min(64, n - R0), Br = min(64, n + 1 - R0);
+        const int np = (Bp + 15) >> 4;
+        const int skk = SL(kc, kc);
+        const bool fz = kb != 0;
+        const int s1 = fz ? SL(kc + 1, kc) : 0, nr1 = fz ? min(64, n + 1 - R0 - 64) : 0;
+        if (tid == 0)   // all updates of (k,k) but the last one, which is applied here
+          shi[1] = poll_ge(&ver[skk], ka >= 0 ? d.fin[skk] - 2 : 0, abort_w, d.flag) ? 1 : 0;
         __syncthreads();
-        if (!__builtin_amdgcn_readfirstlane(shi[3])) break;
-        tile_load(rM, sl, Br, 64, T1);
+        if (!__builtin_amdgcn_readfirstlane(shi[1])) { alive = false; break; }
+        CH_STAMPT(tcur, 1);
+        // wave w >= 1 loads rows [rlo, rhi) of tile (k+1,k) into tB (16, 16, 32 rows)
+        const int rlo = wave == 1 ? 0 : wave == 2 ? 16 : 32, rhi = wave == 1 ? 16 : wave == 2 ? 32 : 64;
+        bool ld = false;
+        auto load_below = [&](bool block) -> bool {   // this wave's rows of (k+1,k), once final but for the trsm
+          if (ld || !fz || wave == 0) return true;
+          const int tgt = d.fin[s1] - 1;
+          if (block) {
+            if (!wave_poll_ge(&ver[s1], tgt, abort_w, d.flag)) return false;
+          } else if (wave_ld(&ver[s1]) < tgt) {
+            return true;
+          }
+          rows_load(rM, s1, nr1, Bp, tB, rlo, rhi - rlo, lane);
+          ld = true;
+          return true;
+        };
+
+        dbl2 pre[8];
+        tile_issue(rM, skk, Br, Bp, pre);  // A(k,k) is final but for (k,k,klast): load while L(k,klast) is awaited
+        if (ka >= 0 && !haveL) {
+          const int sl = SL(kc, ka);
+          if (tid == 0) shi[3] = poll_ge(&ver[sl], d.fin[sl], abort_w, d.flag) ? 1 : 0;
+          __syncthreads();
+          if (!__builtin_amdgcn_readfirstlane(shi[3])) { alive = false; break; }
+          tile_load(rM, sl, Br, 64, tL);
+        }
         tile_commit(pre, T0);
         __syncthreads();
-        dbl4 acc[2][2];
-        acc_load(T0, acc, wr, wc, lane);
-        gemm_nt64(T1, T1, acc, wr, wc, lane, -1.0);
-        acc_store(T0, acc, wr, wc, lane);
-      } else {
-        tile_commit(pre, T0);
-      }
-      __syncthreads();
-      CH_STAMP(2);
-      for (int c0 = 0; c0 < Bp; c0 += 16) {  // whole 16-wide panels (unit-padded)
+        if (ka >= 0) {  // the last update's block column 0 (one 16x16 block per wave): panel 0 needs only it
+          blk_sub<16>(T0, 16 * wave, 0, tL, 16 * wave, 0, tL, 0, 0, lane);
+          __syncthreads();
+        }
+        CH_STAMPT(tcur, 2);
+        for (int p = 0; p < np; ++p) {
+          if (wave == 0) {
+              CH_STAMPT(tcur, 8 + 2 * p);
+              panel_factor2(T0, dinv, 16 * p, Bp, lane, d.flag, scr);
+              CH_STAMPT(tcur, 9 + 2 * p);
+          } else {
+            int job = 0;
+            if (p == 0) {  // the rest of the last update (block columns >= 1)
+              if (ka >= 0)
+                for (int C = 1; C < np; ++C)
+                  for (int R = C; R < 4; ++R, ++job)
+                    if (job % 3 == wave - 1) blk_sub<16>(T0, 16 * R, 16 * C, tL, 16 * R, 0, tL, 16 * C, 0, lane);
+            } else {       // panel p-1's update of the block columns after the next
+              for (int C = p + 1; C < np; ++C)
+                for (int R = C; R < 4; ++R, ++job)
+                  if (job % 3 == wave - 1)
+                    blk_sub<4>(T0, 16 * R, 16 * C, T0, 16 * R, 16 * (p - 1), T0, 16 * C, 16 * (p - 1), lane);
+            }
+            load_below(false);
+          }
+          __syncthreads();
+          if (p + 1 < np) {  // the next block column gets panel p's update (rows p+1..3, one block per wave)
+            const int R = p + wave;
+            if (wave >= 1 && R < 4)
+              blk_sub<4>(T0, 16 * R, 16 * (p + 1), T0, 16 * R, 16 * p, T0, 16 * (p + 1), 16 * p, lane);
+            __syncthreads();
+          }
+        }
+        CH_STAMPT(tcur, 3);
+        const bool rhs0 = Br > Bp;                    // the rhs row inside the pivot tile
+        const bool rhs1 = fz && kc + 1 == nbr - 1;    // ... or in tile (k+1,k)
         if (wave == 0) {
-          if (DROID_CHOL_PANEL4) panel_factor4(T0, vec + 128, c0, Bp, lane, d.flag, scr);
-          else panel_factor(T0, vec + 128, c0, Bp, lane, d.flag, scr);
+          // L_kk (rows and columns < Bp) goes out now (counted on lkk after the solve)
+#pragma unroll 4
+          for (int q = 0; q < 32; ++q) {
+            const int rr = q * 2 + (lane >> 5), cc2 = (lane & 31) * 2;
+            if (rr < Bp && cc2 < Bp)
+              st2(rM, (unsigned)(((size_t)skk * kTile + rr * 64 + cc2) * 8), *reinterpret_cast<const dbl2*>(&T0[rr * LT + cc2]));
+          }
+        } else if (wave == 1) {
+          // y_k (the solved rhs row), the rows past Bp cleared (L_kk^-1 is
+          // unit-padded there), then the diagonal-block inverses D_p = L_pp^-1
+          // into tL's diagonal blocks; lane = 16 * block + column
+          if (rhs0 && lane < 32)
+            st2(rY, (unsigned)((R0 + 2 * lane) * 8), *reinterpret_cast<const dbl2*>(&T0[Bp * LT + 2 * lane]));
+          for (int r = Bp; r < 64; ++r) T0[r * LT + lane] = 0.0;
+          if (lane >= Bp) dinv[lane] = 1.0;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          const int base = 16 * (lane >> 4), cc = lane & 15;
+          double xv[16];
+#pragma unroll
+          for (int t = 0; t < 16; ++t) {
+            double sacc = (t == cc) ? 1.0 : 0.0;
+#pragma unroll
+            for (int u = 0; u < t; ++u) sacc = fma(-T0[(base + t) * LT + base + u], xv[u], sacc);
+            xv[t] = sacc * dinv[base + t];  // 1 / L[t][t] from the panel
+          }
+#pragma unroll
+          for (int t = 0; t < 16; ++t) {
+            tL[(base + t) * LT + base + cc] = xv[t];
+            st1(rL, (unsigned)(((size_t)kc * kTile + (base + t) * 64 + base + cc) * 8), xv[t]);
+          }
         }
-        __syncthreads();
-        const int s0 = c0 + 16;
-        const int nt = (64 - s0) / 16;
-        for (int ti = wave; ti < nt * nt; ti += 4) {
-          const int R = s0 + 16 * (ti / nt), C = s0 + 16 * (ti % nt);
-          if (C > R) continue;
-          dbl4 acc;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc[q] = T0[(R + 4 * q + fk) * LT + C + fr];
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk)
-            acc = mfma64(-T0[(R + fr) * LT + c0 + 4 * kk + fk], T0[(C + fr) * LT + c0 + 4 * kk + fk], acc);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) T0[(R + 4 * q + fk) * LT + C + fr] = acc[q];
+        if (!all_ok(load_below(true))) { alive = false; break; }
+        CH_STAMPT(tcur, 6);
+        if (fz) tall_solve(tB, T0, tL, scr, wave, fr, fk);   // trsm(k+1,k) with the D_p, each wave 16 rows
+        if (wave <= 1) {
+          // waves 0 / 1 stored L_kk / the D_p before the solve: each counts its
+          // own stores on lkk once they have landed (Guideline 16 R1)
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) __hip_atomic_fetch_add(&lkk[kc], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        __syncthreads();
-      }
-      CH_STAMP(3);
-      const bool below = tb != 0;  // trsm(k+1, k) runs in this task
-      const int R1 = R0 + 64, nr1 = below ? min(64, n + 1 - R1) : 0;
-      const int sb = below ? SL(k + 1, k) : 0;
-      if (below && tid == 0) shi[2] = poll_ge(&ver[sb], d.fin[sb] - 1, abort_w, d.flag) ? 1 : 0;
-      CH_STAMP(6);   // profiling: A(k+1,k) has all its updates but this task's (tid 0 polled it)
-      // lower-triangular copy of the Bp x Bp pivot block (unit-diagonal padding past Bp)
-      for (int idx = tid; idx < 64 * 64; idx += 256) {
-        const int r = idx >> 6, c = idx & 63;
-        T2[r * LT + c] = (r < Bp) ? (c <= r ? T0[r * LT + c] : 0.0) : (r == c ? 1.0 : 0.0);
-        T1[r * LT + c] = 0.0;
-      }
-      if (tid >= Bp && tid < 64) vec[128 + tid] = 1.0;  // unit padding of the pivot block
-      __syncthreads();
-      if (below) {
-        if (!__builtin_amdgcn_readfirstlane(shi[2])) break;
-        tile_issue(rM, sb, nr1, Bp, pre);  // lands during the diagonal-block inverses
-      }
-      tile_store(rM, skk, Br, Bp, T0);
-      const bool rhs = Br > Bp;
-      if (rhs && tid < 32) st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[Bp * LT + 2 * tid]));
-      if (wave == 0) {  // the four 16x16 diagonal blocks of L^-1; lane = 16 * block + column
-        const int base = 16 * (lane >> 4), cc = lane & 15;
-        double xv[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-          double sacc = (t == cc) ? 1.0 : 0.0;
-#pragma unroll
-          for (int u = 0; u < t; ++u) sacc = fma(-T2[(base + t) * LT + base + u], xv[u], sacc);
-          xv[t] = sacc * vec[128 + base + t];  // 1 / L[t][t] from the panel
+        if (fz) {
+          __syncthreads();
+          tile_store(rM, s1, nr1, Bp, tB);
+          if (rhs1 && tid < 32)
+            st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&tB[(n - R0 - 64) * LT + 2 * tid]));
         }
-#pragma unroll
-        for (int t = 0; t < 16; ++t) T1[(base + t) * LT + base + cc] = xv[t];
-      }
-      // L_kk^-1 itself is finished below, after the publish: only the trsm and
-      // back-solve tasks of later tiles read it, off the factorisation's chain
-      if (below) {
-        // trsm(k+1, k) in this task, by the same blocked forward substitution
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __syncthreads();  // T0's store reads are done
-        tile_commit(pre, T0);
-        __syncthreads();
-        tall_solve(T0, T2, T1, scr, wave, fr, fk);
-        __syncthreads();
-        CH_STAMP(5);
-        tile_store(rM, sb, nr1, Bp, T0);
-        const bool rhs1 = (k + 1 == nbr - 1);
-        if (rhs1 && tid < 32) st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[(n - R1) * LT + 2 * tid]));
-        publish(&ver[skk], d.fin[skk], &ver[sb], d.fin[sb], rhs1 ? &yver[k] : nullptr, 1);
-      } else {
-        publish(&ver[skk], d.fin[skk], rhs ? &yver[k] : nullptr, 1);
-      }
-      for (int I = 1; I < 4; ++I) {  // Linv[I][J] = -Dinv_I sum_{K=J}^{I-1} L[I][K] Linv[K][J]
-        if (wave < I) {
-          const int J = wave;
-          dbl4 S = {0.0, 0.0, 0.0, 0.0};
-          for (int K = J; K < I; ++K)
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-              S = mfma64(T2[(16 * I + fr) * LT + 16 * K + 4 * kk + fk], T1[(16 * K + 4 * kk + fk) * LT + 16 * J + fr], S);
-          double* sw = scr + wave * 272;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) sw[(4 * q + fk) * 17 + fr] = S[q];
-          asm volatile("" ::: "memory");
-          dbl4 R = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk)
-            R = mfma64(-T1[(16 * I + fr) * LT + 16 * I + 4 * kk + fk], sw[(4 * kk + fk) * 17 + fr], R);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) T1[(16 * I + 4 * q + fk) * LT + 16 * J + fr] = R[q];
+        publish(&ver[skk], d.fin[skk], fz ? &ver[s1] : nullptr, fz ? d.fin[s1] : 0, (rhs0 || rhs1) ? &yver[kc] : nullptr, 1);
+        CH_STAMPT(tcur, 5);
+        // chained successor: potrf(k+1), whose last update is L(k+1,k) L(k+1,k)^T
+        const int nxt = __builtin_amdgcn_readfirstlane(rec[6]);
+        if (nxt <= 0) break;
+        CH_STAMPT(tcur, 7);
+        tcur = nxt - 1;
+        rec = d.tasks + kTaskInts * tcur;
+        const int ntype = __builtin_amdgcn_readfirstlane(rec[0]), nk = __builtin_amdgcn_readfirstlane(rec[3]);
+        const int na = __builtin_amdgcn_readfirstlane(rec[4]), nb = __builtin_amdgcn_readfirstlane(rec[5]);
+        if (tcur >= d.ntasks || ntype != kPotrf || nk != kc + 1 || na != kc || !fz ||
+            !task_record_ok(d, kPotrf, nk, nk, nk, nb)) {
+          if (tid == 0) state_fault(abort_w, d.flag);
+          alive = false;
+          break;
         }
-        __syncthreads();
+        CH_STAMPT(tcur, 0);
+        kc = nk; ka = na; kb = nb;
+        double* t = tL; tL = tB; tB = t;   // L(k+1,k) is the next task's last-update operand
+        haveL = true;
       }
-      CH_STAMP(4);
-      tile_store(rL, k, 64, 64, T1);
-      publish(&lver[k], 1);
+      if (!alive) break;
+      CH_STAMPT(tcur, 7);
+      continue;
     } else if (type == kTrsm) {
+      // X = A L_kk^-T by blocked forward substitution (tall_solve: 40 f64 MFMAs
+      // per wave) against L_kk and its diagonal-block inverses, which potrf(k)
+      // stores right after its panels (round 6: the product with the whole
+      // L_kk^-1 waited for the end of potrf(k)).  b = 1: then also the update
+      // (i,k+1,k) - always that tile's last - with X still in LDS and L(k+1,k)
+      // from potrf(k); it is version a+1 of (i,k+1).
       const int R0 = 64 * i, C0 = 64 * k, nr = min(64, n + 1 - R0), nc = min(64, n - C0);
       const int s = SL(i, k);
-      // the product with L_kk^-1 (64 f64 MFMAs per wave, two tile loads); the
-      // blocked forward substitution against L_kk and its diagonal-block
-      // inverses (tall_solve, as potrf does for (k+1, k)) measured slower here:
-      // C3 BA(itrs=2) 2.44 vs 2.34 ms (profiles/r04/r04f_ba_*.txt) - these tiles
-      // are off the factorisation's chain, where the extra load and the four
-      // serial block steps cost more than the MFMAs they save
-      tile_load(rM, s, nr, nc, T0);
-      tile_load(rL, k, 64, 64, T1);
+      dbl2 pa[8], pd[8];
+      tile_issue(rM, s, nr, nc, pa);
+      tile_issue(rL, k, 64, 64, pd);   // the D_p (the rest of the tile: not read)
+      tile_load(rM, SL(k, k), nc, nc, T1);
+      tile_commit(pa, T0);
+      tile_commit(pd, T2);
       __syncthreads();
-      dbl4 acc[2][2] = {};
-      gemm_nt64(T0, T1, acc, wr, wc, lane, 1.0);
+      CH_STAMP(2);
+      tall_solve(T0, T1, T2, scr, wave, fr, fk);
       __syncthreads();
-      acc_store(T0, acc, wr, wc, lane);
-      __syncthreads();
+      CH_STAMP(3);
       tile_store(rM, s, nr, nc, T0);
       const bool rhs = (i == nbr - 1);
       if (rhs && tid < 32) st2(rY, (unsigned)((C0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&T0[(n - R0) * LT + 2 * tid]));
       publish(&ver[s], d.fin[s], rhs ? &yver[k] : nullptr, 1);
+      if (tb) {
+        const int su = SL(i, k + 1), sk = SL(k + 1, k);
+        const int nc1 = min(64, n - C0 - 64);
+        if (tid == 0)
+          shi[3] = (poll_ge(&ver[su], ta, abort_w, d.flag) && poll_ge(&ver[sk], d.fin[sk], abort_w, d.flag)) ? 1 : 0;
+        __syncthreads();
+        if (!__builtin_amdgcn_readfirstlane(shi[3])) break;
+        if (tid == 0 && __hip_atomic_load(&ver[su], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ta) {
+          state_fault(abort_w, d.flag);   // this chain applies the tile's updates alone: more is a stale counter
+          shi[3] = 0;
+        }
+        tile_load(rM, sk, nc1, 64, T1);
+        tile_load(rM, su, nr, nc1, T2);
+        __syncthreads();
+        if (!__builtin_amdgcn_readfirstlane(shi[3])) break;
+        CH_STAMP(4);
+        dbl4 acc[2][2];
+        acc_load(T2, acc, wr, wc, lane);
+        gemm_nt64(T0, T1, acc, wr, wc, lane, -1.0);
+        acc_store(T2, acc, wr, wc, lane);
+        __syncthreads();
+        tile_store(rM, su, nr, nc1, T2);
+        publish(&ver[su], ta + 1);
+      }
     } else if (type == kUpdate) {
       const int Ri = 64 * i, Rj = 64 * j, Ck = 64 * k;
       const int nri = min(64, n + 1 - Ri), ncj = min(64, n - Rj), nck = min(64, n - Ck);
@@ -1309,70 +1528,125 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       tile_load(rM, SL(j, k), ncj, nck, T1);
       tile_load(rM, s, nri, ncj, T2);
       __syncthreads();
+      CH_STAMP(2);
       dbl4 acc[2][2];
       acc_load(T2, acc, wr, wc, lane);
       gemm_nt64(T0, T1, acc, wr, wc, lane, -1.0);
       acc_store(T2, acc, wr, wc, lane);
       __syncthreads();
+      CH_STAMP(3);
       tile_store(rM, s, nri, ncj, T2);
       publish(&ver[s], ta + 1);
-    } else if (type == kBsolve) {  // x_i = L_ii^-T y_i, then (fused) y_{i-1} -= L(i,i-1)^T x_i
-      const int C0 = 64 * i, Bp = min(64, n - C0);
-      // the back-solve chain is bsolve(i) -> y_{i-1} -> bsolve(i-1): L_ii^-1 and
-      // L(i,i-1) (final long before) are in flight while y_i is awaited
-      dbl2 pl[8], pb[8];
-      tile_issue(rL, i, 64, 64, pl);
-      if (ta) tile_issue(rM, SL(i, i - 1), Bp, 64, pb);
-      if (tid == 0) shi[3] = poll_ge(&yver[i], d.ycnt[i], abort_w, d.flag) ? 1 : 0;
-      __syncthreads();
-      if (!__builtin_amdgcn_readfirstlane(shi[3])) break;
-      tile_commit(pl, T1);
-      if (ta) tile_commit(pb, T0);
+    } else {
+      // kBcol (round 6): the whole back solve of block column c in one task.
+      // x_c = L_cc^-T (y_c - sum_{r>c} L_rc^T x_r).  The rows r > c are the
+      // ancestors of c in the elimination tree, so the parent p (the smallest
+      // r) publishes last: its term is folded into H = L_pc L_cc^-1, computed
+      // while the chain is still above, and x_c = z_c - H^T x_p with z_c =
+      // L_cc^-T (y_c - sum_{r>p} L_rc^T x_r).  The chain step is then one
+      // granule wait, one 64x64 GEMV and one granule store.
+      const int c = i, C0 = 64 * c, Bc = min(64, n - C0);
+      int par = c + 1;
+      while (par < nbc && SL(par, c) < 0) ++par;
+      const bool haspar = par < nbc;
+      dbl2 pd[8], pc[8], pp[8];
+      tile_issue(rL, c, 64, 64, pd);                 // the D_p (diagonal blocks; the rest is not written)
+      tile_issue(rM, SL(c, c), Bc, Bc, pc);          // L_cc
+      if (haspar) tile_issue(rM, SL(par, c), min(64, n - 64 * par), Bc, pp);
       if (tid < 32) {
-        const dbl2 yv = ld2(rY, 2 * tid < Bp ? (unsigned)((C0 + 2 * tid) * 8) : kOobOff);
+        const dbl2 yv = ld2(rY, 2 * tid < Bc ? (unsigned)((C0 + 2 * tid) * 8) : kOobOff);
         vec[2 * tid] = yv[0];
         vec[2 * tid + 1] = yv[1];
       }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {   // T2 = the D_p on the diagonal, zeros elsewhere
+        const int p = tid + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
+        *reinterpret_cast<dbl2*>(&T2[rr * LT + cc]) = ((rr >> 4) == (cc >> 4)) ? pd[q] : dbl2{0.0, 0.0};
+      }
+      tile_commit(pc, T1);
       __syncthreads();
+      // L_cc^-1 in T2: Linv[I][J] = -D_I sum_{K=J}^{I-1} L[I][K] Linv[K][J]
+      for (int I = 1; I < 4; ++I) {
+        if (wave < I) {
+          const int J = wave;
+          dbl4 S = {0.0, 0.0, 0.0, 0.0};
+          for (int K = J; K < I; ++K)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+              S = mfma64(T1[(16 * I + fr) * LT + 16 * K + 4 * kk + fk], T2[(16 * K + 4 * kk + fk) * LT + 16 * J + fr], S);
+          double* sw = scr + wave * 272;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sw[(4 * q + fk) * 17 + fr] = S[q];
+          asm volatile("" ::: "memory");
+          dbl4 R = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+            R = mfma64(-T2[(16 * I + fr) * LT + 16 * I + 4 * kk + fk], sw[(4 * kk + fk) * 17 + fr], R);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) T2[(16 * I + 4 * q + fk) * LT + 16 * J + fr] = R[q];
+        }
+        __syncthreads();
+      }
+      if (haspar) {  // H = L_pc Linv_c -> T1 (each wave a 32x32 quadrant)
+        tile_commit(pp, T0);
+        __syncthreads();
+        dbl4 acc[2][2] = {};
+#pragma unroll 4
+        for (int k0 = 0; k0 < 64; k0 += 4) {
+          const double a0v = T0[(wr + fr) * LT + k0 + fk], a1v = T0[(wr + 16 + fr) * LT + k0 + fk];
+          const double b0v = T2[(k0 + fk) * LT + wc + fr], b1v = T2[(k0 + fk) * LT + wc + 16 + fr];
+          acc[0][0] = mfma64(a0v, b0v, acc[0][0]);
+          acc[0][1] = mfma64(a0v, b1v, acc[0][1]);
+          acc[1][0] = mfma64(a1v, b0v, acc[1][0]);
+          acc[1][1] = mfma64(a1v, b1v, acc[1][1]);
+        }
+        acc_store(T1, acc, wr, wc, lane);
+      }
+      // the other rows, descending, one tile in flight ahead
+      int r = nbc - 1;
+      while (r > par && SL(r, c) < 0) --r;
+      dbl2 pt[8];
+      if (r > par) tile_issue(rM, SL(r, c), min(64, n - 64 * r), Bc, pt);
+      __syncthreads();
+      double* part = scr;   // [4][64]
+      bool alive = true;
+      while (r > par) {
+        int rn = r - 1;
+        while (rn > par && SL(rn, c) < 0) --rn;
+        tile_commit(pt, T0);
+        if (rn > par) tile_issue(rM, SL(rn, c), min(64, n - 64 * rn), Bc, pt);
+        if (!all_ok(gran_wait(rG, 64 * r + 16 * wave, vec + 64 + 16 * wave, lane, abort_w, d.flag))) {
+          alive = false;
+          break;
+        }
+        gemv_t_part(T0, vec + 64, part, wave, lane);
+        __syncthreads();
+        if (wave == 0) vec[lane] -= ((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane];
+        __syncthreads();
+        r = rn;
+      }
+      if (!alive) break;
+      CH_STAMP(2);
+      gemv_t_part(T2, vec, part, wave, lane);   // z_c = Linv_c^T y_c
+      __syncthreads();
+      double xc = ((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane];
+      if (haspar) {
+        __syncthreads();   // the partials are read
+        if (!all_ok(gran_wait(rG, 64 * par + 16 * wave, vec + 64 + 16 * wave, lane, abort_w, d.flag))) break;
+        CH_STAMP(3);
+        gemv_t_part(T1, vec + 64, part, wave, lane);
+        __syncthreads();
+        xc -= ((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane];
+      }
       if (wave == 0) {
-        double sacc = 0.0;
-#pragma unroll 8
-        for (int t = 0; t < 64; ++t) sacc = fma(T1[t * LT + lane], vec[t], sacc);
+        const double xv = lane < Bc ? xc : 0.0;
+        const unsigned long long u = __builtin_bit_cast(unsigned long long, xv);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)u, (unsigned)(u >> 32), 1u, 0u}, rG,
+                                               (int)((64 * c + lane) * 16), 0, kSc1);
         const bool failed = (__hip_atomic_load(d.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1) != 0;
-        if (lane < Bp) {
-          st1(rX, (unsigned)((C0 + lane) * 8), sacc);
-          d.dx[d.outmap[C0 + lane]] = failed ? 0.0f : (float)sacc;
-        }
-        vec[64 + lane] = lane < Bp ? sacc : 0.0;
+        if (lane < Bc) d.dx[d.outmap[C0 + lane]] = failed ? 0.0f : (float)xv;
       }
-      publish(&xdone[i], 1);
-      if (ta) {
-        if (tid == 0) shi[1] = poll_ge(&yver[i - 1], d.ycnt[i - 1] - 1, abort_w, d.flag) ? 1 : 0;
-        __syncthreads();
-        if (!__builtin_amdgcn_readfirstlane(shi[1])) break;
-        if (tid < 64) vec[128 + tid] = ld1(rY, (unsigned)((C0 - 64 + tid) * 8));
-        __syncthreads();
-        if (wave == 0) {
-          double sacc = vec[128 + lane];
-#pragma unroll 8
-          for (int t = 0; t < 64; ++t) sacc = fma(-T0[t * LT + lane], vec[64 + t], sacc);
-          st1(rY, (unsigned)((C0 - 64 + lane) * 8), sacc);
-        }
-        publish(&yver[i - 1], d.ycnt[i - 1]);
-      }
-    } else {  // kBupd: y_c -= L_rc^T x_r
-      const int R0 = 64 * i, C0 = 64 * j, nr = min(64, n - R0), nc = min(64, n - C0);
-      tile_load(rM, SL(i, j), nr, nc, T0);
-      if (tid < 64) vec[tid] = ld1(rX, tid < nr ? (unsigned)((R0 + tid) * 8) : kOobOff);
-      else if (tid < 128) vec[tid] = ld1(rY, tid - 64 < nc ? (unsigned)((C0 + tid - 64) * 8) : kOobOff);
-      __syncthreads();
-      if (wave == 0) {
-        double sacc = vec[64 + lane];
-#pragma unroll 8
-        for (int t = 0; t < 64; ++t) sacc = fma(-T0[t * LT + lane], vec[t], sacc);
-        if (lane < nc) st1(rY, (unsigned)((C0 + lane) * 8), sacc);
-      }
-      publish(&yver[j], 2 + ta);
+      __syncthreads();   // vec / scr / T0-T2 are reused by the next task
     }
     CH_STAMP(7);
   }
@@ -1549,13 +1823,13 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_
   c.n = p.n; c.nbc = p.cs.nbc; c.nbr = p.cs.nbr;
   c.tasks = I + p.o_tasks;
   c.ntasks = p.cs.ntasks;
-  c.slot = I + p.o_slot; c.fin = I + p.o_fin; c.ycnt = I + p.o_ycnt; c.outmap = I + p.o_outmap;
+  c.slot = I + p.o_slot; c.fin = I + p.o_fin; c.outmap = I + p.o_outmap;
   c.nslots = p.cs.nslots;
   c.sync = reinterpret_cast<int*>(ws + p.off_sync);
+  c.gran = reinterpret_cast<unsigned*>(ws + p.off_sync + chol_gran_off(p.cs.nslots, p.cs.nbc));
   c.flag = reinterpret_cast<int*>(ws + p.off_flag);
   c.linv = reinterpret_cast<double*>(ws + p.off_linv);
   c.ybuf = reinterpret_cast<double*>(ws + p.off_ybuf);
-  c.x = reinterpret_cast<double*>(ws + p.off_x);
   c.dx = dx;
   // test hook (droid_chol_set_fault_inject): a timeout in every solve, in the
   // next solve only, or the next solve launched on a stale sync area
@@ -1597,9 +1871,8 @@ int droid_chol_set_fault_inject(int mode) {
   return kOk;
 }
 
-// Profiling builds (make prof): per Cholesky task, 8 int64 s_memrealtime
-// stamps (100 MHz): start, dependencies met, [potrf: last update applied,
-// panels factored, Linv done, trsm(k+1,k) done], end.
+// Profiling builds (make prof): per Cholesky task, 16 int64 s_memrealtime
+// stamps (100 MHz), scripts/chol_timeline.py names them.
 int droid_chol_set_profile(void* buf) {
 #if DROID_CONV_PROFILE
   g_chol_prof = static_cast<long long*>(buf);

@@ -126,13 +126,12 @@ void build_chol_structure(int n, const std::vector<char>& pattern, CholStructure
         cs.fin[sl(i, j)] = (int)U.size() + 1;
         if (i == j && !U.empty()) klast[i] = U.back();
       }
-  // back-solve rows of each y_c, descending
+  // back-solve rows of each x_c (the nonzero tiles below its diagonal), descending
   std::vector<std::vector<int>> yrows(nbc);
-  for (int c = 0; c < nbc; ++c) {
+  for (int c = 0; c < nbc; ++c)
     for (int r = nbc - 1; r > c; --r)
       if (nz(r, c)) yrows[c].push_back(r);
-    cs.ycnt[c] = 1 + (int)yrows[c].size();
-  }
+  cs.ycnt.assign(nbc, 1);   // y_c: only its forward-solved value is published (version 1)
 
   // ---- task graph ----
   struct Node { int rec[kTaskInts]; double cost; std::vector<int> succ; int npred; double bl; };
@@ -141,43 +140,45 @@ void build_chol_structure(int n, const std::vector<char>& pattern, CholStructure
   auto key = [](int type, int i, int j, int k) {
     return (uint64_t)type | ((uint64_t)(uint32_t)i << 4) | ((uint64_t)(uint32_t)j << 24) | ((uint64_t)(uint32_t)k << 44);
   };
-  auto add = [&](int type, int i, int j, int k, int a, int b, double cost) {
+  auto add = [&](int type, int i, int j, int k, int a, int b, int c, double cost) {
     id[key(type, i, j, k)] = (int)t.size();
-    Node nd{{type, i, j, k, a, b, 0, 0}, cost, {}, 0, 0.0};
+    Node nd{{type, i, j, k, a, b, c, 0}, cost, {}, 0, 0.0};
     t.push_back(std::move(nd));
   };
+  // potrf(k) also solves tile (k+1,k) when it exists
   std::vector<char> below(nbc, 0);
-  for (int k = 0; k < nbc; ++k) {
+  auto fused = [&](int i, int k) { return i == k + 1 && below[k]; };
+  for (int k = 0; k < nbc; ++k)
     below[k] = (k + 1 < nbr && nz(k + 1, k)) ? 1 : 0;
-    add(kPotrf, k, k, k, klast[k], below[k], 10.0);
+  // trsm(i,k) also applies the update (i,k+1,k) - always the last of tile
+  // (i,k+1) - when tile (k+1,k) exists: fusedu(i,k)
+  auto fusedu = [&](int i, int k) { return k + 1 < nbc && i > k + 1 && below[k] && nz(i, k + 1); };
+  for (int k = 0; k < nbc; ++k) {
+    add(kPotrf, k, k, k, klast[k], below[k], 0, 10.0);
     for (int i = k + 1; i < nbr; ++i)
-      if (nz(i, k) && !(i == k + 1 && below[k])) add(kTrsm, i, k, k, 0, 0, 2.0);
+      if (nz(i, k) && !fused(i, k)) {
+        int seq = 0;
+        if (fusedu(i, k)) { ulist(i, k + 1, U); seq = (int)U.size() - 1; }
+        add(kTrsm, i, k, k, seq, fusedu(i, k) ? 1 : 0, 0, 2.0);
+      }
   }
   for (int i = 0; i < nbr; ++i)
     for (int j = 0; j <= std::min(i, nbc - 1); ++j)
       if (nz(i, j)) {
         ulist(i, j, U);
         for (int s = 0; s < (int)U.size(); ++s)
-          if (!(i == j && U[s] == klast[i])) add(kUpdate, i, j, U[s], s, 0, 2.0);
+          if (!(i == j && U[s] == klast[i]) && !(U[s] == j - 1 && fusedu(i, j - 1))) add(kUpdate, i, j, U[s], s, 0, 0, 2.0);
       }
-  for (int c = 0; c < nbc; ++c) {
-    add(kBsolve, c, c, c, (c >= 1 && nz(c, c - 1)) ? 1 : 0, 0, 2.0);
-    for (int s = 0; s < (int)yrows[c].size(); ++s)
-      if (yrows[c][s] != c + 1) add(kBupd, yrows[c][s], c, c, s, 0, 1.0);
-  }
+  for (int c = 0; c < nbc; ++c) add(kBcol, c, c, c, 0, 0, 0, 2.0);
   auto get = [&](int type, int i, int j, int k) { return id.at(key(type, i, j, k)); };
   auto fin_task = [&](int i, int k) {  // the task that makes tile (i,k) final
-    if (i == k || (i == k + 1 && below[k])) return get(kPotrf, k, k, k);
+    if (i == k || fused(i, k)) return get(kPotrf, k, k, k);
     return get(kTrsm, i, k, k);
   };
   auto upd_task = [&](int i, int j, int s) {  // the task that publishes version s+1 of (i,j)
     ulist(i, j, U);
+    if (U[s] == j - 1 && fusedu(i, j - 1)) return get(kTrsm, i, j - 1, j - 1);
     return get(kUpdate, i, j, U[s]);
-  };
-  auto yprod = [&](int c, int v) {  // the task that publishes version v of y_c
-    if (v == 1) return fin_task(nbr - 1, c);
-    const int r = yrows[c][v - 2];
-    return r == c + 1 ? get(kBsolve, r, r, r) : get(kBupd, r, c, c);
   };
   auto edge = [&](int a, int b) {
     for (int x : t[a].succ)
@@ -192,30 +193,27 @@ void build_chol_structure(int n, const std::vector<char>& pattern, CholStructure
         const int nu = nupd[sl(k, k)];
         if (nu >= 2) edge(upd_task(k, k, nu - 2), v);
         if (a >= 0) edge(fin_task(k, a), v);
-        if (t[v].rec[5] && nupd[sl(k + 1, k)] >= 1) edge(upd_task(k + 1, k, nupd[sl(k + 1, k)] - 1), v);
+        if (t[v].rec[5] && nupd[sl(k + 1, k)] >= 1)   // the fused tile's last update (awaited inside the task)
+          edge(upd_task(k + 1, k, nupd[sl(k + 1, k)] - 1), v);
         break;
       }
       case kTrsm:
         edge(get(kPotrf, k, k, k), v);
         if (nupd[sl(i, k)] >= 1) edge(upd_task(i, k, nupd[sl(i, k)] - 1), v);
+        if (t[v].rec[5] && a >= 1) edge(upd_task(i, k + 1, a - 1), v);   // the fused update's predecessor
         break;
       case kUpdate:
         if (a >= 1) edge(upd_task(i, j, a - 1), v);
         edge(fin_task(i, k), v);
         edge(fin_task(j, k), v);
         break;
-      case kBsolve:
+      default:  // kBcol (c = i): L_cc^-1, y_c's forward value, the tiles below and their x_r
         edge(get(kPotrf, i, i, i), v);
-        edge(yprod(i, cs.ycnt[i]), v);
-        if (a) {
-          edge(fin_task(i, i - 1), v);
-          edge(yprod(i - 1, cs.ycnt[i - 1] - 1), v);
+        edge(fin_task(nbr - 1, i), v);
+        for (int r : yrows[i]) {
+          edge(fin_task(r, i), v);
+          edge(get(kBcol, r, r, r), v);
         }
-        break;
-      default:  // kBupd (r = i, c = j)
-        edge(get(kBsolve, i, i, i), v);
-        edge(fin_task(i, j), v);
-        edge(yprod(j, 1 + a), v);
         break;
     }
   }
@@ -244,14 +242,26 @@ void build_chol_structure(int n, const std::vector<char>& pattern, CholStructure
     indeg[v] = t[v].npred;
     if (!indeg[v]) ready.push((int)v);
   }
+  std::vector<int> ticket(t.size(), -1);
   while (!ready.empty()) {
     const int v = ready.top();
     ready.pop();
+    ticket[v] = (int)cs.tasks.size() / kTaskInts;
     cs.tasks.insert(cs.tasks.end(), t[v].rec, t[v].rec + kTaskInts);
     for (int s2 : t[v].succ)
       if (--indeg[s2] == 0) ready.push(s2);
   }
   cs.ntasks = (int)cs.tasks.size() / kTaskInts;
+  // Chains of pivots: potrf(k) runs potrf(k+1) itself when tile (k+1,k) is
+  // solved in potrf(k) and is the last update of (k+1,k+1) - L(k+1,k) stays in
+  // LDS.  potrf(k+1)'s ticket stays in the list as a placeholder, so the list
+  // is still a topological order (a task never waits on one not yet handed out).
+  for (int k = 0; k + 1 < nbc; ++k)
+    if (below[k] && klast[k + 1] == k) {
+      const int a = ticket[get(kPotrf, k, k, k)], b = ticket[get(kPotrf, k + 1, k + 1, k + 1)];
+      cs.tasks[(size_t)a * kTaskInts + 6] = b + 1;
+      cs.tasks[(size_t)b * kTaskInts + 7] = 1;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -768,7 +778,7 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, co
   p.o_widef = put(p.wide_f); p.o_wideeoff = put(p.wide_eoff); p.o_widetasks = put(p.wide_tasks);
   if (p.ints.empty()) p.ints.push_back(0);
   const int nbc = p.cs.nbc;
-  p.sync_bytes = align_up((size_t)(4 + p.cs.nslots + 3 * nbc) * 4, 16);
+  p.sync_bytes = chol_sync_bytes(p.cs.nslots, nbc);
   if ((size_t)std::max(p.cs.nslots, 1) * kTile * 8 >= 0x80000000ull)
     return fail(kUnsupported, "ba: factor tiles exceed the 2 GB buffer-resource range");
 
@@ -842,7 +852,7 @@ int droid_chol_plan_create(int n, void** plan_out) {
   p->o_slot = put(p->cs.slot); p->o_fin = put(p->cs.fin); p->o_ycnt = put(p->cs.ycnt);
   p->o_outmap = put(p->outmap);
   if (p->ints.empty()) p->ints.push_back(0);
-  p->sync_bytes = align_up((size_t)(4 + p->cs.nslots + 3 * nbc) * 4, 16);
+  p->sync_bytes = chol_sync_bytes(p->cs.nslots, nbc);
   size_t off = 0;
   p->off_ints = off; off = align_up(off + p->ints.size() * 4, 256);
   p->off_M = off; off = align_up(off + (size_t)std::max(p->cs.nslots, 1) * kTile * 8, 256);

@@ -115,7 +115,7 @@ int droid_conv_set_tile(int mode);
  * conv_band2_kernel, 0 = the 8-wave band tile, 2 = the opt-in 4-wave z|r tile,
  * -1 = none (DROID_UNSUPPORTED).  Queries the device's CU count. */
 int droid_conv_gate_tile(int epi, int B, int H, int W);
-/* profiling builds only (make prof): Cholesky task timeline, 8 int64 per task */
+/* profiling builds only (make prof): Cholesky task timeline, 16 int64 per task */
 int droid_chol_set_profile(void* buf);
 /* Test hook for the dataflow solve's failure handling (no reference
  * counterpart): 0 off, 1 every solve aborts as on a dependency-wait timeout

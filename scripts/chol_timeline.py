@@ -25,7 +25,7 @@ t = {k: torch.from_numpy(prob[k]).to(dev) for k in ("poses", "disps", "intrinsic
                                                      "weights", "eta")}
 N, H, W = prob["disps"].shape
 plan = droid_backends.BaPlan(prob["ii"], prob["jj"], N, H, W, prob["t0"], prob["t1"], prob["eta"].shape[0], False, dev)
-prof = torch.zeros((plan.ntasks, 8), dtype=torch.int64, device=dev)
+prof = torch.zeros((plan.ntasks, 16), dtype=torch.int64, device=dev)
 for it in range(3):
     if it == 2:
         assert lib.droid_chol_set_profile(ctypes.c_void_p(prof.data_ptr())) == 0
@@ -40,33 +40,69 @@ lib.droid_chol_set_profile(ctypes.c_void_p(0))
 p = prof.cpu().numpy().astype(np.float64) / 100.0   # us
 t0 = p[p[:, 0] > 0, 0].min()
 print("%s: n=%d tasks=%d, Cholesky span %.1f us" % (cfg, plan.P * 6, plan.ntasks, p[:, 7].max() - t0))
-pot = np.nonzero(p[:, 3] > 0)[0]
+nt = plan.ntasks
+tasks = np.zeros(8 * nt, np.int32)
+assert lib.droid_chol_plan_tasks(plan._h, tasks.ctypes.data_as(ctypes.c_void_p)) == 0
+tasks = tasks.reshape(nt, 8)
+typ = tasks[:, 0]
+key = {(int(t[0]), int(t[1]), int(t[2]), int(t[3])): q for q, t in enumerate(tasks)}
+pot = np.nonzero(typ == 0)[0]
 pot = pot[np.argsort(p[pot, 0])]
-# stamps: 0 ticket, 1 deps met, 2 last update applied, 3 panels done, 6 A(k+1,k) ready,
-# 5 trsm(k+1,k) done (pivot tiles published right after), 4 L_kk^-1 done, 7 task end
-names = ["wait deps", "last update", "panels", "diag inv + trsm(k+1,k)", "stores+publish+Linv", "Linv store"]
+# potrf stamps: 0 ticket (or chained start), 1 deps met, 2 last update's block column 0 applied (panels
+# start), 3 panels done, 6 tile (k+1,k) in LDS and the D_p formed, 5 (k+1,k) solved + published, 7 end;
+# 8 + 2p / 9 + 2p: wave 0's panel p start / end
+names = ["wait deps", "L(k,klast) + col 0", "panels", "wait A(k+1,k)", "D + trsm(k+1,k) + publish", "end"]
 rows = []
 for a, k in enumerate(pot):
     r = p[k]
-    b5 = r[5] if r[5] > 0 else r[3]
-    ph = [r[1] - r[0], r[2] - r[1], r[3] - r[2], b5 - r[3], r[4] - b5, r[7] - r[4]]
+    ph = [r[1] - r[0], r[2] - r[1], r[3] - r[2], r[6] - r[3], r[5] - r[6], r[7] - r[5]]
     step = (p[pot[a + 1], 2] - r[2]) if a + 1 < len(pot) else np.nan
     rows.append(ph + [r[7] - r[0], step])
 rows = np.array(rows)
 print("potrf tasks (%d): median us: " % len(pot) + ", ".join("%s %.2f" % (nm, v) for nm, v in zip(
     names + ["total", "chain step (panels start -> next panels start)"], np.nanmedian(rows, 0))))
-below = p[pot, 5] > 0
-wa = (p[pot, 6] - p[pot, 3])[below]
-print("wait for A(k+1,k)'s other updates after the panels: median %.2f us, p90 %.2f, %d of %d > 0.5 us" % (
-    np.median(wa), np.percentile(wa, 90), int((wa > 0.5).sum()), len(wa)))
-other = np.setdiff1d(np.nonzero(p[:, 7] > 0)[0], pot)
-dur = p[other, 7] - p[other, 1]
-print("other tasks (%d): median work %.2f us, median wait %.2f us" % (len(other), np.median(dur), np.median(p[other, 1] - p[other, 0])))
-# where the chain waits: potrf(k+1)'s other updates done (its stamp 1) vs potrf(k)'s trsm(k+1,k) (stamp 5)
-late = np.array([p[pot[a + 1], 1] - p[pot[a], 5] for a in range(len(pot) - 1)])
-print("other updates of A(k+1,k+1) done after potrf(k) published: %d of %d steps, median %.2f us (p90 %.2f); "
-      "last-update phase when not late: median %.2f us" % ((late > 0).sum(), len(late), np.median(late),
-                                                            np.percentile(late, 90),
-                                                            np.median(rows[1:, 1][late <= 0]) if (late <= 0).any() else np.nan))
+fac_end = p[pot, 5].max()
+print("factor: first ticket -> last (k+1,k) publish %.1f us" % (fac_end - t0))
+for ty, nm in ((1, "trsm"), (2, "update")):
+    q = np.nonzero(typ == ty)[0]
+    if len(q):
+        print("%s tasks (%d): median us: wait deps %.2f, loads %.2f, compute %.2f, store+publish %.2f" % (
+            nm, len(q), *np.median(np.stack([p[q, 1] - p[q, 0], p[q, 2] - p[q, 1], p[q, 3] - p[q, 2],
+                                             p[q, 7] - p[q, 3]]), 1)))
+# the second chain into potrf(k)'s tail: potrf(k-1) L_kk flag -> trsm(k+1,k-1) -> update(k+1,k,k-1) -> potrf(k) stamp 6
+ch = []
+for k in range(2, len(pot) - 1):
+    tr = key.get((1, k + 1, k - 1, k - 1))
+    up = key.get((2, k + 1, k, k - 1), tr)   # fused into the trsm task (its stamp 4: the update's inputs loaded)
+    pk, pk1 = key[(0, k - 1, k - 1, k - 1)], key[(0, k, k, k)]
+    if tr is None or up is None:
+        continue
+    base = p[pk, 3]
+    up1 = p[up, 1] if up != tr else p[tr, 4]
+    ch.append([p[tr, 1] - base, p[tr, 3] - base, up1 - base, p[up, 7] - base, p[pk1, 3] - base, p[pk1, 6] - base])
+if ch:
+    print("second chain, us after potrf(k-1)'s panels end (median): trsm(k+1,k-1) deps met %.2f / solved %.2f, "
+          "update(k+1,k,k-1) inputs in %.2f / end %.2f; potrf(k) panels end %.2f, A(k+1,k) in LDS %.2f"
+          % tuple(np.median(np.array(ch), 0)))
+bc = np.nonzero(typ == 3)[0]
+if len(bc):
+    print("back solve: %d bcol tasks, last potrf publish -> last bcol end %.1f us; per bcol median: parent wait -> end %.2f us"
+          % (len(bc), p[bc, 7].max() - fac_end, np.median((p[bc, 7] - np.where(p[bc, 3] > 0, p[bc, 3], p[bc, 2])))))
+pp = []
+for k in pot:   # wave 0's panels (stamps 8 + 2p / 9 + 2p) and the gaps between them (period overrun + lookahead)
+    r = p[k]
+    if r[8] > 0 and r[15] > 0:
+        pp.append([r[9] - r[8], r[11] - r[10], r[13] - r[12], r[15] - r[14], r[10] - r[9], r[12] - r[11], r[14] - r[13]])
+if pp:
+    print("panels (wave 0), median us: p0 %.2f p1 %.2f p2 %.2f p3 %.2f; gaps p0->p1 %.2f p1->p2 %.2f p2->p3 %.2f"
+          % tuple(np.median(np.array(pp), 0)))
+pp = []
+for k in pot:   # wave 0's panels (stamps 8 + 2p / 9 + 2p) and the gaps between them (period overrun + lookahead)
+    r = p[k]
+    if r[8] > 0 and r[15] > 0:
+        pp.append([r[9] - r[8], r[11] - r[10], r[13] - r[12], r[15] - r[14], r[10] - r[9], r[12] - r[11], r[14] - r[13]])
+if pp:
+    print("panels (wave 0), median us: p0 %.2f p1 %.2f p2 %.2f p3 %.2f; gaps p0->p1 %.2f p1->p2 %.2f p2->p3 %.2f"
+          % tuple(np.median(np.array(pp), 0)))
 for a in range(min(6, len(pot))):
     print("  potrf #%d: " % a + " ".join("%.2f" % v for v in rows[a]))

@@ -1,19 +1,21 @@
 """Host-side check of the dataflow Cholesky's plan (ba_plan.cpp
 build_chol_structure): the task list is executed sequentially in ticket order
 by a numpy model of each task (the kernel's tile algebra, chol_dataflow_kernel;
-potrf(k) also applies its tile's last update and solves tile (k+1,k); bsolve(c)
-also applies bupd(c,c-1)); every version the kernel polls for must already
-hold, every tile's updates must arrive in sequence, every task must run exactly
-once, and the result must be the damped SPD solution.  Dense systems (the
-chol-only plan) and the tile-sparse, pose-permuted reduced systems of BA plans
-(C2, C3 and a C5-shaped 2048-keyframe graph) are covered.  No GPU needed."""
+potrf(k) also applies its tile's last update and solves tile (k+1,k) when it
+exists, and may run potrf(k+1) next (a chain); trsm(i,k) may also apply the
+update (i,k+1,k); bcol(c) is the whole back solve of block column c);
+every version the kernel polls for must already hold, every tile's updates must
+arrive in sequence, every task must run exactly once, and the result must be
+the damped SPD solution.  Dense systems (the chol-only plan) and the
+tile-sparse, pose-permuted reduced systems of BA plans (C2, C3 and a C5-shaped
+2048-keyframe graph) are covered.  No GPU needed."""
 import ctypes
 import time
 
 import numpy as np
 import pytest
 
-POTRF, TRSM, UPD, BSOLVE, BUPD = range(5)
+POTRF, TRSM, UPD, BCOL = range(4)
 
 
 def _lib():
@@ -89,7 +91,14 @@ def emulate(M, n, st):
     col = lambda k: slice(64 * k, min(64 * k + 64, n))
     S = lambda i, j: slot[i, j]
     seen = set()
-    for t, i, j, k, a, b, _, _ in st["tasks"]:
+    tasks = st["tasks"]
+    for q, (t, i, j, k, a, b, c, ch) in enumerate(tasks):
+        if t == POTRF and c:                                         # chained: potrf(k) runs potrf(k+1) next
+            nx = tasks[c - 1]
+            assert c - 1 > q and nx[0] == POTRF and nx[3] == k + 1 and nx[4] == k and nx[7] == 1 and b
+        if t == POTRF and ch:                                        # the placeholder of a chained potrf
+            assert any(tt[0] == POTRF and tt[6] == q + 1 for tt in tasks[:q])
+    for t, i, j, k, a, b, c, _ in tasks:
         key = (t, i, j, k)
         assert key not in seen
         seen.add(key)
@@ -111,17 +120,18 @@ def emulate(M, n, st):
             M[R, col(k)] = T
             linv[k] = np.linalg.inv(L)
             ver[s] = fin[s]
-            if b:                                                    # trsm(k+1, k)
-                sb = S(k + 1, k)
-                assert sb >= 0 and ver[sb] >= fin[sb] - 1
-                # blocked forward substitution against L_kk itself (not via L_kk^-1)
-                M[blk(k + 1), col(k)] = np.linalg.solve(L, M[blk(k + 1), col(k)].T).T
-                if k + 1 == nbr - 1:
-                    y[64 * k:64 * k + Bp] = M[n, col(k)]
-                    yver[k] = 1
-                ver[sb] = fin[sb]
-            else:
-                assert k + 1 >= nbr or S(k + 1, k) < 0
+            for d, fused in ((1, b),):                               # the tile (k+1,k)
+                if fused:
+                    sb = S(k + d, k)
+                    assert sb >= 0 and ver[sb] >= fin[sb] - 1
+                    # forward substitution against L_kk itself (not via L_kk^-1)
+                    M[blk(k + d), col(k)] = np.linalg.solve(L, M[blk(k + d), col(k)].T).T
+                    if k + d == nbr - 1:
+                        y[64 * k:64 * k + Bp] = M[n, col(k)]
+                        yver[k] = 1
+                    ver[sb] = fin[sb]
+                else:                                                # the plan fuses (k+1,k) whenever it exists
+                    assert k + d >= nbr or S(k + d, k) < 0
             lver[k] = 1
         elif t == TRSM:
             s = S(i, k)
@@ -131,27 +141,28 @@ def emulate(M, n, st):
                 y[64 * k:64 * k + (col(k).stop - col(k).start)] = M[n, col(k)]
                 yver[k] = 1
             ver[s] = fin[s]
+            if b:                                                    # + the update (i,k+1,k), the tile's last
+                su = S(i, k + 1)
+                assert su >= 0 and ver[su] == a and ver[S(k + 1, k)] >= fin[S(k + 1, k)] and a == fin[su] - 2
+                M[blk(i), col(k + 1)] -= M[blk(i), col(k)] @ M[col(k + 1), col(k)].T
+                ver[su] = a + 1
         elif t == UPD:
             s = S(i, j)
             assert s >= 0 and ver[s] == a                           # updates arrive in sequence
             assert ver[S(i, k)] >= fin[S(i, k)] and ver[S(j, k)] >= fin[S(j, k)]
             M[blk(i), col(j)] -= M[blk(i), col(k)] @ M[col(j), col(k)].T
             ver[s] = a + 1
-        elif t == BSOLVE:                                            # + bupd(c, c-1) when fused
+        else:                                                        # bcol(c): the whole back solve of x_c
             c = i
-            assert lver[c] and yver[c] >= ycnt[c]
+            assert lver[c] and yver[c] >= 1
             Bp = col(c).stop - col(c).start
-            x[col(c)] = linv[c].T @ y[64 * c:64 * c + Bp]
+            yc = y[64 * c:64 * c + Bp].copy()
+            rows = [r for r in range(nbc - 1, c, -1) if S(r, c) >= 0]
+            for r in rows:                                           # x_r published, L_rc final
+                assert xdone[r] and ver[S(r, c)] >= fin[S(r, c)]
+                yc -= M[col(r), col(c)].T @ x[col(r)]
+            x[col(c)] = linv[c].T @ yc
             xdone[c] = 1
-            if a:
-                assert S(c, c - 1) >= 0 and ver[S(c, c - 1)] >= fin[S(c, c - 1)] and yver[c - 1] == ycnt[c - 1] - 1
-                y[64 * (c - 1):64 * c] -= M[col(c), col(c - 1)].T @ x[col(c)]
-                yver[c - 1] = ycnt[c - 1]
-        else:
-            r, c = i, j
-            assert xdone[r] and ver[S(r, c)] >= fin[S(r, c)] and yver[c] == 1 + a
-            y[64 * c:64 * c + 64] -= M[col(r), col(c)].T @ x[col(r)]
-            yver[c] = 2 + a
     assert np.all(ver == fin) and np.all(yver == ycnt) and np.all(xdone == 1) and np.all(lver == 1)
     return x, len(seen)
 
@@ -213,10 +224,12 @@ def test_dense_task_list_solves_spd(n):
     rng = np.random.default_rng(n)
     st = chol_plan(n)
     nbc, nbr = (n + 63) // 64, (n + 64) // 64
-    # the dense DAG: potrf + trsm below the fused one + updates but the fused
-    # ones + bsolve + bupd but the fused ones
-    expect = nbc + sum(max(0, nbr - k - 2) for k in range(nbc)) \
-        + sum((nbr - jb) * jb for jb in range(1, nbc)) - (nbc - 1) + nbc + nbc * (nbc - 1) // 2 - (nbc - 1)
+    # the dense DAG: potrf + trsm below the fused tile + updates but the ones
+    # fused into potrf (the diagonal's last) and into trsm (each (i,k+1,k)) +
+    # one back-solve task per block column
+    ntrsm = sum(max(0, nbr - k - 2) for k in range(nbc))
+    expect = nbc + ntrsm + sum((nbr - jb) * jb for jb in range(1, nbc)) - (nbc - 1) \
+        - sum(max(0, nbr - k - 2) for k in range(nbc - 1)) + nbc
     assert len(st["tasks"]) == expect
     assert st["nslots"] == st["nslots_input"] == sum(min(i + 1, nbc) for i in range(nbr))
     Q, _ = np.linalg.qr(rng.normal(size=(n, n)))
