@@ -125,7 +125,7 @@ struct BaPlan {
   size_t sync_bytes = 0;                // ticket, abort, tile versions, y versions, x flags, L^-1 flags
   // device layout (byte offsets into the workspace)
   size_t off_ints = 0, off_hpart = 0, off_gram = 0, off_qw = 0, off_ei = 0, off_M = 0, off_x = 0,
-         off_flag = 0, off_sync = 0, off_linv = 0, off_ybuf = 0, total = 0;
+         off_flag = 0, off_sync = 0, off_ybuf = 0, total = 0;
   // offsets (in ints) of each int array inside the int section
   size_t o_ii, o_jj, o_kx, o_feptr, o_fedges, o_frptr, o_rpose, o_redge, o_fnb, o_fgoff,
       o_blka, o_blkb, o_blkcptr, o_rhscptr, o_rhspos, o_contrib, o_rhscontrib, o_tasks,

@@ -720,7 +720,6 @@ struct CholDev {
   int* sync;    // [0] ticket [1] abort [4..] ver[nslots] | yver[nbc] | lkk[nbc]  (ba.hpp chol_sync_bytes)
   unsigned* gran;  // x hand-off granules {double x, tag, 0}, 64 per block column (inside the sync area)
   int* flag;    // bit 0: factorisation failed (dx = 0), bit 1: spin timeout
-  double* linv; // [nbc][64][64]
   double* ybuf; // [nbc*64]
   float* dx;    // [n]
   int inject;   // test hook (droid_chol_set_fault_inject): raise the abort at once, as a timeout would
@@ -733,10 +732,15 @@ struct CholDev {
 #if DROID_CONV_PROFILE
 #define CH_STAMPT(t, ph)                                                                      \
   do {                                                                                        \
-    if (d.prof && tid == 0) d.prof[(long)(t) * 16 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+    if (d.prof && tid == 0) d.prof[(long)(t) * 24 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define CH_STAMPW(t, ph)   /* lane 0 of the calling wave */                                 \
+  do {                                                                                        \
+    if (d.prof && lane == 0) d.prof[(long)(t) * 24 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define CH_STAMPT(t, ph) do { } while (0)
+#define CH_STAMPW(t, ph) do { } while (0)
 #endif
 #define CH_STAMP(ph) CH_STAMPT(tk, ph)
 
@@ -1193,10 +1197,44 @@ __device__ bool gran_wait(__amdgpu_buffer_rsrc_t rg, unsigned g0, double* dst, i
 // sums rows 16w..16w+15 into part[w][j] (the caller adds the four partials in
 // wave order after a barrier: a fixed reduction order)
 __device__ __forceinline__ void gemv_t_part(const double* M, const double* v, double* part, int wave, int lane) {
+  // the wave's 16 v values by eight 16-B broadcast reads from one base, M's
+  // rows from one base + immediate offsets (no per-element address registers)
+  const dbl2* vv = reinterpret_cast<const dbl2*>(v + 16 * wave);
+  const double* m = M + 16 * wave * LT + lane;
+  double x[16];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const dbl2 t = vv[q];
+    x[2 * q] = t[0];
+    x[2 * q + 1] = t[1];
+  }
   double s = 0.0;
 #pragma unroll
-  for (int t = 0; t < 16; ++t) s = fma(M[(16 * wave + t) * LT + lane], v[16 * wave + t], s);
+  for (int t = 0; t < 16; ++t) s = fma(m[t * LT], x[t], s);
   part[64 * wave + lane] = s;
+}
+
+// One wave: the four 16x16 diagonal-block inverses D_p = L_pp^-1 of a factored
+// 64x64 pivot block (lower triangle of L, row stride LT; rows past the real
+// block zero and dinv = 1 there, so D_p is unit-padded) into D's diagonal
+// blocks; lane = 16 * block + column.  Right-looking forward substitution down
+// the column: once x_t is final it leaves column t of L out of the rows below,
+// so the dependent chain per row is one fma and one multiply (the left-looking
+// form summed each row's t terms in sequence: a 120-fma chain).
+__device__ __forceinline__ void diag_inv_blocks(const double* L, double* D, const double* dinv, int lane) {
+  const int base = 16 * (lane >> 4), cc = lane & 15;
+  double acc[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc[t] = (t == cc) ? 1.0 : 0.0;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const double x = acc[t] * dinv[base + t];
+    acc[t] = x;
+#pragma unroll
+    for (int m = t + 1; m < 16; ++m) acc[m] = fma(-L[(base + m) * LT + base + t], x, acc[m]);
+  }
+#pragma unroll
+  for (int t = 0; t < 16; ++t) D[(base + t) * LT + base + cc] = acc[t];
 }
 
 // every tile a task record names lies in the plan's slot map (wave-uniform)
@@ -1228,14 +1266,13 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
   const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
   const int n = d.n, nbc = d.nbc, nbr = d.nbr;
   const __amdgpu_buffer_rsrc_t rM = mkrs(d.M, (size_t)d.nslots * kTile * 8);
-  const __amdgpu_buffer_rsrc_t rL = mkrs(d.linv, (size_t)nbc * kTile * 8);
   const __amdgpu_buffer_rsrc_t rY = mkrs(d.ybuf, (size_t)nbc * 64 * 8);
   const __amdgpu_buffer_rsrc_t rG = mkrs(d.gran, (size_t)nbc * 64 * 16);
   int* ticket = d.sync;
   int* abort_w = d.sync + 1;
   int* ver = d.sync + 4;
   int* yver = ver + d.nslots;
-  int* lkk = yver + nbc;    // L_kk and its D_p stored: potrf(k)'s waves 0 and 1 each add 1 after their stores
+  int* lkk = yver + nbc;    // L_kk stored (potrf(k)'s wave 0 flags it right after its panels)
   auto SL = [&](int i, int j) { return d.slot[i * nbc + j]; };
   if (d.inject && blockIdx.x == 0 && tid == 0) {
     __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1283,7 +1320,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           break;
         case kTrsm: {
           const int s = SL(i, k);
-          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&lkk[k], 2, abort_w, d.flag);
+          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&lkk[k], 1, abort_w, d.flag);
           break;
         }
         case kUpdate: {
@@ -1299,7 +1336,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           break;
         }
         default: {  // kBcol: L_cc with its diagonal-block inverses, and the forward value of y_c
-          ok = poll_ge(&lkk[i], 2, abort_w, d.flag) && poll_ge(&yver[i], 1, abort_w, d.flag);
+          ok = poll_ge(&lkk[i], 1, abort_w, d.flag) && poll_ge(&yver[i], 1, abort_w, d.flag);
           break;
         }
       }
@@ -1327,6 +1364,10 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       const int* rec = tsk;
       bool haveL = false;   // L(k,klast) already in tL (chained from potrf(k-1))
       bool alive = true;
+      // inside a pivot chain the publish of tile (k+1,k) and y_k waits for the
+      // next potrf's first barrier (its stores have landed by then): the chain
+      // does not stall on the store drain
+      int pend_s = -1, pend_fin = 0, pend_y = -1;
       for (;;) {
         const int R0 = 64 * kc, Bp = min(64, n - R0), Br = min(64, n + 1 - R0);
         const int np = (Bp + 15) >> 4;
@@ -1369,6 +1410,10 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           blk_sub<16>(T0, 16 * wave, 0, tL, 16 * wave, 0, tL, 0, 0, lane);
           __syncthreads();
         }
+        if (pend_s >= 0) {   // the previous potrf's deferred publish
+          publish(&ver[pend_s], pend_fin, pend_y >= 0 ? &yver[pend_y] : nullptr, 1);
+          pend_s = -1;
+        }
         CH_STAMPT(tcur, 2);
         for (int p = 0; p < np; ++p) {
           if (wave == 0) {
@@ -1402,13 +1447,17 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         const bool rhs0 = Br > Bp;                    // the rhs row inside the pivot tile
         const bool rhs1 = fz && kc + 1 == nbr - 1;    // ... or in tile (k+1,k)
         if (wave == 0) {
-          // L_kk (rows and columns < Bp) goes out now (counted on lkk after the solve)
+          // L_kk (rows and columns < Bp) goes out now and is flagged as soon as
+          // it has landed (one storing wave: its own vmcnt(0), Guideline 16 R1);
+          // the drain runs beside wave 1's D_p
 #pragma unroll 4
           for (int q = 0; q < 32; ++q) {
             const int rr = q * 2 + (lane >> 5), cc2 = (lane & 31) * 2;
             if (rr < Bp && cc2 < Bp)
               st2(rM, (unsigned)(((size_t)skk * kTile + rr * 64 + cc2) * 8), *reinterpret_cast<const dbl2*>(&T0[rr * LT + cc2]));
           }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) __hip_atomic_store(&lkk[kc], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else if (wave == 1) {
           // y_k (the solved rhs row), the rows past Bp cleared (L_kk^-1 is
           // unit-padded there), then the diagonal-block inverses D_p = L_pp^-1
@@ -1418,40 +1467,35 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           for (int r = Bp; r < 64; ++r) T0[r * LT + lane] = 0.0;
           if (lane >= Bp) dinv[lane] = 1.0;
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          const int base = 16 * (lane >> 4), cc = lane & 15;
-          double xv[16];
-#pragma unroll
-          for (int t = 0; t < 16; ++t) {
-            double sacc = (t == cc) ? 1.0 : 0.0;
-#pragma unroll
-            for (int u = 0; u < t; ++u) sacc = fma(-T0[(base + t) * LT + base + u], xv[u], sacc);
-            xv[t] = sacc * dinv[base + t];  // 1 / L[t][t] from the panel
-          }
-#pragma unroll
-          for (int t = 0; t < 16; ++t) {
-            tL[(base + t) * LT + base + cc] = xv[t];
-            st1(rL, (unsigned)(((size_t)kc * kTile + (base + t) * 64 + base + cc) * 8), xv[t]);
-          }
+          CH_STAMPW(tcur, 16);
+          diag_inv_blocks(T0, tL, dinv, lane);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          CH_STAMPW(tcur, 17);
         }
         if (!all_ok(load_below(true))) { alive = false; break; }
         CH_STAMPT(tcur, 6);
         if (fz) tall_solve(tB, T0, tL, scr, wave, fr, fk);   // trsm(k+1,k) with the D_p, each wave 16 rows
-        if (wave <= 1) {
-          // waves 0 / 1 stored L_kk / the D_p before the solve: each counts its
-          // own stores on lkk once they have landed (Guideline 16 R1)
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (lane == 0) __hip_atomic_fetch_add(&lkk[kc], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        CH_STAMPT(tcur, 18);
         if (fz) {
           __syncthreads();
           tile_store(rM, s1, nr1, Bp, tB);
           if (rhs1 && tid < 32)
             st2(rY, (unsigned)((R0 + 2 * tid) * 8), *reinterpret_cast<const dbl2*>(&tB[(n - R0 - 64) * LT + 2 * tid]));
         }
-        publish(&ver[skk], d.fin[skk], fz ? &ver[s1] : nullptr, fz ? d.fin[s1] : 0, (rhs0 || rhs1) ? &yver[kc] : nullptr, 1);
-        CH_STAMPT(tcur, 5);
+        CH_STAMPT(tcur, 19);
         // chained successor: potrf(k+1), whose last update is L(k+1,k) L(k+1,k)^T
         const int nxt = __builtin_amdgcn_readfirstlane(rec[6]);
+        if (nxt > 0 && fz) {   // (the diagonal tile's own version is read by no task)
+          __syncthreads();     // the tile stores have read tB
+          pend_s = s1;
+          pend_fin = d.fin[s1];
+          pend_y = (rhs0 || rhs1) ? kc : -1;
+        } else {
+          publish(&ver[skk], d.fin[skk], fz ? &ver[s1] : nullptr, fz ? d.fin[s1] : 0,
+                  (rhs0 || rhs1) ? &yver[kc] : nullptr, 1);
+        }
+        CH_STAMPT(tcur, 5);
         if (nxt <= 0) break;
         CH_STAMPT(tcur, 7);
         tcur = nxt - 1;
@@ -1481,12 +1525,16 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       // from potrf(k); it is version a+1 of (i,k+1).
       const int R0 = 64 * i, C0 = 64 * k, nr = min(64, n + 1 - R0), nc = min(64, n - C0);
       const int s = SL(i, k);
-      dbl2 pa[8], pd[8];
+      dbl2 pa[8];
       tile_issue(rM, s, nr, nc, pa);
-      tile_issue(rL, k, 64, 64, pd);   // the D_p (the rest of the tile: not read)
       tile_load(rM, SL(k, k), nc, nc, T1);
       tile_commit(pa, T0);
-      tile_commit(pd, T2);
+      __syncthreads();
+      if (wave == 0) {   // the D_p, from L_kk itself
+        vec[lane] = lane < nc ? 1.0 / T1[lane * LT + lane] : 1.0;   // 1 / L[t][t]
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        diag_inv_blocks(T1, T2, vec, lane);
+      }
       __syncthreads();
       CH_STAMP(2);
       tall_solve(T0, T1, T2, scr, wave, fr, fk);
@@ -1546,11 +1594,11 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       // L_cc^-T (y_c - sum_{r>p} L_rc^T x_r).  The chain step is then one
       // granule wait, one 64x64 GEMV and one granule store.
       const int c = i, C0 = 64 * c, Bc = min(64, n - C0);
+      const int om = (wave == 0 && lane < Bc) ? d.outmap[C0 + lane] : 0;   // dx index of this lane's variable
       int par = c + 1;
       while (par < nbc && SL(par, c) < 0) ++par;
       const bool haspar = par < nbc;
-      dbl2 pd[8], pc[8], pp[8];
-      tile_issue(rL, c, 64, 64, pd);                 // the D_p (diagonal blocks; the rest is not written)
+      dbl2 pc[8], pp[8];
       tile_issue(rM, SL(c, c), Bc, Bc, pc);          // L_cc
       if (haspar) tile_issue(rM, SL(par, c), min(64, n - 64 * par), Bc, pp);
       if (tid < 32) {
@@ -1558,12 +1606,14 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         vec[2 * tid] = yv[0];
         vec[2 * tid + 1] = yv[1];
       }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {   // T2 = the D_p on the diagonal, zeros elsewhere
-        const int p = tid + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
-        *reinterpret_cast<dbl2*>(&T2[rr * LT + cc]) = ((rr >> 4) == (cc >> 4)) ? pd[q] : dbl2{0.0, 0.0};
-      }
+      for (int idx = tid; idx < 64 * 64; idx += 256) T2[(idx >> 6) * LT + (idx & 63)] = 0.0;
       tile_commit(pc, T1);
+      __syncthreads();
+      if (wave == 0) {   // the D_p on T2's diagonal
+        vec[128 + lane] = lane < Bc ? 1.0 / T1[lane * LT + lane] : 1.0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        diag_inv_blocks(T1, T2, vec + 128, lane);
+      }
       __syncthreads();
       // L_cc^-1 in T2: Linv[I][J] = -D_I sum_{K=J}^{I-1} L[I][K] Linv[K][J]
       for (int I = 1; I < 4; ++I) {
@@ -1643,13 +1693,18 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         const unsigned long long u = __builtin_bit_cast(unsigned long long, xv);
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)u, (unsigned)(u >> 32), 1u, 0u}, rG,
                                                (int)((64 * c + lane) * 16), 0, kSc1);
-        const bool failed = (__hip_atomic_load(d.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1) != 0;
-        if (lane < Bc) d.dx[d.outmap[C0 + lane]] = failed ? 0.0f : (float)xv;
+        if (lane < Bc) d.dx[om] = (float)xv;   // a failed factorisation zeroes dx after the launch
       }
       __syncthreads();   // vec / scr / T0-T2 are reused by the next task
     }
     CH_STAMP(7);
   }
+}
+
+// the dense chol API (droid_chol_solve): dx = 0 when the factorisation failed
+__global__ void chol_fail_zero_kernel(float* dx, int n, const int* flag) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < n && (*flag & 1)) dx[v] = 0.0f;
 }
 
 // ---------------------------------------------------------------------------
@@ -1662,6 +1717,7 @@ __global__ void __launch_bounds__(256) ba_backsub_kernel(BaDev d) {
   __shared__ float Tsh[256 * 8];
   __shared__ float dxs[256 * 8];
   if (*d.flag & 2) return;
+  const bool failed = (*d.flag & 1) != 0;   // not SPD: dx = 0 (the solve leaves x undefined there)
   const int f = blockIdx.y;
   const int HW = d.HW;
   const int px = blockIdx.x * 256 + threadIdx.x;
@@ -1683,8 +1739,8 @@ __global__ void __launch_bounds__(256) ba_backsub_kernel(BaDev d) {
       const int e = d.fedges[base + t];
       stash_rel_pose(d, kf, e, Tsh + 8 * t);
       const int pr = d.jj[e] - d.t0;
-      for (int k = 0; k < 6; ++k) dxs[8 * t + k] = (pr > 0 && pr < d.P) ? d.dx[6 * pr + k] : 0.0f;
-      dxs[8 * t + 6] = (pr > 0 && pr < d.P) ? 1.0f : 0.0f;
+      for (int k = 0; k < 6; ++k) dxs[8 * t + k] = (pr > 0 && pr < d.P && !failed) ? d.dx[6 * pr + k] : 0.0f;
+      dxs[8 * t + 6] = (pr > 0 && pr < d.P && !failed) ? 1.0f : 0.0f;
     }
     __syncthreads();
     if (!live) continue;
@@ -1716,7 +1772,7 @@ __global__ void __launch_bounds__(256) ba_backsub_kernel(BaDev d) {
     }
   }
   if (!live) return;
-  if (use_ei) {
+  if (use_ei && !failed) {
     float dw = 0.f;
 #pragma unroll
     for (int nn = 0; nn < 6; ++nn) dw += Ei[nn] * d.dx[6 * pi + nn];
@@ -1729,10 +1785,17 @@ __global__ void __launch_bounds__(256) ba_backsub_kernel(BaDev d) {
   d.disps[(long)kf * HW + px] = disp + dzv;
 }
 
-// poses <- Exp(dx) poses; a timed-out factorisation (flag bit 1) changes nothing
-__global__ void ba_retract_kernel(float* poses, const float* dx, int t0, int P, const int* flag) {
+// poses <- Exp(dx) poses; a timed-out factorisation (flag bit 1) changes
+// nothing; a failed one (bit 0, not SPD) gives dx = 0, as the reference
+// (droid_kernels.cu:1197): the output dx is zeroed here, after the back
+// substitution read it as zero
+__global__ void ba_retract_kernel(float* poses, float* dx, int t0, int P, const int* flag) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= P || (*flag & 2)) return;
+  if (*flag & 1) {
+    for (int n = 0; n < 6; ++n) dx[6 * k + n] = 0.0f;
+    return;
+  }
   float xi[6];
   for (int n = 0; n < 6; ++n) xi[n] = dx[6 * k + n];
   retr_se3(xi, poses + 7 * (t0 + k));
@@ -1828,7 +1891,6 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_
   c.sync = reinterpret_cast<int*>(ws + p.off_sync);
   c.gran = reinterpret_cast<unsigned*>(ws + p.off_sync + chol_gran_off(p.cs.nslots, p.cs.nbc));
   c.flag = reinterpret_cast<int*>(ws + p.off_flag);
-  c.linv = reinterpret_cast<double*>(ws + p.off_linv);
   c.ybuf = reinterpret_cast<double*>(ws + p.off_ybuf);
   c.dx = dx;
   // test hook (droid_chol_set_fault_inject): a timeout in every solve, in the
@@ -1861,6 +1923,7 @@ using namespace droid;
 
 extern "C" {
 
+#if DROID_TESTING
 // Test hook for the dataflow solve's failure handling: 0 off, 1 every solve
 // aborts as on a dependency-wait timeout (status bit 1), 2 only the next solve
 // does, 3 the next solve is launched without zeroing its sync area (the
@@ -1870,8 +1933,10 @@ int droid_chol_set_fault_inject(int mode) {
   g_chol_inject = mode;
   return kOk;
 }
+#endif  // DROID_TESTING
 
-// Profiling builds (make prof): per Cholesky task, 16 int64 s_memrealtime
+#if DROID_TESTING
+// Profiling builds (make prof): per Cholesky task, 24 int64 s_memrealtime
 // stamps (100 MHz), scripts/chol_timeline.py names them.
 int droid_chol_set_profile(void* buf) {
 #if DROID_CONV_PROFILE
@@ -1882,6 +1947,7 @@ int droid_chol_set_profile(void* buf) {
   return fail(kUnsupported, "chol_set_profile: build with make prof (DROID_CONV_PROFILE=1)");
 #endif
 }
+#endif  // DROID_TESTING
 
 int droid_ba_plan_upload(void* plan, void* workspace, hipStream_t stream) {
   auto* p = static_cast<BaPlan*>(plan);
@@ -2062,7 +2128,10 @@ int droid_chol_solve(void* plan, void* workspace, float lm, float ep, float* dx,
   ba_damp_kernel<<<ceil_div(std::max(p->n, 1), 256), 256, 0, stream>>>(M, slot, p->cs.nbc, p->n, lm, ep, flag, 1);
   DROID_LAUNCH_CHECK();
   if (p->n == 0) return kOk;
-  return launch_chol_dataflow(*p, ws, dx, stream);
+  if (int st = launch_chol_dataflow(*p, ws, dx, stream)) return st;
+  chol_fail_zero_kernel<<<ceil_div(p->n, 256), 256, 0, stream>>>(dx, p->n, flag);
+  DROID_LAUNCH_CHECK();
+  return kOk;
 }
 
 // Full ba(): `iterations` GN steps on one device (droid_backends.ba).

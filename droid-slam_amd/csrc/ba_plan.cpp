@@ -793,7 +793,6 @@ static int build_plan(BaPlan& p, const int64_t* ii, const int64_t* jj, int E, co
   p.off_x = off; off = align_up(off + (size_t)(p.n + 1) * 8, 256);
   p.off_flag = off; off = align_up(off + 64, 256);
   p.off_sync = off; off = align_up(off + p.sync_bytes, 256);
-  p.off_linv = off; off = align_up(off + (size_t)std::max(nbc, 1) * kTile * 8, 256);
   p.off_ybuf = off; off = align_up(off + (size_t)std::max(nbc, 1) * 64 * 8, 256);
   p.total = off;
   return kOk;
@@ -859,7 +858,6 @@ int droid_chol_plan_create(int n, void** plan_out) {
   p->off_x = off; off = align_up(off + (size_t)(n + 1) * 8, 256);
   p->off_flag = off; off = align_up(off + 64, 256);
   p->off_sync = off; off = align_up(off + p->sync_bytes, 256);
-  p->off_linv = off; off = align_up(off + (size_t)std::max(nbc, 1) * kTile * 8, 256);
   p->off_ybuf = off; off = align_up(off + (size_t)std::max(nbc, 1) * 64 * 8, 256);
   p->total = off;
   *plan_out = p;

@@ -49,6 +49,13 @@ int fail(int code, const std::string& msg);
 #ifndef DROID_AB
 #define DROID_AB 0
 #endif
+#ifndef DROID_CONV_PROFILE
+#define DROID_CONV_PROFILE 0
+#endif
+// The testing builds (make ab, make prof) also export the hooks declared in
+// include/droid_backends_testing.h (A/B variant and tile setters, fault
+// injection, profile buffers); the product library exports none of them.
+#define DROID_TESTING (DROID_AB || DROID_CONV_PROFILE)
 inline int ab_knob(const char* name, int dflt) {
 #if DROID_AB
   const char* e = getenv(name);

@@ -2686,6 +2686,7 @@ extern "C" {
 // 3 head (fp32 out32, sigmoid on co >= 2); 4 GRU global mean (atomic fp32 out32, zeroed by caller).
 static long long* g_conv_prof = nullptr;
 
+#if DROID_TESTING
 // Timeline of the next band-kernel launches (debug/profiling): buf receives 6
 // int64 per workgroup (hardware id, s_memtime at entry / loop start / loop end /
 // epilogue stores issued / stores drained); null turns it off.  Only the profiling build (make prof ->
@@ -2700,6 +2701,7 @@ int droid_conv_set_profile(void* buf) {
   return droid::fail(droid::kUnsupported, "conv_set_profile: build with make prof (DROID_CONV_PROFILE=1)");
 #endif
 }
+#endif  // DROID_TESTING
 
 static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstride, int nsrc,
                           const void* wp, const float* bias, const float* bbias, int B, int H, int W,
@@ -2837,6 +2839,7 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
   return launch_conv<16>(a, stream);
 }
 
+#if DROID_TESTING
 // Tile policy of the W == 64 3x3 convs: -1 = default (plain convs and small
 // gate-conv grids on the two-workgroups-per-CU tile, C3-sized gate convs on the
 // 8-wave band tiles), 0 = 8-wave band tiles only, 1 = the two-workgroup tile
@@ -2849,6 +2852,7 @@ int droid_conv_set_tile(int mode) {
   band2_mode() = mode;
   return prev;
 }
+#endif  // DROID_TESTING
 
 #if DROID_AB
 // A/B build only (not in include/droid_backends.h): the 64-channel band tile's
@@ -2860,6 +2864,7 @@ int droid_conv_set_pair(int on) {
 }
 #endif
 
+#if DROID_TESTING
 // Which kernel droid_conv_gru_pre_f16 runs for a ConvGRU gate conv (epi 1: z|r,
 // Cout 256; epi 2: q, Cout 128) over B images of H x W under the current tile
 // policy: 1 = conv_band2_kernel, 0 = the 8-wave band tile (<256,256> for z|r,
@@ -2875,6 +2880,7 @@ int droid_conv_gate_tile(int epi, int B, int H, int W) {
   if (epi == EPI_GRU_ZR) return ((H * W) % 256 == 0 && band_fits<256, 256>(W, &ns_, &nh_)) ? 0 : -1;
   return ((H * W) % 384 == 0 && band_fits<384, 128>(W, &ns_, &nh_)) ? 0 : -1;
 }
+#endif  // DROID_TESTING
 
 int droid_conv_nhwc_f16(const void* const* srcs, const int* C, const int* cstride, int nsrc,
                         const void* wp, const float* bias, const float* bbias, int B, int H, int W,

@@ -1162,6 +1162,7 @@ static int& alt2_cv() {
 
 extern "C" {
 
+#if DROID_TESTING
 // Profiling builds (make prof): per workgroup, for its first 32 stages, 8 int64:
 // s_memtime at stage start / box landed / C done / C barrier / bilinear done /
 // lookup barrier / stage end, then (box taps * 2 + slow-path flag).
@@ -1174,6 +1175,7 @@ int droid_alt_set_profile(void* buf) {
   return fail(kUnsupported, "alt_set_profile: build with make prof (DROID_CONV_PROFILE=1)");
 #endif
 }
+#endif  // DROID_TESTING
 
 int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int* Wl, const int* f1, const int* f2,
                                const int* order, const float* coords, const void* w, const float* bias, void* out,
@@ -1273,6 +1275,7 @@ int droid_corr_alt_ce0_ordered(const void* const* pyr, const int* Hl, const int*
   return kOk;
 }
 
+#if DROID_TESTING
 // A/B hook: corr_alt2_kernel's XCD chunk in edges (0, the default = the plain
 // interleaved walk; in the A/B build env DROID_ALT_CHUNK sets the initial value)
 int droid_alt_set_chunk(int edges) {
@@ -1280,7 +1283,9 @@ int droid_alt_set_chunk(int edges) {
   alt_chunk_edges() = edges;
   return kOk;
 }
+#endif  // DROID_TESTING
 
+#if DROID_TESTING
 // A/B hook: 2 = corr_alt2_kernel (the product kernel); in the A/B build only:
 // 1 = the one-workgroup-per-CU kernel, 3 = corr_alt2_kernel<V3>, and the
 // round-5 pieces apart - 4 = the round-4 V2 (CV 0), 5 = row-K lookup tile only
@@ -1298,5 +1303,6 @@ int droid_alt_set_variant(int v) {
 #endif
   return kOk;
 }
+#endif  // DROID_TESTING
 
 }  // extern "C"

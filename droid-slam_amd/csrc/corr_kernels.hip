@@ -645,10 +645,12 @@ static bool coop_ok(int HW, const void* out, long maxslice) {
 
 extern "C" {
 
+#if DROID_TESTING
 int droid_lookup_set_coop(int on) {
   lookup_coop() = on ? 1 : 0;
   return kOk;
 }
+#endif  // DROID_TESTING
 
 // dtype codes: 0 = fp16, 1 = fp32, 2 = fp64
 int droid_corr_index_forward(int dtype, const void* volume, const float* coords, void* corr,

@@ -19,6 +19,7 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
+from . import _lib
 from ._lib import EXPORTS, check, lib
 
 __all__ = ["ba", "frame_distance", "projmap", "depth_filter", "iproj", "altcorr_forward",
@@ -305,31 +306,31 @@ def chol_set_fault_inject(mode):
     dataflow solve abort as on a dependency-wait timeout, CHOL_INJECT_ONCE only
     the next one, CHOL_INJECT_STALE launches the next solve on a sync area that
     was not zeroed (the kernel's entry check reports it)."""
-    check(lib.droid_chol_set_fault_inject(int(mode)), "chol_set_fault_inject")
+    check(_lib.testing_hook("droid_chol_set_fault_inject")(int(mode)), "chol_set_fault_inject")
 
 
 def alt_set_variant(v):
     """A/B hook (droid_alt_set_variant): 2 = corr_alt2_kernel (the product); the A/B
     build adds 1 = corr_alt_ce0_kernel, 3 = corr_alt2_kernel<V3>, 4 = the round-4 V2,
     5 = V2 with the row-K lookup tile, 6 = V2 with the pixel-major C layout."""
-    check(lib.droid_alt_set_variant(int(v)), "alt_set_variant")
+    check(_lib.testing_hook("droid_alt_set_variant")(int(v)), "alt_set_variant")
 
 
 def lookup_set_coop(on):
     """A/B hook (droid_lookup_set_coop): the cooperative NCHW lookup (1, default) or the per-thread kernel (0)."""
-    check(lib.droid_lookup_set_coop(1 if on else 0), "lookup_set_coop")
+    check(_lib.testing_hook("droid_lookup_set_coop")(1 if on else 0), "lookup_set_coop")
 
 
 def alt_set_chunk(edges):
     """A/B hook (droid_alt_set_chunk): edges per XCD chunk of corr_alt2_kernel's walk, 0 = interleaved."""
-    check(lib.droid_alt_set_chunk(int(edges)), "alt_set_chunk")
+    check(_lib.testing_hook("droid_alt_set_chunk")(int(edges)), "alt_set_chunk")
 
 
 def conv_set_tile(mode):
     """Tile policy of the W=64 3x3 band convs (droid_conv_set_tile): -1 default,
     0 = 8-wave band tiles only, 1 = the two-workgroups-per-CU tile wherever it
     applies.  Returns the previous policy."""
-    prev = lib.droid_conv_set_tile(int(mode))
+    prev = _lib.testing_hook("droid_conv_set_tile")(int(mode))
     if prev == -2:
         raise RuntimeError("conv_set_tile: mode must be -1, 0 or 1")
     return prev
@@ -338,7 +339,7 @@ def conv_set_tile(mode):
 def conv_gate_tile(epi, B, H, W):
     """droid_conv_gate_tile: the kernel a gate conv of this shape runs on
     (1 band2, 0 the 8-wave band tile, 2 the 4-wave z|r tile, -1 none)."""
-    return int(lib.droid_conv_gate_tile(int(epi), int(B), int(H), int(W)))
+    return int(_lib.testing_hook("droid_conv_gate_tile")(int(epi), int(B), int(H), int(W)))
 
 
 EPI_ACT, EPI_GRU_ZR, EPI_GRU_Q, EPI_HEAD, EPI_GLO = 0, 1, 2, 3, 4

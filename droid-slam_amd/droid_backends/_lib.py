@@ -33,13 +33,6 @@ _SIGS = {
     "droid_corr_lookup_ce0": ([_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_corr_lookup_ce0_tiled": ([_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_corr_lookup_ce0_tiled_slots": ([_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
-    "droid_conv_set_profile": ([_p], _i),
-    "droid_alt_set_profile": ([_p], _i),
-    "droid_alt_set_variant": ([_i], _i),
-    "droid_alt_set_chunk": ([_i], _i),
-    "droid_lookup_set_coop": ([_i], _i),
-    "droid_conv_set_tile": ([_i], _i),
-    "droid_conv_gate_tile": ([_i, _i, _i, _i], _i),
     "droid_corr_volume_pyramid": ([_p, _p, _p, _i, _i, _i, _i, _p, _i, _p], _i),
     "droid_corr_alt_ce0": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
     "droid_corr_alt_ce0_ordered": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p], _i),
@@ -63,8 +56,6 @@ _SIGS = {
     "droid_altcorr_backward": ([_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p], _i),
     "droid_projective_transform": ([_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p], _i),
     "droid_frame_distance": ([_p, _p, _p, _p, _p, _i, _i, _i, _f, _p, _p], _i),
-    "droid_chol_set_profile": ([_p], _i),
-    "droid_chol_set_fault_inject": ([_i], _i),
     "droid_instance_norm_workspace": ([_i, _i, _i], _sz),
     "droid_instance_norm_act_f16": ([_p, _p, _p, _i, _i, _i, _i, _f, _p, _sz, _p], _i),
     "droid_proximity_workspace": ([_i, _i, _i], _sz),
@@ -101,7 +92,22 @@ _SIGS = {
     "droid_ba_run": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _f, _f, _p, _p, _p], _i),
 }
 
+# the testing builds' hooks (include/droid_backends_testing.h): bound when the
+# loaded library exports them (lib/ab, lib/prof); the product library does not
+_TEST_SIGS = {
+    "droid_conv_set_profile": ([_p], _i),
+    "droid_alt_set_profile": ([_p], _i),
+    "droid_alt_set_variant": ([_i], _i),
+    "droid_alt_set_chunk": ([_i], _i),
+    "droid_lookup_set_coop": ([_i], _i),
+    "droid_conv_set_tile": ([_i], _i),
+    "droid_conv_gate_tile": ([_i, _i, _i, _i], _i),
+    "droid_chol_set_profile": ([_p], _i),
+    "droid_chol_set_fault_inject": ([_i], _i),
+}
+
 EXPORTS = tuple(_SIGS)
+TEST_EXPORTS = tuple(_TEST_SIGS)
 
 for _name, (_args, _res) in _SIGS.items():
     if os.environ.get("DROID_HIP_LIB") and not hasattr(lib, _name):
@@ -109,6 +115,22 @@ for _name, (_args, _res) in _SIGS.items():
     _fn = getattr(lib, _name)
     _fn.argtypes = _args
     _fn.restype = _res
+for _name, (_args, _res) in _TEST_SIGS.items():
+    if hasattr(lib, _name):
+        _fn = getattr(lib, _name)
+        _fn.argtypes = _args
+        _fn.restype = _res
+HAS_TESTING_HOOKS = all(hasattr(lib, _n) for _n in _TEST_SIGS)
+
+
+def testing_hook(name):
+    """A hook of include/droid_backends_testing.h, or a RuntimeError naming
+    the build that has it (the product library exports none)."""
+    if not hasattr(lib, name):
+        raise RuntimeError("%s is a testing hook: only the A/B and profiling builds export it "
+                           "(make -C droid-slam_amd/csrc ab prof; tests use the ab_backends fixture); "
+                           "loaded library: %s" % (name, LIB_PATH))
+    return getattr(lib, name)
 
 
 def check(status, what):

@@ -3,6 +3,9 @@
 corr_alt2_kernel's walk: edge order vs edges grouped by target frame, times the
 XCD chunk size (droid_alt_set_chunk)."""
 import os
+# its knobs are testing hooks (include/droid_backends_testing.h): the A/B library by default
+os.environ.setdefault("DROID_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                    "droid-slam_amd", "lib", "ab", "libdroid_hip.so"))
 import sys
 
 sys.path[:0] = [os.path.dirname(os.path.abspath(__file__)), os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."),

@@ -25,7 +25,7 @@ t = {k: torch.from_numpy(prob[k]).to(dev) for k in ("poses", "disps", "intrinsic
                                                      "weights", "eta")}
 N, H, W = prob["disps"].shape
 plan = droid_backends.BaPlan(prob["ii"], prob["jj"], N, H, W, prob["t0"], prob["t1"], prob["eta"].shape[0], False, dev)
-prof = torch.zeros((plan.ntasks, 16), dtype=torch.int64, device=dev)
+prof = torch.zeros((plan.ntasks, 24), dtype=torch.int64, device=dev)
 for it in range(3):
     if it == 2:
         assert lib.droid_chol_set_profile(ctypes.c_void_p(prof.data_ptr())) == 0
@@ -50,7 +50,7 @@ pot = np.nonzero(typ == 0)[0]
 pot = pot[np.argsort(p[pot, 0])]
 # potrf stamps: 0 ticket (or chained start), 1 deps met, 2 last update's block column 0 applied (panels
 # start), 3 panels done, 6 tile (k+1,k) in LDS and the D_p formed, 5 (k+1,k) solved + published, 7 end;
-# 8 + 2p / 9 + 2p: wave 0's panel p start / end
+# 8 + 2p / 9 + 2p: wave 0's panel p start / end; 16 / 17 wave 1's D_p start / end; 18 tile solved; 19 stores issued
 names = ["wait deps", "L(k,klast) + col 0", "panels", "wait A(k+1,k)", "D + trsm(k+1,k) + publish", "end"]
 rows = []
 for a, k in enumerate(pot):
@@ -88,6 +88,20 @@ bc = np.nonzero(typ == 3)[0]
 if len(bc):
     print("back solve: %d bcol tasks, last potrf publish -> last bcol end %.1f us; per bcol median: parent wait -> end %.2f us"
           % (len(bc), p[bc, 7].max() - fac_end, np.median((p[bc, 7] - np.where(p[bc, 3] > 0, p[bc, 3], p[bc, 2])))))
+if len(bc) and os.environ.get("TL_BCOL"):
+    o = bc[np.argsort(-tasks[bc, 1])]
+    print("bcol c: ticket, deps met, rows done, parent x in, end (us after the last (k+1,k) publish)")
+    for q in o:
+        print("  bcol %3d: " % tasks[q, 1] + " ".join("%8.2f" % (p[q, s] - fac_end if p[q, s] > 0 else np.nan)
+                                                  for s in (0, 1, 2, 3, 7)))
+tl = []
+for k in pot:   # the tail: wave 1's D_p (16 -> 17), the barrier (6), the tile solve (18), stores issued (19)
+    r = p[k]
+    if r[16] > 0 and r[19] > 0:
+        tl.append([r[16] - r[3], r[17] - r[16], r[6] - r[17], r[18] - r[6], r[19] - r[18], r[5] - r[19]])
+if tl:
+    print("tail, median us: panels end -> D start %.2f, D_p %.2f, D end -> barrier %.2f, tall_solve %.2f, "
+          "tile store issue %.2f, -> stamp 5 %.2f" % tuple(np.median(np.array(tl), 0)))
 pp = []
 for k in pot:   # wave 0's panels (stamps 8 + 2p / 9 + 2p) and the gaps between them (period overrun + lookahead)
     r = p[k]
@@ -96,6 +110,20 @@ for k in pot:   # wave 0's panels (stamps 8 + 2p / 9 + 2p) and the gaps between 
 if pp:
     print("panels (wave 0), median us: p0 %.2f p1 %.2f p2 %.2f p3 %.2f; gaps p0->p1 %.2f p1->p2 %.2f p2->p3 %.2f"
           % tuple(np.median(np.array(pp), 0)))
+if len(bc) and os.environ.get("TL_BCOL"):
+    o = bc[np.argsort(-tasks[bc, 1])]
+    print("bcol c: ticket, deps met, rows done, parent x in, end (us after the last (k+1,k) publish)")
+    for q in o:
+        print("  bcol %3d: " % tasks[q, 1] + " ".join("%8.2f" % (p[q, s] - fac_end if p[q, s] > 0 else np.nan)
+                                                  for s in (0, 1, 2, 3, 7)))
+tl = []
+for k in pot:   # the tail: wave 1's D_p (16 -> 17), the barrier (6), the tile solve (18), stores issued (19)
+    r = p[k]
+    if r[16] > 0 and r[19] > 0:
+        tl.append([r[16] - r[3], r[17] - r[16], r[6] - r[17], r[18] - r[6], r[19] - r[18], r[5] - r[19]])
+if tl:
+    print("tail, median us: panels end -> D start %.2f, D_p %.2f, D end -> barrier %.2f, tall_solve %.2f, "
+          "tile store issue %.2f, -> stamp 5 %.2f" % tuple(np.median(np.array(tl), 0)))
 pp = []
 for k in pot:   # wave 0's panels (stamps 8 + 2p / 9 + 2p) and the gaps between them (period overrun + lookahead)
     r = p[k]

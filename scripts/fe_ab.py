@@ -8,6 +8,9 @@ Run with DROID_HIP_LIB=droid-slam_amd/lib/ab/libdroid_hip.so."""
 import ctypes
 import hashlib
 import os
+# its knobs are testing hooks (include/droid_backends_testing.h): the A/B library by default
+os.environ.setdefault("DROID_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                    "droid-slam_amd", "lib", "ab", "libdroid_hip.so"))
 import sys
 
 import torch

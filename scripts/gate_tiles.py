@@ -3,6 +3,9 @@ term) and a plain 3x3 128->128 band conv at the C3 shape (2048 edges of 48x64,
 256 source frames) on each W=64 tile policy (droid_conv_set_tile: 0 = 8-wave
 band tiles, 1 = the two-workgroups-per-CU tile).  HIP events, median of 5."""
 import os
+# its knobs are testing hooks (include/droid_backends_testing.h): the A/B library by default
+os.environ.setdefault("DROID_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                    "droid-slam_amd", "lib", "ab", "libdroid_hip.so"))
 import sys
 
 import numpy as np

@@ -9,7 +9,7 @@ export PYTHONUNBUFFERED=1
 timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
   tests/test_gpu_chol.py tests/test_gpu_ba.py tests/test_gpu_ba_scale.py tests/test_gpu_trajectory.py > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
 tail -2 $O/pytest.txt
-timeout -k 10 300 python -u scripts/chol_timeline.py C3 > $O/chol_timeline_C3.txt 2>&1 || exit 1
+TL_BCOL=1 timeout -k 10 300 python -u scripts/chol_timeline.py C3 > $O/chol_timeline_C3.txt 2>&1 || exit 1
 grep -E "span|potrf tasks|panels \(|second|back solve" $O/chol_timeline_C3.txt
 for rep in 1 2; do
   timeout -k 10 300 python -u scripts/ba_bench.py C3 C5 --reps 7 > $O/ba_new_$rep.txt 2>&1 || exit 1

@@ -6,7 +6,8 @@ rank on cuda:0.  Writes <out>.rank<R>.npz: poses, disps, dx and the [lo, hi)
 frames whose depths this rank owns.
 
 With a 4th argument "inject", rank 0 alone makes its dataflow solves abort
-(droid_chol_set_fault_inject): first in every GN iteration of one call, then
+(droid_chol_set_fault_inject, so the worker binds the A/B library, which
+exports it): first in every GN iteration of one call, then
 in the first iteration of a second call.  The status words are all-reduced
 before each step is applied, so every rank must skip the same steps and raise;
 the npz then also holds each call's poses / disps and whether it raised.
@@ -29,6 +30,8 @@ import torch  # noqa: E402
 def main():
     out, H, W = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     inject = len(sys.argv) > 4 and sys.argv[4] == "inject"
+    if inject:   # the fault-injection hook ships in the testing builds only (include/droid_backends_testing.h)
+        os.environ["DROID_HIP_LIB"] = os.path.join(ROOT, "droid-slam_amd", "lib", "ab", "libdroid_hip.so")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     dev = torch.device("cuda", 0)

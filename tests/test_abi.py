@@ -1,6 +1,7 @@
 """The C-ABI library loads on a GPU-less host and exports every entry point
-include/droid_backends.h declares; host-only plan construction works (no
-device calls are made here)."""
+include/droid_backends.h declares and none of include/droid_backends_testing.h
+(the A/B and profiling builds export both); host-only plan construction works
+(no device calls are made here)."""
 import ctypes
 import os
 import re
@@ -11,8 +12,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _header_symbols():
-    text = open(os.path.join(ROOT, "include", "droid_backends.h")).read()
+def _header_symbols(name="droid_backends.h"):
+    text = open(os.path.join(ROOT, "include", name)).read()
     return sorted(set(re.findall(r"\b(droid_[a-z0-9_]+)\s*\(", text)))
 
 
@@ -25,6 +26,22 @@ def test_library_exports_header():
         assert hasattr(_lib.lib, s), s
     assert set(syms) == set(_lib.EXPORTS)
     assert _lib.lib.droid_abi_version() == 1
+    # the boundary a maintainer binds carries no testing hook:
+    # those are declared apart and exported by the A/B and profiling builds only
+    test_syms = _header_symbols("droid_backends_testing.h")
+    assert len(test_syms) == 9 and not set(test_syms) & set(syms)
+    assert set(test_syms) == set(_lib.TEST_EXPORTS)
+    for s in test_syms:
+        assert not hasattr(_lib.lib, s), s
+    assert not _lib.HAS_TESTING_HOOKS
+    with pytest.raises(RuntimeError, match="testing hook"):
+        droid_backends.alt_set_variant(2)
+    for sub in ("ab", "prof"):
+        path = os.path.join(ROOT, "droid-slam_amd", "lib", sub, "libdroid_hip.so")
+        if os.path.exists(path):
+            other = ctypes.CDLL(path)
+            for s in syms + test_syms:
+                assert hasattr(other, s), (sub, s)
     for name in ("ba", "frame_distance", "projmap", "depth_filter", "iproj", "altcorr_forward",
                  "altcorr_backward", "corr_index_forward", "corr_index_backward"):
         assert callable(getattr(droid_backends, name))
@@ -38,8 +55,7 @@ def test_product_library_takes_no_kernel_choice_from_env(monkeypatch):
     import ctypes as ct
     from droid_backends import _lib
     assert _lib.lib.droid_build_info() == 0
-    assert all(_lib.lib.droid_alt_set_variant(v) == 2 for v in (1, 3, 4, 5, 6))   # kUnsupported
-    assert _lib.lib.droid_alt_set_variant(2) == 0
+    assert not hasattr(_lib.lib, "droid_alt_set_variant")   # no variant setter at all
     # an order forced through the ABI, not the environment: DROID_BA_ORDER is ignored
     monkeypatch.setenv("DROID_BA_ORDER", "rcm")
     from droid_mi355x import synthetic
@@ -68,6 +84,7 @@ def test_product_library_takes_no_kernel_choice_from_env(monkeypatch):
         assert lab.droid_build_info() & 1
         for s in _header_symbols():
             assert hasattr(lab, s), s
+        assert all(lab.droid_alt_set_variant(v) == 0 for v in (1, 3, 4, 5, 6, 2))   # the dropped variants live here
 
 
 def _plan(ii, jj, N=6, H=4, W=6, t0=1, t1=5, eta_rows=None, motion_only=0, own=(0, 2 ** 31 - 1)):

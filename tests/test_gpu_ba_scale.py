@@ -34,8 +34,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 C5_HW = (16, 24)
 
 
-def _gpu_ba(prob, iterations, lm, ep):
+def _gpu_ba(prob, iterations, lm, ep, bk=None):
     import droid_backends
+    droid_backends = bk or droid_backends
     poses, disps = dev(prob["poses"]), dev(prob["disps"])
     dx, dz = droid_backends.ba(poses, disps, dev(prob["intrinsics"]), dev(prob["disps_sens"]), dev(prob["targets"]),
                                dev(prob["weights"]), dev(prob["eta"]), dev(prob["ii"]), dev(prob["jj"]), prob["t0"],
@@ -121,11 +122,11 @@ def test_ba_c5_sharded_two_ranks(c5, tmp_path):
     assert covered.all() and edges == len(prob["ii"])
 
 
-def test_chol_timeout_is_reported_and_state_untouched():
+def test_chol_timeout_is_reported_and_state_untouched(ab_backends):
     """The dataflow solve's safety net (bounded spins -> abort, flag bit 1):
     forced here with the test hook, ba() must raise and leave poses/disps as
     they were (the abort used to corrupt them silently)."""
-    import droid_backends
+    droid_backends = ab_backends   # the fault-injection hook ships in the testing builds only
     prob = synthetic.ba_problem("C3", H=16, W=24)
     poses, disps = dev(prob["poses"]), dev(prob["disps"])
     droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_ALL)
@@ -138,15 +139,15 @@ def test_chol_timeout_is_reported_and_state_untouched():
         droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_OFF)
     np.testing.assert_array_equal(host(poses), prob["poses"])
     np.testing.assert_array_equal(host(disps), prob["disps"])
-    got = _gpu_ba(prob, 1, 1e-4, 0.1)          # and the next solve on the same plan is clean
+    got = _gpu_ba(prob, 1, 1e-4, 0.1, ab_backends)          # and the next solve on the same plan is clean
     assert np.isfinite(got["dx"]).all()
 
 
-def test_chol_timeout_in_first_gn_iteration_is_still_reported():
+def test_chol_timeout_in_first_gn_iteration_is_still_reported(ab_backends):
     """the status word used to be cleared by every solve, so a
     timeout in GN iteration 1 of ba(iterations=2) vanished when iteration 2
     succeeded.  The sticky word keeps it: ba() raises."""
-    import droid_backends
+    droid_backends = ab_backends   # the fault-injection hook ships in the testing builds only
     prob = synthetic.ba_problem("C3", H=16, W=24, seed=7)
     poses, disps = dev(prob["poses"]), dev(prob["disps"])
     droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_ONCE)
@@ -157,18 +158,18 @@ def test_chol_timeout_in_first_gn_iteration_is_still_reported():
                               prob["t1"], 2, 1e-4, 0.1, False)
     finally:
         droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_OFF)
-    got = _gpu_ba(prob, 2, 1e-4, 0.1)          # the next call on the same plan starts clean
+    got = _gpu_ba(prob, 2, 1e-4, 0.1, ab_backends)          # the next call on the same plan starts clean
     assert np.isfinite(got["dx"]).all()
 
 
-def test_chol_stale_sync_area_is_detected():
+def test_chol_stale_sync_area_is_detected(ab_backends):
     """the dataflow kernel checks its entry state.  A solve
     launched on a sync area that was not zeroed (the previous launch's ticket
     and version counters) must report status bit 2 and change nothing, not run
     tasks against stale hand-off counters; the solve after it is clean."""
-    import droid_backends
+    droid_backends = ab_backends   # the fault-injection hook ships in the testing builds only
     prob = synthetic.ba_problem("C3", H=16, W=24, seed=11)
-    ref1 = _gpu_ba(prob, 1, 1e-4, 0.1)          # a clean solve leaves the counters at their final values
+    ref1 = _gpu_ba(prob, 1, 1e-4, 0.1, ab_backends)          # a clean solve leaves the counters at their final values
     poses, disps = dev(prob["poses"]), dev(prob["disps"])
     droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_STALE)
     try:
@@ -180,7 +181,7 @@ def test_chol_stale_sync_area_is_detected():
         droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_OFF)
     np.testing.assert_array_equal(host(poses), prob["poses"])
     np.testing.assert_array_equal(host(disps), prob["disps"])
-    got = _gpu_ba(prob, 1, 1e-4, 0.1)
+    got = _gpu_ba(prob, 1, 1e-4, 0.1, ab_backends)
     for k in ("dx", "poses", "disps"):
         np.testing.assert_array_equal(got[k], ref1[k], err_msg=k)   # bitwise: the BA is deterministic
 

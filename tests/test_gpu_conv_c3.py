@@ -7,8 +7,9 @@ band tile (conv_band_kernel<256,256,..,ZRP>) above 8 x 256 tiles of 256
 pixels, i.e. above 170 edges at 48x64 - the C3 bench path; the q gate takes
 conv_band2_kernel at every size since round 4 (its 8-wave tile,
 conv_band_kernel<384,128,..,QP>, stays reachable with policy 0).
-droid_conv_set_tile forces either tile per call, so both are compared with
-torch fp32 in one process here (reference: modules/gru.py:19-32,
+droid_conv_set_tile (a testing hook: the A/B library) forces either tile per
+call, so both are compared with torch fp32 in one process here, and the
+product library's default with them (reference: modules/gru.py:19-32,
 droid_net.py:111-143)."""
 import numpy as np
 import pytest
@@ -31,11 +32,12 @@ def _conv_ref(xs, w, bias, bb):
 
 
 @pytest.fixture
-def tile_policy():
-    import droid_backends
-    prev = droid_backends.conv_set_tile(-1)
-    yield droid_backends.conv_set_tile
-    droid_backends.conv_set_tile(prev)
+def tiles(ab_backends):
+    """the A/B library's module instance, its tile policy restored afterwards
+    (droid_conv_set_tile is a testing hook: include/droid_backends_testing.h)"""
+    prev = ab_backends.conv_set_tile(-1)
+    yield ab_backends
+    ab_backends.conv_set_tile(prev)
 
 
 def _gates(B, H, W, F_, seed):
@@ -55,7 +57,7 @@ def _gates(B, H, W, F_, seed):
 def _pre_term(t, H, W):
     """the per-source-frame gate term conv3x3(inp_frames) (a plain conv: its own
     tile choice, so it is computed once and shared by the runs compared)."""
-    import droid_backends
+    import droid_backends   # the product library
     from droid_mi355x.fused import pack_conv
     pre = torch.empty((t["inp_f"].shape[0], H, W, 384), dtype=torch.float16, device=DEV)
     droid_backends.conv_nhwc_f16([(t["inp_f"], 0, 128)],
@@ -64,9 +66,9 @@ def _pre_term(t, H, W):
     return pre
 
 
-def _run_gates(t, H, W, pre):
-    """z, r*h and the GRU update through droid_conv_gru_pre_f16 (per-frame inp term)."""
-    import droid_backends
+def _run_gates(t, H, W, pre, droid_backends):
+    """z, r*h and the GRU update through droid_conv_gru_pre_f16 (per-frame inp
+    term) of the given module instance (the product or the A/B library)."""
     from droid_backends import EPI_GRU_Q, EPI_GRU_ZR
     from droid_mi355x.fused import pack_conv
     B = t["h"].shape[0]
@@ -85,12 +87,15 @@ def _run_gates(t, H, W, pre):
 
 
 @pytest.mark.parametrize("B", [192, 256])
-def test_conv_gru_gates_c3_shape_both_tiles(B, tile_policy):
+def test_conv_gru_gates_c3_shape_both_tiles(B, tiles):
     """z|r and q gates at 48x64 over B >= 192 edges (above the band2 threshold)
     on the 8-wave band tiles (policy 0, and the default, which must pick them
     here: bitwise the same outputs) and on the two-workgroup tile (policy 1),
-    each vs torch fp32 over the full 448 input channels."""
-    import droid_backends
+    each vs torch fp32 over the full 448 input channels.  The tiles are forced
+    on the A/B library (a testing hook); the product library runs the default
+    and must give its bytes."""
+    import droid_backends as product
+    droid_backends = tiles
     from droid_backends import EPI_GRU_Q, EPI_GRU_ZR
     H, W = 48, 64
     t = _gates(B, H, W, B // 8, seed=31)
@@ -101,12 +106,12 @@ def test_conv_gru_gates_c3_shape_both_tiles(B, tile_policy):
     # (mode, z|r tile, q tile): the default runs z|r on the 8-wave tile and q on
     # the two-workgroup tile at this size
     for mode, tzr, tq in ((0, 0, 0), (1, 1, 1), (-1, 0, 1)):
-        tile_policy(mode)
+        droid_backends.conv_set_tile(mode)
         # the kernel each gate conv is routed to (the rocprof trace of this test,
         # profiles/r04/, shows conv_band_kernel<256,256,..,6,8> / <384,128,..,7,8>)
         assert droid_backends.conv_gate_tile(EPI_GRU_ZR, B, H, W) == tzr, mode
         assert droid_backends.conv_gate_tile(EPI_GRU_Q, B, H, W) == tq, mode
-        outs[mode] = _run_gates(t, H, W, pre)
+        outs[mode] = _run_gates(t, H, W, pre, droid_backends)
     for mode in (0, 1, -1):
         z, rn, hn = outs[mode]
         assert _maxdiff(z, gates[..., :128]) < 3e-3, mode
@@ -123,39 +128,42 @@ def test_conv_gru_gates_c3_shape_both_tiles(B, tile_policy):
     # or two of the gates
     for a, b in zip(outs[-1][:2], outs[0][:2]):
         assert torch.equal(a, b)
+    for a, b in zip(_run_gates(t, H, W, pre, product), outs[-1]):
+        assert torch.equal(a, b)
     for a, b in zip(outs[1], outs[0]):
         assert _maxdiff(a, b) < 4e-3
 
 
-def test_conv_gru_gates_small_grid_default_is_band2(tile_policy):
-    """Below the threshold (96 edges, C2) the default takes the two-workgroup tile."""
-    import droid_backends
+def test_conv_gru_gates_small_grid_default_is_band2(tiles):
+    """Below the threshold (96 edges, C2) the default takes the two-workgroup
+    tile (policy forced on the A/B library; the product's default: the same bytes)."""
+    import droid_backends as product
+    droid_backends = tiles
     from droid_backends import EPI_GRU_Q, EPI_GRU_ZR
     H, W, B = 48, 64, 96
     t = _gates(B, H, W, 12, seed=37)
     pre = _pre_term(t, H, W)
     outs = {}
     for mode in (1, -1):
-        tile_policy(mode)
+        droid_backends.conv_set_tile(mode)
         assert droid_backends.conv_gate_tile(EPI_GRU_ZR, B, H, W) == 1
         assert droid_backends.conv_gate_tile(EPI_GRU_Q, B, H, W) == 1
-        outs[mode] = _run_gates(t, H, W, pre)
+        outs[mode] = _run_gates(t, H, W, pre, droid_backends)
     for a, b in zip(outs[-1], outs[1]):
+        assert torch.equal(a, b)
+    for a, b in zip(_run_gates(t, H, W, pre, product), outs[-1]):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("mode", [-1, 1])
-def test_fused_update_matches_reference_module_c3_edges(mode, tile_policy):
+def test_fused_update_matches_reference_module_c3_edges(tiles):
     """FusedUpdateModule vs the pinned UpdateModule (update_module.npz) at the
     bench shape: 256 edges of 48x64 over 32 source frames, 8 edges per frame -
-    the default policy runs the gate convs on the 8-wave band tiles here
-    (policy 1: everything on the two-workgroup tile)."""
+    the product's default policy runs the gate convs on the 8-wave band tiles
+    here (the other tile at this shape: test_conv_gru_gates_c3_shape_both_tiles)."""
     from droid_mi355x.fused import FusedUpdateModule, edge_segments
     from droid_mi355x.update import UpdateModule
-    import droid_backends
     E, H, W, NF = 256, 48, 64, 32
-    tile_policy(mode)
-    assert droid_backends.conv_gate_tile(droid_backends.EPI_GRU_ZR, E, H, W) == (0 if mode == -1 else 1)
+    assert tiles.conv_gate_tile(tiles.EPI_GRU_ZR, E, H, W) == 0   # the default policy (same code as the product)
     m = UpdateModule().to(DEV).eval()
     det_fill(m)
     f = FusedUpdateModule(m)

@@ -95,13 +95,26 @@ def test_tiled_pool_lookup_bitexact():
     np.testing.assert_array_equal(host(got)[:, :2].view(np.uint16), ora.view(np.uint16))
 
 
-def test_coop_lookup_bitwise_equals_per_thread_kernel():
+def _ab_lookup(bk, blk, coords):
+    """CorrBlock.__call__ (droid_mi355x/corr.py) through another instance of the module (bk)."""
+    batch, num, ht, wd, _ = coords.shape
+    c = coords.reshape(batch * num, ht, wd, 2).float().contiguous()
+    if blk.tiled:
+        out = bk.corr_pyramid_lookup_tiled(blk._pyr, blk.level_shapes, c, blk.slot_tensor())
+    else:
+        out = bk.corr_pyramid_lookup(blk.reference_pyramid(), c, blk.radius)
+    return out.view(batch, num, -1, ht, wd)
+
+
+def test_coop_lookup_bitwise_equals_per_thread_kernel(ab_backends):
     """droid_corr_pyramid_lookup(_tiled)'s cooperative NCHW kernel (a wave per
     64 pixels, staged 16-B stores) == the per-thread kernel (droid_lookup_set_coop(0)),
     bit for bit, on the row-major and the tiled volume, with coordinates far off
     the map and on the borders; a 40x56 image (H*W % 64 == 0, 35 waves) and a
-    20x36 one (H*W % 64 != 0: the per-thread kernel either way)."""
-    import droid_backends
+    20x36 one (H*W % 64 != 0: the per-thread kernel either way).  The switch is
+    a testing hook (A/B library); the product library's output is the same bytes."""
+    import droid_backends as product
+    droid_backends = ab_backends   # the coop switch ships in the testing builds only
     from droid_mi355x.corr import CorrBlock
     rng = np.random.default_rng(15)
     try:
@@ -118,12 +131,14 @@ def test_coop_lookup_bitwise_equals_per_thread_kernel():
             with torch.no_grad():
                 for tiled in (False, True):
                     blk = CorrBlock(f1, f2, tiled=tiled)
+                    prod = blk(c)   # the product library (cooperative kernel where it applies)
                     droid_backends.lookup_set_coop(1)
-                    got = blk(c)
+                    got = _ab_lookup(droid_backends, blk, c)
                     droid_backends.lookup_set_coop(0)
-                    ref = blk(c)
+                    ref = _ab_lookup(droid_backends, blk, c)
                     torch.cuda.synchronize()
                     assert torch.equal(got, ref), (H, W, tiled)
+                    assert torch.equal(prod, got), (H, W, tiled)
     finally:
         droid_backends.lookup_set_coop(1)
 

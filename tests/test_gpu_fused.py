@@ -540,26 +540,28 @@ def test_corr_alt_ordered_walk_is_bitwise_the_same(ab_backends):
     f1, f2 = torch.as_tensor(ii, device=DEV), torch.as_tensor(jj, device=DEV)
     order = torch.as_tensor(np.argsort(jj, kind="stable").astype(np.int32), device=DEV)
     try:
-        for bk, v in ((droid_backends, 2), (ab_backends, 3)):   # V3: the A/B build only
-            bk.alt_set_variant(v)
-            ref = bk.corr_alt_ce0(pyr, f1, f2, c, w224, b)
-            out = bk.corr_alt_ce0(pyr, f1, f2, c, w224, b, order=order)
+        ref = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)   # the product library
+        out = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b, order=order)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+        for v in (2, 3):   # the A/B library: the product kernel and V3
+            ab_backends.alt_set_variant(v)
+            ref_v = ab_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
+            out = ab_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b, order=order)
             torch.cuda.synchronize()
-            bk.alt_set_variant(2)
-            assert torch.equal(out, ref), v
-        # the XCD chunking of the walk (droid_alt_set_chunk): interleaved, one
-        # edge, a chunk that does not divide the 40 edges, more than all of them
-        droid_backends.alt_set_variant(2)
-        ref = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b)
+            ab_backends.alt_set_variant(2)
+            assert torch.equal(out, ref_v), v
+        # the XCD chunking of the walk (droid_alt_set_chunk, a testing hook):
+        # interleaved, one edge, a chunk that does not divide the 40 edges, more than all of them
         for chunk in (0, 1, 3, 64):
-            droid_backends.alt_set_chunk(chunk)
+            ab_backends.alt_set_chunk(chunk)
             for o in (None, order):
-                out = droid_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b, order=o)
+                out = ab_backends.corr_alt_ce0(pyr, f1, f2, c, w224, b, order=o)
                 torch.cuda.synchronize()
                 assert torch.equal(out, ref), (chunk, o is None)
     finally:
-        droid_backends.alt_set_variant(2)
-        droid_backends.alt_set_chunk(0)
+        ab_backends.alt_set_variant(2)
+        ab_backends.alt_set_chunk(0)
 
 
 def test_corr_volume_slot_pool_matches_fresh_block():
