@@ -492,6 +492,7 @@ def main():
             zr.active = zrp.active = True
         if graph.comm is not None:
             graph.comm["_ar_events"] = []
+            graph.comm["_solve_events"] = []
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step_fn()
@@ -507,15 +508,26 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    allreduce = None
+    allreduce = serial = None
     if graph.comm is not None:
         evs, graph.comm["_ar_events"] = graph.comm["_ar_events"], None
+        sevs, graph.comm["_solve_events"] = graph.comm["_solve_events"], None
         torch.cuda.synchronize(device)
         if evs:
             allreduce = {"collective": "all_reduce(SUM) of the reduced camera system's input tiles (fp64)",
                          "backend": dist.get_backend(), "payload_bytes": int(evs[0][2]),
                          "per_update": len(evs) // args.steps,
                          "ms_per_gn_iteration": float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))}
+        if sevs:
+            # the replicated part of a sharded GN iteration: every rank
+            # damps and factors the same all-reduced system (dataflow Cholesky + back
+            # solve, one launch) - per rank, gathered so the line shows the spread
+            solve = torch.tensor([float(np.mean([a.elapsed_time(b) for a, b in sevs]))], dtype=torch.float64,
+                                 device=device)
+            every = [torch.zeros_like(solve) for _ in range(world)]
+            dist.all_gather(every, solve)
+            serial = {"solve_ms_per_gn_iteration_per_rank": [float(t.item()) for t in every],
+                      "gn_per_update": len(sevs) // args.steps}
     finite = bool(torch.isfinite(video.poses).all() and torch.isfinite(video.disps).all())
     lookup_ms = lookup.mean_ms()
     zr_ms = zr.mean_ms() if zr else None
@@ -605,6 +617,14 @@ def main():
             result["roofline_lookup"] = lookup_roof
         if allreduce:
             result["allreduce"] = allreduce
+        if serial:
+            # the serial term of the sharded step: replicated solve + all-reduce per GN
+            # iteration (max over ranks), times GN iterations per update, over the step
+            per_gn = max(serial["solve_ms_per_gn_iteration_per_rank"]) + (allreduce["ms_per_gn_iteration"]
+                                                                          if allreduce else 0.0)
+            serial["serial_ms_per_update"] = per_gn * serial["gn_per_update"]
+            serial["serial_fraction"] = serial["serial_ms_per_update"] / ms
+            result["serial"] = serial
         # whole-iteration fraction: max(HBM floor, MFMA floor) / measured update()
         hw = (args.ht // 8) * (args.wd // 8)
         # edges the update operator runs on (C2: the active window; the stored ones only join the BA)

@@ -684,18 +684,24 @@ __global__ void chol_scatter_kernel(double* M, const int* slot, int nbc, int n, 
 // version counters: ver(tile) = number of updates applied, fin(tile) = that
 // count + 1 once the tile is final.  A task is handed out only after all its
 // predecessors were, so it never waits on a workgroup that has not started and
-// progress does not depend on residency.
+// progress does not depend on residency.  A chained potrf(k+1) runs in the
+// workgroup of potrf(k), right after it (its own ticket is a placeholder that
+// keeps the order topological: whatever it waits for was handed out earlier).
 //
 // Cross-workgroup hand-off follows cdna_hip_programming.md Guideline 16 R1:
-// every handed-off byte (tiles, Linv, y, x) is stored AND loaded with sc1
-// buffer operations (write-through / L1 bypass), every storing wave drains
-// vmcnt before the workgroup barrier, then one lane stores the counter with
-// an agent-scope atomic; consumers poll relaxed.  Spins are bounded (an
-// abort word stops every workgroup and flag bit 1 is raised; the host then
-// reports the timeout and leaves poses and disparities untouched).  Tiles are
-// products of f64 MFMA (v_mfma_f64_16x16x4f64); the diagonal factor is
-// panel-blocked (16 wide) with register rows and LDS column broadcasts, and
-// also returns L_kk^-1 so the off-diagonal solves are GEMMs.
+// every handed-off byte (tiles, y) is stored AND loaded with sc1 buffer
+// operations (write-through / L1 bypass), every storing wave drains vmcnt
+// before the workgroup barrier (or, where one wave stores alone, before its
+// own count), then one lane stores the counter with an agent-scope atomic;
+// consumers poll relaxed.  The back solve's x values travel as 16-B {x, tag}
+// granules (one sc1 store each, polled directly: no separate counter).  Spins
+// are bounded (an abort word stops every workgroup and flag bit 1 is raised;
+// the host then reports the timeout and leaves poses and disparities
+// untouched).  Tiles are products of f64 MFMA (v_mfma_f64_16x16x4f64); the
+// diagonal factor is panel-blocked (16 wide, register rows, readlane pivots)
+// and the off-diagonal solves are blocked forward substitutions with the
+// diagonal-block inverses D_p (tall_solve).  Round 6 restructured the chain;
+// DESIGN.md §3 has the timeline.
 // ---------------------------------------------------------------------------
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef double dbl2 __attribute__((ext_vector_type(2)));
@@ -723,6 +729,7 @@ struct CholDev {
   double* ybuf; // [nbc*64]
   float* dx;    // [n]
   int inject;   // test hook (droid_chol_set_fault_inject): raise the abort at once, as a timeout would
+  int epoch;    // this launch's number (never 0): a sync area that holds another launch's number is stale
   long long* prof;  // profiling builds: s_memrealtime per (task, stamp < 16), or null
 };
 
@@ -876,88 +883,30 @@ __device__ __forceinline__ double bcast_lane(double v, int src) {
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
-// 1/sqrt(x) in fp64: v_rsq_f64 + two Newton steps (no division, no sqrt
-// expansion on the critical path; ~1 ulp, far inside the 1e-4 parity bar)
-__device__ __forceinline__ double rsqrt_f64(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  const double hx = 0.5 * x;
-  y = y * fma(-hx * y, y, 1.5);
-  y = y * fma(-hx * y, y, 1.5);
-  return y;
-}
-
-// 16-wide panel of the diagonal factor: wave 0, lane r owns row r's panel
-// values in registers; each pivot comes by one v_readlane pair, each scaled
-// column by one LDS store and wave-uniform (broadcast) LDS reads, and the next
-// pivot is formed ahead of the column update.  Lanes above the diagonal
-// update their (never read) upper-triangle entries too, and pivot columns past
-// the block's Bp real columns use a unit pivot, so every panel is a full,
-// branch-free 16 columns.  dinv[c] = 1 / L[c][c]; colbuf: 64 doubles of LDS.
-// (DROID_CHOL_PANEL_LDS=0: the column by v_readlane, 2.84 vs 2.0 us per panel.)
-#ifndef DROID_CHOL_PANEL_LDS
-#define DROID_CHOL_PANEL_LDS 1
-#endif
-__device__ __forceinline__ void panel_factor(double* T, double* dinv, int c0, int Bp, int lane, int* flag,
-                                             double* colbuf) {
-  double v[16], invs[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) v[q] = T[lane * LT + c0 + q];
-  bool bad = false;
-  // the next pivot is formed first, from the pivot lane's own entries (its
-  // update needs no broadcast), so the pivot chain never waits on the column
-  // broadcast: per column it is rsqrt -> scale -> one fma -> one v_readlane pair
-  double piv = c0 < Bp ? bcast_lane(v[0], c0) : 1.0;
-#pragma unroll
-  for (int jj = 0; jj < 16; ++jj) {
-    bad |= !(piv > 0.0 && piv < 1e300);
-    const double inv = rsqrt_f64(piv);
-    invs[jj] = inv;
-    v[jj] *= inv;  // the diagonal lane gets piv / sqrt(piv)
-    if (jj < 15) {
-      const double pn = fma(-v[jj], v[jj], v[jj + 1]);
-      piv = c0 + jj + 1 < Bp ? bcast_lane(pn, c0 + jj + 1) : 1.0;   // wave-uniform condition
-#if DROID_CHOL_PANEL_LDS
-      // the column's entries below the pivot reach every lane as wave-uniform LDS
-      // reads (one store, broadcast loads on the LDS pipe) instead of 2 v_readlane each
-      colbuf[lane] = v[jj];
-      double lq[16];
-#pragma unroll
-      for (int q = jj + 1; q < 16; ++q) lq[q] = colbuf[c0 + q];
-#pragma unroll
-      for (int q = jj + 1; q < 16; ++q) v[q] = fma(-v[jj], lq[q], v[q]);
-#else
-#pragma unroll
-      for (int q = jj + 1; q < 16; ++q) v[q] = fma(-v[jj], bcast_lane(v[jj], c0 + q), v[q]);
-#endif
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 16; ++q) T[lane * LT + c0 + q] = v[q];
-  double mine = 0.0;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) mine = (lane == q) ? invs[q] : mine;
-  if (lane < 16) dinv[c0 + lane] = mine;
-  if (bad && lane == 0) atomicOr(flag, 1);
-}
-
 // 1/sqrt(x) in fp64 with ONE Newton step after v_rsq_f64 (~2^-23 relative ->
-// ~2^-46): the pivot chain of the blocked panel below; far inside the 1e-4 parity bar
+// ~2^-46; no division or sqrt expansion on the pivot chain; far inside the 1e-4
+// parity bar)
 __device__ __forceinline__ double rsqrt_f64_1(double x) {
   const double y = __builtin_amdgcn_rsq(x);
   return y * fma(-0.5 * x * y, y, 1.5);
 }
 
-// Round 6 panel: the same 16-column factor as panel_factor, with every
-// cross-lane value on the column-to-column critical path taken by v_readlane:
-// lane r keeps its own running diagonal dg = A(r,r) - sum_m L(r,m)^2 (its own
-// x values only), so the next pivot is readlane(dg) right after this column's
-// scale; the next column's entry L(c+1,c) comes by one readlane pair too.
-// Only the columns two or more ahead get this column through the LDS
-// broadcast, which then has a full column step to land.  Per column the chain
-// is: scale -> fma(dg) -> readlane -> rsq + one Newton step -> scale.  Same
-// arithmetic as panel_factor (the diagonal's updates in the same order), one
-// Newton step in the rsqrt (~2^-46 relative).
-__device__ __forceinline__ void panel_factor2(double* T, double* dinv, int c0, int Bp, int lane, int* flag,
+// 16-wide panel of the diagonal factor (wave 0; lane r owns row r's 16 panel
+// values in registers; pivot columns past the block's Bp real columns take a
+// unit pivot, so every panel is a full, branch-free 16 columns; lanes above the
+// diagonal update their never-read upper-triangle entries too).  Every
+// cross-lane value on the column-to-column chain comes by v_readlane: lane r
+// keeps its own running diagonal dg = A(r,r) - sum_m L(r,m)^2 (its own x values
+// only), so the next pivot is readlane(dg) right after this column's scale, and
+// the next column's entry L(c+1,c) comes by one readlane pair too.  Only the
+// columns two or more ahead get this column through the LDS broadcast (colbuf),
+// which then has a full column step to land.  Chain per column: scale ->
+// fma(dg) -> readlane -> rsq + one Newton step -> scale.  dinv[c] = 1/L[c][c];
+// flag bit 0 on a non-SPD pivot.  (Round 6; measured at the round-5 column
+// panel's 2.0 us per 16 columns: the panel is issue-bound, not chain-bound -
+// scripts/probe/f64_latency.hip prices a readlane hop at ~40 clk, an LDS round
+// trip at ~130, a dependent f64 op at ~6-7.)
+__device__ __forceinline__ void panel_factor(double* T, double* dinv, int c0, int Bp, int lane, int* flag,
                                               double* colbuf) {
   double v[16], invs[16];
 #pragma unroll
@@ -998,74 +947,6 @@ __device__ __forceinline__ void panel_factor2(double* T, double* dinv, int c0, i
   if (bad && lane == 0) atomicOr(flag, 1);
 }
 
-// Round 4: the 16-wide panel in blocks of 4 columns.  The column-at-a-time
-// panel above pays per column an LDS broadcast round trip AND the pivot chain
-// (readlane -> rsqrt -> scale -> next diagonal -> readlane; ~270 clk per column,
-// profiles/r02/chol_timeline_c3_r02af.txt: 2.08 us per 16 columns).  Here, per
-// block of 4 columns: the block's 4x4 diagonal (10 values) reaches every lane by
-// v_readlane, every lane factors it redundantly (4 chained rsqrts, no cross-lane
-// traffic inside the chain), each lane forms its own row of the block's 4
-// columns, and ONE LDS broadcast of those rows updates the panel's later
-// columns - one cross-lane round trip per 4 columns instead of per column.
-// Same outputs as panel_factor: L in T (upper triangle: junk, never read), dinv,
-// unit pivots past Bp, flag bit 0 on a non-SPD pivot.
-__device__ __forceinline__ void panel_factor4(double* T, double* dinv, int c0, int Bp, int lane, int* flag,
-                                              double* xb) {
-  double v[16], invs[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) v[q] = T[lane * LT + c0 + q];
-  bool bad = false;
-#pragma unroll
-  for (int jb = 0; jb < 16; jb += 4) {
-    double D[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b <= a; ++b) D[a][b] = bcast_lane(v[jb + b], c0 + jb + a);
-    double Lb[4][4], iv[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-#pragma unroll
-      for (int b = 0; b < a; ++b) {
-        double s = D[a][b];
-#pragma unroll
-        for (int c = 0; c < b; ++c) s = fma(-Lb[a][c], Lb[b][c], s);
-        Lb[a][b] = s * iv[b];
-      }
-      double p = D[a][a];
-#pragma unroll
-      for (int c = 0; c < a; ++c) p = fma(-Lb[a][c], Lb[a][c], p);
-      if (c0 + jb + a >= Bp) p = 1.0;   // wave-uniform: unit pivot past the block's real columns
-      bad |= !(p > 0.0 && p < 1e300);
-      iv[a] = rsqrt_f64_1(p);
-      invs[jb + a] = iv[a];
-    }
-    double x[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      double s = v[jb + a];
-#pragma unroll
-      for (int b = 0; b < a; ++b) s = fma(-x[b], Lb[a][b], s);
-      x[a] = s * iv[a];
-      v[jb + a] = x[a];
-    }
-    if (jb < 12) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a) xb[lane * 4 + a] = x[a];
-#pragma unroll
-      for (int q = jb + 4; q < 16; ++q)
-#pragma unroll
-        for (int a = 0; a < 4; ++a) v[q] = fma(-x[a], xb[(c0 + q) * 4 + a], v[q]);
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 16; ++q) T[lane * LT + c0 + q] = v[q];
-  double mine = 0.0;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) mine = (lane == q) ? invs[q] : mine;
-  if (lane < 16) dinv[c0 + lane] = mine;
-  if (bad && lane == 0) atomicOr(flag, 1);
-}
 // X <- X L^-T for a 64-row tile X in T (trsm against a factored pivot block) by
 // blocked forward substitution, X_p = (A_p - sum_{j<p} X_j L_pj^T) D_p^-T per
 // 16-column block p: L's strictly-lower 16x16 blocks are read from Lt, the
@@ -1098,13 +979,6 @@ __device__ __forceinline__ void tall_solve(double* T, const double* Lt, const do
     asm volatile("" ::: "memory");
   }
 }
-
-// panel_factor4 measured no faster than the column panel (first 16-column panel
-// 2.20 vs 2.08 us, profiles/r04/r04f_timeline_C3.txt: the single wave's f64
-// VALU issue, not the pivot chain, bounds it); the column panel stays default
-#ifndef DROID_CHOL_PANEL4
-#define DROID_CHOL_PANEL4 0
-#endif
 
 // 16x16 block C(cr.., cc..) -= A(ar.., a0 + [0, 4 NK)) B(br.., b0 + [0, 4 NK))^T
 // on f64 MFMA, all operands in LDS tiles of row stride LT (one wave).
@@ -1272,7 +1146,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
   int* abort_w = d.sync + 1;
   int* ver = d.sync + 4;
   int* yver = ver + d.nslots;
-  int* lkk = yver + nbc;    // L_kk stored (potrf(k)'s wave 0 flags it right after its panels)
+  int* lkk = yver + nbc;    // L_kk stored: 3 once potrf(k)'s three storing waves have counted
   auto SL = [&](int i, int j) { return d.slot[i * nbc + j]; };
   if (d.inject && blockIdx.x == 0 && tid == 0) {
     __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1285,14 +1159,28 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
     return __builtin_amdgcn_readfirstlane(shi[4] & shi[5] & shi[6] & shi[7]) != 0;
   };
 
+  // Entry invariant (kFlagState), exact: the sync area was zeroed before this
+  // launch.  Every workgroup claims it for this launch (word 2: 0 -> epoch)
+  // before it takes a ticket, so an area any earlier launch touched - run to
+  // completion or aborted anywhere - holds that launch's number, not 0.
+  if (tid == 0) {
+    const int e = atomicCAS(d.sync + 2, 0, d.epoch);
+    shi[1] = (e == 0 || e == d.epoch) ? 1 : 0;
+  }
+  __syncthreads();
+  if (__builtin_amdgcn_readfirstlane(shi[1]) == 0) {
+    if (tid == 0) state_fault(abort_w, d.flag);
+    return;
+  }
   for (bool first = true;; first = false) {
     if (tid == 0) shi[0] = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const int tk = __builtin_amdgcn_readfirstlane(shi[0]);
-    // Entry invariant (kFlagState): the sync area was zeroed before this
-    // launch.  A launch hands out exactly ntasks + gridDim.x tickets when no
-    // worker aborts, so a workgroup's first ticket lies below that unless the
-    // counter kept a previous launch's value.
+    // Second line of the entry check, for replays of a captured graph (whose
+    // kernel arguments, the epoch included, are frozen): a launch hands out
+    // exactly ntasks + gridDim.x tickets when no worker aborts, so a
+    // workgroup's first ticket lies below that unless the counter kept a
+    // completed launch's value.
     if (tk < 0 || (first && tk >= d.ntasks + (int)gridDim.x)) {
       if (tid == 0) state_fault(abort_w, d.flag);
       break;
@@ -1320,7 +1208,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           break;
         case kTrsm: {
           const int s = SL(i, k);
-          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&lkk[k], 1, abort_w, d.flag);
+          ok = poll_ge(&ver[s], d.fin[s] - 1, abort_w, d.flag) && poll_ge(&lkk[k], 3, abort_w, d.flag);
           break;
         }
         case kUpdate: {
@@ -1336,7 +1224,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           break;
         }
         default: {  // kBcol: L_cc with its diagonal-block inverses, and the forward value of y_c
-          ok = poll_ge(&lkk[i], 1, abort_w, d.flag) && poll_ge(&yver[i], 1, abort_w, d.flag);
+          ok = poll_ge(&lkk[i], 3, abort_w, d.flag) && poll_ge(&yver[i], 1, abort_w, d.flag);
           break;
         }
       }
@@ -1352,12 +1240,14 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
       // 1-3), and waves 1-3 load tile (k+1,k) as soon as it has its other
       // updates; between two panels only the next block column's update (3
       // blocks, 4 MFMAs each) sits on the chain.  After the panels wave 1 forms
-      // the diagonal-block inverses D_p while wave 0 stores L_kk; the workgroup
-      // solves tile (k+1,k) (tall_solve), publishes it, and - when the plan
-      // chains potrf(k+1) to this task - goes straight on to potrf(k+1) with
-      // L(k+1,k) still in LDS (no hand-off, no reload).  L_kk and the D_p are
-      // what the trsm tasks below and the back solve read.
-      double* tL = T1;   // L(k,klast) for the last update, then the D_p
+      // the diagonal-block inverses D_p while waves 0, 2, 3 store L_kk and flag
+      // it (the trsm tasks below and the back solve read L_kk and form their
+      // own D_p); the workgroup solves tile (k+1,k) (tall_solve), publishes it,
+      // and - when the plan chains potrf(k+1) to this task - goes straight on
+      // to potrf(k+1) with L(k+1,k) still in LDS (no hand-off, no reload; the
+      // publish then waits for that task's first barrier, after the stores
+      // have landed).
+      double* tL = T1;   // L(k,klast) for the last update, then the D_p (diagonal blocks)
       double* tB = T2;   // tile (k+1,k)
       double* dinv = vec + 128;
       int kc = k, ka = ta, kb = tb, tcur = tk;
@@ -1418,7 +1308,7 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         for (int p = 0; p < np; ++p) {
           if (wave == 0) {
               CH_STAMPT(tcur, 8 + 2 * p);
-              panel_factor2(T0, dinv, 16 * p, Bp, lane, d.flag, scr);
+              panel_factor(T0, dinv, 16 * p, Bp, lane, d.flag, scr);
               CH_STAMPT(tcur, 9 + 2 * p);
           } else {
             int job = 0;
@@ -1446,18 +1336,21 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
         CH_STAMPT(tcur, 3);
         const bool rhs0 = Br > Bp;                    // the rhs row inside the pivot tile
         const bool rhs1 = fz && kc + 1 == nbr - 1;    // ... or in tile (k+1,k)
-        if (wave == 0) {
-          // L_kk (rows and columns < Bp) goes out now and is flagged as soon as
-          // it has landed (one storing wave: its own vmcnt(0), Guideline 16 R1);
-          // the drain runs beside wave 1's D_p
-#pragma unroll 4
+        if (wave != 1) {
+          // L_kk (rows and columns < Bp) goes out now, a third of it from each
+          // of waves 0, 2, 3 (wave 1 forms the D_p meanwhile); each counts its
+          // own stores on lkk once they have landed (its own vmcnt(0),
+          // Guideline 16 R1): the trsm tasks below and the back solve wait for 3.
+          // Split three ways the drain stays under the D_p, off the barrier.
+          const int sw = wave == 0 ? 0 : wave - 1;
+#pragma unroll
           for (int q = 0; q < 32; ++q) {
             const int rr = q * 2 + (lane >> 5), cc2 = (lane & 31) * 2;
-            if (rr < Bp && cc2 < Bp)
+            if (q % 3 == sw && rr < Bp && cc2 < Bp)
               st2(rM, (unsigned)(((size_t)skk * kTile + rr * 64 + cc2) * 8), *reinterpret_cast<const dbl2*>(&T0[rr * LT + cc2]));
           }
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (lane == 0) __hip_atomic_store(&lkk[kc], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) __hip_atomic_fetch_add(&lkk[kc], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else if (wave == 1) {
           // y_k (the solved rhs row), the rows past Bp cleared (L_kk^-1 is
           // unit-padded there), then the diagonal-block inverses D_p = L_pp^-1
@@ -1899,6 +1792,9 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_
   if (inj == kInjectOnce || inj == kInjectStale) g_chol_inject = kInjectOff;
   c.inject = (inj == kInjectAll || inj == kInjectOnce) ? 1 : 0;
   c.prof = g_chol_prof;
+  static int epoch = 0;
+  epoch = epoch == 0x7fffffff ? 1 : epoch + 1;
+  c.epoch = epoch;
   static bool attr = false;
   if (!attr) {
     DROID_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&chol_dataflow_kernel),

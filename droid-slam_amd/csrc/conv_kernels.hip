@@ -101,6 +101,7 @@ struct ConvArgs {
   const __half* pre;
   const long long* pre_idx;
   int pre_cstride, pre_coff;
+  int ab_no_h;   // A/B build only (DROID_ZR_NO_H): the z|r epilogue skips its h re-read (a timing bound)
 };
 
 constexpr int TM = 128, BK = 64;
@@ -875,7 +876,7 @@ constexpr int kLdsMax = 163840;
 // profiling builds: int64 slots per workgroup (hw id, entry, loop start, loop end,
 // epilogue stores issued, drained (wave 0), pass 1 written, pass-2 loads issued,
 // staging barrier passed, last wave drained)
-constexpr int kProfSlots = 10;
+constexpr int kProfSlots = 12;   // [10] / [11]: s_memrealtime at loop start / end (in-kernel clock)
 
 __device__ __forceinline__ void wait_vmcnt(int n) {
   // n is wave-uniform; s_waitcnt takes an immediate
@@ -1103,6 +1104,13 @@ __device__ __forceinline__ void band_epilogue_core(const ConvArgs& a, _Float16* 
   stage1(static_cast<const float*>(bl), act);
   if (prof && tid == 0) prof[6] = (long long)__builtin_amdgcn_s_memtime();  // pass 1 written
   // h (and z) pieces of rounds [q0, q0 + RB)
+#if DROID_AB
+  // A/B timing bound only (wrong r*h): DROID_ZR_NO_H=1 skips the z|r epilogue's
+  // global re-read of h - what serving h from LDS could at most save
+  const bool no_h = a.ab_no_h != 0;
+#else
+  constexpr bool no_h = false;
+#endif
   auto load_h = [&](int q0) {
     if constexpr (kPreH) {
       const __half* const hp = a.h + (mrow + (long)q0 * RQ) * a.h_cstride + c - (EB == EPI_GRU_ZR ? a.gru_ch : 0);
@@ -1113,7 +1121,7 @@ __device__ __forceinline__ void band_epilogue_core(const ConvArgs& a, _Float16* 
         if constexpr (EB == EPI_GRU_Q) {
           hpre[q] = *reinterpret_cast<const half8*>(hp + q * hstep);
           zpre[q] = *reinterpret_cast<const half8*>(zp + q * zstep);
-        } else if (rhalf) {
+        } else if (rhalf && !no_h) {
           hpre[q] = *reinterpret_cast<const half8*>(hp + q * hstep);
         }
       }
@@ -1175,7 +1183,7 @@ __device__ __forceinline__ void band_epilogue_core(const ConvArgs& a, _Float16* 
         }
       }
       if (epi == EPI_GRU_ZR) {
-        if (rhalf) {
+        if (rhalf && !no_h) {
           half8 h;
           if constexpr (kPreH) h = hpre[q];
           else h = *reinterpret_cast<const half8*>(a.h + m * a.h_cstride + c - a.gru_ch);
@@ -1500,7 +1508,10 @@ conv_band_kernel(ConvArgs a) {
   }
   if (prof) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (tid == 0) prof[2] = (long long)__builtin_amdgcn_s_memtime();
+    if (tid == 0) {
+      prof[2] = (long long)__builtin_amdgcn_s_memtime();
+      prof[10] = (long long)__builtin_amdgcn_s_memrealtime();   // 100 MHz: the in-kernel clock over the loop
+    }
   }
   if constexpr (NW == 4) {
     // One wave per SIMD: nothing else on the SIMD hides this wave's LDS
@@ -1715,7 +1726,10 @@ conv_band_kernel(ConvArgs a) {
   }
   }   // NW == 4
   if constexpr (NW == 4) mfma_acc_drain();
-  if (prof && tid == 0) prof[3] = (long long)__builtin_amdgcn_s_memtime();
+  if (prof && tid == 0) {
+    prof[3] = (long long)__builtin_amdgcn_s_memtime();
+    prof[11] = (long long)__builtin_amdgcn_s_memrealtime();
+  }
   if constexpr (DWHEAD) {
     static_assert(TMX == 256 && TN == 256 && NW == 8, "dw/head fusion runs on the 8-wave 256x256 tile");
     dwhead_epilogue<FM, FN>(a, acc, smem, m0, wm, wn, lane, tid, bcol, prof);
@@ -2718,6 +2732,7 @@ static int conv_nhwc_impl(const void* const* srcs, const int* C, const int* cstr
     return fail(kUnsupported, "conv_nhwc_f16: global-context epilogue needs H*W % 128 == 0");
   ConvArgs a{};
   a.prof = g_conv_prof;
+  a.ab_no_h = ab_knob("DROID_ZR_NO_H", 0);
   int chunks = 0;
   for (int s = 0; s < nsrc; ++s) {
     if (C[s] % 8 || cstride[s] % 8 || cstride[s] < C[s] || (reinterpret_cast<uintptr_t>(srcs[s]) & 15))
@@ -2949,6 +2964,7 @@ int droid_conv_dw_head_f16(const void* const* srcs, const int* C, const int* cst
   if ((long)B * H * W * 8 > 0x7fffffffL) return fail(kUnsupported, "conv_dw_head_f16: too many pixels");
   ConvArgs a{};
   a.prof = g_conv_prof;
+  a.ab_no_h = ab_knob("DROID_ZR_NO_H", 0);
   int chunks = 0;
   for (int s = 0; s < nsrc; ++s) {
     if (C[s] % 8 || cstride[s] % 8 || cstride[s] < C[s] || (reinterpret_cast<uintptr_t>(srcs[s]) & 15))

@@ -190,7 +190,7 @@ def ba_sharded(poses, disps, intrinsics, disps_sens, target, weight, eta, ii_hos
     (9.6 MB at C3, 66 MB at C5 instead of the dense 603 MB).
 
     Failures are agreed on, not per rank: after each GN iteration's Cholesky
-    the status words are all-reduced (MAX, 8 bytes) on the device BEFORE the
+    the status words are OR-reduced (per bit, 64 bytes) on the device BEFORE the
     back-substitution and retraction, so if any rank's dataflow solve timed out
     every rank skips that step (the replicated poses never diverge), and every
     rank raises at its next BA call (or droid_backends.check_status()) - no
@@ -220,17 +220,30 @@ def ba_sharded(poses, disps, intrinsics, disps_sens, target, weight, eta, ii_hos
         if timing is not None:
             ev[1].record()
             timing.append(ev + (flat.numel() * flat.element_size(),))
+        sev = comm.get("_solve_events")   # bench: HIP events around the replicated solve, or None
+        if sev is not None:
+            se = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            se[0].record()
         plan.solve_system(lm, ep, dx)
-        # the status words agreed before the step is applied (a word is 0, 1, or
-        # one of 2, 3, 6, 7 when bit 1 - timeout or corrupt state - is set, so
-        # MAX keeps the skip bit of any rank):
-        # a rank whose dataflow solve timed out makes EVERY rank skip this step's
-        # back-substitution and retraction, so the replicated poses stay equal
-        dist.all_reduce(status, op=dist.ReduceOp.MAX, group=group)
+        if sev is not None:
+            se[1].record()
+            sev.append(se)
+        # the status words agreed before the step is applied: a bitwise OR over
+        # the ranks (one int per bit, all-reduced MAX, repacked - ADVICE r5: a
+        # MAX of the packed words kept the skip bit but could drop another
+        # rank's non-SPD bit).  A rank whose dataflow solve timed out makes EVERY
+        # rank skip this step's back-substitution and retraction, so the
+        # replicated poses stay equal
+        bits = (status.unsqueeze(-1) >> _STATUS_SHIFTS.to(status.device, status.dtype)) & 1
+        dist.all_reduce(bits, op=dist.ReduceOp.MAX, group=group)
+        status.copy_((bits << _STATUS_SHIFTS.to(status.device, status.dtype)).sum(-1, dtype=status.dtype))
         plan.apply_update(poses, disps, intrinsics, disps_sens, target, weight, eta, dx, dz)
     plan._record_status()     # the agreed words (identical on every rank)
     comm["_last_plan"] = plan
     return [dx, dz]
+
+
+_STATUS_SHIFTS = torch.arange(8)   # the status word's bits (0 non-SPD, 1 skipped, 2 corrupt state; spare to 7)
 
 
 def global_edges(ii_host, jj_host, comm, call_key):

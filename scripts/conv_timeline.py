@@ -60,9 +60,20 @@ if os.environ.get("TL_TILE"):   # tile policy (droid_conv_set_tile): 0 8-wave, 2
 for _ in range(3):
     run()
 torch.cuda.synchronize()
+warm = float(os.environ.get("TL_WARM_S", "0"))   # back-to-back launches first (MI355X_MICROARCH.md, DVFS item 6)
+if warm > 0:
+    import time
+    t_end = time.time() + warm
+    nw = 0
+    while time.time() < t_end:
+        for _ in range(8):
+            run()
+        torch.cuda.synchronize()
+        nw += 8
+    print("%d back-to-back launches over %.1f s before the profiled one" % (nw, warm))
 tile = {256: 256, 128: 384}[cout]
 nwg = E * H * W // tile
-prof = torch.zeros(nwg * 10, dtype=torch.int64, device=dev)
+prof = torch.zeros(nwg * 12, dtype=torch.int64, device=dev)
 lib.droid_conv_set_profile(ctypes.c_void_p(prof.data_ptr()))
 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 s.record()
@@ -71,7 +82,7 @@ e.record()
 torch.cuda.synchronize()
 lib.droid_conv_set_profile(None)
 ms = s.elapsed_time(e)
-p = prof.view(nwg, 10).cpu().numpy()
+p = prof.view(nwg, 12).cpu().numpy()
 assert (p[:, 1] > 0).all(), "profile not written (kernel not the band kernel?)"
 hw = p[:, 0]
 cu = ((hw >> 32) & 15) * 256 + ((hw >> 8) & 0xff)   # XCC id, then SE_ID[15:13] | SH_ID[12] | CU_ID[11:8]
@@ -105,3 +116,11 @@ elif (p[:, 6] > 0).all():   # band_epilogue sub-phases (wave 0) and the last wav
 print("  main loop per stage: %.0f clk (%d stages); MFMA-only floor %d clk/stage" % (np.median(loop) / stages, stages,
                                                                                      floor))
 print("  implied clock: %.2f GHz (median WG cycle x WGs per CU / kernel time)" % (span_clk / (ms * 1e-3) / 1e9))
+if (p[:, 11] > p[:, 10]).all():   # in-kernel clock over the main loop: s_memtime ticks per s_memrealtime (100 MHz)
+    clk = (p[:, 3] - p[:, 2]) / ((p[:, 11] - p[:, 10]) / 100e6) / 1e9
+    flops = {"zr": 2 * 256 * 448 * 9, "zrp": 2 * 256 * 320 * 9, "q": 2 * 128 * 448 * 9, "qp": 2 * 128 * 320 * 9,
+             "ce2": 2 * 128 * 128 * 9, "dw": 2 * 256 * 128 * 9, "dwh": 2 * 256 * 128 * 9}[which] * E * H * W
+    print("  in-kernel clock over the main loop: median %.3f GHz (p10 %.3f, p90 %.3f); %.1f TFLOP/s over the launch "
+          "= %.3f of the 2.5 PF spec, %.3f of the fp16 MFMA peak at that clock"
+          % (np.median(clk), np.percentile(clk, 10), np.percentile(clk, 90), flops / (ms * 1e-3) / 1e12,
+             flops / (ms * 1e-3) / 2.5e15, flops / (ms * 1e-3) / (2.5e15 * np.median(clk) / 2.4)))

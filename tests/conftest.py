@@ -41,7 +41,8 @@ def ab_backends():
     import importlib.util
     path = os.path.join(PKG, "lib", "ab", "libdroid_hip.so")
     if not os.path.exists(path):
-        pytest.fail("the A/B library is missing: make -C droid-slam_amd/csrc ab (__graft_entry__.build() does)")
+        pytest.fail("the A/B library is missing: make -C droid-slam_amd/csrc (the default target builds it; "
+                    "`make ab` alone does too, and so does __graft_entry__.build())")
     mod = sys.modules.get("droid_backends_ab")
     if mod is None:
         old = os.environ.get("DROID_HIP_LIB")

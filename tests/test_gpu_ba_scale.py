@@ -186,6 +186,32 @@ def test_chol_stale_sync_area_is_detected(ab_backends):
         np.testing.assert_array_equal(got[k], ref1[k], err_msg=k)   # bitwise: the BA is deterministic
 
 
+def test_chol_stale_sync_area_after_an_aborted_solve_is_detected(ab_backends):
+    """the entry check used to catch only the counters of a launch
+    that ran to completion; an aborted launch leaves its ticket counter
+    anywhere.  With the per-launch epoch the solve after an abort, launched on
+    its unzeroed sync area, must still report status bit 2."""
+    droid_backends = ab_backends   # the fault-injection hook ships in the testing builds only
+    prob = synthetic.ba_problem("C3", H=16, W=24, seed=13)
+    args = lambda p, d: (p, d, dev(prob["intrinsics"]), dev(prob["disps_sens"]), dev(prob["targets"]),
+                         dev(prob["weights"]), dev(prob["eta"]), dev(prob["ii"]), dev(prob["jj"]), prob["t0"],
+                         prob["t1"], 1, 1e-4, 0.1, False)
+    poses, disps = dev(prob["poses"]), dev(prob["disps"])
+    try:
+        droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_ONCE)
+        with pytest.raises(RuntimeError, match="timed out"):
+            droid_backends.ba(*args(poses, disps))
+        droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_STALE)
+        with pytest.raises(RuntimeError, match="state corrupt"):
+            droid_backends.ba(*args(poses, disps))
+    finally:
+        droid_backends.chol_set_fault_inject(droid_backends.CHOL_INJECT_OFF)
+    np.testing.assert_array_equal(host(poses), prob["poses"])
+    np.testing.assert_array_equal(host(disps), prob["disps"])
+    got = _gpu_ba(prob, 1, 1e-4, 0.1, ab_backends)          # and the next solve on the same plan is clean
+    assert np.isfinite(got["dx"]).all()
+
+
 def _torchrun(nproc, args, timeout):
     env = dict(os.environ, PYTHONUNBUFFERED="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):

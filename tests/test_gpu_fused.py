@@ -969,6 +969,38 @@ def test_reference_layout_module_under_inference_mode():
         assert torch.equal(x, y)
 
 
+def test_reference_layout_module_inference_refill_in_place():
+    """under inference_mode the per-frame check is keyed on a
+    content fingerprint, not identity alone.  Refilling the same inp buffer
+    in place so that edges of one frame no longer share their rows must turn
+    the factored gates off: the result equals a fresh module's on the new
+    contents."""
+    from droid_mi355x.fused import ReferenceLayoutUpdateModule
+    from droid_mi355x.update import UpdateModule
+    E, H, W = 6, 48, 64
+    m = UpdateModule().to(DEV).eval()
+    det_fill(m)
+    g = torch.Generator(device=DEV).manual_seed(45)
+    net = torch.tanh(torch.randn((1, E, 128, H, W), generator=g, device=DEV)).half()
+    frm = torch.relu(torch.randn((3, 128, H, W), generator=g, device=DEV)).half()
+    corr = (2 * torch.randn((1, E, 196, H, W), generator=g, device=DEV)).half()
+    flow = (4 * torch.randn((1, E, 4, H, W), generator=g, device=DEV)).clamp(-64, 64)
+    ii = torch.tensor([0, 0, 1, 1, 2, 2], device=DEV)
+    jj = torch.tensor([1, 2, 0, 2, 0, 1], device=DEV)
+    other = torch.relu(torch.randn((1, E, 128, H, W), generator=g, device=DEV)).half()   # per edge: no sharing
+    with torch.inference_mode():
+        d = ReferenceLayoutUpdateModule(m)
+        inp = frm[ii].unsqueeze(0).contiguous()
+        d(net, inp, corr, flow, ii, jj)
+        assert d._frames[3] is not None          # shared rows: the factored gates
+        inp.copy_(other)
+        a = d(net, inp, corr, flow, ii, jj)
+        assert d._frames[3] is None              # refilled: per-edge gates
+        b = ReferenceLayoutUpdateModule(m)(net, other.clone(), corr, flow, ii, jj)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
 def test_fused_pre_term_follows_in_place_refill():
     """The per-frame gate-term cache is keyed on the inp_frames tensor's version:
     refilling the same buffer in place gives the term of the new contents."""
