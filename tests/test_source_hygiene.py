@@ -1,25 +1,33 @@
 """Source checks for hand-written HIP that the compiler gets wrong silently.
 
-hipcc in this image (ROCm 7.2) miscompiles ``__builtin_bit_cast(T, v[i])`` and
-``__builtin_bit_cast(T, v.y)`` when ``v`` is an ext_vector value: the result is
-element 0 (or an unrelated register), with no diagnostic.  Round 5 hit it in
-the on-demand lookup's weight load (scripts/alt_level_diff.py found it: every
-pixel of every level off).  Element accesses go through a named scalar first
-(``const unsigned w1 = v.y; __builtin_bit_cast(h2_t, w1)``) or through a plain
-array.  This test keeps the pattern out of the kernels: a bit-cast whose
-operand is a subscript or swizzle of a variable declared with a vector type."""
+hipcc in this image (ROCm 7.2) miscompiles ``__builtin_bit_cast(T, w[i])`` and
+``__builtin_bit_cast(T, w.y)`` when ``w`` has a clang ext_vector type (a
+``typedef ... __attribute__((ext_vector_type(N)))``): the cast reads the
+vector's base address, i.e. element 0, with no diagnostic.
+``scripts/probe/bitcast_vec.hip`` reproduces it and ``bitcast_vec.txt`` holds
+the ISA (one ``ds_read_b32`` of element 0 stored for both casts, where the
+named-scalar and HIP ``uint2`` forms read both dwords); the test below
+re-derives that ISA so a fixed compiler shows up.  Round 5 hit it in the
+on-demand lookup's weight load (every pixel of every level off).  The rule
+the kernels follow: an element of an ext_vector goes through a named scalar
+first (``const unsigned w1 = v[1]; __builtin_bit_cast(h2_t, w1)``); a member
+of HIP's struct vector types (``uint2.y``) and a plain array element are cast
+correctly.  The source check flags a bit-cast whose operand is a subscript or
+swizzle of a variable declared with an ext_vector type."""
 import glob
 import os
 import re
+import subprocess
 
 import pytest
 
 CSRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "droid-slam_amd", "csrc")
-HIP_VECTORS = {"uint2", "uint3", "uint4", "int2", "int4", "float2", "float4", "half2", "ushort2", "ushort4"}
+PROBE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "scripts", "probe", "bitcast_vec.hip")
+HIPCC = "/opt/rocm/bin/hipcc"
 
 
 def _vector_types(text):
-    return HIP_VECTORS | set(re.findall(r"typedef\s+[\w\s]+?\s+(\w+)\s+__attribute__\(\(ext_vector_type", text))
+    return set(re.findall(r"typedef\s+[\w\s]+?\s+(\w+)\s+__attribute__\(\(ext_vector_type", text))
 
 
 def _declared_as_vector(text, name, pos, vtypes):
@@ -45,3 +53,25 @@ def test_no_bit_cast_of_vector_elements(path):
         if _declared_as_vector(text, m.group(1), m.start(), vtypes):
             bad.append("%s:%d %s" % (os.path.basename(path), text[:m.start()].count("\n") + 1, m.group(0)))
     assert not bad, "bit-cast of an ext_vector element (miscompiled to element 0): " + "; ".join(bad)
+
+
+def _kernel_body(asm, name):
+    start = re.search(r"^%s:" % name, asm, re.M)
+    end = asm.index("s_endpgm", start.end())
+    return asm[start.end():end]
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not in this image")
+def test_bitcast_probe_still_shows_the_miscompile(tmp_path):
+    """The probe's ISA: the ext_vector forms read one dword (element 0), the
+    named-scalar and HIP uint2 forms read both.  If this starts failing, the
+    compiler changed - re-check the rule above before relaxing it."""
+    out = str(tmp_path / "bitcast_vec.s")
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-S", "--cuda-device-only", PROBE, "-o", out],
+                   check=True, capture_output=True, timeout=300)
+    asm = open(out).read()
+    for bad in ("ext_subscript", "ext_swizzle"):
+        body = _kernel_body(asm, bad)
+        assert "ds_read_b32" in body and "ds_read_b64" not in body, bad
+    for good in ("ext_named", "hip_uint2"):
+        assert "ds_read_b64" in _kernel_body(asm, good), good
