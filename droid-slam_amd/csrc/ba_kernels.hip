@@ -792,6 +792,20 @@ __device__ __forceinline__ void tile_load(__amdgpu_buffer_rsrc_t r, int s, int n
   tile_commit(v, T);
 }
 __device__ __forceinline__ void tile_store(__amdgpu_buffer_rsrc_t r, int s, int nr, int nc, const double* T) {
+  if (nr == 64 && nc == 64) {   // a full tile: all eight LDS reads, then the eight stores (no per-store mask)
+    dbl2 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
+      v[q] = *reinterpret_cast<const dbl2*>(&T[rr * LT + cc]);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
+      st2(r, (unsigned)(((size_t)s * kTile + rr * 64 + cc) * 8), v[q]);
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int p = threadIdx.x + 256 * q, rr = p >> 5, cc = (p & 31) * 2;
@@ -1343,11 +1357,26 @@ __global__ void __launch_bounds__(256) chol_dataflow_kernel(CholDev d) {
           // Guideline 16 R1): the trsm tasks below and the back solve wait for 3.
           // Split three ways the drain stays under the D_p, off the barrier.
           const int sw = wave == 0 ? 0 : wave - 1;
+          if (Bp == 64) {   // row pairs sw, sw + 3, ...: all the LDS reads, then the stores
+            // (the 32nd pair is stored by two waves - the same bytes)
+            dbl2 sv[11];
 #pragma unroll
-          for (int q = 0; q < 32; ++q) {
-            const int rr = q * 2 + (lane >> 5), cc2 = (lane & 31) * 2;
-            if (q % 3 == sw && rr < Bp && cc2 < Bp)
-              st2(rM, (unsigned)(((size_t)skk * kTile + rr * 64 + cc2) * 8), *reinterpret_cast<const dbl2*>(&T0[rr * LT + cc2]));
+            for (int j = 0; j < 11; ++j) {
+              const int rr = min(sw + 3 * j, 31) * 2 + (lane >> 5), cc2 = (lane & 31) * 2;
+              sv[j] = *reinterpret_cast<const dbl2*>(&T0[rr * LT + cc2]);
+            }
+#pragma unroll
+            for (int j = 0; j < 11; ++j) {
+              const int rr = min(sw + 3 * j, 31) * 2 + (lane >> 5), cc2 = (lane & 31) * 2;
+              st2(rM, (unsigned)(((size_t)skk * kTile + rr * 64 + cc2) * 8), sv[j]);
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < 32; ++q) {
+              const int rr = q * 2 + (lane >> 5), cc2 = (lane & 31) * 2;
+              if (q % 3 == sw && rr < Bp && cc2 < Bp)
+                st2(rM, (unsigned)(((size_t)skk * kTile + rr * 64 + cc2) * 8), *reinterpret_cast<const dbl2*>(&T0[rr * LT + cc2]));
+            }
           }
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if (lane == 0) __hip_atomic_fetch_add(&lkk[kc], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
