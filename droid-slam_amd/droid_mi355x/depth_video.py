@@ -234,9 +234,7 @@ def ba_sharded(poses, disps, intrinsics, disps_sens, target, weight, eta, ii_hos
         # rank's non-SPD bit).  A rank whose dataflow solve timed out makes EVERY
         # rank skip this step's back-substitution and retraction, so the
         # replicated poses stay equal
-        bits = (status.unsqueeze(-1) >> _STATUS_SHIFTS.to(status.device, status.dtype)) & 1
-        dist.all_reduce(bits, op=dist.ReduceOp.MAX, group=group)
-        status.copy_((bits << _STATUS_SHIFTS.to(status.device, status.dtype)).sum(-1, dtype=status.dtype))
+        or_reduce_status(status, group)
         plan.apply_update(poses, disps, intrinsics, disps_sens, target, weight, eta, dx, dz)
     plan._record_status()     # the agreed words (identical on every rank)
     comm["_last_plan"] = plan
@@ -244,6 +242,18 @@ def ba_sharded(poses, disps, intrinsics, disps_sens, target, weight, eta, ii_hos
 
 
 _STATUS_SHIFTS = torch.arange(8)   # the status word's bits (0 non-SPD, 1 skipped, 2 corrupt state; spare to 7)
+
+
+def or_reduce_status(status, group=None):
+    """In place: the bitwise OR of the int status words over the ranks of
+    `group` - one int per bit, all-reduced with MAX, repacked (a MAX of the
+    packed words keeps the highest word, dropping the other ranks' lower bits)."""
+    import torch.distributed as dist
+    shifts = _STATUS_SHIFTS.to(status.device, status.dtype)
+    bits = (status.unsqueeze(-1) >> shifts) & 1
+    dist.all_reduce(bits, op=dist.ReduceOp.MAX, group=group)
+    status.copy_((bits << shifts).sum(-1, dtype=status.dtype))
+    return status
 
 
 def global_edges(ii_host, jj_host, comm, call_key):

@@ -230,6 +230,39 @@ def test_global_edges_regather_agreed_across_ranks():
     assert res[0][1] is not None and "not in the global edge list" in res[0][1]
 
 
+def _status_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from droid_mi355x.depth_video import or_reduce_status
+        # [this solve, sticky]: rank 0 non-SPD (bit 0) then a timeout (bit 1);
+        # rank 1 corrupt state (bits 1 and 2) - MAX of the packed words would give 6 / 6
+        words = {0: [1, 3], 1: [6, 6]}[rank]
+        status = torch.tensor(words, dtype=torch.int32)
+        or_reduce_status(status)
+        q.put((rank, status.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_status_words_or_reduced_per_bit():
+    """the sharded BA agrees on the status words per bit (OR), so a
+    rank's non-SPD bit survives another rank's higher timeout / corrupt word."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_status_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1] == [7, 7]
+
+
 def test_plan_rejects_local_edges_missing_from_global_list():
     """ADVICE r2 (ba_plan.cpp): a local edge whose blocks have no input tile in
     the factor structure built from the global list is an error, not a write
