@@ -230,7 +230,7 @@ def ba(poses, disps, intrinsics, disps_sens, targets, weights, eta, ii, jj, t0, 
         C = accum(Cii, ii, kx) + m * ALPHA + (1 - m) * eta2
         w = accum(bz, ii, kx) - m * ALPHA * (disps[kx] - disps_sens[kx]).reshape(-1, HW)
         Q = 1.0 / C
-        Ei = accum(Eii.reshape(len(ii), -1), ii, ts).reshape(P, 6, HW)
+        Ei = accum(Eii.reshape(len(ii), 6 * HW), ii, ts).reshape(P, 6, HW)   # (explicit: E may be 0)
         Erows = np.concatenate([Ei, Eij], axis=0)     # (P+E, 6, HW)
 
         # schur_block :1222-1311 -- pairs of rows sharing a depth map
