@@ -51,7 +51,10 @@ pot = pot[np.argsort(p[pot, 0])]
 # potrf stamps: 0 ticket (or chained start), 1 deps met, 2 last update's block column 0 applied (panels
 # start), 3 panels done, 6 tile (k+1,k) in LDS and the D_p formed, 5 (k+1,k) solved + published, 7 end;
 # 8 + 2p / 9 + 2p: wave 0's panel p start / end; 16 / 17 wave 1's D_p start / end; 18 tile solved; 19 stores issued
-names = ["wait deps", "L(k,klast) + col 0", "panels", "wait A(k+1,k)", "D + trsm(k+1,k) + publish", "end"]
+# (phase 4 - stamps 3 -> 6 - is the D_p, the L_kk stores and the barrier after which tile (k+1,k)
+# is in LDS; phase 5 the tall_solve of (k+1,k), its stores and publish; until round 6 the labels
+# read "wait A(k+1,k)" / "D + trsm(k+1,k) + publish")
+names = ["wait deps", "L(k,klast) + col 0", "panels", "D_p + L_kk stores + barrier", "trsm(k+1,k) + publish", "end"]
 rows = []
 for a, k in enumerate(pot):
     r = p[k]
