@@ -241,7 +241,7 @@ def ba_sharded(poses, disps, intrinsics, disps_sens, target, weight, eta, ii_hos
     return [dx, dz]
 
 
-_STATUS_SHIFTS = torch.arange(8)   # the status word's bits (0 non-SPD, 1 skipped, 2 corrupt state; spare to 7)
+_STATUS_BITS = 8   # the status word's bits (0 non-SPD, 1 skipped, 2 corrupt state; spare to 7)
 
 
 def or_reduce_status(status, group=None):
@@ -249,7 +249,9 @@ def or_reduce_status(status, group=None):
     `group` - one int per bit, all-reduced with MAX, repacked (a MAX of the
     packed words keeps the highest word, dropping the other ranks' lower bits)."""
     import torch.distributed as dist
-    shifts = _STATUS_SHIFTS.to(status.device, status.dtype)
+    # made on the device (a host tensor's .to() would be a pageable H2D copy per
+    # GN iteration, which waits for the stream)
+    shifts = torch.arange(_STATUS_BITS, device=status.device, dtype=status.dtype)
     bits = (status.unsqueeze(-1) >> shifts) & 1
     dist.all_reduce(bits, op=dist.ReduceOp.MAX, group=group)
     status.copy_((bits << shifts).sum(-1, dtype=status.dtype))
