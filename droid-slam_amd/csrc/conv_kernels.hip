@@ -1214,32 +1214,48 @@ __device__ __forceinline__ void band_epilogue_core(const ConvArgs& a, _Float16* 
 // EPI_DWHEAD (band <256,256> only): the delta/weight heads (droid_net.py:
 // 95-103: conv3x3 128->256 + ReLU, then conv3x3 256->2 per head) in one launch.
 // The 256-channel hidden map dw of the tile's R image rows never leaves the CU:
-//   (1) T = relu(acc + bias) -> LDS fp16 [256 px][264];
+//   (1) T = relu(acc + bias) -> LDS fp16, stored channel-major [256 ch][256 px]
+//       (see dwh_t_off): a lane's accumulators are 4 consecutive pixels of one
+//       channel, so each fragment is ONE 8-B store with no lane exchange;
 //   (2) Y[p][tap*4 + c] = sum_ch T[p][ch] Wh[c][ch][tap] for all 9 taps at once
 //       (one 256 x 48 x 256 MFMA GEMM: the taps ride on the N dimension, so the
-//       tile needs no halo);
+//       tile needs no halo); its pixel operand comes back channel-contiguous by
+//       ds_read_b64_tr_b16 (cdna_hip_programming.md T10);
 //   (3) out[o][c] = sum over taps of Y[o + shift(tap)][tap*4 + c] for the output
 //       rows y0-1 .. y0+R that this tile's rows feed, atomically added into the
 //       zero-initialised fp32 out32 (E,H,W,4).  Each output pixel receives at most
 //       two contributions (this tile and one neighbour), so the result does not
 //       depend on their order.  Head bias and the weight sigmoid are applied by
 //       the caller.
+// Byte offset of the 4-pixel chunk ch (pixels 4 ch .. + 3, 8 B) of channel row r
+// in the channel-major T image: 512-B rows, the chunk index XORed with a
+// function of r & 15.  Bits 0-1 of the XOR are (r >> 2) & 3 and bits 2-4 are
+// (r & 3) | ((r >> 3) & 1) << 2, which makes both accesses conflict-free:
+//   pass-1 ds_write_b64 (banks mod 32, 16-lane groups): one chunk of 16
+//     consecutive rows -> (chunk ^ x) mod 16 takes 16 distinct values;
+//   ds_read_b64_tr_b16 (banks mod 64, 32-lane halves): rows r0 + {0..3, 8..11}
+//     (+4), chunks 4F .. 4F+3 -> (chunk ^ x) mod 32 takes 32 distinct values.
+__device__ __forceinline__ int dwh_t_off(int r, int ch) {
+  const int x = ((r >> 2) & 3) | ((r & 3) << 2) | (((r >> 3) & 1) << 4);
+  return r * 512 + ((ch ^ x) << 3);
+}
+
 template <int FM, int FN, int WM = 4, bool CONTIG = false>
 __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc)[FM][FN], _Float16* smem, long m0,
                                                 int wm, int wn, int lane, int tid, float bcol,
                                                 long long* prof = nullptr) {
-  constexpr int TMX = 256, TS = 264, YS = 37, NT = 512;
+  constexpr int TMX = 256, YS = 37, NT = 512;
   const int W = a.W, H = a.H, HW = H * W;
   const int R = TMX / W;
   const int b = (int)(m0 / HW);
   const int y0 = (int)((m0 % HW) / W);
   const int fr = lane & 15, fq = lane >> 4;
-  _Float16* T = smem;             // [256][TS]
+  char* const T = reinterpret_cast<char*>(smem);   // [256 ch][256 px] fp16, dwh_t_off
   // head weights [48][256] fp16, unpadded 512-B rows with the 16-B piece p of
   // row r stored at slot p ^ (r & 15) (the 16 rows of a B fragment read one
   // piece each: 16 distinct 16-B slots of one 256-B span, conflict-free)
-  _Float16* Bh = smem + TMX * TS;
-  float* const bl = reinterpret_cast<float*>(smem + TMX * TS + 48 * 256);  // [256] column biases
+  _Float16* Bh = smem + TMX * 256;
+  float* const bl = reinterpret_cast<float*>(smem + TMX * 256 + 48 * 256);  // [256] column biases
   __syncthreads();  // main-loop LDS reads are done
   {
     // the head weights (24 KB) by LDS-DMA now, so they land during pass 1 and
@@ -1257,16 +1273,29 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
   }
   if (tid < 256) bl[tid] = bcol;
   __syncthreads();
-  // lane (fr, fq) of fragment (i, j): pixels frag_row(i) + 4 fq .. + 3 of channel 16 j + fr
+  // lane (fr, fq) of fragment (i, j): pixels frag_row(i) + 4 fq .. + 3 of
+  // channel 16 j + fr = one 8-B chunk of channel row c.  ReLU after the fp16
+  // rounding: round(max(x, 0)) == max(round(x), 0) (rounding is monotone and
+  // keeps 0), up to the sign of a zero, which no later sum can see.
+  {
+    typedef float f2_t __attribute__((ext_vector_type(2)));
+    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+    const h2_t zero2 = {(_Float16)0.f, (_Float16)0.f};
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int c = wn * FN * 16 + j * 16 + fr;
-    const float bv = bl[c];
+    for (int j = 0; j < FN; ++j) {
+      const int c = wn * FN * 16 + j * 16 + fr;
+      const float bv = bl[c];
+      const f2_t b2 = {bv, bv};
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
-      stage_pixel_pairs(T, frag_row<FM, WM, CONTIG>(wm, i) + fq * 4, c, TS, fr,
-                        pack_f16x2(fmaxf(acc[i][j][0] + bv, 0.f), fmaxf(acc[i][j][1] + bv, 0.f)),
-                        pack_f16x2(fmaxf(acc[i][j][2] + bv, 0.f), fmaxf(acc[i][j][3] + bv, 0.f)));
+      for (int i = 0; i < FM; ++i) {
+        const h2_t lo = __builtin_elementwise_max(
+            __builtin_convertvector(f2_t{acc[i][j][0], acc[i][j][1]} + b2, h2_t), zero2);
+        const h2_t hi = __builtin_elementwise_max(
+            __builtin_convertvector(f2_t{acc[i][j][2], acc[i][j][3]} + b2, h2_t), zero2);
+        const half4_t o = {lo.x, lo.y, hi.x, hi.y};
+        *reinterpret_cast<half4_t*>(T + dwh_t_off(c, (frag_row<FM, WM, CONTIG>(wm, i) >> 2) + fq)) = o;
+      }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's head-weight DMAs landed
   __syncthreads();
@@ -1278,12 +1307,28 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
   for (int f = 0; f < 2; ++f)
 #pragma unroll
     for (int n = 0; n < 3; ++n) y[f][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // A operand of pixel fragment F = 2 wave + f, k-step s, by two transposed
+  // reads: lane (i = fr, g = fq) gets channels 32 s + 8 g + 4 t .. + 3 (t = 0, 1)
+  // of pixel 16 F + i; as the address-supplying lane 4 q + p of its 16-lane
+  // group it points at channel row 32 s + 8 g + 4 t + q, pixels 16 F + 4 p .. + 3
+  typedef short s4_t __attribute__((vector_size(8)));
+  int toff[2][2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) toff[f][t] = dwh_t_off(8 * fq + 4 * t + (fr >> 2), 4 * (2 * wave + f) + (fr & 3));
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     half8 af[2], bf[3];
 #pragma unroll
-    for (int f = 0; f < 2; ++f)
-      af[f] = *reinterpret_cast<const half8*>(&T[((2 * wave + f) * 16 + fr) * TS + s * 32 + fq * 8]);
+    for (int f = 0; f < 2; ++f) {
+      const s4_t r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s4_t*)(T + toff[f][0] + s * 32 * 512));
+      const s4_t r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s4_t*)(T + toff[f][1] + s * 32 * 512));
+      const half4_t h0 = __builtin_bit_cast(half4_t, r0), h1 = __builtin_bit_cast(half4_t, r1);
+      af[f] = half8{h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    }
 #pragma unroll
     for (int n = 0; n < 3; ++n) {
       const int row = n * 16 + fr;
@@ -1314,16 +1359,27 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
     const int orow = px / W - 1, x = px - (px / W) * W;
     const int oy = y0 + orow;
     if (oy < 0 || oy >= H) continue;
+    // all nine taps read first (clamped in-tile addresses), the out-of-tile ones
+    // then summed as +0: the same sum in the same order as skipping them (the
+    // running sum starts at +0 and so is never -0)
+    float v[9];
+#pragma unroll
+    for (int ty = -1; ty <= 1; ++ty) {
+      const int sr = min(max(orow + ty, 0), R - 1);
+#pragma unroll
+      for (int tx = -1; tx <= 1; ++tx) {
+        const int sx = min(max(x + tx, 0), W - 1);
+        v[(ty + 1) * 3 + tx + 1] = Y[(sr * W + sx) * YS + ((ty + 1) * 3 + tx + 1) * 4 + c];
+      }
+    }
     float sum = 0.f;
 #pragma unroll
     for (int ty = -1; ty <= 1; ++ty) {
-      const int sr = orow + ty;
-      if (sr < 0 || sr >= R) continue;
+      const bool rok = orow + ty >= 0 && orow + ty < R;
 #pragma unroll
       for (int tx = -1; tx <= 1; ++tx) {
-        const int sx = x + tx;
-        if (sx < 0 || sx >= W) continue;
-        sum += Y[(sr * W + sx) * YS + ((ty + 1) * 3 + tx + 1) * 4 + c];
+        const bool ok = rok && x + tx >= 0 && x + tx < W;
+        sum += ok ? v[(ty + 1) * 3 + tx + 1] : 0.f;
       }
     }
     atomicAdd(a.out32 + ((long)b * HW + (long)oy * W + x) * 4 + c, sum);
