@@ -1281,11 +1281,19 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
     typedef float f2_t __attribute__((ext_vector_type(2)));
     typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
     const h2_t zero2 = {(_Float16)0.f, (_Float16)0.f};
+    // every column bias read before the first store (lgkmcnt counts both: a read
+    // issued between stores waits for them), and one address per pixel fragment:
+    // dwh_t_off(c + 16 j, ch) = dwh_t_off(c, ch) + 16 j * 512 (the XOR depends on
+    // c & 15 only), so the channel blocks are immediate offsets
+    float bv[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bv[j] = bl[wn * FN * 16 + j * 16 + fr];
+    char* tb[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) tb[i] = T + dwh_t_off(wn * FN * 16 + fr, (frag_row<FM, WM, CONTIG>(wm, i) >> 2) + fq);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int c = wn * FN * 16 + j * 16 + fr;
-      const float bv = bl[c];
-      const f2_t b2 = {bv, bv};
+      const f2_t b2 = {bv[j], bv[j]};
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const h2_t lo = __builtin_elementwise_max(
@@ -1293,7 +1301,7 @@ __device__ __forceinline__ void dwhead_epilogue(const ConvArgs& a, floatx4 (&acc
         const h2_t hi = __builtin_elementwise_max(
             __builtin_convertvector(f2_t{acc[i][j][2], acc[i][j][3]} + b2, h2_t), zero2);
         const half4_t o = {lo.x, lo.y, hi.x, hi.y};
-        *reinterpret_cast<half4_t*>(T + dwh_t_off(c, (frag_row<FM, WM, CONTIG>(wm, i) >> 2) + fq)) = o;
+        *reinterpret_cast<half4_t*>(tb[i] + j * 16 * 512) = o;
       }
     }
   }
