@@ -1832,10 +1832,13 @@ static int launch_chol_dataflow(const BaPlan& p, char* ws, float* dx, hipStream_
   }
   if (inj != kInjectStale)
     if (int st = ba_zero(c.sync, p.sync_bytes, stream)) return st;
-  // one worker per two CUs: the same makespan at C3 (2.38 vs 2.41 ms for
-  // BA(itrs=2)) and 10 % less at C5 (11.6 vs 12.9 ms) than one per CU - fewer
-  // workers polling the hand-off counters (profiles/r02/chol_grid_r02dn.txt)
-  int grid = std::min(p.cs.ntasks, std::max(1, num_cus() / 2));
+  // workers: one per CU on the small task graphs (C3, 2.3k tasks: BA(itrs=2)
+  // 1.88 vs 1.95 ms with one per two CUs, the chain's tasks start sooner) and
+  // three per four CUs on the large ones (C5, 23.9k tasks: 10.9 vs 11.3 ms; one
+  // per CU 11.7 - the extra workers' polling of the hand-off counters costs
+  // more than they add), round 6, profiles/r06/r06zd_chol_grid.txt
+  const int ncu = num_cus();
+  int grid = std::min(p.cs.ntasks, std::max(1, p.cs.ntasks <= 8192 ? ncu : 3 * ncu / 4));
   if (const int g = ab_knob("DROID_CHOL_GRID", 0)) grid = std::max(1, std::min(p.cs.ntasks, g));  // A/B runs
   chol_dataflow_kernel<<<grid, 256, kCholLds, stream>>>(c);
   DROID_LAUNCH_CHECK();
