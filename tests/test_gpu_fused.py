@@ -206,7 +206,7 @@ def test_conv_gru_epilogues(B, H, W):
     np.testing.assert_allclose(host(hn.float()), host(ref), atol=3e-3)
 
 
-@pytest.mark.parametrize("B,H,W", [(2, 8, 64), (3, 16, 32), (1, 48, 64)])
+@pytest.mark.parametrize("B,H,W", [(2, 8, 64), (3, 16, 32), (2, 32, 16), (1, 48, 64)])
 def test_conv_dw_head_fused(B, H, W):
     """relu(conv3x3 128->256) -> block-diagonal conv3x3 256->4 in one launch vs torch fp32."""
     import droid_backends
